@@ -1,0 +1,577 @@
+"""BEASTBsplineTokenizer -- drop-in for beast/beast_bspline_tokenizer.py:45-720.
+
+Same constructor, attributes, methods, return types, on-disk format and error
+types as the reference; every per-batch computation runs in libbeast_hip.so on a
+ROCm GPU (MI355X / gfx950):
+
+* ``encode``          -> ``beast_encode_f32``: fit + clamp + quantise + (d t)->(t d)
+                         + LLM offset in one kernel (reference :399-428)
+* ``compute_weights`` -> ``beast_encode_f32`` without the quantiser (:344-360)
+* ``decode``          -> ``beast_reconstruct_f32`` dequantise only (:483-496)
+* ``reconstruct_traj``-> ``beast_reconstruct_f32`` (:498-536)
+* ``fit_parameters``  -> fit kernel + GPU radix-select quantiles (:181-220)
+
+Tensors on the CPU are moved to ``self.device`` exactly as the reference does
+(``trajs.to(self.device)``); a non-GPU device raises ``RuntimeError`` when
+compute is requested (config / serialisation work anywhere).
+
+Deliberate divergences:
+* ``from_pretrained`` works: the reference passes ``tokenizer_type`` back into
+  ``__init__`` and raises TypeError (:322, :333); here ``__init__`` accepts it.
+* ``compute_reconstruction_error(..., return_tokens=True)`` (used by
+  train/eval.py:34) is accepted.
+* ``reconstruct_traj_continuous`` implements the intent of ``denormalize_tensor``
+  (beast/utils.py:42 raises TypeError in the reference).
+* ``init_cond_order`` / ``end_cond_order`` != 0 raise NotImplementedError
+  (BEAST's default is 0).
+"""
+from __future__ import annotations
+
+import json
+import numbers
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .base_tokenizer import TokenizerBase
+from .bspline import DeviceBasis
+
+CONFIG_FILENAME = "beast_tokenizer_config.json"
+
+
+def _tqdm(it, **kw):
+    try:
+        from tqdm import tqdm
+        return tqdm(it, **kw)
+    except Exception:  # pragma: no cover
+        return it
+
+
+class _MPInfo:
+    """Lightweight stand-in for the reference's ``self.mp`` / ``self.gripper_mp``
+    objects (mp_pytorch UniformBSpline): carries their configuration only."""
+
+    def __init__(self, num_dof: int, num_basis: int, degree_p: int, tau: float):
+        self.num_dof, self.num_basis, self.degree_p, self.tau = num_dof, num_basis, degree_p, tau
+
+    def __repr__(self) -> str:
+        return (f"UniformBSpline(num_dof={self.num_dof}, num_basis={self.num_basis}, degree_p={self.degree_p}, "
+                f"tau={self.tau:.6g})")
+
+
+class BEASTBsplineTokenizer(TokenizerBase):
+
+    def __init__(self, num_dof=1, num_basis=10, duration=2 * torch.pi, seq_len=50, vocab_size=256,
+                 degree_p=4, gripper_zero_order=False, gripper_indices=None,
+                 init_cond_order=0, end_cond_order=0, init_pos=True,
+                 use_bpe=False, device="cuda", llm_vocab_size: Optional[int] = None,
+                 tokenizer_type: Optional[str] = None):
+        super().__init__()
+        if init_cond_order != 0 or end_cond_order != 0:
+            raise NotImplementedError("init/end condition order != 0 is not supported by the HIP path")
+
+        self.dt = 0.01  # reference :53
+
+        # reference :55-70
+        if gripper_indices is None or not gripper_zero_order:
+            gripper_indices = []
+        self.gripper_indices = sorted(gripper_indices)
+        if not gripper_zero_order or len(self.gripper_indices) == 0:
+            self.gripper_dof = 0
+        else:
+            self.gripper_dof = len(self.gripper_indices)
+        self.joint_dof = num_dof - self.gripper_dof
+        all_indices = set(range(num_dof))
+        self.joint_indices = sorted(list(all_indices - set(self.gripper_indices)))
+
+        self.bspline_config = {
+            "mp_type": "uni_bspline", "device": device, "num_dof": self.joint_dof, "tau": duration,
+            "mp_args": {"num_basis": num_basis, "degree_p": degree_p, "init_condition_order": init_cond_order,
+                        "end_condition_order": end_cond_order, "dt": 0.01},
+        }
+        self.init_pos = init_pos
+        self.mp = _MPInfo(self.joint_dof, num_basis, degree_p, duration)
+        self.gripper_mp = None
+        if gripper_zero_order and self.gripper_dof > 0:
+            self.gripper_mp_config = {"mp_type": "uni_bspline", "device": device, "num_dof": self.gripper_dof,
+                                      "tau": duration, "mp_args": {"num_basis": num_basis, "degree_p": 0}}
+            self.gripper_mp = _MPInfo(self.gripper_dof, num_basis, 0, duration)
+            print(
+                f"Gripper MP initialized with {num_basis} basis functions for "
+                f"{self.gripper_dof} DOFs at indices {self.gripper_indices}"
+            )
+
+        self.device = device
+        self.num_dof = self.joint_dof + self.gripper_dof
+        self.num_basis = num_basis
+        self.degree_p = degree_p
+        self.vocab_size = vocab_size
+        self.duration = duration
+        self.seq_length = seq_len
+        self.use_bpe = use_bpe
+
+        self._basis = DeviceBasis(num_basis, degree_p, duration, self.gripper_mp is not None)
+        self._times_version = 0
+        # tensor_linspace(0, duration, seq_len) == torch.linspace in fp32 (util_matrix.py:114-116)
+        self.times = torch.linspace(0, duration, seq_len).to(device)
+
+        dev = torch.device(device)
+        buf_dev = dev if dev.type == "cuda" else torch.device("cpu")
+        self.register_buffer("w_min", -0.02 * torch.ones((num_dof * num_basis), device=buf_dev))
+        self.register_buffer("w_max", 0.02 * torch.ones((num_dof * num_basis), device=buf_dev))
+        self.llm_vocab_size = None
+        self._dof_cache = {}
+
+        self._config = {
+            'tokenizer_type': 'beast_bspline',
+            'num_dof': num_dof,
+            'num_basis': num_basis,
+            'duration': float(duration),
+            'seq_len': seq_len,
+            'vocab_size': vocab_size,
+            'degree_p': degree_p,
+            'gripper_zero_order': gripper_zero_order,
+            'gripper_indices': list(self.gripper_indices),
+            'init_cond_order': init_cond_order,
+            'end_cond_order': end_cond_order,
+            'init_pos': init_pos,
+            'use_bpe': use_bpe,
+            'device': device,
+        }
+
+        if llm_vocab_size is not None:
+            self.set_llm_vocab_size(llm_vocab_size)
+
+    # ===============================================
+    #           - device plumbing -
+    # ===============================================
+
+    @property
+    def times(self) -> torch.Tensor:
+        return self._times
+
+    @times.setter
+    def times(self, value: torch.Tensor) -> None:
+        self._times = value
+        self._times_version = getattr(self, "_times_version", 0) + 1
+
+    def _dev(self) -> torch.device:
+        dev = torch.device(self.device)
+        if dev.type != "cuda":
+            raise RuntimeError(
+                f"BEASTBsplineTokenizer(device={self.device!r}): the BEAST hot path runs only on a ROCm GPU "
+                "(MI355X, gfx950); there is no CPU fallback")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        _lib.load()
+        return dev
+
+    def _constants(self, dev: torch.device):
+        t = self.times.to(dev, dtype=torch.float32).reshape(-1)
+        return self._basis.constants(t, self._times_version)
+
+    def _dof_maps(self, dev: torch.device):
+        hit = self._dof_cache.get(dev)
+        if hit is None:
+            order = self.joint_indices + self.gripper_indices
+            src = torch.tensor(order, dtype=torch.int32, device=dev)
+            hit = (src, src.clone())  # dof_src (encode) == dof_dst (reconstruct)
+            self._dof_cache[dev] = hit
+        return hit
+
+    def _bounds(self, dev: torch.device):
+        return (self.w_min.to(dev, torch.float32).contiguous(), self.w_max.to(dev, torch.float32).contiguous())
+
+    def _offset(self, respect_llm_vocab_size: bool) -> int:
+        if respect_llm_vocab_size and self.llm_vocab_size is not None:
+            return self._llm_vocab_offset()
+        return 0
+
+    def _fit(self, trajs: torch.Tensor, tokens_offset: Optional[int], dev: torch.device):
+        """Launch the fused fit (+ quantise) kernel. Returns (params, tokens or None)."""
+        if trajs.dim() != 3 or trajs.shape[1] != self.times.numel():
+            # learn_mp_params_from_trajs asserts trajs.shape[:-1] == times.shape (uni_bspline.py:487)
+            raise AssertionError(f"trajectory shape {tuple(trajs.shape)} does not match [B, {self.times.numel()}, "
+                                 f"num_dof] time grid")
+        B, T, Din = trajs.shape
+        if Din < self.num_dof and (self.joint_indices + self.gripper_indices):
+            top = max(self.joint_indices + self.gripper_indices)
+            if top >= Din:
+                raise IndexError(f"index {top} is out of bounds for dimension 2 with size {Din}")
+        if trajs.stride(2) != 1 and trajs.numel():
+            trajs = trajs.contiguous()
+        _, proj = self._constants(dev)
+        src, _ = self._dof_maps(dev)
+        D, N = self.num_dof, self.num_basis
+        params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
+        tokens = None
+        wmn = wmx = None
+        if tokens_offset is not None:
+            tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
+            wmn, wmx = self._bounds(dev)
+        _lib.run("beast_encode_f32", trajs.data_ptr(), B, T, trajs.stride(0), trajs.stride(1), trajs.stride(2),
+                 Din, D, self.joint_dof, src.data_ptr(), proj.data_ptr(), N, _lib.ptr(wmn), _lib.ptr(wmx),
+                 self.vocab_size, tokens_offset or 0, params.data_ptr(), _lib.ptr(tokens), _lib.stream_of(dev))
+        return params, tokens
+
+    # ===============================================
+    #           - tokenizer preparation -
+    # ===============================================
+
+    def set_llm_vocab_size(self, llm_vocab_size: Optional[int]):
+        """Specify the upstream LLM vocabulary size (reference :145-168)."""
+        if llm_vocab_size is None:
+            self.llm_vocab_size = None
+            self._config.pop('llm_vocab_size', None)
+            return
+        if not isinstance(llm_vocab_size, numbers.Integral):
+            raise TypeError("llm_vocab_size must be an integer or None")
+        llm_vocab_size = int(llm_vocab_size)
+        if llm_vocab_size < self.vocab_size:
+            raise ValueError(
+                "llm_vocab_size must be greater or equal to tokenizer vocab size"
+            )
+        self.llm_vocab_size = llm_vocab_size
+        self._config['llm_vocab_size'] = llm_vocab_size
+
+    def update_vlm_vocab_size(self, vlm_vocab_size):
+        """Backward-compatible alias for :meth:`set_llm_vocab_size`."""
+        self.set_llm_vocab_size(vlm_vocab_size)
+
+    def _llm_vocab_offset(self) -> int:
+        if self.llm_vocab_size is None:
+            raise ValueError("LLM vocab size is not set.")
+        return self.llm_vocab_size - self.vocab_size
+
+    @torch.no_grad()
+    def fit_parameters(self, dataloader, max_samples=None, verbose=True, *, process_group=None):
+        """Fit w_min/w_max as the 1%/99% quantiles of the fitted params (reference :181-220).
+
+        ``max_samples`` counts batches, as in the reference.  With
+        ``process_group`` (torch.distributed, RCCL) every rank fits its own shard
+        and the quantiles are those of the union of all ranks' params.
+        """
+        from .quantile import column_quantiles
+        from .bpe_train import no_reduce, torch_dist_reducer
+
+        dev = self._dev()
+        params = []
+        sample_limit = max_samples if max_samples is not None else float("inf")
+        iterator = _tqdm(dataloader, total=max_samples, desc="precomputing weight normalizer of MP",
+                         unit="batch") if verbose else dataloader
+        sample_count = 0
+        for batch in iterator:
+            if "actions" not in batch:
+                raise KeyError("Expected batch to contain an 'actions' entry.")
+            act_chunks = batch["actions"][..., : self.num_dof]
+            params.append(self.compute_weights(act_chunks))
+            sample_count += 1
+            if sample_count >= sample_limit:
+                if verbose:
+                    print("Precomputed enough samples for weight normalizer of MP")
+                break
+        if not params and process_group is None:
+            raise RuntimeError("No parameters were gathered from the dataloader.")
+        allp = torch.cat(params, dim=0) if params else torch.empty((0, self.num_dof * self.num_basis),
+                                                                   device=dev)
+        reduce = no_reduce if process_group is None else torch_dist_reducer(
+            None if process_group is True else process_group)
+        q = column_quantiles(allp, [0.01, 0.99], reduce)
+        self.w_min.copy_(q[0].to(self.w_min.device))
+        self.w_max.copy_(q[1].to(self.w_max.device))
+
+    # ===============================================
+    #           - tokenizer serialization -
+    # ===============================================
+
+    def get_config(self):
+        config = self._config.copy()
+        if self.llm_vocab_size is not None:
+            config['llm_vocab_size'] = self.llm_vocab_size
+        return config
+
+    def state_dict(self):
+        """Config + fitted bounds as JSON-able lists (reference :235-245)."""
+        return {
+            'config': self.get_config(),
+            'w_min': self.w_min.cpu().numpy().tolist(),
+            'w_max': self.w_max.cpu().numpy().tolist(),
+            'llm_vocab_size': self.llm_vocab_size,
+        }
+
+    def load_state_dict(self, state_dict):
+        """Reference :248-269."""
+        if 'w_min' in state_dict:
+            w_min = torch.tensor(state_dict['w_min'], dtype=torch.float32, device=self.w_min.device)
+            self.w_min.copy_(w_min)
+        if 'w_max' in state_dict:
+            w_max = torch.tensor(state_dict['w_max'], dtype=torch.float32, device=self.w_max.device)
+            self.w_max.copy_(w_max)
+        llm_size = state_dict.get('llm_vocab_size')
+        if llm_size is None:
+            llm_size = state_dict.get('vlm_vocab_size')
+        if llm_size is not None:
+            self.set_llm_vocab_size(llm_size)
+        print(f"✓ Loaded fitted parameters (w_min, w_max) with shape {self.w_min.shape}")
+
+    def save_pretrained(self, save_directory):
+        """Write ``beast_tokenizer_config.json`` (reference :272-290)."""
+        save_directory = Path(save_directory)
+        save_directory.mkdir(parents=True, exist_ok=True)
+        state = self.state_dict()
+        config_path = save_directory / CONFIG_FILENAME
+        with open(config_path, 'w') as f:
+            json.dump(state, f, indent=2)
+        print(f"✓ Saved tokenizer to {save_directory}")
+        print(f"  - Config: {config_path}")
+
+    @classmethod
+    def from_pretrained(cls, pretrained_path, device=None):
+        """Reference :293-338 (works: ``tokenizer_type`` is accepted by ``__init__``)."""
+        pretrained_path = Path(pretrained_path)
+        config_path = pretrained_path / CONFIG_FILENAME
+        if not config_path.exists():
+            raise FileNotFoundError(f"Config file not found: {config_path}")
+        with open(config_path, 'r') as f:
+            state = json.load(f)
+        config = state['config'].copy()
+        tokenizer_type = config.get('tokenizer_type')
+        if tokenizer_type not in {'beast_bspline', None}:
+            raise ValueError(
+                "Loaded configuration does not describe a BEAST B-Spline tokenizer."
+            )
+        config['tokenizer_type'] = 'beast_bspline'
+        if device is not None:
+            config['device'] = device
+        print(f"✓ Loading tokenizer from {pretrained_path}")
+        print(f"  - Config: num_dof={config['num_dof']}, num_basis={config['num_basis']}, "
+              f"gripper_indices={config['gripper_indices']}")
+        tokenizer = cls(**config)
+        tokenizer.load_state_dict(state)
+        return tokenizer
+
+    # ===============================================
+    #              - tokenizer utils -
+    # ===============================================
+
+    @torch.no_grad()
+    def compute_weights(self, demos):
+        """Fitted params [B, num_dof*num_basis] in (d n) order (reference :344-360)."""
+        dev = self._dev()
+        demos = demos.to(dev, dtype=torch.float32)
+        params, _ = self._fit(demos, None, dev)
+        return params
+
+    @torch.no_grad()
+    def update_weights_bounds(self, demos):
+        """w_min/w_max <- column min/max of the batch's params (reference :362-378)."""
+        from .quantile import column_minmax
+        weights = self.compute_weights(demos)
+        mn, mx = column_minmax(weights)
+        self.w_min.copy_(mn.to(self.w_min.device))
+        self.w_max.copy_(mx.to(self.w_max.device))
+
+    @torch.no_grad()
+    def update_weights_bounds_per_batch(self, weights):
+        """Widen w_min/w_max by the batch extremes beyond a 1e-4 margin (reference :379-389)."""
+        from .quantile import column_minmax
+        weights = weights.reshape(-1, self.num_dof * self.num_basis)
+        batch_min, batch_max = column_minmax(weights)
+        wmin = self.w_min.to(batch_min.device)
+        wmax = self.w_max.to(batch_max.device)
+        smaller_mask = batch_min < (wmin - 1e-4)
+        larger_mask = batch_max > (wmax + 1e-4)
+        self.w_min.copy_(torch.where(smaller_mask, batch_min, wmin).to(self.w_min.device))
+        self.w_max.copy_(torch.where(larger_mask, batch_max, wmax).to(self.w_max.device))
+
+    def update_times(self, times):
+        self.times = times.to(self.device)
+
+    # ===============================================
+    #           - tokenizer encoding -
+    # ===============================================
+
+    @torch.no_grad()
+    def encode(self, trajs, update_bounds=False, *, respect_llm_vocab_size=True):
+        """(tokens int64 [B, num_basis*num_dof], params_dict) -- reference :399-428."""
+        dev = self._dev()
+        trajs = trajs.to(dev, dtype=torch.float32)
+        offset = self._offset(respect_llm_vocab_size)
+        if update_bounds:
+            params, _ = self._fit(trajs, None, dev)
+            self.update_weights_bounds_per_batch(params)
+            tokens = self._quantize(params, offset, dev, mode=0)
+        else:
+            params, tokens = self._fit(trajs, offset, dev)
+        params_dict = {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+        return tokens, params_dict
+
+    def _quantize(self, params: torch.Tensor, offset: int, dev: torch.device, mode: int):
+        B = params.shape[0]
+        D, N = self.num_dof, self.num_basis
+        wmn, wmx = self._bounds(dev)
+        params = params.contiguous()
+        if mode == 0:
+            out = torch.empty((B, N * D), dtype=torch.int64, device=dev)
+            _lib.run("beast_quantize_f32", params.data_ptr(), B, D, N, wmn.data_ptr(), wmx.data_ptr(),
+                     self.vocab_size, offset, 0, out.data_ptr(), None, _lib.stream_of(dev))
+        else:
+            out = torch.empty((B, N * D), dtype=torch.float32, device=dev)
+            _lib.run("beast_quantize_f32", params.data_ptr(), B, D, N, wmn.data_ptr(), wmx.data_ptr(),
+                     self.vocab_size, 0, 1, None, out.data_ptr(), _lib.stream_of(dev))
+        return out
+
+    @torch.no_grad()
+    def encode_continuous(self, trajs, update_bounds=False):
+        """Normalised params in [-1, 1], (t d) order (reference :430-450)."""
+        dev = self._dev()
+        trajs = trajs.to(dev, dtype=torch.float32)
+        params, _ = self._fit(trajs, None, dev)
+        if update_bounds:
+            self.update_weights_bounds_per_batch(params)
+        tokens = self._quantize(params, 0, dev, mode=1)
+        params_dict = {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+        return tokens, params_dict
+
+    # ===============================================
+    #           - tokenizer LLM tokenization -
+    # ===============================================
+
+    def tokens_to_llm_tokens(self, tokens):
+        tokens = tokens.to(self.device)
+        if len(tokens.shape) == 3:
+            tokens = tokens.reshape(tokens.shape[0], -1)
+        if self.llm_vocab_size is None:
+            raise ValueError("LLM vocab size is not set.")
+        return tokens + self._llm_vocab_offset()
+
+    def llm_tokens_to_mp_tokens(self, llm_tokens):
+        if self.llm_vocab_size is None:
+            raise ValueError("LLM vocab size is not set.")
+        tokens = llm_tokens - self._llm_vocab_offset()
+        if len(tokens.shape) == 2:
+            tokens = tokens.reshape(tokens.shape[0], self.num_basis, self.num_dof)
+        return tokens
+
+    # ===============================================
+    #            - tokenizer decoding -
+    # ===============================================
+
+    def reconstruct_from_llm_tokens(self, llm_tokens, times=None, **kwargs):
+        # reference :479-481 (subtracts the offset here AND in decode: kept as-is)
+        tokens = self.llm_tokens_to_mp_tokens(llm_tokens)
+        return self.reconstruct_traj(tokens, times=times, **kwargs)
+
+    def _token_rows(self, tokens, dev):
+        tokens = tokens.to(dev)
+        if tokens.dim() == 3:
+            tokens = tokens.reshape(tokens.shape[0], -1)
+        elif tokens.dim() != 2:
+            raise ValueError(f"Unexpected token shape {tokens.shape}")
+        if tokens.shape[1] != self.num_basis * self.num_dof:
+            raise ValueError(f"Token dimension {tokens.shape[1]} does not match expected "
+                             f"{self.num_basis * self.num_dof}.")
+        if tokens.dtype != torch.int64:
+            tokens = tokens.to(torch.int64)
+        return tokens.contiguous()
+
+    @torch.no_grad()
+    def decode(self, tokens, *, respect_llm_vocab_size=True):
+        """Dequantised params [B, num_dof*num_basis] in (d n) order (reference :483-496)."""
+        dev = self._dev()
+        tokens = self._token_rows(tokens, dev)
+        B = tokens.shape[0]
+        D, N = self.num_dof, self.num_basis
+        wmn, wmx = self._bounds(dev)
+        params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
+        _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, self.joint_dof, N, self.vocab_size,
+                 self._offset(respect_llm_vocab_size), wmn.data_ptr(), wmx.data_ptr(), None, 0, 0, None, D, None,
+                 0, None, params.data_ptr(), None, None, _lib.stream_of(dev))
+        return params
+
+    def _basis_for(self, times, B: int, dev: torch.device):
+        """(basis ptr tensor, batch stride, T_out) for reconstruct; default grid is cached."""
+        N = self.num_basis
+        if times is None:
+            phi, _ = self._constants(dev)
+            return phi, 0, phi.shape[1]
+        t = times.to(dev, dtype=torch.float32)
+        if t.dim() == 2 and t.shape[0] == B and (B == 1 or torch.equal(t, t[:1].expand_as(t))):
+            t = t[0]
+        if t.dim() == 1:
+            Tn = t.numel()
+            phi = torch.zeros((2, Tn, N), dtype=torch.float32, device=dev)
+            phi[: self._basis.n_kinds] = self._basis.basis_at(t)
+            return phi, 0, Tn
+        if t.dim() != 2 or t.shape[0] != B:
+            raise ValueError(f"times must be [T] or [B, T]; got {tuple(t.shape)} for B={B}")
+        Tn = t.shape[1]
+        phi_k = self._basis.basis_at(t)                       # [kinds, B, T, N]
+        phi = torch.zeros((B, 2, Tn, N), dtype=torch.float32, device=dev)
+        phi[:, : self._basis.n_kinds] = phi_k.permute(1, 0, 2, 3)
+        return phi, 2 * Tn * N, Tn
+
+    def _reconstruct(self, tokens, ntokens, times, init_p, respect_llm_vocab_size, dev):
+        src = tokens if tokens is not None else ntokens
+        B = src.shape[0]
+        D, N = self.num_dof, self.num_basis
+        wmn, wmx = self._bounds(dev)
+        phi, basis_sb, Tn = self._basis_for(times, B, dev)
+        _, dst = self._dof_maps(dev)
+        pos = torch.empty((B, Tn, D), dtype=torch.float32, device=dev)
+        ip = ip_src = None
+        if self.init_pos and init_p is not None and self.joint_dof > 0:
+            ip = torch.as_tensor(init_p).to(dev, dtype=torch.float32)
+            if ip.dim() != 2 or ip.shape[0] != B:
+                raise ValueError(f"init_p must be [B, num_dof]; got {tuple(ip.shape)}")
+            if ip.stride(1) != 1:
+                ip = ip.contiguous()
+            ip_src = dst[: self.joint_dof]
+        offset = self._offset(respect_llm_vocab_size) if tokens is not None else 0
+        _lib.run("beast_reconstruct_f32", _lib.ptr(tokens), B, D, self.joint_dof, N, self.vocab_size, offset,
+                 wmn.data_ptr(), wmx.data_ptr(), phi.data_ptr(), basis_sb, Tn, dst.data_ptr(), D, _lib.ptr(ip),
+                 ip.stride(0) if ip is not None else 0, _lib.ptr(ip_src), None, pos.data_ptr(), _lib.ptr(ntokens),
+                 _lib.stream_of(dev))
+        return pos
+
+    @torch.no_grad()
+    def reconstruct_traj(self, tokens, times=None, **kwargs):
+        """Positions [B, T, num_dof] from tokens (reference :498-536); kwargs: init_p [B, num_dof]."""
+        dev = self._dev()
+        tokens = self._token_rows(tokens, dev)
+        return self._reconstruct(tokens, None, times, kwargs.get("init_p"), True, dev)
+
+    @torch.no_grad()
+    def reconstruct_traj_continuous(self, params, times=None, **kwargs):
+        """Positions from normalised params in (t d) order (reference :538-582)."""
+        dev = self._dev()
+        params = params.to(dev)
+        if len(params.shape) == 3:
+            params = params.reshape(params.shape[0], -1)
+        if params.shape[-1] != self.num_basis * self.num_dof:
+            raise ValueError(
+                f"Token dimension {params.shape[-1]} does not match expected {self.num_basis * self.num_dof}."
+            )
+        params = params.to(torch.float32).contiguous()
+        return self._reconstruct(None, params, times, kwargs.get("init_p"), False, dev)
+
+    # ===============================================
+    #           - tokenizer evaluation -
+    # ===============================================
+
+    def compute_reconstruction_error(self, raw_traj, return_tokens=False):
+        """(mean squared error, mean signed error) of encode -> reconstruct (reference :589-597)."""
+        dev = self._dev()
+        raw_traj = raw_traj.to(dev, dtype=torch.float32)
+        if len(raw_traj.shape) == 2:
+            raw_traj = raw_traj.unsqueeze(0)
+        tokens, _ = self.encode(raw_traj)
+        reconstruct_trajs = self.reconstruct_traj(tokens)
+        error_l2 = torch.mean((raw_traj - reconstruct_trajs) ** 2)
+        error_l1 = torch.mean(raw_traj - reconstruct_trajs)
+        if return_tokens:
+            return error_l2, error_l1, tokens
+        return error_l2, error_l1

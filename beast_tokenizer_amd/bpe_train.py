@@ -1,0 +1,271 @@
+"""GPU byte-level BPE trainer.
+
+Replaces HF ``tokenizers``' ``BpeTrainer::do_train`` as FIGBPE drives it
+(beast/beast_bpe_trainer.py:61-98, ``ByteLevelBPETokenizer`` + ``BpeTrainer(
+vocab_size, min_frequency, special_tokens, initial_alphabet=chr(0..K),
+max_token_length)``).  Semantics restated from the HF trainer and pinned by
+tests/golden/bpe_hf.json (HF 0.22.2 outputs):
+
+* words = ByteLevel pre-tokenised pieces of ``chr(tok - min_token)`` strings;
+* alphabet = byte-level chars seen in words + the initial alphabet, ids by
+  ascending code point after the special tokens;
+* repeat while ``len(vocab) < vocab_size``: take the live pair with the largest
+  count (ties: smallest ``(id_a, id_b)``); stop if ``count < min_frequency``; the
+  new token is the concatenated string (an existing id is reused); merge it
+  left-to-right non-overlapping in every word; apply HF's pair-count changes;
+  the merged pair is retired.
+
+The driver below is written against a small ``ops`` interface so the same code
+runs the HIP kernels (:class:`GpuBpeOps`) and, in the CPU tests, a numpy stand-in;
+``reduce`` is the cross-rank all-reduce (``torch.distributed`` = RCCL over xGMI
+on MI355X; a no-op on one GPU).  Pair counts are additive over shards of the
+corpus, so data-parallel training all-reduces the initial pair table once and
+the four per-merge delta vectors ``[4][Vt]`` every merge; every rank then holds
+the same table and takes the same decisions.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .pretok import bytes_to_unicode, class_lut
+
+Reducer = Callable[[torch.Tensor, str], None]
+
+
+def no_reduce(t: torch.Tensor, op: str) -> None:  # single GPU
+    return None
+
+
+def torch_dist_reducer(group=None) -> Reducer:
+    import torch.distributed as dist
+    ops = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+    def red(t: torch.Tensor, op: str) -> None:
+        dist.all_reduce(t, op=ops[op], group=group)
+    return red
+
+
+@dataclass
+class BPEResult:
+    vocab: Dict[str, int]
+    merges: List[Tuple[str, str]]
+    min_token: int
+    max_token: int
+    stats: Dict[str, float] = field(default_factory=dict)
+
+
+class GpuBpeOps:
+    """The HIP kernels of csrc/bpe.hip behind the driver's ops interface."""
+
+    def __init__(self, device: torch.device):
+        self.device = torch.device(device)
+        self.stream = _lib.stream_of(self.device)
+        self._host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+
+    # -- small helpers
+    def _read_i64(self, t: torch.Tensor, n: int) -> List[int]:
+        h = self._host[:n]
+        h.copy_(t[:n], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return [int(v) for v in h.tolist()]
+
+    def minmax(self, tokens: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(2, dtype=torch.int64, device=self.device)
+        _lib.run("beast_i64_minmax", tokens.data_ptr(), tokens.numel(), out.data_ptr(), self.stream)
+        return out
+
+    def read(self, t: torch.Tensor) -> List[int]:
+        return self._read_i64(t, t.numel())
+
+    def to_numpy(self, t: torch.Tensor) -> np.ndarray:
+        return t.cpu().numpy()
+
+    def presence(self, tokens: torch.Tensor, mn: int, n_cp: int) -> torch.Tensor:
+        pr = torch.empty(n_cp, dtype=torch.uint8, device=self.device)
+        _lib.run("beast_bpe_cp_presence", tokens.data_ptr(), tokens.numel(), mn, pr.data_ptr(), n_cp, self.stream)
+        return pr
+
+    def pretokenize(self, tokens, seq_off, mn, lut: np.ndarray, byte2id: np.ndarray):
+        dev, s = self.device, self.stream
+        S = seq_off.numel() - 1
+        lut_d = torch.from_numpy(np.ascontiguousarray(lut)).to(dev)
+        b2i = torch.from_numpy(np.ascontiguousarray(byte2id, dtype=np.uint16).view(np.int16)).to(dev)
+        wps = torch.empty(S, dtype=torch.int64, device=dev)
+        sps = torch.empty(S, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_pretok_count", tokens.data_ptr(), seq_off.data_ptr(), S, mn, lut_d.data_ptr(),
+                 lut_d.numel(), wps.data_ptr(), sps.data_ptr(), s)
+        ws = torch.empty(_lib.load().beast_scan_workspace_bytes(S), dtype=torch.uint8, device=dev)
+        woff = torch.empty(S + 1, dtype=torch.int64, device=dev)
+        soff = torch.empty(S + 1, dtype=torch.int64, device=dev)
+        _lib.run("beast_exclusive_scan_i64", wps.data_ptr(), woff.data_ptr(), S, ws.data_ptr(), s)
+        _lib.run("beast_exclusive_scan_i64", sps.data_ptr(), soff.data_ptr(), S, ws.data_ptr(), s)
+        nw, ns = self._read_i64(torch.stack([woff[S], soff[S]]), 2)
+        if ns >= 2 ** 32:
+            raise NotImplementedError("BPE corpus has >= 2^32 byte symbols on one GPU; shard it over more ranks")
+        sym = torch.empty(max(ns, 1), dtype=torch.int16, device=dev)
+        wstart = torch.empty(max(nw, 1), dtype=torch.int32, device=dev)
+        wlen = torch.empty(max(nw, 1), dtype=torch.int32, device=dev)
+        _lib.run("beast_bpe_pretok_emit", tokens.data_ptr(), seq_off.data_ptr(), S, mn, lut_d.data_ptr(),
+                 lut_d.numel(), woff.data_ptr(), soff.data_ptr(), b2i.data_ptr(), sym.data_ptr(), wstart.data_ptr(),
+                 wlen.data_ptr(), s)
+        return {"sym": sym, "wstart": wstart, "wlen": wlen, "n_words": nw, "n_syms": ns}
+
+    def count_pairs(self, words, Vt: int) -> torch.Tensor:
+        table = torch.zeros(Vt * Vt, dtype=torch.int32, device=self.device)
+        _lib.run("beast_bpe_count_pairs", words["sym"].data_ptr(), words["wstart"].data_ptr(),
+                 words["wlen"].data_ptr(), None, words["n_words"], table.data_ptr(), Vt, self.stream)
+        return table
+
+    def new_state(self, Vt: int, tlen: np.ndarray):
+        self._res = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._deltas = torch.zeros(4 * Vt, dtype=torch.int32, device=self.device)
+        self._tlen = torch.from_numpy(tlen.astype(np.int32)).to(self.device)
+
+    def argmax(self, table: torch.Tensor, Vt: int, vcur: int) -> int:
+        _lib.run("beast_bpe_argmax", table.data_ptr(), Vt, vcur, self._res.data_ptr(), self.stream)
+        return self._read_i64(self._res, 1)[0] & 0xFFFFFFFFFFFFFFFF
+
+    def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int) -> torch.Tensor:
+        _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                 None, words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len, self._deltas.data_ptr(), Vt,
+                 self.stream)
+        return self._deltas
+
+    def apply(self, table: torch.Tensor, deltas: torch.Tensor, Vt: int, a: int, b: int, nid: int) -> None:
+        _lib.run("beast_bpe_apply", table.data_ptr(), deltas.data_ptr(), Vt, a, b, nid, self._tlen.data_ptr(),
+                 self.stream)
+
+
+def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special_tokens: Sequence[str]):
+    """HF BpeTrainer: special tokens first, then compute_alphabet sorted by code point."""
+    b2u = bytes_to_unicode()
+    seen_bytes = set()
+    for cp in np.flatnonzero(present):
+        seen_bytes.update(chr(int(cp)).encode("utf-8"))
+    chars = {b2u[b] for b in seen_bytes} | set(initial_alphabet)
+    id2str: List[str] = []
+    str2id: Dict[str, int] = {}
+    for t in special_tokens:
+        if t not in str2id:
+            str2id[t] = len(id2str)
+            id2str.append(t)
+    for c in sorted(chars, key=ord):
+        if c not in str2id:
+            str2id[c] = len(id2str)
+            id2str.append(c)
+    byte2id = np.full(256, 0xFFFF, dtype=np.uint16)
+    for b in seen_bytes:
+        byte2id[b] = str2id[b2u[b]]
+    return id2str, str2id, byte2id
+
+
+def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
+              special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
+              initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
+              mn_mx: Optional[Tuple[int, int]] = None) -> BPEResult:
+    """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard)."""
+    import time
+    t0 = time.perf_counter()
+    if ops is None:
+        ops = GpuBpeOps(tokens.device)
+    if mn_mx is None:
+        mm = ops.minmax(tokens) if tokens.numel() else torch.tensor([2 ** 62, -2 ** 62], device=ops.device)
+        lo = mm[:1].clone()
+        hi = mm[1:].clone()
+        reduce(lo, "min")
+        reduce(hi, "max")
+        mn, mx = ops.read(torch.cat([lo, hi]))
+    else:
+        mn, mx = mn_mx
+    K = mx - mn
+    if K < 0:
+        raise ValueError("No non-empty sequences provided for BPE training.")
+    if K >= 0xD800:
+        raise NotImplementedError("BPE alphabet reaches the UTF-16 surrogate range (max - min token >= 55296)")
+    n_cp = K + 1
+    pr = ops.presence(tokens, mn, n_cp)
+    reduce(pr, "max")
+    present = ops.to_numpy(pr).astype(bool)
+    if initial_alphabet is None:
+        initial_alphabet = [chr(i) for i in range(n_cp)]
+    id2str, str2id, byte2id = build_alphabet(present, initial_alphabet, special_tokens)
+    Vt = max(int(vocab_size), len(id2str))
+    if Vt > 32768:
+        raise NotImplementedError(f"dense pair table needs Vt <= 32768 (got {Vt})")
+    lut = class_lut(n_cp)
+    words = ops.pretokenize(tokens, seq_off, mn, lut, byte2id)
+    table = ops.count_pairs(words, Vt)
+    reduce(table, "sum")
+    tlen = np.zeros(Vt, dtype=np.int64)
+    for i, s in enumerate(id2str):
+        tlen[i] = len(s.encode("utf-8"))
+    ops.new_state(Vt, tlen)
+    max_len = int(max_token_length) if max_token_length is not None else 2 ** 31 - 1
+    merges: List[Tuple[str, str]] = []
+    t1 = time.perf_counter()
+    while len(id2str) < vocab_size:
+        key = ops.argmax(table, Vt, len(id2str))
+        count = key >> 32
+        if count < 1 or count < min_frequency:
+            break
+        idx = 0xFFFFFFFF - (key & 0xFFFFFFFF)
+        a, b = divmod(idx, Vt)
+        new_tok = id2str[a] + id2str[b]
+        nid = str2id.get(new_tok)
+        if nid is None:
+            nid = len(id2str)
+            str2id[new_tok] = nid
+            id2str.append(new_tok)
+        merges.append((id2str[a], id2str[b]))
+        deltas = ops.merge(words, a, b, nid, max_len, Vt)
+        reduce(deltas, "sum")
+        ops.apply(table, deltas, Vt, a, b, nid)
+    t2 = time.perf_counter()
+    stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": words["n_words"],
+             "n_syms": words["n_syms"], "Vt": Vt}
+    return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
+
+
+def sequences_to_device(sequences, device: torch.device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Flatten int sequences (tensors / arrays / lists) into (tokens int64, seq_off int64) on device."""
+    parts, lens = [], []
+    on_dev = []
+    for seq in sequences:
+        if isinstance(seq, torch.Tensor):
+            t = seq.detach().reshape(-1)
+            if t.numel() == 0:
+                continue
+            if t.device.type == "cuda":
+                on_dev.append(t.to(device=device, dtype=torch.int64))
+                lens.append(t.numel())
+                parts.append(None)
+                continue
+            a = t.cpu().numpy()
+        else:
+            a = np.asarray(seq).reshape(-1)
+        if a.size == 0:
+            continue
+        parts.append(a.astype(np.int64))
+        on_dev.append(None)
+        lens.append(a.size)
+    if not lens:
+        raise ValueError("No non-empty sequences provided for BPE training.")
+    if all(p is not None for p in parts):
+        flat = torch.from_numpy(np.concatenate(parts)).to(device)
+    else:
+        flat = torch.cat([d if d is not None else torch.from_numpy(p).to(device) for p, d in zip(parts, on_dev)])
+    off = torch.zeros(len(lens) + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)
+    return flat, off.to(device)
+
+
+def fixed_rows_to_device(tokens: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """[S, L] token rows already on device -> (flat, seq_off) without a host round trip."""
+    S, L = tokens.shape
+    off = torch.arange(0, (S + 1) * L, L, dtype=torch.int64, device=tokens.device)
+    return tokens.reshape(-1).to(torch.int64).contiguous(), off

@@ -1,0 +1,470 @@
+// Byte-level BPE training kernels for gfx950 (replaces HF tokenizers' BpeTrainer as
+// driven by beast/beast_bpe_trainer.py:61-98; semantics in SURVEY.md §8a H9-H11).
+//
+//   k_minmax / k_bitmap      global min/max bin, occupied code points (alphabet)
+//   k_pretok<EMIT>           GPT-2 regex pre-tokeniser as a per-sequence state machine
+//                            over a code-point class LUT; pass 1 counts words / byte
+//                            symbols, pass 2 writes byte symbols as vocab ids
+//   k_scan_*                 exclusive prefix sums (word / symbol offsets)
+//   k_count_pairs            dense [Vt][Vt] uint32 pair table += word count
+//   k_argmax                 (count, -pair) max over the live table -> one u64 key
+//   k_merge                  one thread per word: HF Word::merge left-to-right,
+//                            in place; HF's pair-count changes are accumulated in
+//                            LDS-privatised delta vectors [4][Vt] and flushed once
+//                            per workgroup
+//   k_apply                  table += deltas, retire the merged pair
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
+
+// ------------------------------------------------------------- min / max --
+__global__ void k_minmax(const long long* __restrict__ x, int64_t n, long long* __restrict__ out) {
+  long long mn = 0x7FFFFFFFFFFFFFFFLL, mx = (long long)0x8000000000000000ULL;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long v = x[i];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&out[0], mn);
+    atomicMax(&out[1], mx);
+  }
+}
+
+__global__ void k_minmax_init(long long* out) {
+  out[0] = 0x7FFFFFFFFFFFFFFFLL;
+  out[1] = (long long)0x8000000000000000ULL;
+}
+
+__global__ void k_presence(const long long* __restrict__ x, int64_t n, long long mn, uint8_t* __restrict__ pr,
+                           int64_t ncp) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long c = x[i] - mn;
+    if (c >= 0 && c < ncp) pr[c] = 1;  // every writer stores the same byte
+  }
+}
+
+// ---------------------------------------------------------- pre-tokenise --
+__device__ __forceinline__ int cls_of(long long cp, const uint8_t* __restrict__ lut, int64_t lut_n) {
+  return (cp >= 0 && cp < lut_n) ? lut[cp] : CLS_OTHER;
+}
+
+__device__ __forceinline__ int utf8_len(long long cp) { return cp < 0x80 ? 1 : cp < 0x800 ? 2 : cp < 0x10000 ? 3 : 4; }
+
+__device__ __forceinline__ void utf8_bytes(long long cp, uint8_t* b) {
+  if (cp < 0x80) { b[0] = (uint8_t)cp; }
+  else if (cp < 0x800) { b[0] = (uint8_t)(0xC0 | (cp >> 6)); b[1] = (uint8_t)(0x80 | (cp & 0x3F)); }
+  else if (cp < 0x10000) {
+    b[0] = (uint8_t)(0xE0 | (cp >> 12)); b[1] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F)); b[2] = (uint8_t)(0x80 | (cp & 0x3F));
+  } else {
+    b[0] = (uint8_t)(0xF0 | (cp >> 18)); b[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+    b[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F)); b[3] = (uint8_t)(0x80 | (cp & 0x3F));
+  }
+}
+
+// Length of the GPT-2 contraction ('s|'t|'re|'ve|'m|'ll|'d) starting at s[i] == '\'', or 0.
+__device__ __forceinline__ int contraction(const long long* __restrict__ s, int64_t i, int64_t n, long long mn) {
+  if (i + 1 >= n) return 0;
+  const long long c1 = s[i + 1] - mn;
+  if (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd') return 2;
+  if (i + 2 >= n) return 0;
+  const long long c2 = s[i + 2] - mn;
+  if ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l')) return 3;
+  return 0;
+}
+
+// One thread per sequence.  Regex alternatives, leftmost first:
+//   contraction | ' '?L+ | ' '?N+ | ' '?[^\s L N]+ | \s+(?!\S) | \s+
+template <bool EMIT>
+__global__ void k_pretok(const long long* __restrict__ tok, const int64_t* __restrict__ seq_off, int64_t n_seq,
+                         long long mn, const uint8_t* __restrict__ lut, int64_t lut_n,
+                         int64_t* __restrict__ words_per_seq, int64_t* __restrict__ syms_per_seq,
+                         const int64_t* __restrict__ word_off, const int64_t* __restrict__ sym_off,
+                         const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym,
+                         uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlen) {
+  const int64_t sidx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (sidx >= n_seq) return;
+  const long long* s = tok + seq_off[sidx];
+  const int64_t n = seq_off[sidx + 1] - seq_off[sidx];
+  int64_t nw = 0, ns = 0;
+  int64_t wo = EMIT ? word_off[sidx] : 0, so = EMIT ? sym_off[sidx] : 0;
+  int64_t i = 0;
+  while (i < n) {
+    const long long c = s[i] - mn;
+    int64_t j;
+    int k = cls_of(c, lut, lut_n);
+    const int con = (c == '\'') ? contraction(s, i, n, mn) : 0;
+    if (con) {
+      j = i + con;
+    } else {
+      int64_t st = i;
+      if (c == ' ' && i + 1 < n) {
+        const int k1 = cls_of(s[i + 1] - mn, lut, lut_n);
+        if (k1 != CLS_WS) { k = k1; st = i + 1; }
+      }
+      if (k != CLS_WS) {
+        j = st + 1;
+        while (j < n && cls_of(s[j] - mn, lut, lut_n) == k) ++j;
+      } else {
+        j = i + 1;
+        while (j < n && cls_of(s[j] - mn, lut, lut_n) == CLS_WS) ++j;
+        if (j < n && j - i >= 2) --j;  // \s+(?!\S): leave the last blank for the next word
+      }
+    }
+    // word = code points [i, j)
+    int64_t wsyms = 0;
+    for (int64_t p = i; p < j; ++p) wsyms += utf8_len(s[p] - mn);
+    if (EMIT) {
+      wstart[wo + nw] = (uint32_t)(so + ns);
+      wlen[wo + nw] = (uint32_t)wsyms;
+      int64_t o = so + ns;
+      for (int64_t p = i; p < j; ++p) {
+        uint8_t b[4];
+        const long long cp = s[p] - mn;
+        const int L = utf8_len(cp);
+        utf8_bytes(cp, b);
+        for (int q = 0; q < L; ++q) sym[o++] = byte2id[b[q]];
+      }
+    }
+    ns += wsyms;
+    ++nw;
+    i = j;
+  }
+  if (!EMIT) {
+    words_per_seq[sidx] = nw;
+    syms_per_seq[sidx] = ns;
+  }
+}
+
+// ------------------------------------------------------------------ scan --
+constexpr int SCAN_T = 256;
+constexpr int SCAN_PER = 4;
+constexpr int SCAN_TILE = SCAN_T * SCAN_PER;
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* sh, int64_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int64_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int64_t off = 0;
+  for (int k = 0; k < w; ++k) off += sh[k];
+  total = 0;
+  for (int k = 0; k < SCAN_T / 64; ++k) total += sh[k];
+  __syncthreads();
+  return off + x - v;
+}
+
+__global__ void k_scan_tiles(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t n,
+                             int64_t* __restrict__ tile_sums) {
+  __shared__ int64_t sh[SCAN_T / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+  int64_t v[SCAN_PER], s = 0;
+  for (int k = 0; k < SCAN_PER; ++k) {
+    v[k] = (base + k < n) ? in[base + k] : 0;
+    s += v[k];
+  }
+  int64_t total;
+  int64_t pre = block_excl_scan(s, sh, total);
+  for (int k = 0; k < SCAN_PER; ++k) {
+    if (base + k < n) out[base + k] = pre;
+    pre += v[k];
+  }
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+__global__ void k_scan_add(int64_t* __restrict__ out, int64_t n, const int64_t* __restrict__ tile_off) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+  const int64_t add = tile_off[blockIdx.x];
+  for (int k = threadIdx.x; k < SCAN_TILE; k += SCAN_T)
+    if (base + k < n) out[base + k] += add;
+}
+
+__global__ void k_scan_total(const int64_t* __restrict__ in, int64_t* __restrict__ out, int64_t n) {
+  // out[n] = out[n-1] + in[n-1]
+  if (threadIdx.x == 0 && blockIdx.x == 0) out[n] = (n > 0) ? out[n - 1] + in[n - 1] : 0;
+}
+
+int64_t scan_ws_elems(int64_t n) {
+  int64_t total = 0;
+  while (n > 1) {
+    const int64_t t = (n + SCAN_TILE - 1) / SCAN_TILE;
+    total += 2 * t + 1;
+    n = t;
+  }
+  return total + 2;
+}
+
+int scan_rec(const int64_t* in, int64_t* out, int64_t n, int64_t* ws, hipStream_t s) {
+  const int64_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  int64_t* sums = ws;
+  int64_t* offs = ws + tiles;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(SCAN_T), 0, s, in, out, n, sums);
+  BEAST_LAUNCHED("k_scan_tiles");
+  if (tiles > 1) {
+    int rc = scan_rec(sums, offs, tiles, ws + 2 * tiles + 1, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_add, dim3(tiles), dim3(SCAN_T), 0, s, out, n, offs);
+    BEAST_LAUNCHED("k_scan_add");
+  }
+  return BEAST_OK;
+}
+
+// ----------------------------------------------------------- pair table --
+__global__ void k_count_pairs(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                              const uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount, int64_t nw,
+                              uint32_t* __restrict__ table, int Vt) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t st = wstart[w], L = wlen[w];
+    const uint32_t cnt = wcount ? wcount[w] : 1u;
+    if (L < 2) continue;
+    uint32_t prev = sym[st];
+    for (uint32_t i = 1; i < L; ++i) {
+      const uint32_t cur = sym[st + i];
+      atomicAdd(&table[(size_t)prev * Vt + cur], cnt);
+      prev = cur;
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+
+__global__ void k_argmax(const uint32_t* __restrict__ table, int Vt, int vcur, unsigned long long* __restrict__ res) {
+  __shared__ unsigned long long sh[4];
+  unsigned long long best = 0;
+  const int64_t total = (int64_t)vcur * vcur;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(e / vcur), y = (int)(e % vcur);
+    const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
+    const uint32_t c = table[idx];
+    if (c) best = umax64(best, ((unsigned long long)c << 32) | (unsigned long long)(~idx));
+  }
+  for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) best = umax64(best, sh[k]);
+    if (best) atomicMax(res, best);
+  }
+}
+
+// ------------------------------------------------------------------ merge --
+// LDS-privatised deltas when 4*Vt int32 fit in 64 KiB, else global atomics.
+template <bool LDS>
+__global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                               uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
+                                               int64_t nw, int a, int b, int nid, const uint32_t* __restrict__ tlen,
+                                               int max_len, int32_t* __restrict__ deltas, int Vt) {
+  extern __shared__ __attribute__((aligned(16))) int32_t dl[];
+  __shared__ int touched;
+  int32_t* dv = LDS ? dl : deltas;
+  if (LDS) {
+    for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) dl[i] = 0;
+    if (threadIdx.x == 0) touched = 0;
+    __syncthreads();
+  }
+  const uint32_t newlen = tlen[a] + tlen[b];
+  int32_t* colA = dv;
+  int32_t* colN = dv + Vt;
+  int32_t* rowB = dv + 2 * Vt;
+  int32_t* rowN = dv + 3 * Vt;
+  bool any = false;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t L = wlen[w];
+    if (L < 2) continue;
+    uint16_t* s = sym + wstart[w];
+    // read-only probe first: most words do not contain the pair
+    bool hit = false;
+    for (uint32_t i = 0; i + 1 < L; ++i)
+      if (s[i] == a && s[i + 1] == b) { hit = true; break; }
+    if (!hit) continue;
+    any = true;
+    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+    uint32_t r = 0, o = 0;
+    while (r < L) {
+      const int x = s[r];
+      if (x == a && r + 1 < L && s[r + 1] == b) {
+        if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
+          const int p = s[o - 1];
+          atomicAdd(&colA[p], -cnt);
+          if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
+        }
+        if (r + 2 < L) {                       // HF: ((b, next), -1), ((new, next), +1)
+          const int nx = s[r + 2];
+          atomicAdd(&rowB[nx], -cnt);
+          if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
+        }
+        s[o++] = (uint16_t)nid;
+        r += 2;
+      } else {
+        s[o++] = (uint16_t)x;
+        r += 1;
+      }
+    }
+    wlen[w] = o;
+  }
+  if (LDS) {
+    if (any) touched = 1;
+    __syncthreads();
+    if (touched)
+      for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) {
+        const int32_t v = dl[i];
+        if (v) atomicAdd(&deltas[i], v);
+      }
+  }
+}
+
+__global__ void k_apply(uint32_t* __restrict__ table, int32_t* __restrict__ deltas, int Vt, int a, int b, int nid,
+                        uint32_t* __restrict__ tlen) {
+  for (int x = threadIdx.x; x < Vt; x += blockDim.x) {
+    int32_t v;
+    if ((v = deltas[x])) atomicAdd(&table[(size_t)x * Vt + a], (uint32_t)v);
+    if ((v = deltas[Vt + x])) atomicAdd(&table[(size_t)x * Vt + nid], (uint32_t)v);
+    if ((v = deltas[2 * Vt + x])) atomicAdd(&table[(size_t)b * Vt + x], (uint32_t)v);
+    if ((v = deltas[3 * Vt + x])) atomicAdd(&table[(size_t)nid * Vt + x], (uint32_t)v);
+    deltas[x] = 0;
+    deltas[Vt + x] = 0;
+    deltas[2 * Vt + x] = 0;
+    deltas[3 * Vt + x] = 0;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicExch(&table[(size_t)a * Vt + b], 0u);   // merged pair retired (HF never re-picks it)
+    tlen[nid] = tlen[a] + tlen[b];
+  }
+}
+
+int grid_for(int64_t n, int per_block, int cap) {
+  const int64_t g = (n + per_block - 1) / per_block;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
+}
+
+}  // namespace
+
+// =================================================================== C-ABI ==
+extern "C" int beast_i64_minmax(const int64_t* x, int64_t n, int64_t* out2, void* stream) {
+  BEAST_REQUIRE(x && out2 && n >= 1, "beast_i64_minmax: bad args");
+  hipStream_t s = beast::as_stream(stream);
+  hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1), 0, s, reinterpret_cast<long long*>(out2));
+  hipLaunchKernelGGL(k_minmax, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, reinterpret_cast<const long long*>(x),
+                     n, reinterpret_cast<long long*>(out2));
+  BEAST_LAUNCHED("k_minmax");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_cp_presence(const int64_t* tok, int64_t n, int64_t min_tok, uint8_t* present, int64_t n_cp,
+                                     void* stream) {
+  BEAST_REQUIRE(tok && present && n >= 0 && n_cp >= 1, "beast_bpe_cp_presence: bad args");
+  hipStream_t s = beast::as_stream(stream);
+  BEAST_HIP(hipMemsetAsync(present, 0, (size_t)n_cp, s), "presence memset");
+  if (n == 0) return BEAST_OK;
+  hipLaunchKernelGGL(k_presence, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s,
+                     reinterpret_cast<const long long*>(tok), n, (long long)min_tok, present, n_cp);
+  BEAST_LAUNCHED("k_presence");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_pretok_count(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                                      const uint8_t* cls_lut, int64_t lut_n, int64_t* words_per_seq,
+                                      int64_t* syms_per_seq, void* stream) {
+  BEAST_REQUIRE(tok && seq_off && cls_lut && words_per_seq && syms_per_seq, "beast_bpe_pretok_count: null pointer");
+  if (n_seq <= 0) return BEAST_OK;
+  hipLaunchKernelGGL(k_pretok<false>, dim3((n_seq + 127) / 128), dim3(128), 0, beast::as_stream(stream),
+                     reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n,
+                     words_per_seq, syms_per_seq, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+  BEAST_LAUNCHED("k_pretok<count>");
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_scan_workspace_bytes(int64_t n) { return (size_t)scan_ws_elems(n) * sizeof(int64_t); }
+
+extern "C" int beast_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* workspace, void* stream) {
+  BEAST_REQUIRE(in && out && workspace && n >= 0, "beast_exclusive_scan_i64: bad args");
+  hipStream_t s = beast::as_stream(stream);
+  if (n > 0) {
+    int rc = scan_rec(in, out, n, reinterpret_cast<int64_t*>(workspace), s);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(64), 0, s, in, out, n);
+  BEAST_LAUNCHED("k_scan_total");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                                     const uint8_t* cls_lut, int64_t lut_n, const int64_t* word_off,
+                                     const int64_t* sym_off, const uint16_t* byte2id, uint16_t* sym,
+                                     uint32_t* wstart, uint32_t* wlen, void* stream) {
+  BEAST_REQUIRE(tok && seq_off && cls_lut && word_off && sym_off && byte2id && sym && wstart && wlen,
+                "beast_bpe_pretok_emit: null pointer");
+  if (n_seq <= 0) return BEAST_OK;
+  hipLaunchKernelGGL(k_pretok<true>, dim3((n_seq + 127) / 128), dim3(128), 0, beast::as_stream(stream),
+                     reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n,
+                     nullptr, nullptr, word_off, sym_off, byte2id, sym, wstart, wlen);
+  BEAST_LAUNCHED("k_pretok<emit>");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                                     const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && table && Vt >= 1 && Vt <= 65535, "beast_bpe_count_pairs: bad args");
+  if (n_words <= 0) return BEAST_OK;
+  hipLaunchKernelGGL(k_count_pairs, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, beast::as_stream(stream), sym,
+                     wstart, wlen, wcount, n_words, table, Vt);
+  BEAST_LAUNCHED("k_count_pairs");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* result, void* stream) {
+  BEAST_REQUIRE(table && result && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
+  hipStream_t s = beast::as_stream(stream);
+  BEAST_HIP(hipMemsetAsync(result, 0, sizeof(uint64_t), s), "argmax memset");
+  const int64_t total = (int64_t)vcur * vcur;
+  hipLaunchKernelGGL(k_argmax, dim3(grid_for(total, 256 * 8, 2048)), dim3(256), 0, s, table, Vt, vcur,
+                     reinterpret_cast<unsigned long long*>(result));
+  BEAST_LAUNCHED("k_argmax");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
+                               int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
+                               int32_t* deltas, int Vt, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && tlen && deltas, "beast_bpe_merge: null pointer");
+  BEAST_REQUIRE(a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt && Vt <= 65535,
+                "beast_bpe_merge: ids out of range (a=%d b=%d new=%d Vt=%d)", a, b, new_id, Vt);
+  if (n_words <= 0) return BEAST_OK;
+  hipStream_t s = beast::as_stream(stream);
+  const int grid = grid_for(n_words, 256, 2048);
+  const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  if (lds <= 64 * 1024)
+    hipLaunchKernelGGL(k_merge<true>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
+                       tlen, max_token_length, deltas, Vt);
+  else
+    hipLaunchKernelGGL(k_merge<false>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
+                       tlen, max_token_length, deltas, Vt);
+  BEAST_LAUNCHED("k_merge");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, int b, int new_id, uint32_t* tlen,
+                               void* stream) {
+  BEAST_REQUIRE(table && deltas && tlen && a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt,
+                "beast_bpe_apply: bad args");
+  hipLaunchKernelGGL(k_apply, dim3(1), dim3(1024), 0, beast::as_stream(stream), table, deltas, Vt, a, b, new_id, tlen);
+  BEAST_LAUNCHED("k_apply");
+  return BEAST_OK;
+}

@@ -1,0 +1,656 @@
+// Fused BEAST encode / reconstruct kernels for gfx950.
+//
+//   k_encode       params = P . y on v_mfma_f64_16x16x4_f64, fused with the clamp /
+//                  quantise / (d n)->(n d) / LLM-offset epilogue (reference
+//                  beast/beast_bspline_tokenizer.py:399-428, mp/uni_bspline.py:539-586)
+//   k_reconstruct  dequantise + init_p + Phi . W on v_mfma_f32_16x16x4_f32 + scatter
+//                  to the joint / gripper columns (reference :483-536, uni_bspline.py:114-177)
+//
+// Layout.  A workgroup (4 waves) walks tiles of TB consecutive trajectories (grid-stride,
+// constants staged once per workgroup).  A tile's trajectories, params, tokens and
+// positions are each contiguous in HBM, so every tile moves through LDS with 16-byte
+// loads / stores; all of a thread's global loads of a stage are issued before its
+// first LDS store (one HBM round trip per stage).  The MFMA column index enumerates
+// (trajectory, DoF) pairs grouped by basis kind, so one 16-column tile never mixes the
+// joint and gripper projections; the last tile of a kind may be partial (masked).
+// Every operand the MFMA loops read is zero-padded in LDS (P to [16][Tp], Phi to
+// [16*RT][Np], W to [Np]) so the loops are branch-free.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace {
+
+constexpr int NTHREADS = 256;
+constexpr int NWAVES = NTHREADS / 64;
+constexpr int MAX_T = 256;
+constexpr int MAX_N = 16;
+constexpr int MAX_D = 64;
+constexpr int TILES = 4;  // independent MFMA accumulation chains per wave
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+
+__host__ __device__ constexpr int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// x / d for x * d < 2^32 by multiply-high (d uniform, m = ceil(2^32 / d)).
+struct FastDiv {
+  uint32_t d, m;
+};
+inline FastDiv make_fd(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  f.m = d <= 1 ? 0u : (uint32_t)((0x100000000ull + d - 1) / d);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, FastDiv f) { return f.d <= 1 ? x : __umulhi(x, f.m); }
+
+// ------------------------------------------------------------- staging --
+template <int MAXK>
+__device__ __forceinline__ void burst16(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
+  for (int base = 0; base < n16; base += MAXK * NTHREADS) {
+    uint4 r[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) r[k] = src[min(base + k * NTHREADS + (int)threadIdx.x, n16 - 1)];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+      const int i = base + k * NTHREADS + (int)threadIdx.x;
+      if (i < n16) dst[i] = r[k];
+    }
+  }
+}
+
+template <int MAXK>
+__device__ __forceinline__ void burst4(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, int n) {
+  for (int base = 0; base < n; base += MAXK * NTHREADS) {
+    uint32_t r[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) r[k] = src[min(base + k * NTHREADS + (int)threadIdx.x, n - 1)];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) {
+      const int i = base + k * NTHREADS + (int)threadIdx.x;
+      if (i < n) dst[i] = r[k];
+    }
+  }
+}
+
+// global -> LDS, bytes % 4 == 0; 16-byte path when both ends are 16-byte aligned
+template <int MAXK>
+__device__ __forceinline__ void burst(void* __restrict__ dst, const void* __restrict__ src, int bytes) {
+  if (bytes <= 0) return;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int n16 = bytes >> 4;
+    if (n16) burst16<MAXK>(reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), n16);
+    const int done = n16 << 4;
+    if (done < bytes)
+      burst4<1>(reinterpret_cast<uint32_t*>(static_cast<char*>(dst) + done),
+                reinterpret_cast<const uint32_t*>(static_cast<const char*>(src) + done), (bytes - done) >> 2);
+  } else {
+    burst4<4 * MAXK>(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src), bytes >> 2);
+  }
+}
+
+// LDS -> global, float count
+__device__ __forceinline__ void store_out(float* __restrict__ dst, const float* __restrict__ src, int count) {
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int n4 = count >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (int i = threadIdx.x; i < n4; i += NTHREADS) d4[i] = s4[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
+  }
+}
+
+// -------------------------------------------------------------- geometry --
+struct Geom {
+  int D, nj, N, T, Tp, per;   // per = N * D
+  int nq0, nq;                // column tiles of kind 0, of both kinds
+  FastDiv fd_nj, fd_ng, fd_per, fd_N, fd_nq;
+};
+
+template <int TBT>
+inline Geom make_geom(int D, int nj, int N, int T) {
+  Geom g;
+  g.D = D; g.nj = nj; g.N = N; g.T = T; g.Tp = round_up(T, 4); g.per = N * D;
+  const int ng = D - nj;
+  g.nq0 = (TBT * nj + 15) / 16;
+  g.nq = g.nq0 + (TBT * ng + 15) / 16;
+  g.fd_nj = make_fd(std::max(nj, 1));
+  g.fd_ng = make_fd(std::max(ng, 1));
+  g.fd_per = make_fd(g.per);
+  g.fd_N = make_fd(N);
+  g.fd_nq = make_fd(std::max(g.nq, 1));
+  return g;
+}
+
+// MFMA column (trajectory j, DoF d) of tile q for lane column lc; valid = inside the tile set.
+template <int TBT>
+__device__ __forceinline__ void tile_col(const Geom& g, int q, int lc, int& j, int& d, int& kind, bool& valid) {
+  const int k0 = q < g.nq0 ? 0 : 1;
+  const int dk = k0 ? g.D - g.nj : g.nj;
+  const int c = (q - (k0 ? g.nq0 : 0)) * 16 + lc;
+  valid = c < TBT * dk;
+  const uint32_t cc = valid ? c : TBT * dk - 1;
+  const uint32_t jj = fdiv(cc, k0 ? g.fd_ng : g.fd_nj);
+  j = (int)jj;
+  d = (int)(cc - jj * dk) + (k0 ? g.nj : 0);
+  kind = k0;
+}
+
+// ----------------------------------------------------------------- encode --
+struct EncArgs {
+  const float* traj;
+  int64_t B, sb, st, sd, ntiles;
+  int row_elems, vocab, phases;
+  const int32_t* dof_src;
+  const double* proj;  // [2][16][Tp]
+  const float* w_min;
+  const float* w_max;
+  int64_t tok_offset;
+  float* params_out;
+  long long* tokens_out;
+  Geom g;
+};
+
+struct EncSmem {
+  int P, Y, pb, wlo, whi, wsc, kmap, lcol, total;
+};
+
+template <int TBT>
+__host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N, int nkinds) {
+  EncSmem s;
+  int o = 0;
+  s.P = o;    o += round_up(nkinds * 16 * Tp * 8, 16);
+  s.Y = o;    o += round_up(TBT * T * Dl * 4, 16);
+  s.pb = o;   o += round_up(TBT * D * N * 4, 16);
+  s.wlo = o;  o += round_up(D * N * 4, 16);
+  s.whi = o;  o += round_up(D * N * 4, 16);
+  s.wsc = o;  o += round_up(D * N * 4, 16);
+  s.kmap = o; o += round_up(D * N * 2, 16);
+  s.lcol = o; o += round_up(D * 4, 16);
+  s.total = o;
+  return s;
+}
+
+template <int TBT, bool FAST>
+__global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Geom& g = a.g;
+  const int D = g.D, N = g.N, T = g.T, Tp = g.Tp, per = g.per, DN = D * N;
+  const int Dl = FAST ? a.row_elems : D;
+  const int nkinds = (g.nj < D) ? 2 : 1;
+  const EncSmem L = enc_smem<TBT>(T, Tp, Dl, D, N, nkinds);
+  double* P = reinterpret_cast<double*>(smem + L.P);
+  float* Y = reinterpret_cast<float*>(smem + L.Y);
+  float* pb = reinterpret_cast<float*>(smem + L.pb);
+  float* wlo = reinterpret_cast<float*>(smem + L.wlo);
+  float* whi = reinterpret_cast<float*>(smem + L.whi);
+  float* wsc = reinterpret_cast<float*>(smem + L.wsc);
+  uint16_t* kmap = reinterpret_cast<uint16_t*>(smem + L.kmap);
+  int* lcol = reinterpret_cast<int*>(smem + L.lcol);
+  const int tid = threadIdx.x;
+  const bool quant = a.tokens_out != nullptr;
+
+  // ---- constants, once per workgroup: one round trip for all of them
+  {
+    float lo[4], hi[4];
+    int lc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = min(tid + i * NTHREADS, DN - 1);
+      lo[i] = quant ? a.w_min[k] : 0.0f;
+      hi[i] = quant ? a.w_max[k] : 0.0f;
+    }
+    if (tid < D) lc = a.dof_src[tid];
+    burst<2>(P, a.proj, nkinds * 16 * Tp * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = tid + i * NTHREADS;
+      if (k < DN) {
+        wlo[k] = lo[i];
+        whi[k] = hi[i];
+        const float s = __fsub_rn(hi[i], lo[i]);
+        wsc[k] = (s < 1e-8f) ? 1e-8f : s;   // torch.clamp(max - min, min=1e-8), NaN kept
+      }
+    }
+    if (tid < D) lcol[tid] = FAST ? min(max(lc, 0), a.row_elems - 1) : tid;
+    for (int r = tid; r < per; r += NTHREADS) {   // (n d) slot -> (d n) index
+      const int n = r / D, d = r - n * D;
+      kmap[r] = (uint16_t)(d * N + n);
+    }
+  }
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const float vm1 = (float)(a.vocab - 1);
+
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * TBT;
+    const int nb = (int)min<int64_t>(TBT, a.B - b0);
+
+    // ---- stage the trajectory tile (HBM -> LDS)
+    if (a.phases & 1) {
+      if (FAST) {
+        burst<(TBT * 4 * 50 * 14 + 4095) / 4096>(Y, a.traj + b0 * a.sb, nb * T * a.row_elems * 4);
+      } else {
+        const int pt = T * D;
+        for (int e = tid; e < nb * pt; e += NTHREADS) {
+          const int j = e / pt, r = e - j * pt, t = r / D, d = r - t * D;
+          const int col = a.dof_src[d];
+          Y[e] = (col >= 0 && col < a.row_elems)
+                     ? a.traj[(b0 + j) * a.sb + (int64_t)t * a.st + (int64_t)col * a.sd] : 0.0f;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f64 MFMA 16x16x4; A = P, B = y)
+    for (int q0 = wave; (a.phases & 2) && q0 < g.nq; q0 += NWAVES * TILES) {
+      const double* Pk[TILES];
+      const float* Yc[TILES];
+      int jj[TILES], dd[TILES];
+      bool ok[TILES];
+      double4_t acc[TILES];
+#pragma unroll
+      for (int u = 0; u < TILES; ++u) {
+        const int q = min(q0 + u * NWAVES, g.nq - 1);
+        int kind;
+        tile_col<TBT>(g, q, lr, jj[u], dd[u], kind, ok[u]);
+        ok[u] = ok[u] && (q0 + u * NWAVES < g.nq) && jj[u] < nb;
+        Pk[u] = P + (kind * 16 + lr) * Tp + lk;
+        Yc[u] = Y + jj[u] * T * Dl + lcol[dd[u]];
+        acc[u] = double4_t{0.0, 0.0, 0.0, 0.0};
+      }
+      for (int s = 0; s < Tp; s += 4) {
+        const int tc = min(s + lk, T - 1);   // rows t >= T meet a zero A column
+#pragma unroll
+        for (int u = 0; u < TILES; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(Pk[u][s], (double)Yc[u][tc * Dl], acc[u], 0, 0, 0);
+      }
+      // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * r
+#pragma unroll
+      for (int u = 0; u < TILES; ++u) {
+        if (!ok[u]) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = lk + 4 * r;
+          if (n < N) pb[jj[u] * DN + dd[u] * N + n] = (float)acc[u][r];
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- epilogue: params (d n) and tokens (n d), both contiguous per tile
+    if (a.params_out != nullptr && (a.phases & 4)) store_out(a.params_out + b0 * DN, pb, nb * DN);
+    if (quant && (a.phases & 8)) {
+      const int total = nb * per;
+      long long* tout = a.tokens_out + b0 * per;
+      const bool vec = ((((uintptr_t)tout) & 15) == 0);
+      for (int e2 = tid; 2 * e2 < total; e2 += NTHREADS) {
+        long long v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t e = min(2 * e2 + h, total - 1);
+          const uint32_t j = fdiv(e, g.fd_per);
+          const int k = kmap[e - j * per];
+          v[h] = beast::quantize_scaled(pb[j * DN + k], wlo[k], whi[k], wsc[k], vm1) + a.tok_offset;
+        }
+        if (vec && 2 * e2 + 1 < total) {
+          *reinterpret_cast<longlong2*>(tout + 2 * e2) = make_longlong2(v[0], v[1]);
+        } else {
+          tout[2 * e2] = v[0];
+          if (2 * e2 + 1 < total) tout[2 * e2 + 1] = v[1];
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ reconstruct --
+struct RecArgs {
+  const long long* tokens;
+  const float* ntokens;
+  int64_t B, ntiles, tok_offset, basis_sb, init_p_sb;
+  int vocab, Tout, ndo, phases;
+  const float* w_min;
+  const float* w_max;
+  const float* basis;      // [2][Tout][N] (shared) or per trajectory with stride basis_sb
+  const int32_t* dof_dst;
+  const float* init_p;
+  const int32_t* init_p_src;
+  float* params_out;
+  float* pos_out;
+  Geom g;
+};
+
+struct RecSmem {
+  int phi, pb, tok, wlo, whi, pmap, kq, kpb, dst, col2d, out, total;
+  bool stage_out;
+};
+
+template <int TBT>
+__host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, bool shared, int nkinds) {
+  RecSmem s;
+  const int Np = round_up(N, 4), RTp = round_up(Tout, 16), per = N * D;
+  int o = 0;
+  s.phi = o;   o += shared ? round_up(nkinds * RTp * Np * 4, 16) : 0;
+  s.pb = o;    o += round_up(TBT * D * Np * 4, 16);
+  s.tok = o;   o += round_up(TBT * per * 8, 16);
+  s.wlo = o;   o += round_up(per * 4, 16);
+  s.whi = o;   o += round_up(per * 4, 16);
+  s.pmap = o;  o += round_up(per * 2, 16);   // (n d) slot -> pb offset d*Np + n
+  s.kq = o;    o += round_up(per * 2, 16);   // (n d) slot -> (d n) index d*N + n
+  s.kpb = o;   o += round_up(per * 2, 16);   // (d n) index -> pb offset
+  s.dst = o;   o += round_up(D * 4, 16);
+  s.col2d = o; o += round_up(ndo * 4, 16);
+  const int outb = round_up(TBT * Tout * ndo * 4, 16);
+  s.stage_out = (o + outb) <= 96 * 1024;
+  s.out = o;   o += s.stage_out ? outb : 0;
+  s.total = o;
+  return s;
+}
+
+template <int TBT, bool SHARED>
+__global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Geom& g = a.g;
+  const int D = g.D, N = g.N, nj = g.nj, per = g.per, Np = round_up(N, 4);
+  const int Tout = a.Tout, ndo = a.ndo, RTp = round_up(Tout, 16);
+  const int nkinds = (nj < D) ? 2 : 1;
+  const bool pos = a.pos_out != nullptr;
+  const RecSmem L = rec_smem<TBT>(Tout, D, N, ndo, SHARED && pos, nkinds);
+  float* phi = reinterpret_cast<float*>(smem + L.phi);
+  float* pb = reinterpret_cast<float*>(smem + L.pb);
+  float* wlo = reinterpret_cast<float*>(smem + L.wlo);
+  float* whi = reinterpret_cast<float*>(smem + L.whi);
+  uint16_t* pmap = reinterpret_cast<uint16_t*>(smem + L.pmap);
+  uint16_t* kpb = reinterpret_cast<uint16_t*>(smem + L.kpb);
+  uint16_t* kq = reinterpret_cast<uint16_t*>(smem + L.kq);
+  int* dst = reinterpret_cast<int*>(smem + L.dst);
+  int* col2d = reinterpret_cast<int*>(smem + L.col2d);
+  float* ob = reinterpret_cast<float*>(smem + L.out);
+  const int tid = threadIdx.x;
+  const float vm1 = (float)(a.vocab - 1);
+
+  // ---- constants, once per workgroup
+  {
+    float lo[4], hi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = min(tid + i * NTHREADS, per - 1);
+      lo[i] = a.w_min[k];
+      hi[i] = a.w_max[k];
+    }
+    int dd = 0;
+    if (pos && tid < D) dd = a.dof_dst[tid];
+    if (SHARED && pos) {   // Phi zero-padded to [kinds][RTp][Np]: clamped loads, then select
+      const int tot = nkinds * RTp * Np;
+      for (int base = 0; base < tot; base += 8 * NTHREADS) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = min(base + u * NTHREADS + tid, tot - 1);
+          const int k = i / (RTp * Np), r = i - k * RTp * Np, t = r / Np, n = r - t * Np;
+          const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
+          v[u] = (t < Tout && n < N) ? x : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = base + u * NTHREADS + tid;
+          if (i < tot) phi[i] = v[u];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = tid + i * NTHREADS;
+      if (k < per) { wlo[k] = lo[i]; whi[k] = hi[i]; }
+    }
+    for (int r = tid; r < per; r += NTHREADS) {
+      const int n = r / D, d = r - n * D;
+      pmap[r] = (uint16_t)(d * Np + n);
+      kq[r] = (uint16_t)(d * N + n);
+      const int d2 = r / N, n2 = r - d2 * N;
+      kpb[r] = (uint16_t)(d2 * Np + n2);
+    }
+    for (int e = tid; e < TBT * D * (Np - N); e += NTHREADS) {   // zero W pad columns once
+      const int row = e / (Np - N), n = N + (e - row * (Np - N));
+      pb[row * Np + n] = 0.0f;
+    }
+    if (pos) {
+      for (int c = tid; c < ndo; c += NTHREADS) col2d[c] = -1;
+      if (tid < D) dst[tid] = dd;
+      __syncthreads();
+      if (tid < D) {
+        if (dd >= 0 && dd < ndo) col2d[dd] = tid;
+        else dst[tid] = 0;   // out-of-range destination: precondition violated; keep stores in bounds
+      }
+    }
+  }
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nt = (RTp / 16) * g.nq;
+
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * TBT;
+    const int nb = (int)min<int64_t>(TBT, a.B - b0);
+
+    // ---- stage the token tile (HBM -> LDS)
+    if (a.phases & 1) {
+      if (a.ntokens) burst<(TBT * 140 * 4 + 4095) / 4096>(smem + L.tok, a.ntokens + b0 * per, nb * per * 4);
+      else burst<(TBT * 140 * 8 + 4095) / 4096>(smem + L.tok, a.tokens + b0 * per, nb * per * 8);
+    }
+    __syncthreads();
+
+    // ---- decode (H6): (n d) tokens -> W[j][d][n], bit-exact discrete_to_continuous
+    if (a.phases & 16) {
+      const long long* tin = reinterpret_cast<const long long*>(smem + L.tok);
+      const float* fin = reinterpret_cast<const float*>(smem + L.tok);
+      for (int e = tid; e < nb * per; e += NTHREADS) {
+        const uint32_t j = fdiv(e, g.fd_per);
+        const int r = e - j * per;
+        const int po = pmap[r], k = kq[r];
+        pb[j * D * Np + po] = a.ntokens ? beast::denormalize_one(fin[e], wlo[k], whi[k])
+                                        : beast::dequantize_one(tin[e] - a.tok_offset, wlo[k], whi[k], vm1);
+      }
+    }
+    __syncthreads();
+    if (a.params_out != nullptr) {
+      float* pout = a.params_out + b0 * per;
+      for (int e = tid; e < nb * per; e += NTHREADS) {
+        const uint32_t j = fdiv(e, g.fd_per);
+        pout[e] = pb[j * D * Np + kpb[e - j * per]];
+      }
+    }
+    if (!pos) continue;
+    if (a.init_p != nullptr) {   // coefficient 0 of the joint DoFs <- init_p (reference :505-510)
+      __syncthreads();
+      for (int e = tid; e < nb * nj; e += NTHREADS) {
+        const int j = e / nj, d = e - j * nj;
+        pb[(j * D + d) * Np] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];
+      }
+      __syncthreads();
+    }
+
+    float* gout = a.pos_out + b0 * (int64_t)Tout * ndo;
+    if (SHARED) {
+      // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W)
+      for (int w0 = wave; (a.phases & 2) && w0 < nt; w0 += NWAVES * TILES) {
+        const float* Ph[TILES];
+        const float* Wc[TILES];
+        int jj[TILES], cc[TILES], rt[TILES];
+        bool ok[TILES];
+        float4_t acc[TILES];
+#pragma unroll
+        for (int u = 0; u < TILES; ++u) {
+          const int w = min(w0 + u * NWAVES, nt - 1);
+          const int r = (int)fdiv(w, g.fd_nq), q = w - r * g.nq;
+          int d, kind;
+          tile_col<TBT>(g, q, lr, jj[u], d, kind, ok[u]);
+          ok[u] = ok[u] && (w0 + u * NWAVES < nt) && jj[u] < nb;
+          Ph[u] = phi + (kind * RTp + r * 16 + lr) * Np + lk;
+          Wc[u] = pb + (jj[u] * D + d) * Np + lk;
+          cc[u] = dst[d];
+          rt[u] = r;
+          acc[u] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+        for (int s = 0; s < Np; s += 4) {
+#pragma unroll
+          for (int u = 0; u < TILES; ++u)
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ph[u][s], Wc[u][s], acc[u], 0, 0, 0);
+        }
+        // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+        for (int u = 0; u < TILES; ++u) {
+          if (!ok[u]) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = rt[u] * 16 + lk * 4 + r;
+            if (t < Tout) {
+              if (L.stage_out) ob[(jj[u] * Tout + t) * ndo + cc[u]] = acc[u][r];
+              else gout[((int64_t)jj[u] * Tout + t) * ndo + cc[u]] = acc[u][r];
+            }
+          }
+        }
+      }
+    } else {
+      // per-trajectory basis (custom times per row): sequential fma over n, the MFMA chain's order
+      for (int e = tid; (a.phases & 2) && e < nb * Tout * ndo; e += NTHREADS) {
+        const int j = e / (Tout * ndo), r = e - j * Tout * ndo, t = r / ndo, c = r - t * ndo;
+        const int d = col2d[c];
+        float acc = 0.0f;
+        if (d >= 0) {
+          const int kind = (d < nj) ? 0 : 1;
+          const float* Phr = a.basis + (b0 + j) * a.basis_sb + (int64_t)kind * Tout * N + (int64_t)t * N;
+          const float* Wr = pb + (j * D + d) * Np;
+          for (int n = 0; n < N; ++n) acc = fmaf(Phr[n], Wr[n], acc);
+        }
+        if (L.stage_out) ob[e] = acc; else gout[e] = acc;
+      }
+    }
+    if (L.stage_out && (a.phases & 4)) {
+      __syncthreads();
+      store_out(gout, ob, nb * Tout * ndo);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- launch --
+// Diagnostic knob: BEAST_DEBUG_PHASES=<bitmask> skips kernel phases (1 stage, 2 MFMA,
+// 4 store, 8 quantise, 16 dequantise) to attribute time; default: all phases.
+int debug_phases() {
+  static const int v = [] {
+    const char* e = getenv("BEAST_DEBUG_PHASES");
+    return e ? atoi(e) : 0xFF;
+  }();
+  return v;
+}
+
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+int64_t grid_for(int64_t ntiles, int lds_bytes) {
+  const int per_cu = std::max(1, std::min(8, (160 * 1024) / std::max(lds_bytes, 1)));
+  return std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cu_count() * per_cu * 2));
+}
+
+template <int TBT>
+int launch_encode(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t s) {
+  a.g = make_geom<TBT>(D, nj, N, T);
+  a.ntiles = (a.B + TBT - 1) / TBT;
+  const int Dl = fast ? a.row_elems : D;
+  const EncSmem L = enc_smem<TBT>(T, a.g.Tp, Dl, D, N, nj < D ? 2 : 1);
+  BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "encode tile needs %d B of LDS", L.total);
+  const int64_t grid = grid_for(a.ntiles, L.total);
+  if (fast) hipLaunchKernelGGL((k_encode<TBT, true>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  else hipLaunchKernelGGL((k_encode<TBT, false>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  BEAST_LAUNCHED("k_encode");
+  return BEAST_OK;
+}
+
+template <int TBT>
+int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t s) {
+  a.g = make_geom<TBT>(D, nj, N, 1);
+  a.ntiles = (a.B + TBT - 1) / TBT;
+  const bool pos = a.pos_out != nullptr;
+  const RecSmem L = rec_smem<TBT>(a.Tout, D, N, a.ndo, shared && pos, nj < D ? 2 : 1);
+  BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
+  const int64_t grid = grid_for(a.ntiles, L.total);
+  if (shared && pos) hipLaunchKernelGGL((k_reconstruct<TBT, true>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  else hipLaunchKernelGGL((k_reconstruct<TBT, false>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  BEAST_LAUNCHED("k_reconstruct");
+  return BEAST_OK;
+}
+
+// tiles of 16 trajectories once there are >= 2 per CU, else 8 (more workgroups in flight)
+bool small_batch(int64_t B) { return (B + 15) / 16 < 2 * (int64_t)cu_count(); }
+
+}  // namespace
+
+// =================================================================== C-ABI ==
+extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st, int64_t sd,
+                                int row_elems, int D, int n_joint, const int32_t* dof_src, const double* proj,
+                                int N, const float* w_min, const float* w_max, int vocab, int64_t tok_offset,
+                                float* params_out, int64_t* tokens_out, void* stream) {
+  BEAST_REQUIRE(traj && dof_src && proj, "beast_encode_f32: null input pointer");
+  BEAST_REQUIRE(params_out || tokens_out, "beast_encode_f32: no output requested");
+  BEAST_REQUIRE(T >= 1 && T <= MAX_T, "seq_len T=%d outside [1, %d]", T, MAX_T);
+  BEAST_REQUIRE(N >= 1 && N <= MAX_N, "num_basis N=%d outside [1, %d]", N, MAX_N);
+  BEAST_REQUIRE(D >= 1 && D <= MAX_D && n_joint >= 0 && n_joint <= D, "bad DoF split D=%d n_joint=%d", D, n_joint);
+  BEAST_REQUIRE(row_elems >= 1, "row_elems must be >= 1");
+  BEAST_REQUIRE(!tokens_out || (w_min && w_max && vocab >= 2), "quantisation needs w_min/w_max and vocab >= 2");
+  if (B <= 0) return BEAST_OK;
+  EncArgs a{};
+  a.traj = traj; a.B = B; a.sb = sb; a.st = st; a.sd = sd; a.row_elems = row_elems; a.vocab = vocab;
+  a.phases = debug_phases(); a.dof_src = dof_src; a.proj = proj; a.w_min = w_min; a.w_max = w_max;
+  a.tok_offset = tok_offset; a.params_out = params_out; a.tokens_out = reinterpret_cast<long long*>(tokens_out);
+  const bool fast16 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems &&
+                       16 * T * row_elems * 4 <= 64 * 1024);
+  const bool fast8 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems && 8 * T * row_elems * 4 <= 64 * 1024);
+  hipStream_t s = beast::as_stream(stream);
+  if (small_batch(B)) return launch_encode<8>(a, T, D, n_joint, N, fast8, s);
+  return launch_encode<16>(a, T, D, n_joint, N, fast16, s);
+}
+
+extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, int n_joint, int N, int vocab,
+                                     int64_t tok_offset, const float* w_min, const float* w_max,
+                                     const float* basis, int64_t basis_sb, int T_out, const int32_t* dof_dst,
+                                     int num_dof_out, const float* init_p, int64_t init_p_sb,
+                                     const int32_t* init_p_src, float* params_out, float* pos_out,
+                                     const float* ntokens, void* stream) {
+  BEAST_REQUIRE((tokens || ntokens) && w_min && w_max, "beast_reconstruct_f32: null input pointer");
+  BEAST_REQUIRE(params_out || pos_out, "beast_reconstruct_f32: no output requested");
+  BEAST_REQUIRE(N >= 1 && N <= MAX_N, "num_basis N=%d outside [1, %d]", N, MAX_N);
+  BEAST_REQUIRE(D >= 1 && D <= MAX_D && n_joint >= 0 && n_joint <= D, "bad DoF split D=%d n_joint=%d", D, n_joint);
+  BEAST_REQUIRE(vocab >= 2 || ntokens, "vocab must be >= 2");
+  BEAST_REQUIRE(!pos_out || (basis && dof_dst && T_out >= 1 && T_out <= 4096 && num_dof_out >= D &&
+                             num_dof_out <= 4096),
+                "reconstruct: need basis, dof_dst, 1 <= T_out <= 4096, D <= num_dof_out <= 4096");
+  BEAST_REQUIRE(!init_p || init_p_src, "init_p needs init_p_src");
+  if (B <= 0) return BEAST_OK;
+  RecArgs a{};
+  a.tokens = reinterpret_cast<const long long*>(tokens); a.ntokens = ntokens; a.B = B; a.tok_offset = tok_offset;
+  a.basis_sb = basis_sb; a.init_p_sb = init_p_sb; a.vocab = vocab; a.Tout = pos_out ? T_out : 1;
+  a.ndo = pos_out ? num_dof_out : 1; a.phases = debug_phases(); a.w_min = w_min; a.w_max = w_max; a.basis = basis;
+  a.dof_dst = dof_dst; a.init_p = init_p; a.init_p_src = init_p_src; a.params_out = params_out; a.pos_out = pos_out;
+  const bool shared = (basis_sb == 0);
+  hipStream_t s = beast::as_stream(stream);
+  if (small_batch(B)) return launch_reconstruct<8>(a, D, n_joint, N, shared, s);
+  return launch_reconstruct<16>(a, D, n_joint, N, shared, s);
+}

@@ -1,0 +1,108 @@
+// Shared helpers for libbeast_hip.so (gfx950).  Error plumbing for the C-ABI and
+// the bit-exact fp32 helpers the quantiser / dequantiser need.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+
+#include "beast_hip.h"
+
+namespace beast {
+
+void set_error(const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// torch.clamp(x, min=lo_tensor, max=hi_tensor): std::min(std::max(x, lo), hi) with
+// NaN propagation (ATen clamp kernel; NaN bounds -> NaN).
+__device__ __forceinline__ float clamp_t(float x, float lo, float hi) {
+  if (lo != lo || hi != hi) return __builtin_nanf("");
+  float r = (x < lo) ? lo : x;
+  return (hi < r) ? hi : r;
+}
+
+// beast/utils.py:12-16, one element: sub, div, clamp, mul, rint -> int64.
+// -ffp-contract=off is set for the whole library, and division is IEEE
+// (correctly rounded), so every op rounds exactly like ATen's fp32 CPU kernels.
+__device__ __forceinline__ long long quantize_one(float p, float lo, float hi, float vm1) {
+  float x = clamp_t(p, lo, hi);                         // beast_bspline_tokenizer.py:419
+  float s = __fsub_rn(hi, lo);
+  s = (s < 1e-8f) ? 1e-8f : s;                          // clamp(max-min, min=1e-8), NaN kept
+  float u = __fdiv_rn(__fsub_rn(x, lo), s);
+  u = (u < 0.0f) ? 0.0f : u;                            // clamp(., 0, 1), NaN kept
+  u = (1.0f < u) ? 1.0f : u;
+  float r = rintf(__fmul_rn(u, vm1));                   // torch.round = half-to-even
+  if (r != r) return (long long)0x8000000000000000ULL;  // x86 cvtt of NaN (ATen .to(long))
+  return (long long)r;
+}
+
+// quantize_one with the per-column scale s = clamp(hi - lo, min=1e-8) precomputed.
+__device__ __forceinline__ long long quantize_scaled(float p, float lo, float hi, float s, float vm1) {
+  const float x = clamp_t(p, lo, hi);
+  float u = __fdiv_rn(__fsub_rn(x, lo), s);
+  u = (u < 0.0f) ? 0.0f : u;
+  u = (1.0f < u) ? 1.0f : u;
+  const float r = rintf(__fmul_rn(u, vm1));
+  if (r != r) return (long long)0x8000000000000000ULL;
+  return (long long)r;
+}
+
+// beast/utils.py:23-25, one element: int64 -> fp32, div, mul, add, clamp.
+__device__ __forceinline__ float dequantize_one(long long tok, float lo, float hi, float vm1) {
+  float n = __fdiv_rn((float)tok, vm1);
+  float c = __fadd_rn(__fmul_rn(n, __fsub_rn(hi, lo)), lo);
+  return clamp_t(c, lo, hi);
+}
+
+// beast/utils.py:29-35 normalize_tensor, one element (norm range [-1, 1]).
+__device__ __forceinline__ float normalize_one(float p, float lo, float hi) {
+  const float x = clamp_t(p, lo, hi);
+  float s = __fsub_rn(hi, lo);
+  s = (s < 1e-8f) ? 1e-8f : s;
+  const float u = __fdiv_rn(__fsub_rn(x, lo), s);
+  return __fadd_rn(__fmul_rn(u, 2.0f), -1.0f);
+}
+
+// beast/utils.py:38-44 denormalize_tensor, one element.  The reference line 42
+// calls torch.clamp on a Python float and raises TypeError; this implements the
+// evident intent, (clip(x,-1,1) + 1) / 2 * (hi - lo) + lo (documented divergence).
+__device__ __forceinline__ float denormalize_one(float x, float lo, float hi) {
+  float c = (x < -1.0f) ? -1.0f : x;
+  c = (1.0f < c) ? 1.0f : c;
+  const float u = __fdiv_rn(__fsub_rn(c, -1.0f), 2.0f);
+  return __fadd_rn(__fmul_rn(u, __fsub_rn(hi, lo)), lo);
+}
+
+}  // namespace beast
+
+#define BEAST_REQUIRE(cond, ...)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      beast::set_error(__VA_ARGS__);             \
+      return BEAST_E_INVALID;                    \
+    }                                            \
+  } while (0)
+
+#define BEAST_REQUIRE_CODE(cond, code, ...)      \
+  do {                                           \
+    if (!(cond)) {                               \
+      beast::set_error(__VA_ARGS__);             \
+      return code;                               \
+    }                                            \
+  } while (0)
+
+#define BEAST_HIP(call, what)                                     \
+  do {                                                            \
+    hipError_t _e = (call);                                       \
+    if (_e != hipSuccess) return beast::hip_fail(_e, what);       \
+  } while (0)
+
+#define BEAST_LAUNCHED(what)                                      \
+  do {                                                            \
+    hipError_t _e = hipGetLastError();                            \
+    if (_e != hipSuccess) return beast::hip_fail(_e, what);       \
+  } while (0)

@@ -1,0 +1,328 @@
+// Exact per-column quantiles (fit_parameters' np.quantile(params, q, axis=0),
+// beast/beast_bspline_tokenizer.py:211-214) by radix select on gfx950.
+//
+// 1. k_keys      transpose x[rows][cols] (row-major params) into order-preserving
+//                uint32 keys [cols][rows] through a 32x33 LDS tile (coalesced both ways)
+// 2. k_hist      per pass (digits of 11, 11, 10 bits from the top) and per target
+//                rank: LDS-privatised 2048-bin histograms of the keys whose
+//                higher bits equal the target's prefix, flushed with u64 atomics.
+//                Multi-GPU: the caller all-reduces the histogram between hist and
+//                select; every rank then selects the same bucket.
+// 3. k_select    one thread per (column, target): walk the histogram to the bucket
+//                holding the remaining rank, extend the prefix.
+// 4. k_finalize  numpy's float32 _lerp between ranks floor(vi) and floor(vi)+1.
+// HBM traffic: rows*cols*4 (read x) + 4*rows*cols*4 (write keys, 3 key passes).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+namespace {
+
+constexpr int MAXQ = 4;
+constexpr int MAXTG = 2 * MAXQ;
+constexpr int NBIN = 2048;
+constexpr int HIST_THREADS = 256;
+constexpr int64_t HIST_CHUNK = 32768;  // keys per workgroup per pass
+
+struct QState {          // per (column, target)
+  uint32_t prefix;       // selected high bits so far
+  uint32_t pad;
+  uint64_t rank;         // remaining rank inside the prefix bucket
+};
+
+struct QHeader {
+  int64_t n_total;
+  int32_t n_q, n_tg;
+  int64_t ranks[MAXTG];
+  float gamma[MAXQ];
+};
+
+struct WsLayout {
+  size_t hdr, state, nan, hist, keys, total;
+};
+
+inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+
+inline WsLayout ws_layout(int64_t rows, int cols, int n_q) {
+  WsLayout w;
+  const int ntg = 2 * n_q;
+  size_t o = 0;
+  w.hdr = o;   o += al(sizeof(QHeader));
+  w.state = o; o += al(sizeof(QState) * (size_t)cols * ntg);
+  w.nan = o;   o += al(sizeof(uint32_t) * (size_t)cols);
+  w.hist = o;  o += al(sizeof(uint64_t) * (size_t)cols * ntg * NBIN);
+  w.keys = o;  o += al(sizeof(uint32_t) * (size_t)cols * (size_t)rows);
+  w.total = o;
+  return w;
+}
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  if (f != f) return 0xFFFFFFFFu;  // every NaN sorts last (numpy sort order)
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ void pass_geom(int pass, int& shift, int& bits) {
+  // 11 + 11 + 10 bits from the most significant end
+  shift = (pass == 0) ? 21 : (pass == 1) ? 10 : 0;
+  bits = (pass == 2) ? 10 : 11;
+}
+
+__global__ void k_keys(const float* __restrict__ x, int64_t rows, int cols, int64_t rs, uint32_t* __restrict__ keys) {
+  __shared__ uint32_t tile[32][33];
+  const int64_t r0 = (int64_t)blockIdx.x * 32;
+  const int c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int64_t r = r0 + k;
+    const int c = c0 + tx;
+    if (r < rows && c < cols) tile[k][tx] = f2key(x[r * rs + c]);
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k;
+    const int64_t r = r0 + tx;
+    if (r < rows && c < cols) keys[(int64_t)c * rows + r] = tile[tx][k];
+  }
+}
+
+__global__ void k_init(QState* __restrict__ st, uint32_t* __restrict__ nanf, QHeader* __restrict__ hdr, int cols,
+                       QHeader h) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *hdr = h;
+  if (i < cols * h.n_tg) {
+    st[i].prefix = 0;
+    st[i].pad = 0;
+    st[i].rank = (uint64_t)h.ranks[i % h.n_tg];
+  }
+  if (i < cols) nanf[i] = 0;
+}
+
+// grid (chunks, cols)
+__global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restrict__ keys, int64_t rows, int ntg,
+                                                       int pass, const QState* __restrict__ st,
+                                                       uint64_t* __restrict__ hist) {
+  __shared__ uint32_t h[MAXTG][NBIN];
+  const int c = blockIdx.y;
+  int shift, bits;
+  pass_geom(pass, shift, bits);
+  const uint32_t mask = (1u << bits) - 1u;
+  const int hi_shift = shift + bits;  // bits above the digit are known
+  // targets that need their own histogram (pass 0: one shared histogram)
+  const int nh = (pass == 0) ? 1 : ntg;
+  uint32_t pref[MAXTG];
+  for (int t = 0; t < nh; ++t) pref[t] = (hi_shift >= 32) ? 0u : (st[c * ntg + t].prefix >> hi_shift);
+  for (int i = threadIdx.x; i < nh * NBIN; i += HIST_THREADS) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t* kc = keys + (int64_t)c * rows;
+  const int64_t i0 = (int64_t)blockIdx.x * HIST_CHUNK;
+  const int64_t i1 = min<int64_t>(rows, i0 + HIST_CHUNK);
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) {
+    const uint32_t k = kc[i];
+    const uint32_t dg = (k >> shift) & mask;
+    if (pass == 0) {
+      atomicAdd(&h[0][dg], 1u);
+    } else {
+      const uint32_t hk = k >> hi_shift;
+      for (int t = 0; t < nh; ++t)
+        if (hk == pref[t]) atomicAdd(&h[t][dg], 1u);
+    }
+  }
+  __syncthreads();
+  uint64_t* hc = hist + (int64_t)c * ntg * NBIN;
+  for (int i = threadIdx.x; i < nh * NBIN; i += HIST_THREADS) {
+    const uint32_t v = (&h[0][0])[i];
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(hc + i), (unsigned long long)v);
+  }
+}
+
+// One workgroup per (column, target): 256 threads x 8 bins, block-wide exclusive scan,
+// the thread whose bins hold the remaining rank extends the prefix.
+constexpr int SEL_T = 256;
+__global__ __launch_bounds__(SEL_T) void k_select(QState* __restrict__ st, uint32_t* __restrict__ nanf,
+                                                  const uint64_t* __restrict__ hist, int ntg, int pass) {
+  __shared__ uint64_t wsum[SEL_T / 64];
+  const int i = blockIdx.x;  // (column, target)
+  const int c = i / ntg, t = i % ntg;
+  int shift, bits;
+  pass_geom(pass, shift, bits);
+  const int nbins = 1 << bits;
+  const uint64_t* h = hist + ((int64_t)c * ntg + (pass == 0 ? 0 : t)) * NBIN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int PER = NBIN / SEL_T;  // 8
+  uint64_t v[PER], sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int b = tid * PER + k;
+    v[k] = (b < nbins) ? h[b] : 0;
+    sum += v[k];
+  }
+  // inclusive scan of per-thread sums across the block
+  uint64_t x = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint64_t off = 0;
+  for (int k = 0; k < w; ++k) off += wsum[k];
+  const uint64_t before = off + x - sum;  // exclusive prefix of this thread's first bin
+  const uint64_t r = st[i].rank;
+  if (r >= before && r < before + sum) {
+    uint64_t cum = before;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (r < cum + v[k]) {
+        st[i].prefix |= (uint32_t)(tid * PER + k) << shift;
+        st[i].rank = r - cum;
+        break;
+      }
+      cum += v[k];
+    }
+  }
+  if (pass == 0 && t == 0 && tid == SEL_T - 1 && v[PER - 1] != 0) nanf[c] = 1;  // bucket 2047: NaN keys only
+}
+
+// numpy _lerp in float32 (lib/_function_base_impl.py): a + d*g, or b - d*(1-g) when g >= 0.5
+__global__ void k_finalize(const QState* __restrict__ st, const uint32_t* __restrict__ nanf, int cols,
+                           const QHeader* __restrict__ hp, float* __restrict__ out) {
+  const QHeader& h = *hp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cols * h.n_q) return;
+  const int q = i / cols, c = i % cols;
+  const float a = key2f(st[c * h.n_tg + 2 * q].prefix);
+  const float b = key2f(st[c * h.n_tg + 2 * q + 1].prefix);
+  const float g = h.gamma[q];
+  const float d = __fsub_rn(b, a);
+  float r;
+  if (g >= 0.5f) r = __fsub_rn(b, __fmul_rn(d, __fsub_rn(1.0f, g)));
+  else r = __fadd_rn(a, __fmul_rn(d, g));
+  if (nanf[c]) r = __builtin_nanf("");
+  out[q * cols + c] = r;
+}
+
+// host-side replica of numpy 2.x quantile index math in float32 (see oracle.quantile_ranks)
+void numpy_ranks(int64_t n, float q, int64_t& lo, int64_t& hi, float& gamma) {
+  const float vi = (float)(n - 1) * q;  // Python int weakly promoted to float32
+  if (vi >= (float)(n - 1)) { lo = hi = n - 1; gamma = 0.0f; return; }
+  if (vi < 0.0f) { lo = hi = 0; gamma = 0.0f; return; }
+  const double fl = std::floor((double)vi);
+  lo = (int64_t)fl;
+  hi = lo + 1;
+  gamma = (float)((double)vi - fl);
+}
+
+}  // namespace
+
+extern "C" size_t beast_quantile_workspace_bytes(int64_t rows, int cols, int n_q) {
+  return ws_layout(rows, cols, n_q).total;
+}
+
+extern "C" uint64_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q) {
+  const WsLayout w = ws_layout(0, cols, n_q);
+  return reinterpret_cast<uint64_t*>(static_cast<unsigned char*>(workspace) + w.hist);
+}
+
+extern "C" int64_t beast_quantile_hist_count(int cols, int n_q) { return (int64_t)cols * 2 * n_q * NBIN; }
+
+extern "C" int beast_quantile_prepare(const float* x, int64_t rows, int cols, int64_t row_stride, int64_t n_total,
+                                      int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream) {
+  BEAST_REQUIRE(workspace && host_q, "beast_quantile_prepare: null pointer");
+  BEAST_REQUIRE(n_q >= 1 && n_q <= MAXQ, "n_q must be in [1, %d]", MAXQ);
+  BEAST_REQUIRE(cols >= 1 && rows >= 0 && n_total >= 1 && rows <= n_total, "bad quantile shape rows=%lld n=%lld",
+                (long long)rows, (long long)n_total);
+  BEAST_REQUIRE(rows == 0 || x, "beast_quantile_prepare: null x");
+  BEAST_REQUIRE(rows < (int64_t(1) << 31), "rows per rank must be < 2^31");
+  const WsLayout w = ws_layout(rows, cols, n_q);
+  BEAST_REQUIRE_CODE(ws_bytes >= w.total, BEAST_E_WORKSPACE, "quantile workspace %zu < %zu", ws_bytes, w.total);
+  QHeader h;
+  std::memset(&h, 0, sizeof(h));
+  h.n_total = n_total;
+  h.n_q = n_q;
+  h.n_tg = 2 * n_q;
+  for (int q = 0; q < n_q; ++q) {
+    BEAST_REQUIRE(host_q[q] >= 0.0f && host_q[q] <= 1.0f, "Quantiles must be in the range [0, 1]");
+    int64_t lo, hi;
+    float g;
+    numpy_ranks(n_total, host_q[q], lo, hi, g);
+    h.ranks[2 * q] = lo;
+    h.ranks[2 * q + 1] = hi;
+    h.gamma[q] = g;
+  }
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  hipStream_t s = beast::as_stream(stream);
+  auto* st = reinterpret_cast<QState*>(ws + w.state);
+  auto* nanf = reinterpret_cast<uint32_t*>(ws + w.nan);
+  const int ninit = cols * h.n_tg;
+  hipLaunchKernelGGL(k_init, dim3((ninit + 255) / 256), dim3(256), 0, s, st, nanf,
+                     reinterpret_cast<QHeader*>(ws + w.hdr), cols, h);
+  BEAST_LAUNCHED("k_init");
+  if (rows > 0) {
+    dim3 grid((unsigned)((rows + 31) / 32), (unsigned)((cols + 31) / 32));
+    hipLaunchKernelGGL(k_keys, grid, dim3(256), 0, s, x, rows, cols, row_stride,
+                       reinterpret_cast<uint32_t*>(ws + w.keys));
+    BEAST_LAUNCHED("k_keys");
+  }
+  return BEAST_OK;
+}
+
+extern "C" int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream) {
+  BEAST_REQUIRE(workspace && pass >= 0 && pass <= 2 && n_q >= 1 && n_q <= MAXQ, "beast_quantile_hist: bad args");
+  const WsLayout w = ws_layout(rows, cols, n_q);
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  hipStream_t s = beast::as_stream(stream);
+  const int ntg = 2 * n_q;
+  BEAST_HIP(hipMemsetAsync(ws + w.hist, 0, sizeof(uint64_t) * (size_t)cols * ntg * NBIN, s), "hist memset");
+  if (rows > 0) {
+    dim3 grid((unsigned)((rows + HIST_CHUNK - 1) / HIST_CHUNK), (unsigned)cols);
+    hipLaunchKernelGGL(k_hist, grid, dim3(HIST_THREADS), 0, s, reinterpret_cast<const uint32_t*>(ws + w.keys), rows,
+                       ntg, pass, reinterpret_cast<const QState*>(ws + w.state),
+                       reinterpret_cast<uint64_t*>(ws + w.hist));
+    BEAST_LAUNCHED("k_hist");
+  }
+  return BEAST_OK;
+}
+
+extern "C" int beast_quantile_select(int pass, int cols, int n_q, void* workspace, void* stream) {
+  BEAST_REQUIRE(workspace && pass >= 0 && pass <= 2 && n_q >= 1 && n_q <= MAXQ, "beast_quantile_select: bad args");
+  const WsLayout w = ws_layout(0, cols, n_q);
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  const int n = cols * 2 * n_q;
+  hipLaunchKernelGGL(k_select, dim3(n), dim3(SEL_T), 0, beast::as_stream(stream),
+                     reinterpret_cast<QState*>(ws + w.state), reinterpret_cast<uint32_t*>(ws + w.nan),
+                     reinterpret_cast<const uint64_t*>(ws + w.hist), 2 * n_q, pass);
+  BEAST_LAUNCHED("k_select");
+  return BEAST_OK;
+}
+
+extern "C" int beast_quantile_finalize(int cols, int n_q, void* workspace, float* out, void* stream) {
+  BEAST_REQUIRE(workspace && out && n_q >= 1 && n_q <= MAXQ, "beast_quantile_finalize: bad args");
+  const WsLayout w = ws_layout(0, cols, n_q);
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  const int n = cols * n_q;
+  hipLaunchKernelGGL(k_finalize, dim3((n + 127) / 128), dim3(128), 0, beast::as_stream(stream),
+                     reinterpret_cast<const QState*>(ws + w.state), reinterpret_cast<const uint32_t*>(ws + w.nan),
+                     cols, reinterpret_cast<const QHeader*>(ws + w.hdr), out);
+  BEAST_LAUNCHED("k_finalize");
+  return BEAST_OK;
+}
+
+extern "C" int beast_quantile_f32(const float* x, int64_t rows, int cols, int64_t row_stride, int n_q,
+                                  const float* host_q, float* out, void* workspace, size_t ws_bytes, void* stream) {
+  BEAST_REQUIRE(rows >= 1, "np.quantile of an empty array is undefined (rows=0)");
+  int rc = beast_quantile_prepare(x, rows, cols, row_stride, rows, n_q, host_q, workspace, ws_bytes, stream);
+  for (int p = 0; rc == BEAST_OK && p < 3; ++p) {
+    rc = beast_quantile_hist(p, rows, cols, n_q, workspace, stream);
+    if (rc == BEAST_OK) rc = beast_quantile_select(p, cols, n_q, workspace, stream);
+  }
+  if (rc == BEAST_OK) rc = beast_quantile_finalize(cols, n_q, workspace, out, stream);
+  return rc;
+}

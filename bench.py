@@ -1,0 +1,262 @@
+"""BEAST hot-path benchmark on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--no-bpe] [--no-cpu]
+
+One step = BEASTBsplineTokenizer.encode(x) -> reconstruct_traj(tokens) over one
+synthetic batch already resident in HBM (config "1xMI355X: num_dof=14
+num_basis=10 seq_len=50 vocab=256, B=4096").  For N > 1 the driver launches one
+rank per GPU (torch.distributed.run); every rank processes its own B
+trajectories (data-parallel, no collective on this path: weak scaling); the time
+is the max over ranks.  rank 0 prints ONE JSON line.
+
+Extra objects in that line:
+  roofline      dominant kernel: algorithmic bytes / its average launch duration
+                (HIP events on the kernel's stream, one bracketed launch at a time)
+  cpu_baseline  the oracle's restatement of the reference op sequence (oracle/
+                beast_oracle.py, bitwise equal to the reference in the build
+                container) timed on this host's cores on a bounded sample
+  bpe           BEASTBsplineBPETokenizer-style BPE training (vocab 2048) on GPU,
+                merges/s, with HF tokenizers (the reference's BPE) timed on a
+                bounded sample of the same corpus on the host
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib  # noqa: E402
+from beast_tokenizer_amd.synthetic import synth_trajectories  # noqa: E402
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+T, D, N, V = 50, 14, 10, 256
+ENC_BYTES = T * D * 4 + N * D * 8 + D * N * 4    # read traj, write int64 tokens + fp32 params
+REC_BYTES = N * D * 8 + T * D * 4                # read tokens, write positions
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--no-bpe", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--bpe-seqs", type=int, default=500000, help="BPE corpus (trajectories, all ranks)")
+    ap.add_argument("--bpe-vocab", type=int, default=2048)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
+                    help="per-launch HBM bytes from rocprofv3 --pmc (see profiles/README.md)")
+    return ap.parse_args()
+
+
+def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 50) -> float:
+    """Average duration of one launch: each launch is bracketed by events on the
+    kernel's stream, queued behind a short sleep so launch overhead is excluded."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+    with torch.cuda.stream(stream):
+        for i in range(reps):
+            torch.cuda._sleep(20000)
+            starts[i].record(stream)
+            launch()
+            ends[i].record(stream)
+    stream.synchronize()
+    ts = sorted(s.elapsed_time(e) * 1e3 for s, e in zip(starts, ends))
+    return float(np.mean(ts[: max(1, int(0.9 * reps))]))  # trim the slowest 10%
+
+
+def cpu_baseline(tok_bounds, seconds: float):
+    """Oracle port of the reference op sequence (fit via block-diag bmm + linalg.solve,
+    quantise, dequantise, einsum reconstruct) timed on a bounded sample."""
+    from oracle import beast_oracle as O
+    wmin, wmax = tok_bounds
+    lay = O.Layout.make(D, None, False)
+    t = O.times_grid(2 * np.pi, T)
+    pj = O.basis(t, np.float32(2 * np.pi), 4, N)
+    Bc = 512
+    x = synth_trajectories(Bc, T, D, seed=0)
+    O.reconstruct(O.encode(x, pj, pj, lay, wmin, wmax, V)[0], pj, pj, lay, wmin, wmax, V)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        tokens, _ = O.encode(x, pj, pj, lay, wmin, wmax, V)
+        O.reconstruct(tokens, pj, pj, lay, wmin, wmax, V)
+        n += Bc
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": n / el, "unit": "trajectories/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} trajectories in batches of {Bc} (D=14,T=50,N=10,V=256), encode+reconstruct via "
+                      f"oracle/beast_oracle.py (reference ATen op sequence: block-diagonal bmm + "
+                      f"torch.linalg.solve), {el:.1f}s"}
+
+
+def bpe_bench(tok, dev, args, world, rank, reduce):
+    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
+    per_rank = args.bpe_seqs // world
+    rows = []
+    for s in range(0, per_rank, 8192):
+        b = min(8192, per_rank - s)
+        x = torch.from_numpy(synth_trajectories(b, T, D, seed=7, start=rank * per_rank + s)).to(dev)
+        rows.append(tok.encode(x)[0])
+    allrows = torch.cat(rows)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    flat, off = fixed_rows_to_device(allrows)
+    res = train_bpe(flat, off, args.bpe_vocab, reduce=reduce)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = float(tt.item())
+    out = {"metric": "BPE merges/sec (fit_from_trajectories core: pretokenise + count + merge loop)",
+           "value": res.stats["n_merges"] / el, "unit": "merges/s", "merges": res.stats["n_merges"],
+           "seconds": el, "trajectories": per_rank * world, "vocab_size": args.bpe_vocab,
+           "setup_s": res.stats["setup_s"], "merge_loop_s": res.stats["merge_loop_s"],
+           "words": res.stats["n_words"], "symbols": res.stats["n_syms"]}
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = hf_bpe_baseline(allrows[:20000].cpu().numpy(), args.bpe_vocab, res)
+    return out
+
+
+def hf_bpe_baseline(rows: np.ndarray, vocab: int, gpu_res):
+    """HF tokenizers BpeTrainer (the reference's BPE, beast_bpe_trainer.py:61-74) on a bounded sample."""
+    try:
+        from tokenizers import ByteLevelBPETokenizer
+        from tokenizers.trainers import BpeTrainer
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "error": str(e)}
+    lo, hi = int(rows.min()), int(rows.max())
+    strings = ["".join(map(chr, r - lo)) for r in rows]
+    t0 = time.perf_counter()
+    bpe = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=vocab, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=10000)
+    bpe._tokenizer.train_from_iterator(strings, trainer=tr)
+    el = time.perf_counter() - t0
+    nm = len(json.loads(bpe._tokenizer.to_str())["model"]["merges"])
+    return {"value": nm / el, "unit": "merges/s", "kind": "reference",
+            "cores": int(os.environ.get("RAYON_NUM_THREADS", os.cpu_count() or 1)),
+            "sample": f"HF tokenizers {__import__('tokenizers').__version__} BpeTrainer on {len(rows)} sequences "
+                      f"x 140 bins (first rows of the GPU corpus), {nm} merges, {el:.2f}s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from beast_tokenizer_amd.bpe_train import no_reduce, torch_dist_reducer
+    reduce = torch_dist_reducer() if world > 1 else no_reduce
+
+    B = args.batch
+    tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, device=str(dev))
+    fit = [{"actions": torch.from_numpy(synth_trajectories(4096, T, D, seed=1, start=4096 * i))} for i in range(2)]
+    tok.fit_parameters(fit, verbose=False)
+    x = torch.from_numpy(synth_trajectories(B, T, D, seed=100 + rank)).to(dev)
+
+    def step():
+        tokens, _ = tok.encode(x)
+        return tok.reconstruct_traj(tokens)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = float(tt.item())
+    value = B * world * args.steps / el
+
+    # ---- dominant-kernel roofline, measured live on the kernel's stream
+    stream = torch.cuda.current_stream(dev)
+    _, proj = tok._constants(dev)
+    src, dst = tok._dof_maps(dev)
+    wmn, wmx = tok._bounds(dev)
+    params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
+    tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
+    pos = torch.empty((B, T, D), dtype=torch.float32, device=dev)
+    phi, _ = tok._constants(dev)
+    sp = stream.cuda_stream
+
+    def launch_enc():
+        _lib.run("beast_encode_f32", x.data_ptr(), B, T, x.stride(0), x.stride(1), x.stride(2), D, D, D,
+                 src.data_ptr(), proj.data_ptr(), N, wmn.data_ptr(), wmx.data_ptr(), V, 0, params.data_ptr(),
+                 tokens.data_ptr(), sp)
+
+    def launch_rec():
+        _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, D, N, V, 0, wmn.data_ptr(), wmx.data_ptr(),
+                 phi.data_ptr(), 0, T, dst.data_ptr(), D, None, 0, None, None, pos.data_ptr(), None, sp)
+
+    t_enc = kernel_time_us(launch_enc, stream)
+    t_rec = kernel_time_us(launch_rec, stream)
+    if t_enc >= t_rec:
+        kname, tk, kbytes = "k_encode", t_enc, ENC_BYTES * B
+    else:
+        kname, tk, kbytes = "k_reconstruct", t_rec, REC_BYTES * B
+    achieved = kbytes / (tk * 1e-6)
+    traffic = None
+    if os.path.exists(args.pmc):
+        with open(args.pmc) as f:
+            pmc = json.load(f)
+        traffic = pmc.get(kname, {}).get("hbm_bytes_per_launch")
+    roof = {"bound": "hbm", "kernel": kname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": traffic, "algo_bytes_per_launch": kbytes,
+            "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
+
+    bpe = None
+    if not args.no_bpe:
+        bpe = bpe_bench(tok, dev, args, world, rank, reduce)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline((tok.w_min.cpu().numpy(), tok.w_max.cpu().numpy()), args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "trajectories/sec encode+reconstruct (B=4096,T=50,DoF=14)",
+            "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 in/out, f64 fit accumulate, int64 tokens",
+            "data": "synthetic (seeded splitmix64 sinusoids, beast_tokenizer_amd/synthetic.py)",
+            "config": {"workload": "BEASTBsplineTokenizer encode->reconstruct_traj, num_dof=14 num_basis=10 "
+                                   "seq_len=50 vocab=256 degree_p=4", "global_batch": B * world,
+                       "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "bpe": bpe,
+        }
+        if cpu and cpu.get("value"):
+            line["gpu_over_cpu"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,176 @@
+/*
+ * beast_hip.h -- C-ABI of libbeast_hip.so, the MI355X (gfx950) hot path of BEAST.
+ *
+ * The reference (Dont4rootMe/beast_tokenizer) has no native boundary: its
+ * "plugin point" is the mp_pytorch UniformBSpline object, beast/utils.py and the
+ * HF `tokenizers` BpeTrainer.  Each entry point below replaces one of those call
+ * sites (cited per function) and is what a ctypes / cffi binding of the
+ * reference would bind.
+ *
+ * Conventions
+ *   - Plain C types only.  All pointers are DEVICE pointers unless named host_*.
+ *   - The caller allocates every input, output and workspace buffer.
+ *   - Every call is stream-ordered on `stream` (a hipStream_t passed as void*);
+ *     nothing synchronises the device except where a function says so.
+ *   - Return 0 on success or a negative BEAST_E_* code; beast_last_error()
+ *     returns a thread-local message for the last failure.  No C++ exception
+ *     crosses this boundary.
+ *   - Layouts: params are [B][D*N] "(d n)" order, tokens are [B][N*D] "(n d)"
+ *     order, exactly as beast/beast_bspline_tokenizer.py:418-422 produces them.
+ *     The DoF order d is joint_indices ++ gripper_indices (:70, :414); the
+ *     first n_joint DoFs use basis kind 0 (degree p), the rest kind 1
+ *     (degree 0 gripper basis, :88-96).
+ */
+#ifndef BEAST_HIP_H
+#define BEAST_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BEAST_OK 0
+#define BEAST_E_INVALID (-1)     /* bad argument (maps to ValueError)          */
+#define BEAST_E_HIP (-2)         /* HIP runtime / launch failure (RuntimeError) */
+#define BEAST_E_UNSUPPORTED (-3) /* shape outside the kernels' envelope       */
+#define BEAST_E_WORKSPACE (-4)   /* workspace too small                       */
+
+#define BEAST_ABI_VERSION 1
+
+int beast_abi_version(void);
+const char* beast_last_error(void);
+
+/* ---------------------------------------------------------------- H1/H2 ---
+ * Replaces UniBSplineBasis.basis (MP_lite_PyTorch/mp_pytorch/basis_gn/
+ * uni_bspline_basis.py:59-113) with LinearPhaseGenerator.phase
+ * (phase_gn/linear_phase.py:22-24): basis_out[i][n] = B_{n,degree}(clip((t_i -
+ * delay)/tau, 0, 1)) by the same Cox-de Boor recursion, same fp32 op order.
+ * knots: [n_knots] with n_knots == degree + 1 + num_basis.  degree <= 8. */
+int beast_bspline_basis_f32(const float* times, int64_t n_times, float tau, float delay,
+                            const float* knots, int n_knots, int degree, int num_basis,
+                            float* basis_out, void* stream);
+
+/* Ridge projection P = (Phi^T Phi + reg I)^-1 Phi^T in float64: the closed form
+ * of UniformBSpline.learn_mp_params_from_trajs (mp/uni_bspline.py:539-586) for
+ * init/end condition order 0, where the block-diagonal system of
+ * basis_multi_dofs (basis_gn/uni_bspline_basis.py:349-356) decouples per DoF.
+ * Written zero-padded as proj_out[16][Tp], Tp = round_up(T, 4) (the MFMA A-operand
+ * layout of beast_encode_f32).  One workgroup; N <= 16. */
+int beast_bspline_projection_f64(const float* basis, int T, int N, double reg, double* proj_out,
+                                 void* stream);
+
+/* ------------------------------------------------------------- H4 + H5 ---
+ * Replaces BEASTBsplineTokenizer.encode (beast/beast_bspline_tokenizer.py:
+ * 399-428) -> learn_mp_params_from_trajs + clamp + continuous_to_discrete
+ * (beast/utils.py:4-17) + rearrange + LLM offset, as ONE fused kernel.
+ *   traj[b*sb + t*st + dof_src[d]*sd]  fp32 input, element strides
+ *   row_elems   size of the input's last dim (for the contiguous fast path)
+ *   proj        [2][16][Tp] float64 zero-padded projections (kind 0 joint, kind 1
+ *               gripper), as written by beast_bspline_projection_f64
+ *   params_out  [B][D*N] fp32 unclamped fit (params_dict['params']); nullable
+ *   tokens_out  [B][N*D] int64 = round_half_even(clamp01((clamp(p)-wmin)/max(wmax-wmin,1e-8))*(vocab-1))
+ *               + tok_offset; nullable.  vocab <= 0 disables quantisation.
+ * Constraints: N <= 16, T <= 256, D <= 64. */
+int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st, int64_t sd, int row_elems,
+                     int D, int n_joint, const int32_t* dof_src, const double* proj, int N,
+                     const float* w_min, const float* w_max, int vocab, int64_t tok_offset,
+                     float* params_out, int64_t* tokens_out, void* stream);
+
+/* Quantise-only epilogue of the above for already-fitted params [B][D*N] (d n):
+ * used by encode(update_bounds=True) after the bounds move (:415-420).
+ * mode 0: tokens_out int64 [B][N*D] (continuous_to_discrete + offset);
+ * mode 1: ntok_out fp32 [B][N*D] = normalize_tensor (beast/utils.py:29-35),
+ *         the encode_continuous path (:430-450). */
+int beast_quantize_f32(const float* params, int64_t B, int D, int N, const float* w_min, const float* w_max,
+                       int vocab, int64_t tok_offset, int mode, int64_t* tokens_out, float* ntok_out, void* stream);
+
+/* ------------------------------------------------------------- H6 - H8 ---
+ * Replaces BEASTBsplineTokenizer.decode + reconstruct_traj (beast/
+ * beast_bspline_tokenizer.py:483-536) -> discrete_to_continuous (beast/
+ * utils.py:20-26), optional init_p overwrite of coefficient 0 of the joint
+ * DoFs (:505-510), UniformBSpline.get_traj_pos (mp/uni_bspline.py:114-177)
+ * and the scatter to joint/gripper columns (:520-534).
+ *   tokens      [B][N*D] int64 (tok_offset is SUBTRACTED first)
+ *   basis       [2][T_out][N] fp32 per kind; batch stride basis_sb (0 = shared)
+ *   dof_dst     [D] output column of each DoF; pos_out [B][T_out][num_dof_out]
+ *   init_p      nullable [B] rows of stride init_p_sb; init_p_src[d] column for
+ *               joint DoF d (< n_joint)
+ *   params_out  nullable [B][D*N] decoded params (= decode()); pos_out nullable.
+ *   ntokens     nullable: when set, fp32 normalised tokens [B][N*D] in [-1, 1] are
+ *               read instead of `tokens` and mapped back by denormalize_tensor
+ *               (beast/utils.py:38-44): the reconstruct_traj_continuous path (:538-582). */
+int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, int n_joint, int N, int vocab,
+                          int64_t tok_offset, const float* w_min, const float* w_max,
+                          const float* basis, int64_t basis_sb, int T_out,
+                          const int32_t* dof_dst, int num_dof_out,
+                          const float* init_p, int64_t init_p_sb, const int32_t* init_p_src,
+                          float* params_out, float* pos_out, const float* ntokens, void* stream);
+
+/* ------------------------------------------------------------------ H13 ---
+ * Column min / max with NaN propagation (torch.min/max(dim=0)), used by
+ * update_weights_bounds / update_weights_bounds_per_batch (:362-389).
+ * workspace >= beast_colminmax_workspace_bytes(rows, cols). */
+size_t beast_colminmax_workspace_bytes(int64_t rows, int cols);
+int beast_colminmax_f32(const float* x, int64_t rows, int cols, int64_t row_stride, float* out_min,
+                        float* out_max, void* workspace, size_t ws_bytes, void* stream);
+
+/* Exact per-column quantiles with numpy 'linear' semantics in float32
+ * (np.quantile(params, q, axis=0), :213-214) by 3-pass 11/11/10-bit radix
+ * select on order-preserving keys.  Multi-GPU: call prepare, then for pass in
+ * 0..2 { hist; all-reduce(SUM, uint64) of beast_quantile_hist_ptr; select },
+ * then finalize.  n_total = rows summed over all ranks.  n_q <= 4 (host_q). */
+size_t beast_quantile_workspace_bytes(int64_t rows, int cols, int n_q);
+int beast_quantile_prepare(const float* x, int64_t rows, int cols, int64_t row_stride, int64_t n_total,
+                           int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream);
+uint64_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q);
+int64_t beast_quantile_hist_count(int cols, int n_q);
+int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream);
+int beast_quantile_select(int pass, int cols, int n_q, void* workspace, void* stream);
+int beast_quantile_finalize(int cols, int n_q, void* workspace, float* out, void* stream);
+/* single-GPU convenience: all of the above. out [n_q][cols]. */
+int beast_quantile_f32(const float* x, int64_t rows, int cols, int64_t row_stride, int n_q, const float* host_q,
+                       float* out, void* workspace, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------ H9 - H12 ---
+ * Byte-level BPE training, replacing HF tokenizers' BpeTrainer::do_train as
+ * driven by FIGBPE (beast/beast_bpe_trainer.py:61-98).  Tokens are int64 code
+ * points (bins); a sequence is tokens[seq_off[s] .. seq_off[s+1]). */
+int beast_i64_minmax(const int64_t* x, int64_t n, int64_t* out2, void* stream);
+/* present[x - min_tok] = 1 for every token (n_cp = max-min+1); multi-GPU: all-reduce MAX */
+int beast_bpe_cp_presence(const int64_t* tok, int64_t n, int64_t min_tok, uint8_t* present, int64_t n_cp,
+                          void* stream);
+/* GPT-2 ByteLevel pre-tokenisation, pass 1: words and byte-symbols per sequence.
+ * cls_lut[cp] in {0 other, 1 letter, 2 number, 3 whitespace}, cp < lut_n. */
+int beast_bpe_pretok_count(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                           const uint8_t* cls_lut, int64_t lut_n, int64_t* words_per_seq,
+                           int64_t* syms_per_seq, void* stream);
+/* exclusive scan: out[0..n] (out[n] = total). workspace >= beast_scan_workspace_bytes(n) */
+size_t beast_scan_workspace_bytes(int64_t n);
+int beast_exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, void* workspace, void* stream);
+/* pass 2: emit byte symbols as vocab ids (byte2id[256]) and word extents. */
+int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                          const uint8_t* cls_lut, int64_t lut_n, const int64_t* word_off,
+                          const int64_t* sym_off, const uint16_t* byte2id, uint16_t* sym,
+                          uint32_t* wstart, uint32_t* wlen, void* stream);
+/* pair table [Vt][Vt] uint32 += word count for each adjacent pair (BpeTrainer::count_pairs). */
+int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                          const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream);
+/* result = max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)); zeroes *result first. */
+int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* result, void* stream);
+/* Merge (a,b)->new_id in every word, left to right, non-overlapping (HF Word::merge);
+ * accumulate HF's pair-count changes into deltas[4][Vt] int32:
+ * [0]: (x,a)  [1]: (x,new)  [2]: (b,y)  [3]: (new,y). */
+int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
+                    int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
+                    int32_t* deltas, int Vt, void* stream);
+/* table += deltas (then deltas = 0), table[a][b] = 0 (merged pair retired),
+ * tlen[new_id] = tlen[a] + tlen[b]. */
+int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, int b, int new_id, uint32_t* tlen,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BEAST_HIP_H */

@@ -1,0 +1,228 @@
+"""CPU oracle for the BEAST B-spline hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module restates the reference algorithm on the CPU so that tests,
+``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py`` can
+check / time the HIP path.  The product (``beast_tokenizer_amd``) never
+imports it.
+
+Two fits are provided:
+
+* :func:`fit_reference_ops` replays the reference's exact ATen op sequence
+  (block-diagonal basis, ``einsum`` normal equations, ``torch.linalg.solve``),
+  ``MP_lite_PyTorch/mp_pytorch/mp/uni_bspline.py:539-586`` and
+  ``basis_gn/uni_bspline_basis.py:303-359``.  On the same torch build it is
+  bitwise equal to the reference (pinned by ``tests/golden``).  It is the
+  "port" CPU baseline timed by ``bench.py``.
+* :func:`fit_exact` solves the same ridge problem in float64 and rounds once;
+  it is the arbiter for rounding-tie flips (SURVEY.md §7 hard part 1).
+
+Quantise / dequantise restate ``beast/utils.py:4-26`` in numpy float32 with
+the same per-op rounding as torch.  Parity pin: ``tests/golden/*.npz`` were
+produced by importing the reference itself (``tests/golden/gen_goldens.py``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+F32 = np.float32
+
+
+# ---------------------------------------------------------------- H1/H2 ----
+def times_grid(duration: float, seq_len: int) -> np.ndarray:
+    """``tensor_linspace(0, duration, seq_len)`` (util_matrix.py:79-116 -> torch.linspace)."""
+    return torch.linspace(0, duration, seq_len).numpy()
+
+
+def knots(degree: int, num_ctrlp: int) -> np.ndarray:
+    """Clamped uniform knot vector, uni_bspline_basis.py:41-55."""
+    n_knots = degree + 1 + num_ctrlp
+    inner = torch.linspace(0, 1, n_knots - 2 * degree, dtype=torch.float32)
+    return torch.cat([torch.zeros(degree), inner, torch.ones(degree)]).numpy()
+
+
+def phase(times: np.ndarray, tau: float, delay: float = 0.0) -> np.ndarray:
+    """LinearPhaseGenerator.phase, linear_phase.py:22-24 (fp32 sub, div, clip)."""
+    t = np.asarray(times, dtype=F32)
+    return np.clip((t - F32(delay)) / F32(tau), F32(0), F32(1)).astype(F32)
+
+
+def _basis_fn(i: int, k: int, kv: np.ndarray, u: np.ndarray, n_ctrl: int) -> np.ndarray:
+    """Cox-de Boor recursion, uni_bspline_basis.py:82-113, same op order in fp32."""
+    if k == 0:
+        if i == n_ctrl - 1:
+            b = (u >= kv[i]) & (u <= kv[i + 1])
+        else:
+            b = (u >= kv[i]) & (u < kv[i + 1])
+        return b.astype(F32)
+    d1 = F32(kv[i + k] - kv[i])
+    t1 = F32(0.0) if d1 == 0 else ((u - kv[i]) / d1) * _basis_fn(i, k - 1, kv, u, n_ctrl)
+    d2 = F32(kv[i + k + 1] - kv[i + 1])
+    t2 = F32(0.0) if d2 == 0 else ((kv[i + k + 1] - u) / d2) * _basis_fn(i + 1, k - 1, kv, u, n_ctrl)
+    return (t1 + t2).astype(F32)
+
+
+def basis(times: np.ndarray, tau: float, degree: int, num_basis: int, delay: float = 0.0) -> np.ndarray:
+    """Phi ``[..., T, N]`` fp32 (uni_bspline_basis.py:59-80), init/end order 0."""
+    u = phase(times, tau, delay)
+    kv = knots(degree, num_basis)
+    cols = [_basis_fn(i, degree, kv, u, num_basis) for i in range(num_basis)]
+    return np.stack(cols, axis=-1).astype(F32)
+
+
+# ------------------------------------------------------------------- H4 ----
+def fit_reference_ops(trajs: np.ndarray, phi: np.ndarray, reg: float = 1e-9) -> np.ndarray:
+    """Replay uni_bspline.py:539-586 with torch CPU ops. trajs ``[B,T,D]`` -> ``[B, D*N]``."""
+    y = torch.as_tensor(np.ascontiguousarray(trajs), dtype=torch.float32)
+    Bsz, T, D = y.shape
+    N = phi.shape[-1]
+    ph = torch.as_tensor(phi, dtype=torch.float32)
+    basis_b = ph.expand(Bsz, T, N) * torch.ones(N)          # basis(times) * weights_goal_scale
+    bmd = torch.zeros(Bsz, D * T, D * N)                      # basis_multi_dofs, :349-356
+    for i in range(D):
+        bmd[..., i * T:(i + 1) * T, i * N:(i + 1) * N] = basis_b
+    bmd = bmd * 1.0                                           # * weights_scale (:559)
+    A = torch.einsum('...ki,...kj->...ij', bmd, bmd)
+    A += torch.eye(D * N) * reg
+    yt = torch.einsum("...ij->...ji", y).reshape([Bsz, -1])
+    pos_det = torch.zeros(Bsz, D * T)
+    Bv = torch.einsum('...ki,...k->...i', bmd, yt - pos_det)
+    return torch.linalg.solve(A, Bv).numpy()
+
+
+def projection_f64(phi: np.ndarray, reg: float = 1e-9) -> np.ndarray:
+    """``P = (Phi^T Phi + reg I)^-1 Phi^T`` in float64, shape ``[N, T]``."""
+    p = phi.astype(np.float64)
+    G = p.T @ p + reg * np.eye(p.shape[1])
+    return np.linalg.solve(G, p.T)
+
+
+def fit_exact(trajs: np.ndarray, phi: np.ndarray, reg: float = 1e-9) -> np.ndarray:
+    """Same ridge fit in float64, rounded once to fp32. ``[B,T,D]`` -> ``[B, D*N]`` (d n)."""
+    P = projection_f64(phi, reg)                               # [N, T]
+    w = np.einsum('nt,btd->bdn', P, trajs.astype(np.float64))
+    return w.reshape(trajs.shape[0], -1).astype(F32)
+
+
+# ---------------------------------------------------------------- H5/H6 ----
+def _clamp_t(x, lo, hi):
+    """torch.clamp with tensor bounds: min(max(x, lo), hi), NaN propagating."""
+    r = np.where(x < lo, lo, x)
+    return np.where(hi < r, hi, r).astype(F32)
+
+
+def continuous_to_discrete(x: np.ndarray, wmin: np.ndarray, wmax: np.ndarray, num_bins: int) -> np.ndarray:
+    """beast/utils.py:4-17 in fp32: sub, div, clamp, mul, round-half-even."""
+    x = x.astype(F32)
+    scale = np.maximum(wmax.astype(F32) - wmin.astype(F32), F32(1e-8)).astype(F32)
+    n = ((x - wmin.astype(F32)) / scale).astype(F32)
+    n = np.clip(n, F32(0), F32(1)).astype(F32)
+    return np.rint((n * F32(num_bins - 1)).astype(F32)).astype(np.int64)
+
+
+def discrete_to_continuous(tok: np.ndarray, wmin: np.ndarray, wmax: np.ndarray, num_bins: int) -> np.ndarray:
+    """beast/utils.py:20-26 in fp32 (no FMA contraction)."""
+    n = (tok.astype(F32) / F32(num_bins - 1)).astype(F32)
+    c = ((n * (wmax - wmin).astype(F32)).astype(F32) + wmin.astype(F32)).astype(F32)
+    return _clamp_t(c, wmin.astype(F32), wmax.astype(F32))
+
+
+def normalized_units(x: np.ndarray, wmin: np.ndarray, wmax: np.ndarray, num_bins: int) -> np.ndarray:
+    """``normalized * (V-1)`` before rounding (distance to a .5 tie)."""
+    x = _clamp_t(x.astype(F32), wmin.astype(F32), wmax.astype(F32))
+    scale = np.maximum(wmax - wmin, F32(1e-8)).astype(F32)
+    n = np.clip(((x - wmin) / scale).astype(F32), F32(0), F32(1))
+    return (n * F32(num_bins - 1)).astype(F32)
+
+
+# ------------------------------------------------------------- tokenizer ---
+@dataclass
+class Layout:
+    """DoF bookkeeping of beast_bspline_tokenizer.py:55-70."""
+    num_dof: int
+    joint_indices: List[int]
+    gripper_indices: List[int]
+
+    @classmethod
+    def make(cls, num_dof: int, gripper_indices: Optional[Sequence[int]], gripper_zero_order: bool):
+        g = sorted(gripper_indices) if (gripper_indices and gripper_zero_order) else []
+        j = sorted(set(range(num_dof)) - set(g))
+        return cls(num_dof, j, g)
+
+    @property
+    def order(self) -> List[int]:
+        return self.joint_indices + self.gripper_indices
+
+
+def encode(trajs, phi_joint, phi_grip, layout: Layout, wmin, wmax, vocab, offset=0, fit=fit_reference_ops):
+    """beast_bspline_tokenizer.py:399-428. Returns (tokens [B, N*D] int64, params [B, D*N] fp32)."""
+    trajs = np.asarray(trajs, dtype=F32)
+    params = fit(trajs[..., layout.joint_indices], phi_joint)
+    if layout.gripper_indices:
+        params = np.concatenate([params, fit(trajs[..., layout.gripper_indices], phi_grip)], axis=-1)
+    params = params.astype(F32)
+    clamped = _clamp_t(params, wmin, wmax)
+    tok = continuous_to_discrete(clamped, wmin, wmax, vocab)
+    Bsz, N, D = tok.shape[0], phi_joint.shape[-1], layout.num_dof
+    tok = tok.reshape(Bsz, D, N).transpose(0, 2, 1).reshape(Bsz, N * D)     # 'b (d t) -> b (t d)'
+    return tok + offset, params
+
+
+def decode(tokens, layout: Layout, num_basis, wmin, wmax, vocab, offset=0):
+    """beast_bspline_tokenizer.py:483-496 -> params ``[B, D*N]`` (d n)."""
+    t = np.asarray(tokens).reshape(len(tokens), -1) - offset
+    Bsz, D, N = t.shape[0], layout.num_dof, num_basis
+    t = t.reshape(Bsz, N, D).transpose(0, 2, 1).reshape(Bsz, D * N)
+    return discrete_to_continuous(t, wmin, wmax, vocab)
+
+
+def reconstruct(tokens, phi_joint, phi_grip, layout: Layout, wmin, wmax, vocab, offset=0, init_p=None,
+                init_pos=True):
+    """beast_bspline_tokenizer.py:498-536 with get_traj_pos (uni_bspline.py:158-166) as fp32 einsum."""
+    N = phi_joint.shape[-1]
+    params = decode(tokens, layout, N, wmin, wmax, vocab, offset)
+    Bsz, D = params.shape[0], layout.num_dof
+    p = params.reshape(Bsz, D, N).copy()
+    if init_pos and init_p is not None:
+        for i, j in enumerate(layout.joint_indices):
+            p[:, i, 0] = np.asarray(init_p, dtype=F32)[:, j]
+    nj = len(layout.joint_indices)
+    T = phi_joint.shape[-2]
+    pos = np.zeros((Bsz, T, D), dtype=F32)
+    pj = torch.einsum('...ik,...jk->...ij', torch.as_tensor(phi_joint).expand(Bsz, T, N),
+                      torch.as_tensor(p[:, :nj])).numpy()
+    for i, j in enumerate(layout.joint_indices):
+        pos[..., j] = pj[..., i]
+    if layout.gripper_indices:
+        pg = torch.einsum('...ik,...jk->...ij', torch.as_tensor(phi_grip).expand(Bsz, T, N),
+                          torch.as_tensor(p[:, nj:])).numpy()
+        for i, j in enumerate(layout.gripper_indices):
+            pos[..., j] = pg[..., i]
+    return pos
+
+
+# ------------------------------------------------------------------ H13 ----
+def quantile_bounds(params: np.ndarray):
+    """fit_parameters' bound step, beast_bspline_tokenizer.py:211-214."""
+    return (np.quantile(params, 0.01, 0).astype(F32), np.quantile(params, 0.99, 0).astype(F32))
+
+
+def quantile_ranks(n: int, q: float):
+    """numpy 2.x 'linear' method in the input dtype (float32): (lo, hi, gamma)."""
+    vi = F32(n - 1) * F32(q)
+    lo = int(np.floor(vi))
+    if vi >= n - 1:
+        return n - 1, n - 1, F32(0)
+    if vi < 0:
+        return 0, 0, F32(0)
+    return lo, lo + 1, F32(np.float64(vi) - lo)
+
+
+def lerp_np(a, b, g):
+    """numpy ``_lerp`` in fp32 (function_base.py): two formulas split at g >= 0.5."""
+    a, b, g = F32(a), F32(b), F32(g)
+    d = F32(b - a)
+    return F32(b - F32(d * F32(F32(1) - g))) if g >= F32(0.5) else F32(a + F32(d * g))

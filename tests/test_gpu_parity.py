@@ -1,0 +1,364 @@
+"""GPU parity of the HIP path against the reference goldens and the CPU oracle.
+
+Contracts:
+  * basis, quantiser, dequantiser, quantiles, BPE vocab/merges: bit-exact;
+  * params: |gpu - ref| <= 1e-5 * max(1, |ref row|_inf) (the reference's own fp32
+    LU error is ~2e-6 of that scale); vs the float64 oracle fit: <= 2 ulp;
+  * tokens end-to-end: equal to the reference except where the reference's
+    normalised value lies within 1e-3 of a .5 rounding tie (counted);
+  * positions: |gpu - ref| <= 1e-5 * max(1, |ref|_inf per trajectory).
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import CONFIGS, GOLDEN, load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+
+from beast_tokenizer_amd import BEASTBsplineBPETokenizer, BEASTBsplineTokenizer, FIGBPE  # noqa: E402
+from beast_tokenizer_amd.synthetic import synth_trajectories  # noqa: E402
+from oracle import beast_oracle as O  # noqa: E402
+
+sys.path.insert(0, GOLDEN)
+from kat_inputs import quantile_inputs  # noqa: E402
+
+TIE_TOL = 1e-3
+
+
+def make_tok(name, g, dev, cls=BEASTBsplineTokenizer, **kw):
+    tok = cls(device=str(dev), **CONFIGS[name], **kw)
+    tok.load_state_dict({"w_min": g["w_min"].tolist(), "w_max": g["w_max"].tolist()})
+    return tok
+
+
+def phis(g):
+    pj = g["phi_joint"]
+    return pj, g.get("phi_grip", pj)
+
+
+def check_token_flips(tok_gpu, tok_ref, x, g, name, max_flips):
+    """Every token that differs from the reference must sit on a rounding tie of the exact fit."""
+    lay = O.Layout.make(CONFIGS[name]["num_dof"], CONFIGS[name]["gripper_indices"],
+                        CONFIGS[name]["gripper_zero_order"])
+    pj, pg = phis(g)
+    p_exact = O.fit_exact(x[..., lay.joint_indices], pj)
+    if lay.gripper_indices:
+        p_exact = np.concatenate([p_exact, O.fit_exact(x[..., lay.gripper_indices], pg)], axis=-1)
+    units = O.normalized_units(p_exact, g["w_min"], g["w_max"], 256)
+    B, N, D = x.shape[0], 10, lay.num_dof
+    units = units.reshape(B, D, N).transpose(0, 2, 1).reshape(B, N * D)
+    diff = tok_gpu != tok_ref
+    nflip = int(diff.sum())
+    assert nflip <= max_flips, f"{nflip} token flips vs reference"
+    if nflip:
+        frac = np.abs(units[diff] - np.floor(units[diff]) - 0.5)
+        assert frac.max() < TIE_TOL, f"non-tie flip: distance to .5 = {frac.max()}"
+        assert np.abs(tok_gpu[diff] - tok_ref[diff]).max() == 1
+    return nflip
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_basis_bitexact(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    phi, proj = tok._constants(gpu_device)
+    assert np.array_equal(phi[0].cpu().numpy(), g["phi_joint"])
+    if "phi_grip" in g:
+        assert np.array_equal(phi[1].cpu().numpy(), g["phi_grip"])
+    P = O.projection_f64(g["phi_joint"])
+    pp = proj[0].cpu().numpy()
+    assert pp.shape == (16, 52) and not pp[10:].any() and not pp[:, 50:].any()
+    assert np.allclose(pp[:10, :50], P, rtol=1e-12, atol=1e-13)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_encode_params_and_tokens(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    x = g["x"]
+    tokens, pd = tok.encode(torch.from_numpy(x))
+    params = pd["params"].cpu().numpy()
+    ref = g["params"]
+    scale = np.maximum(1.0, np.abs(ref).max(axis=1, keepdims=True))
+    assert np.all(np.abs(params - ref) <= 1e-5 * scale), np.abs(params - ref).max()
+    # vs the float64 oracle: correctly rounded up to the f64 accumulation
+    lay = O.Layout.make(CONFIGS[name]["num_dof"], CONFIGS[name]["gripper_indices"],
+                        CONFIGS[name]["gripper_zero_order"])
+    pj, pg = phis(g)
+    ex = O.fit_exact(x[..., lay.joint_indices], pj)
+    if lay.gripper_indices:
+        ex = np.concatenate([ex, O.fit_exact(x[..., lay.gripper_indices], pg)], axis=-1)
+    ulp = np.spacing(np.abs(ex).astype(np.float32))
+    assert np.all(np.abs(params - ex) <= 2 * ulp + 1e-30)
+    # quantiser given identical params: bit-exact
+    t = tokens.cpu().numpy()
+    want = O.continuous_to_discrete(O._clamp_t(params, g["w_min"], g["w_max"]), g["w_min"], g["w_max"], 256)
+    B, D, N = params.shape[0], lay.num_dof, 10
+    assert np.array_equal(t, want.reshape(B, D, N).transpose(0, 2, 1).reshape(B, N * D))
+    assert tokens.dtype == torch.int64 and tokens.shape == (64, N * D)
+    check_token_flips(t, g["tokens"], x, g, name, max_flips=3)
+    for k in ("init_pos", "init_vel", "end_pos", "end_vel"):
+        assert pd[k] is None
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_quantize_bitexact_on_reference_params(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    p = torch.from_numpy(g["params"]).to(gpu_device)
+    out = tok._quantize(p, 0, gpu_device, mode=0).cpu().numpy()
+    assert np.array_equal(out, g["tokens"])
+    out = tok._quantize(p, 32000 - 256, gpu_device, mode=0).cpu().numpy()
+    assert np.array_equal(out, g["tokens_llm"])
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_decode_bitexact(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    dec = tok.decode(torch.from_numpy(g["tokens"])).cpu().numpy()
+    assert np.array_equal(dec, g["decoded"])
+    tok.set_llm_vocab_size(32000)
+    dec2 = tok.decode(torch.from_numpy(g["tokens_llm"])).cpu().numpy()
+    assert np.array_equal(dec2, g["decoded"])
+    # [B, N, D] input form
+    dec3 = tok.decode(torch.from_numpy(g["tokens_llm"]).reshape(64, 10, -1)).cpu().numpy()
+    assert np.array_equal(dec3, g["decoded"])
+
+
+def _close_pos(a, b):
+    scale = np.maximum(1.0, np.abs(b).max(axis=(1, 2), keepdims=True))
+    err = np.abs(a - b) / scale
+    assert err.max() <= 1e-5, err.max()
+    return float((a == b).mean())
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_reconstruct(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    toks = torch.from_numpy(g["tokens"])
+    pos = tok.reconstruct_traj(toks).cpu().numpy()
+    assert pos.shape == g["pos"].shape and pos.dtype == np.float32
+    _close_pos(pos, g["pos"])
+    pos_ip = tok.reconstruct_traj(toks, init_p=torch.from_numpy(g["init_p"])).cpu().numpy()
+    _close_pos(pos_ip, g["pos_init_p"])
+    t80 = torch.from_numpy(g["times80"])
+    pos80 = tok.reconstruct_traj(toks, times=t80.expand(64, 80)).cpu().numpy()
+    _close_pos(pos80, g["pos_t80"])
+    pos80b = tok.reconstruct_traj(toks, times=t80).cpu().numpy()
+    assert np.array_equal(pos80, pos80b)
+
+
+@pytest.mark.parametrize("name", ["k2", "k3"])
+def test_reconstruct_per_row_times(name, golden, gpu_device):
+    """Different time grid per trajectory -> per-row basis path; vs fp64 numpy."""
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    toks = torch.from_numpy(g["tokens"][:16])
+    rng = np.random.default_rng(5)
+    times = np.sort(rng.uniform(0, 2 * np.pi, size=(16, 33)), axis=1).astype(np.float32)
+    pos = tok.reconstruct_traj(toks, times=torch.from_numpy(times)).cpu().numpy()
+    lay = O.Layout.make(CONFIGS[name]["num_dof"], CONFIGS[name]["gripper_indices"],
+                        CONFIGS[name]["gripper_zero_order"])
+    params = O.decode(g["tokens"][:16], lay, 10, g["w_min"], g["w_max"], 256).reshape(16, lay.num_dof, 10)
+    want = np.zeros_like(pos)
+    for b in range(16):
+        pj = O.basis(times[b], np.float32(2 * np.pi), 4, 10)
+        pg = O.basis(times[b], np.float32(2 * np.pi), 0, 10)
+        for i, d in enumerate(lay.order):
+            ph = pj if i < len(lay.joint_indices) else pg
+            want[b, :, d] = ph.astype(np.float64) @ params[b, i].astype(np.float64)
+    _close_pos(pos, want)
+
+
+@pytest.mark.parametrize("name", ["k2", "k3"])
+def test_flip_census_4096(name, gpu_device):
+    """Full BASELINE size: tokens vs the reference's, every flip a rounding tie."""
+    z = load_npz(f"tokens4096_{name}.npz")
+    gi = CONFIGS[name]["gripper_indices"] or []
+    x = synth_trajectories(4096, 50, 14, seed=0, gripper_indices=gi)
+    assert hashlib.sha256(x.tobytes()).digest() == z["x_sha256"].tobytes(), "synthetic generator drifted"
+    g = dict(load_npz(f"bspline_{name}.npz"))
+    g["w_min"], g["w_max"] = z["w_min"], z["w_max"]
+    tok = make_tok(name, g, gpu_device)
+    tokens, _ = tok.encode(torch.from_numpy(x))
+    n = check_token_flips(tokens.cpu().numpy(), z["tokens"].astype(np.int64), x, g, name, max_flips=60)
+    print(f"{name}: {n} tie flips of {tokens.numel()} tokens")
+
+
+@pytest.mark.parametrize("name", ["k2", "k3"])
+def test_roundtrip_properties(name, golden, gpu_device):
+    """Size-independent properties at B=4096: decode(encode) within one bin, reconstruct(tokens) == Phi.decode."""
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    x = synth_trajectories(4096, 50, 14, seed=11, gripper_indices=CONFIGS[name]["gripper_indices"] or [])
+    tokens, pd = tok.encode(torch.from_numpy(x).to(gpu_device))
+    dec = tok.decode(tokens)
+    clamped = torch.clamp(pd["params"], min=tok.w_min, max=tok.w_max)
+    binw = (tok.w_max - tok.w_min) / 255
+    assert torch.all((dec - clamped).abs() <= 0.5 * binw * (1 + 1e-5) + 1e-7)
+    # idempotence: re-encoding the decoded params' quantisation gives the same tokens
+    again = tok._quantize(dec, 0, gpu_device, 0)
+    assert torch.equal(again, tokens)
+    assert int(tokens.min()) >= 0 and int(tokens.max()) <= 255
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_update_bounds(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    x = torch.from_numpy(g["x"]) * 3.0
+    wmin0, wmax0 = tok.w_min.clone(), tok.w_max.clone()
+    tokens, pd = tok.encode(x, update_bounds=True)
+    p = pd["params"].cpu().numpy()
+    bmin, bmax = p.min(0), p.max(0)
+    wmn, wmx = wmin0.cpu().numpy(), wmax0.cpu().numpy()
+    exp_min = np.where(bmin < (wmn - np.float32(1e-4)), bmin, wmn)
+    exp_max = np.where(bmax > (wmx + np.float32(1e-4)), bmax, wmx)
+    assert np.array_equal(tok.w_min.cpu().numpy(), exp_min)
+    assert np.array_equal(tok.w_max.cpu().numpy(), exp_max)
+    want = O.continuous_to_discrete(O._clamp_t(p, exp_min, exp_max), exp_min, exp_max, 256)
+    B, D = p.shape[0], CONFIGS[name]["num_dof"]
+    assert np.array_equal(tokens.cpu().numpy(), want.reshape(B, D, 10).transpose(0, 2, 1).reshape(B, -1))
+
+
+def test_quantile_kat(gpu_device):
+    from beast_tokenizer_amd.quantile import column_quantiles
+    z = load_npz("quantile_kat.npz")
+    for k, x in quantile_inputs().items():
+        q = column_quantiles(torch.from_numpy(x).to(gpu_device), [0.01, 0.99]).cpu().numpy()
+        assert np.array_equal(q[0], z[k + "_lo"].astype(np.float32)), k
+        assert np.array_equal(q[1], z[k + "_hi"].astype(np.float32)), k
+    xn = quantile_inputs()["n101"].copy()
+    xn[7, 3] = np.nan
+    q = column_quantiles(torch.from_numpy(xn).to(gpu_device), [0.01, 0.99]).cpu().numpy()
+    ref = np.quantile(xn, [0.01, 0.99], axis=0)
+    assert np.array_equal(np.isnan(q), np.isnan(ref)) and np.isnan(q[:, 3]).all()
+    assert np.array_equal(q[~np.isnan(q)], ref[~np.isnan(ref)].astype(np.float32))
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_fit_parameters(name, golden, gpu_device):
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    gi = CONFIGS[name]["gripper_indices"] or []
+    D = CONFIGS[name]["num_dof"]
+    loader = [{"actions": torch.from_numpy(synth_trajectories(1024, 50, D, seed=1, gripper_indices=gi,
+                                                              start=1024 * i))} for i in range(8)]
+    tok.fit_parameters(loader, verbose=False)
+    allp = torch.cat([tok.compute_weights(b["actions"]) for b in loader]).cpu().numpy()
+    lo, hi = O.quantile_bounds(allp)
+    assert np.array_equal(tok.w_min.cpu().numpy(), lo)
+    assert np.array_equal(tok.w_max.cpu().numpy(), hi)
+    bounds = load_json(f"bounds_{name}.json")
+    assert np.allclose(tok.w_min.cpu().numpy(), bounds["w_min"], rtol=1e-4, atol=1e-4)
+    assert np.allclose(tok.w_max.cpu().numpy(), bounds["w_max"], rtol=1e-4, atol=1e-4)
+    with pytest.raises(KeyError):
+        tok.fit_parameters([{"obs": 1}], verbose=False)
+    with pytest.raises(RuntimeError):
+        tok.fit_parameters([], verbose=False)
+
+
+def test_encode_continuous_and_back(golden, gpu_device):
+    g = golden["k3"]
+    tok = make_tok("k3", g, gpu_device)
+    ct, pd = tok.encode_continuous(torch.from_numpy(g["x"]))
+    p = pd["params"].cpu().numpy()
+    wmn, wmx = g["w_min"], g["w_max"]
+    c = O._clamp_t(p, wmn, wmx)
+    want = (((c - wmn) / np.maximum(wmx - wmn, np.float32(1e-8))).astype(np.float32) * np.float32(2)
+            + np.float32(-1)).astype(np.float32)
+    B = p.shape[0]
+    assert np.array_equal(ct.cpu().numpy(), want.reshape(B, 14, 10).transpose(0, 2, 1).reshape(B, -1))
+    pos = tok.reconstruct_traj_continuous(ct).cpu().numpy()
+    # expected: denormalise (evident intent of beast/utils.py:38-44) then Phi . W in float64
+    c = np.clip(ct.cpu().numpy(), -1, 1).reshape(B, 10, 14).transpose(0, 2, 1).reshape(B, -1)
+    w = (((c + np.float32(1)) / np.float32(2)).astype(np.float32) * (wmx - wmn) + wmn).astype(np.float32)
+    lay = O.Layout.make(14, [6, 13], True)
+    pj, pg = phis(g)
+    want = np.zeros_like(pos)
+    for i, d in enumerate(lay.order):
+        ph = pj if i < len(lay.joint_indices) else pg
+        want[:, :, d] = w.reshape(B, 14, 10)[:, i].astype(np.float64) @ ph.T.astype(np.float64)
+    _close_pos(pos, want)
+
+
+# ------------------------------------------------------------------ BPE ----
+BPE_CASES = sorted(load_json("bpe_hf.json").keys()) if os.path.exists(os.path.join(GOLDEN, "bpe_hf.json")) else []
+
+
+@pytest.fixture(scope="module")
+def bpe_golden():
+    return load_json("bpe_hf.json"), load_npz("bpe_corpora.npz")
+
+
+@pytest.mark.parametrize("case", BPE_CASES)
+def test_bpe_train_matches_hf(case, bpe_golden, gpu_device):
+    ref, corpora = bpe_golden
+    cname, vs = case.split("/")
+    arr = corpora[cname]
+    fig = FIGBPE(vocab_size=int(vs), show_progress=False, device=gpu_device)
+    st = fig.fit_from_sequences(list(arr))
+    r = ref[case]
+    assert st.min_token == r["min_token"] and st.max_token == r["max_token"]
+    res = fig.last_result
+    assert res.vocab == r["vocab"]
+    assert [list(m) for m in res.merges] == r["merges"]
+    # the wrapped HF object behaves like the HF-trained one
+    text = "".join(map(chr, (arr[0] - r["min_token"]).astype(int)))
+    ids = st.tokenizer.encode(text, add_special_tokens=False).ids
+    assert st.tokenizer.decode(ids) == text
+
+
+def test_bpe_pretok_words_match_hf(gpu_device):
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, sequences_to_device
+    from beast_tokenizer_amd.pretok import bytes_to_unicode, class_lut
+    samples = [s for s, _ in load_json("pretok.json")["samples"] if s]
+    pieces = [p for _, ps in load_json("pretok.json")["samples"] for p in ps]
+    seqs = [np.array([ord(c) for c in s], dtype=np.int64) for s in samples]
+    tokens, off = sequences_to_device(seqs, gpu_device)
+    K = int(tokens.max())
+    present = np.zeros(K + 1, dtype=bool)
+    present[np.concatenate(seqs)] = True
+    id2str, _, byte2id = build_alphabet(present, [chr(i) for i in range(K + 1)], [])
+    ops = GpuBpeOps(gpu_device)
+    w = ops.pretokenize(tokens, off, 0, class_lut(K + 1), byte2id)
+    sym = w["sym"].cpu().numpy().view(np.uint16)
+    ws, wl = w["wstart"].cpu().numpy(), w["wlen"].cpu().numpy()
+    got = ["".join(id2str[s] for s in sym[a:a + n]) for a, n in zip(ws[: w["n_words"]], wl[: w["n_words"]])]
+    assert got == pieces
+
+
+def test_bpe_tokenizer_end_to_end(gpu_device):
+    g = load_npz("bspline_k2.npz")
+    tok = make_tok("k2", g, gpu_device, cls=BEASTBsplineBPETokenizer, bpe_vocab_size=512)
+    batches = [{"actions": torch.from_numpy(synth_trajectories(512, 50, 14, seed=4, start=512 * i))}
+               for i in range(4)]
+    st = tok.fit_from_trajectories(batches, show_progress=False, max_sequences=1800)
+    assert tok.bpe_tokenizer is not None and st.max_token <= 255
+    x = torch.from_numpy(synth_trajectories(32, 50, 14, seed=9))
+    bpe_ids, params, mp = tok.encode(x, return_mp_tokens=True)
+    # bins >= 128 are 2 UTF-8 bytes, so a row is at most 2*140 BPE ids
+    assert len(bpe_ids) == 32 and all(len(r) <= 280 for r in bpe_ids)
+    back = tok.bpe_to_mp_tokens(bpe_ids)
+    assert torch.equal(back.cpu(), mp.cpu())
+    assert torch.equal(tok.decode(bpe_ids), BEASTBsplineTokenizer.decode(tok, mp))
+    # HF-trained reference on the same bins gives the same merges
+    from tokenizers import ByteLevelBPETokenizer
+    from tokenizers.trainers import BpeTrainer
+    rows = torch.cat([tok.encode_to_mp_tokens(b["actions"])[0] for b in batches])[:1800].cpu().numpy()
+    lo, hi = int(rows.min()), int(rows.max())
+    bpe = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=512, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=10000)
+    bpe._tokenizer.train_from_iterator(["".join(map(chr, r - lo)) for r in rows], trainer=tr)
+    model = json.loads(bpe._tokenizer.to_str())["model"]
+    assert tok._last_bpe_result.vocab == model["vocab"]
+    assert [list(m) for m in tok._last_bpe_result.merges] == model["merges"]
