@@ -1,6 +1,7 @@
 // Fused BEAST encode / reconstruct kernels for gfx950.
 //
-//   k_encode       params = P . y on v_mfma_f64_16x16x4_f64, fused with the clamp /
+//   k_encode       params = P . y on v_mfma_f32_16x16x4_f32 (P = fp32 rounding of the fp64
+//                  ridge projection), fused with the clamp /
 //                  quantise / (d n)->(n d) / LLM-offset epilogue (reference
 //                  beast/beast_bspline_tokenizer.py:399-428, mp/uni_bspline.py:539-586)
 //   k_reconstruct  dequantise + init_p + Phi . W on v_mfma_f32_16x16x4_f32 + scatter
@@ -165,7 +166,7 @@ template <int TBT>
 __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N, int nkinds) {
   EncSmem s;
   int o = 0;
-  s.P = o;    o += round_up(nkinds * 16 * Tp * 8, 16);
+  s.P = o;    o += round_up(nkinds * 16 * Tp * 4, 16);  // fp32 copy of the [16][Tp] projection
   s.Y = o;    o += round_up(TBT * T * Dl * 4, 16);
   s.pb = o;   o += round_up(TBT * D * N * 4, 16);
   s.wlo = o;  o += round_up(D * N * 4, 16);
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
   const int Dl = FAST ? a.row_elems : D;
   const int nkinds = (g.nj < D) ? 2 : 1;
   const EncSmem L = enc_smem<TBT>(T, Tp, Dl, D, N, nkinds);
-  double* P = reinterpret_cast<double*>(smem + L.P);
+  float* P = reinterpret_cast<float*>(smem + L.P);
   float* Y = reinterpret_cast<float*>(smem + L.Y);
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
@@ -207,7 +208,19 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
       hi[i] = quant ? a.w_max[k] : 0.0f;
     }
     if (tid < D) lc = a.dof_src[tid];
-    burst<2>(P, a.proj, nkinds * 16 * Tp * 8);
+    {   // f64 projection -> fp32 LDS copy (all loads issued before the stores)
+      const int tot = nkinds * 16 * Tp;
+      for (int base = 0; base < tot; base += 8 * NTHREADS) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = a.proj[min(base + u * NTHREADS + tid, tot - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = base + u * NTHREADS + tid;
+          if (i < tot) P[i] = (float)v[u];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = tid + i * NTHREADS;
@@ -249,37 +262,43 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
     }
     __syncthreads();
 
-    // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f64 MFMA 16x16x4; A = P, B = y)
-    for (int q0 = wave; (a.phases & 2) && q0 < g.nq; q0 += NWAVES * TILES) {
-      const double* Pk[TILES];
-      const float* Yc[TILES];
-      int jj[TILES], dd[TILES];
-      bool ok[TILES];
-      double4_t acc[TILES];
-#pragma unroll
-      for (int u = 0; u < TILES; ++u) {
-        const int q = min(q0 + u * NWAVES, g.nq - 1);
-        int kind;
-        tile_col<TBT>(g, q, lr, jj[u], dd[u], kind, ok[u]);
-        ok[u] = ok[u] && (q0 + u * NWAVES < g.nq) && jj[u] < nb;
-        Pk[u] = P + (kind * 16 + lr) * Tp + lk;
-        Yc[u] = Y + jj[u] * T * Dl + lcol[dd[u]];
-        acc[u] = double4_t{0.0, 0.0, 0.0, 0.0};
+    // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f32 MFMA 16x16x4; A = P, B = y).
+    //      A wave owns two column tiles per pass (two independent chains), operands
+    //      pointer-stepped through LDS; rows t >= T (tail step) meet a zero A column.
+    for (int q0 = wave; (a.phases & 2) && q0 < g.nq; q0 += NWAVES * 2) {
+      int j0, d0, k0, j1, d1, k1;
+      bool ok0, ok1;
+      tile_col<TBT>(g, q0, lr, j0, d0, k0, ok0);
+      tile_col<TBT>(g, min(q0 + NWAVES, g.nq - 1), lr, j1, d1, k1, ok1);
+      ok0 = ok0 && j0 < nb;
+      ok1 = ok1 && j1 < nb && (q0 + NWAVES < g.nq);
+      const float* pa0 = P + (k0 * 16 + lr) * Tp + lk;
+      const float* pa1 = P + (k1 * 16 + lr) * Tp + lk;
+      const float* yc0 = Y + j0 * T * Dl + lcol[d0];
+      const float* yc1 = Y + j1 * T * Dl + lcol[d1];
+      const float* yb0 = yc0 + lk * Dl;
+      const float* yb1 = yc1 + lk * Dl;
+      float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
+      int s = 0;
+#pragma unroll 4
+      for (; s + 4 <= T; s += 4) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[s], *yb0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[s], *yb1, acc1, 0, 0, 0);
+        yb0 += 4 * Dl;
+        yb1 += 4 * Dl;
       }
-      for (int s = 0; s < Tp; s += 4) {
-        const int tc = min(s + lk, T - 1);   // rows t >= T meet a zero A column
-#pragma unroll
-        for (int u = 0; u < TILES; ++u)
-          acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(Pk[u][s], (double)Yc[u][tc * Dl], acc[u], 0, 0, 0);
+      if (s < T) {   // wave-uniform tail (T % 4 != 0)
+        const int row = min(s + lk, T - 1) * Dl;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[s], yc0[row], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[s], yc1[row], acc1, 0, 0, 0);
       }
-      // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * r
+      // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
-      for (int u = 0; u < TILES; ++u) {
-        if (!ok[u]) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = lk + 4 * r;
-          if (n < N) pb[jj[u] * DN + dd[u] * N + n] = (float)acc[u][r];
+      for (int r = 0; r < 4; ++r) {
+        const int n = lk * 4 + r;
+        if (n < N) {
+          if (ok0) pb[j0 * DN + d0 * N + n] = acc0[r];
+          if (ok1) pb[j1 * DN + d1 * N + n] = acc1[r];
         }
       }
     }
@@ -316,7 +335,7 @@ struct RecArgs {
   const long long* tokens;
   const float* ntokens;
   int64_t B, ntiles, tok_offset, basis_sb, init_p_sb;
-  int vocab, Tout, ndo, phases;
+  int vocab, Tout, ndo, phases, lut_n;
   const float* w_min;
   const float* w_max;
   const float* basis;      // [2][Tout][N] (shared) or per trajectory with stride basis_sb
@@ -326,51 +345,63 @@ struct RecArgs {
   float* params_out;
   float* pos_out;
   Geom g;
+  FastDiv fd_row;          // Tout * ndo
 };
+
+constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divided once
 
 struct RecSmem {
-  int phi, pb, tok, wlo, whi, pmap, kq, kpb, dst, col2d, out, total;
-  bool stage_out;
+  int phi, pb, tok, wlo, whi, wrg, lut, pmap, kq, kpb, dst, col2d, out, total;
+  int Np4, RTR;   // padded basis width, padded output rows
+  bool stage;
 };
 
-template <int TBT>
-__host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, bool shared, int nkinds) {
+// KS > 0: shared basis on MFMA (K-steps of 4 basis functions); KS == 0: per-row basis on VALU
+template <int TBT, int KS>
+__host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, int nkinds, int lut_n) {
   RecSmem s;
-  const int Np = round_up(N, 4), RTp = round_up(Tout, 16), per = N * D;
+  const int per = N * D;
+  s.Np4 = KS ? 4 * KS : round_up(N, 4);
+  s.RTR = KS ? round_up(Tout, 32) : Tout;   // even number of 16-row tiles
   int o = 0;
-  s.phi = o;   o += shared ? round_up(nkinds * RTp * Np * 4, 16) : 0;
-  s.pb = o;    o += round_up(TBT * D * Np * 4, 16);
+  s.phi = o;   o += KS ? round_up(nkinds * s.RTR * s.Np4 * 4, 16) : 0;
+  s.pb = o;    o += round_up(TBT * D * s.Np4 * 4, 16);
   s.tok = o;   o += round_up(TBT * per * 8, 16);
   s.wlo = o;   o += round_up(per * 4, 16);
   s.whi = o;   o += round_up(per * 4, 16);
-  s.pmap = o;  o += round_up(per * 2, 16);   // (n d) slot -> pb offset d*Np + n
+  s.wrg = o;   o += round_up(per * 4, 16);
+  s.lut = o;   o += round_up(lut_n * 4, 16);
+  s.pmap = o;  o += round_up(per * 2, 16);   // (n d) slot -> W offset d*Np4 + n
   s.kq = o;    o += round_up(per * 2, 16);   // (n d) slot -> (d n) index d*N + n
-  s.kpb = o;   o += round_up(per * 2, 16);   // (d n) index -> pb offset
+  s.kpb = o;   o += round_up(per * 2, 16);   // (d n) index -> W offset
   s.dst = o;   o += round_up(D * 4, 16);
   s.col2d = o; o += round_up(ndo * 4, 16);
-  const int outb = round_up(TBT * Tout * ndo * 4, 16);
-  s.stage_out = (o + outb) <= 96 * 1024;
-  s.out = o;   o += s.stage_out ? outb : 0;
+  const int outb = round_up(TBT * s.RTR * ndo * 4, 16);
+  s.stage = KS ? true : (o + outb) <= 96 * 1024;
+  s.out = o;   o += s.stage ? outb : 0;
   s.total = o;
   return s;
 }
 
-template <int TBT, bool SHARED>
+template <int TBT, int KS>
 __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Geom& g = a.g;
-  const int D = g.D, N = g.N, nj = g.nj, per = g.per, Np = round_up(N, 4);
-  const int Tout = a.Tout, ndo = a.ndo, RTp = round_up(Tout, 16);
+  const int D = g.D, N = g.N, nj = g.nj, per = g.per;
+  const int Tout = a.Tout, ndo = a.ndo;
   const int nkinds = (nj < D) ? 2 : 1;
   const bool pos = a.pos_out != nullptr;
-  const RecSmem L = rec_smem<TBT>(Tout, D, N, ndo, SHARED && pos, nkinds);
+  const RecSmem L = rec_smem<TBT, KS>(Tout, D, N, ndo, nkinds, a.lut_n);
+  const int Np4 = L.Np4, RTR = L.RTR;
   float* phi = reinterpret_cast<float*>(smem + L.phi);
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
+  float* wrg = reinterpret_cast<float*>(smem + L.wrg);
+  float* lut = reinterpret_cast<float*>(smem + L.lut);
   uint16_t* pmap = reinterpret_cast<uint16_t*>(smem + L.pmap);
-  uint16_t* kpb = reinterpret_cast<uint16_t*>(smem + L.kpb);
   uint16_t* kq = reinterpret_cast<uint16_t*>(smem + L.kq);
+  uint16_t* kpb = reinterpret_cast<uint16_t*>(smem + L.kpb);
   int* dst = reinterpret_cast<int*>(smem + L.dst);
   int* col2d = reinterpret_cast<int*>(smem + L.col2d);
   float* ob = reinterpret_cast<float*>(smem + L.out);
@@ -388,14 +419,14 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
     }
     int dd = 0;
     if (pos && tid < D) dd = a.dof_dst[tid];
-    if (SHARED && pos) {   // Phi zero-padded to [kinds][RTp][Np]: clamped loads, then select
-      const int tot = nkinds * RTp * Np;
+    if (KS && pos) {   // Phi zero-padded to [kinds][RTR][Np4]: clamped loads, then select
+      const int tot = nkinds * RTR * Np4;
       for (int base = 0; base < tot; base += 8 * NTHREADS) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int i = min(base + u * NTHREADS + tid, tot - 1);
-          const int k = i / (RTp * Np), r = i - k * RTp * Np, t = r / Np, n = r - t * Np;
+          const int k = i / (RTR * Np4), r = i - k * RTR * Np4, t = r / Np4, n = r - t * Np4;
           const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
           v[u] = (t < Tout && n < N) ? x : 0.0f;
         }
@@ -409,18 +440,23 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int k = tid + i * NTHREADS;
-      if (k < per) { wlo[k] = lo[i]; whi[k] = hi[i]; }
+      if (k < per) {
+        wlo[k] = lo[i];
+        whi[k] = hi[i];
+        wrg[k] = __fsub_rn(hi[i], lo[i]);   // (max_val - min_val), beast/utils.py:24
+      }
     }
+    for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
     for (int r = tid; r < per; r += NTHREADS) {
       const int n = r / D, d = r - n * D;
-      pmap[r] = (uint16_t)(d * Np + n);
+      pmap[r] = (uint16_t)(d * Np4 + n);
       kq[r] = (uint16_t)(d * N + n);
       const int d2 = r / N, n2 = r - d2 * N;
-      kpb[r] = (uint16_t)(d2 * Np + n2);
+      kpb[r] = (uint16_t)(d2 * Np4 + n2);
     }
-    for (int e = tid; e < TBT * D * (Np - N); e += NTHREADS) {   // zero W pad columns once
-      const int row = e / (Np - N), n = N + (e - row * (Np - N));
-      pb[row * Np + n] = 0.0f;
+    for (int e = tid; e < TBT * D * (Np4 - N); e += NTHREADS) {   // zero W pad columns once
+      const int row = e / (Np4 - N), n = N + (e - row * (Np4 - N));
+      pb[row * Np4 + n] = 0.0f;
     }
     if (pos) {
       for (int c = tid; c < ndo; c += NTHREADS) col2d[c] = -1;
@@ -435,7 +471,6 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
 
   const int wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
-  const int nt = (RTp / 16) * g.nq;
 
   for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int64_t b0 = tile * TBT;
@@ -456,8 +491,15 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
         const uint32_t j = fdiv(e, g.fd_per);
         const int r = e - j * per;
         const int po = pmap[r], k = kq[r];
-        pb[j * D * Np + po] = a.ntokens ? beast::denormalize_one(fin[e], wlo[k], whi[k])
-                                        : beast::dequantize_one(tin[e] - a.tok_offset, wlo[k], whi[k], vm1);
+        float v;
+        if (a.ntokens) {
+          v = beast::denormalize_one(fin[e], wlo[k], whi[k]);
+        } else {
+          const long long t = tin[e] - a.tok_offset;
+          const float nrm = (t >= 0 && t < a.lut_n) ? lut[t] : __fdiv_rn((float)t, vm1);
+          v = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, wrg[k]), wlo[k]), wlo[k], whi[k]);
+        }
+        pb[j * D * Np4 + po] = v;
       }
     }
     __syncthreads();
@@ -465,7 +507,7 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
       float* pout = a.params_out + b0 * per;
       for (int e = tid; e < nb * per; e += NTHREADS) {
         const uint32_t j = fdiv(e, g.fd_per);
-        pout[e] = pb[j * D * Np + kpb[e - j * per]];
+        pout[e] = pb[j * D * Np4 + kpb[e - j * per]];
       }
     }
     if (!pos) continue;
@@ -473,49 +515,65 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
       __syncthreads();
       for (int e = tid; e < nb * nj; e += NTHREADS) {
         const int j = e / nj, d = e - j * nj;
-        pb[(j * D + d) * Np] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];
+        pb[(j * D + d) * Np4] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];
       }
       __syncthreads();
     }
 
     float* gout = a.pos_out + b0 * (int64_t)Tout * ndo;
-    if (SHARED) {
-      // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W)
-      for (int w0 = wave; (a.phases & 2) && w0 < nt; w0 += NWAVES * TILES) {
-        const float* Ph[TILES];
-        const float* Wc[TILES];
-        int jj[TILES], cc[TILES], rt[TILES];
-        bool ok[TILES];
-        float4_t acc[TILES];
+    if constexpr (KS > 0) {
+      // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W).
+      //      A wave owns a column tile: W stays in registers while it walks pairs of row
+      //      tiles (two independent chains); rows past Tout land in ob's padding.
+      for (int q = wave; (a.phases & 2) && q < g.nq; q += NWAVES) {
+        int j, d, kind;
+        bool ok;
+        tile_col<TBT>(g, q, lr, j, d, kind, ok);
+        ok = ok && j < nb;
+        float w[KS];
+        const float* Wc = pb + (j * D + d) * Np4 + lk;
 #pragma unroll
-        for (int u = 0; u < TILES; ++u) {
-          const int w = min(w0 + u * NWAVES, nt - 1);
-          const int r = (int)fdiv(w, g.fd_nq), q = w - r * g.nq;
-          int d, kind;
-          tile_col<TBT>(g, q, lr, jj[u], d, kind, ok[u]);
-          ok[u] = ok[u] && (w0 + u * NWAVES < nt) && jj[u] < nb;
-          Ph[u] = phi + (kind * RTp + r * 16 + lr) * Np + lk;
-          Wc[u] = pb + (jj[u] * D + d) * Np + lk;
-          cc[u] = dst[d];
-          rt[u] = r;
-          acc[u] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-        for (int s = 0; s < Np; s += 4) {
+        for (int ks = 0; ks < KS; ++ks) w[ks] = Wc[4 * ks];
+        const float* Ph = phi + (kind * RTR + lr) * Np4 + lk;
+        float* oc = ob + (j * RTR + lk * 4) * ndo + dst[d];
+        for (int rt = 0; rt < RTR / 16; rt += 2) {
+          float a0[KS], a1[KS];
 #pragma unroll
-          for (int u = 0; u < TILES; ++u)
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ph[u][s], Wc[u][s], acc[u], 0, 0, 0);
-        }
-        // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+          for (int ks = 0; ks < KS; ++ks) {
+            a0[ks] = Ph[(rt * 16) * Np4 + 4 * ks];
+            a1[ks] = Ph[(rt * 16 + 16) * Np4 + 4 * ks];
+          }
+          float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int u = 0; u < TILES; ++u) {
-          if (!ok[u]) continue;
+          for (int ks = 0; ks < KS; ++ks) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks], w[ks], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[ks], w[ks], acc1, 0, 0, 0);
+          }
+          // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+          if (ok) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = rt[u] * 16 + lk * 4 + r;
-            if (t < Tout) {
-              if (L.stage_out) ob[(jj[u] * Tout + t) * ndo + cc[u]] = acc[u][r];
-              else gout[((int64_t)jj[u] * Tout + t) * ndo + cc[u]] = acc[u][r];
+            for (int r = 0; r < 4; ++r) {
+              oc[(rt * 16 + r) * ndo] = acc0[r];
+              oc[(rt * 16 + 16 + r) * ndo] = acc1[r];
             }
+          }
+        }
+      }
+      __syncthreads();
+      if (a.phases & 4) {   // ob rows [0, Tout) of each trajectory -> contiguous HBM tile
+        const int rowlen = Tout * ndo;
+        if ((rowlen & 3) == 0 && ((RTR * ndo) & 3) == 0 && ((((uintptr_t)gout) & 15) == 0)) {
+          const int n4 = nb * rowlen / 4;
+          for (int i = tid; i < n4; i += NTHREADS) {
+            const uint32_t e = 4 * i;
+            const uint32_t j = fdiv(e, a.fd_row);
+            reinterpret_cast<float4*>(gout)[i] =
+                *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen));
+          }
+        } else {
+          for (int e = tid; e < nb * rowlen; e += NTHREADS) {
+            const uint32_t j = fdiv(e, a.fd_row);
+            gout[e] = ob[j * RTR * ndo + (e - j * rowlen)];
           }
         }
       }
@@ -528,15 +586,15 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
         if (d >= 0) {
           const int kind = (d < nj) ? 0 : 1;
           const float* Phr = a.basis + (b0 + j) * a.basis_sb + (int64_t)kind * Tout * N + (int64_t)t * N;
-          const float* Wr = pb + (j * D + d) * Np;
+          const float* Wr = pb + (j * D + d) * Np4;
           for (int n = 0; n < N; ++n) acc = fmaf(Phr[n], Wr[n], acc);
         }
-        if (L.stage_out) ob[e] = acc; else gout[e] = acc;
+        if (L.stage) ob[e] = acc; else gout[e] = acc;
       }
-    }
-    if (L.stage_out && (a.phases & 4)) {
-      __syncthreads();
-      store_out(gout, ob, nb * Tout * ndo);
+      if (L.stage && (a.phases & 4)) {
+        __syncthreads();
+        store_out(gout, ob, nb * Tout * ndo);
+      }
     }
   }
 }
@@ -584,22 +642,34 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t
   return BEAST_OK;
 }
 
-template <int TBT>
-int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t s) {
-  a.g = make_geom<TBT>(D, nj, N, 1);
-  a.ntiles = (a.B + TBT - 1) / TBT;
-  const bool pos = a.pos_out != nullptr;
-  const RecSmem L = rec_smem<TBT>(a.Tout, D, N, a.ndo, shared && pos, nj < D ? 2 : 1);
+template <int TBT, int KS>
+int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
+  const RecSmem L = rec_smem<TBT, KS>(a.Tout, D, a.g.N, a.ndo, nj < D ? 2 : 1, a.lut_n);
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
-  if (shared && pos) hipLaunchKernelGGL((k_reconstruct<TBT, true>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else hipLaunchKernelGGL((k_reconstruct<TBT, false>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  hipLaunchKernelGGL((k_reconstruct<TBT, KS>), dim3(grid), dim3(NTHREADS), L.total, s, a);
   BEAST_LAUNCHED("k_reconstruct");
   return BEAST_OK;
 }
 
-// tiles of 16 trajectories once there are >= 2 per CU, else 8 (more workgroups in flight)
-bool small_batch(int64_t B) { return (B + 15) / 16 < 2 * (int64_t)cu_count(); }
+template <int TBT>
+int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t s) {
+  a.g = make_geom<TBT>(D, nj, N, 1);
+  a.ntiles = (a.B + TBT - 1) / TBT;
+  a.fd_row = make_fd((uint32_t)(a.Tout * a.ndo));
+  a.lut_n = (a.ntokens == nullptr && a.vocab <= LUT_MAX) ? a.vocab : 0;
+  const bool pos = a.pos_out != nullptr;
+  // MFMA path needs the shared basis and the padded output tile in LDS
+  const bool mfma = shared && pos && rec_smem<TBT, 4>(a.Tout, D, N, a.ndo, 2, a.lut_n).total <= 112 * 1024;
+  if (!mfma) return launch_rec_ks<TBT, 0>(a, D, nj, s);
+  switch ((N + 3) / 4) {
+    case 1: return launch_rec_ks<TBT, 1>(a, D, nj, s);
+    case 2: return launch_rec_ks<TBT, 2>(a, D, nj, s);
+    case 3: return launch_rec_ks<TBT, 3>(a, D, nj, s);
+    default: return launch_rec_ks<TBT, 4>(a, D, nj, s);
+  }
+}
+
 
 }  // namespace
 
@@ -623,9 +693,8 @@ extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb,
   const bool fast16 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems &&
                        16 * T * row_elems * 4 <= 64 * 1024);
   const bool fast8 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems && 8 * T * row_elems * 4 <= 64 * 1024);
-  hipStream_t s = beast::as_stream(stream);
-  if (small_batch(B)) return launch_encode<8>(a, T, D, n_joint, N, fast8, s);
-  return launch_encode<16>(a, T, D, n_joint, N, fast16, s);
+  (void)fast16;
+  return launch_encode<8>(a, T, D, n_joint, N, fast8, beast::as_stream(stream));
 }
 
 extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, int n_joint, int N, int vocab,
@@ -650,7 +719,5 @@ extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, in
   a.ndo = pos_out ? num_dof_out : 1; a.phases = debug_phases(); a.w_min = w_min; a.w_max = w_max; a.basis = basis;
   a.dof_dst = dof_dst; a.init_p = init_p; a.init_p_src = init_p_src; a.params_out = params_out; a.pos_out = pos_out;
   const bool shared = (basis_sb == 0);
-  hipStream_t s = beast::as_stream(stream);
-  if (small_batch(B)) return launch_reconstruct<8>(a, D, n_joint, N, shared, s);
-  return launch_reconstruct<16>(a, D, n_joint, N, shared, s);
+  return launch_reconstruct<8>(a, D, n_joint, N, shared, beast::as_stream(stream));
 }

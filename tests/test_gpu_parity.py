@@ -3,7 +3,8 @@
 Contracts:
   * basis, quantiser, dequantiser, quantiles, BPE vocab/merges: bit-exact;
   * params: |gpu - ref| <= 1e-5 * max(1, |ref row|_inf) (the reference's own fp32
-    LU error is ~2e-6 of that scale); vs the float64 oracle fit: <= 2 ulp;
+    LU error is ~2e-6 of that scale); vs the float64 oracle fit: within the fp32
+    fma-chain bound (T + 8) * 2^-24 * sum_t |P[n,t] y[t]|;
   * tokens end-to-end: equal to the reference except where the reference's
     normalised value lies within 1e-3 of a .5 rounding tie (counted);
   * positions: |gpu - ref| <= 1e-5 * max(1, |ref|_inf per trajectory).
@@ -94,8 +95,14 @@ def test_encode_params_and_tokens(name, golden, gpu_device):
     ex = O.fit_exact(x[..., lay.joint_indices], pj)
     if lay.gripper_indices:
         ex = np.concatenate([ex, O.fit_exact(x[..., lay.gripper_indices], pg)], axis=-1)
-    ulp = np.spacing(np.abs(ex).astype(np.float32))
-    assert np.all(np.abs(params - ex) <= 2 * ulp + 1e-30)
+    # fp32 MFMA fit (fp32 P, k-ordered fma chain over T): |err| <= (T + 8) * 2^-24 * sum_t |P y|
+    S = []
+    for idx, ph in ((lay.joint_indices, pj), (lay.gripper_indices, pg)):
+        if idx:
+            P = np.abs(O.projection_f64(ph))                               # [N, T]
+            S.append(np.einsum('nt,btd->bdn', P, np.abs(x[..., idx].astype(np.float64))).reshape(len(x), -1))
+    S = np.concatenate(S, axis=-1)
+    assert np.all(np.abs(params - ex) <= (50 + 8) * 2.0 ** -24 * S + 1e-30)
     # quantiser given identical params: bit-exact
     t = tokens.cpu().numpy()
     want = O.continuous_to_discrete(O._clamp_t(params, g["w_min"], g["w_max"]), g["w_min"], g["w_max"], 256)
@@ -203,7 +210,8 @@ def test_roundtrip_properties(name, golden, gpu_device):
     dec = tok.decode(tokens)
     clamped = torch.clamp(pd["params"], min=tok.w_min, max=tok.w_max)
     binw = (tok.w_max - tok.w_min) / 255
-    assert torch.all((dec - clamped).abs() <= 0.5 * binw * (1 + 1e-5) + 1e-7)
+    slack = 4e-7 * torch.maximum(tok.w_min.abs(), tok.w_max.abs())   # three fp32 roundings in dequantise
+    assert torch.all((dec - clamped).abs() <= 0.5 * binw * (1 + 1e-5) + slack + 1e-7)
     # idempotence: re-encoding the decoded params' quantisation gives the same tokens
     again = tok._quantize(dec, 0, gpu_device, 0)
     assert torch.equal(again, tokens)
