@@ -685,15 +685,13 @@ extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb,
   BEAST_REQUIRE(D >= 1 && D <= MAX_D && n_joint >= 0 && n_joint <= D, "bad DoF split D=%d n_joint=%d", D, n_joint);
   BEAST_REQUIRE(row_elems >= 1, "row_elems must be >= 1");
   BEAST_REQUIRE(!tokens_out || (w_min && w_max && vocab >= 2), "quantisation needs w_min/w_max and vocab >= 2");
-  if (B <= 0) return BEAST_OK;
+  BEAST_REQUIRE(B >= 0, "batch size B=%lld must be >= 0", (long long)B);
+  if (B == 0) return BEAST_OK;
   EncArgs a{};
   a.traj = traj; a.B = B; a.sb = sb; a.st = st; a.sd = sd; a.row_elems = row_elems; a.vocab = vocab;
   a.phases = debug_phases(); a.dof_src = dof_src; a.proj = proj; a.w_min = w_min; a.w_max = w_max;
   a.tok_offset = tok_offset; a.params_out = params_out; a.tokens_out = reinterpret_cast<long long*>(tokens_out);
-  const bool fast16 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems &&
-                       16 * T * row_elems * 4 <= 64 * 1024);
   const bool fast8 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems && 8 * T * row_elems * 4 <= 64 * 1024);
-  (void)fast16;
   return launch_encode<8>(a, T, D, n_joint, N, fast8, beast::as_stream(stream));
 }
 
@@ -712,7 +710,8 @@ extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, in
                              num_dof_out <= 4096),
                 "reconstruct: need basis, dof_dst, 1 <= T_out <= 4096, D <= num_dof_out <= 4096");
   BEAST_REQUIRE(!init_p || init_p_src, "init_p needs init_p_src");
-  if (B <= 0) return BEAST_OK;
+  BEAST_REQUIRE(B >= 0, "batch size B=%lld must be >= 0", (long long)B);
+  if (B == 0) return BEAST_OK;
   RecArgs a{};
   a.tokens = reinterpret_cast<const long long*>(tokens); a.ntokens = ntokens; a.B = B; a.tok_offset = tok_offset;
   a.basis_sb = basis_sb; a.init_p_sb = init_p_sb; a.vocab = vocab; a.Tout = pos_out ? T_out : 1;

@@ -199,7 +199,8 @@ extern "C" int beast_quantize_f32(const float* params, int64_t B, int D, int N, 
                                   float* ntok_out, void* stream) {
   BEAST_REQUIRE(params && w_min && w_max, "beast_quantize_f32: null input pointer");
   BEAST_REQUIRE((mode == 0 && tokens_out && vocab >= 2) || (mode == 1 && ntok_out), "beast_quantize_f32: bad mode");
-  if (B <= 0) return BEAST_OK;
+  BEAST_REQUIRE(B >= 0, "batch size B=%lld must be >= 0", (long long)B);
+  if (B == 0) return BEAST_OK;
   const int64_t total = B * (int64_t)N * D;
   const int64_t grid = std::min<int64_t>((total + 255) / 256, 4096);
   hipLaunchKernelGGL(k_quantize, dim3(grid), dim3(256), 0, beast::as_stream(stream), params, B, D, N, w_min, w_max,

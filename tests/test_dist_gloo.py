@@ -51,7 +51,7 @@ def _worker(rank, world, port, case, q):
             x[::3, 2] = 0.25
             shard = x[rank * 600: (rank + 1) * 600] if rank == 0 else x[600:]
             out = column_quantiles(torch.from_numpy(shard), [0.01, 0.99], red, ops=NumpyQuantileOps())
-            q.put((rank, out.numpy(), np.quantile(x, [0.01, 0.99], axis=0).astype(np.float32)))
+            q.put((rank, out.numpy(), np.stack([np.quantile(x, q, axis=0) for q in (0.01, 0.99)])))
     finally:
         dist.destroy_process_group()
 

@@ -1,0 +1,112 @@
+"""The C-ABI library loads on a GPU-less host and exports exactly include/beast_hip.h.
+
+No compute entry point is executed here; only argument validation (which runs
+before any HIP call) and the pure size queries are exercised.
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from beast_tokenizer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "beast_hip.h")
+
+
+def header_decls():
+    """name -> parameter count, parsed from the prototypes in include/beast_hip.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"//[^\n]*", "", txt)
+    out = {}
+    for m in re.finditer(r"\b(beast_\w+)\s*\(([^;{]*?)\)\s*;", txt, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_header_parses():
+    d = header_decls()
+    assert len(d) >= 25 and "beast_encode_f32" in d and "beast_bpe_merge" in d
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    so = lib._name
+    nm = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in nm.splitlines() if " T " in ln}
+    decl = header_decls()
+    missing = set(decl) - exported
+    assert not missing, missing
+    # no undeclared beast_* entry points leak out of the library
+    assert {s for s in exported if s.startswith("beast_")} == set(decl)
+
+
+def test_ctypes_signatures_match_header():
+    decl = header_decls()
+    assert set(_lib.SIGNATURES) == set(decl)
+    for name, n in decl.items():
+        assert len(_lib.SIGNATURES[name][1]) == n, name
+
+
+def test_abi_version():
+    assert _lib.load().beast_abi_version() == _lib.ABI_VERSION
+
+
+@pytest.mark.parametrize("name,args", [
+    ("beast_quantize_f32", (None, 4, 14, 10, None, None, 256, 0, 0, None, None, None)),
+    ("beast_encode_f32", (None, 4, 50, 700, 14, 1, 14, 14, 14, None, None, 10, None, None, 256, 0, None, None,
+                          None)),
+    ("beast_reconstruct_f32", (None, 4, 14, 14, 10, 256, 0, None, None, None, 0, 50, None, 14, None, 0, None,
+                               None, None, None, None)),
+    ("beast_bpe_argmax", (None, 300, 300, None, None)),
+])
+def test_null_pointers_are_rejected_before_any_hip_call(name, args):
+    rc = getattr(_lib.load(), name)(*args)
+    assert rc == _lib.BEAST_E_INVALID
+    assert name.encode() in _lib.load().beast_last_error()
+    with pytest.raises(ValueError):
+        _lib.check(rc, name)
+
+
+def test_shape_validation():
+    lib = _lib.load()
+    fake = C.c_void_p(16)                   # never dereferenced: validation fails first
+    # N > 16 (the MFMA tile) is reported as unsupported
+    rc = lib.beast_encode_f32(fake, 4, 50, 700, 14, 1, 14, 14, 14, None, fake, 17, fake, fake, 256, 0, fake, fake,
+                              None)
+    assert rc in (_lib.BEAST_E_INVALID, _lib.BEAST_E_UNSUPPORTED)
+    rc = lib.beast_quantize_f32(fake, -1, 14, 10, fake, fake, 256, 0, 0, fake, None, None)
+    assert rc == _lib.BEAST_E_INVALID
+
+
+def test_workspace_queries_are_pure():
+    lib = _lib.load()
+    assert lib.beast_quantile_hist_count(14, 2) == 14 * 2 * 2048 * 2
+    assert lib.beast_quantile_workspace_bytes(1000, 14, 2) > 1000 * 14 * 4
+    assert lib.beast_scan_workspace_bytes(1 << 20) > 0
+    assert lib.beast_colminmax_workspace_bytes(10 ** 6, 14) > 0
+
+
+def test_product_refuses_cpu_tensors():
+    """There is no CPU fallback: host tensors are refused loudly."""
+    from beast_tokenizer_amd import BEASTBsplineTokenizer
+    tok = BEASTBsplineTokenizer(num_dof=7, num_basis=10, seq_len=50, device="cpu")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        tok.encode(torch.zeros(2, 50, 7))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.require_gpu(torch.zeros(3), "x")
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    saved = _lib._lib
+    try:
+        _lib._lib = None
+        with pytest.raises(RuntimeError, match="no CPU fallback"):
+            _lib.load(str(tmp_path / "nope.so"))
+    finally:
+        _lib._lib = saved
