@@ -113,8 +113,14 @@ def ptr(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+def raw_stream(index: int) -> int:
+    """hipStream_t of the current stream of device ``index`` (cheap: no Stream object)."""
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
 def stream_of(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 def require_gpu(t: torch.Tensor, what: str = "tensor") -> None:

@@ -62,6 +62,36 @@ class _MPInfo:
                 f"tau={self.tau:.6g})")
 
 
+class _Plan:
+    """Launch state of the hot path on one device: the cached constants (basis Phi,
+    fp32 projection P, DoF maps) and the bound tensors, kept as raw pointers so a
+    call costs two allocations and one C call.  Rebuilt when the time grid or the
+    bound tensors change (in-place updates of ``w_min`` / ``w_max`` keep it valid)."""
+
+    __slots__ = ("dev", "idx", "version", "wmin", "wmax", "keep", "T", "min_din",
+                 "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec")
+
+    def __init__(self, tok: "BEASTBsplineTokenizer", dev: torch.device):
+        lib = _lib.load()
+        phi, _, proj32 = tok._constants(dev)
+        src, dst = tok._dof_maps(dev)
+        wmn, wmx = tok._bounds(dev)
+        self.dev, self.idx, self.version = dev, dev.index, tok._times_version
+        self.wmin, self.wmax = tok.w_min, tok.w_max
+        self.keep = (phi, proj32, src, dst, wmn, wmx)          # owns every pointer below
+        self.T = phi.shape[1]
+        order = tok.joint_indices + tok.gripper_indices
+        self.min_din = (max(order) + 1) if order else 0
+        self.p_phi, self.p_proj = phi.data_ptr(), proj32.data_ptr()
+        self.p_src, self.p_dst = src.data_ptr(), dst.data_ptr()
+        self.p_wmn, self.p_wmx = wmn.data_ptr(), wmx.data_ptr()
+        self.enc, self.rec = lib.beast_encode_f32, lib.beast_reconstruct_f32
+
+    def cacheable(self) -> bool:
+        # bounds living elsewhere were copied to the device: do not reuse the copy
+        return self.keep[4] is self.wmin and self.keep[5] is self.wmax
+
+
 class BEASTBsplineTokenizer(TokenizerBase):
 
     def __init__(self, num_dof=1, num_basis=10, duration=2 * torch.pi, seq_len=50, vocab_size=256,
@@ -124,6 +154,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
         self.register_buffer("w_max", 0.02 * torch.ones((num_dof * num_basis), device=buf_dev))
         self.llm_vocab_size = None
         self._dof_cache = {}
+        self._plans = {}
+        self._dev_of = {}
 
         self._config = {
             'tokenizer_type': 'beast_bspline',
@@ -159,15 +191,30 @@ class BEASTBsplineTokenizer(TokenizerBase):
         self._times_version = getattr(self, "_times_version", 0) + 1
 
     def _dev(self) -> torch.device:
-        dev = torch.device(self.device)
-        if dev.type != "cuda":
-            raise RuntimeError(
-                f"BEASTBsplineTokenizer(device={self.device!r}): the BEAST hot path runs only on a ROCm GPU "
-                "(MI355X, gfx950); there is no CPU fallback")
+        dev = self._dev_of.get(self.device)
+        if dev is None:
+            dev = torch.device(self.device)
+            if dev.type != "cuda":
+                raise RuntimeError(
+                    f"BEASTBsplineTokenizer(device={self.device!r}): the BEAST hot path runs only on a ROCm GPU "
+                    "(MI355X, gfx950); there is no CPU fallback")
+            _lib.load()
+            self._dev_of[self.device] = dev
         if dev.index is None:
-            dev = torch.device("cuda", torch.cuda.current_device())
-        _lib.load()
+            idx = torch.cuda.current_device()
+            dev = self._dev_of.get(idx)
+            if dev is None:
+                dev = self._dev_of[idx] = torch.device("cuda", idx)
         return dev
+
+    def _plan(self) -> _Plan:
+        dev = self._dev()
+        p = self._plans.get(dev.index)
+        if p is None or p.version != self._times_version or p.wmin is not self.w_min or p.wmax is not self.w_max:
+            p = _Plan(self, dev)
+            if p.cacheable():
+                self._plans[dev.index] = p
+        return p
 
     def _constants(self, dev: torch.device):
         t = self.times.to(dev, dtype=torch.float32).reshape(-1)
@@ -190,31 +237,33 @@ class BEASTBsplineTokenizer(TokenizerBase):
             return self._llm_vocab_offset()
         return 0
 
-    def _fit(self, trajs: torch.Tensor, tokens_offset: Optional[int], dev: torch.device):
+    def _fit(self, trajs: torch.Tensor, tokens_offset: Optional[int], p: _Plan):
         """Launch the fused fit (+ quantise) kernel. Returns (params, tokens or None)."""
-        if trajs.dim() != 3 or trajs.shape[1] != self.times.numel():
+        if trajs.device != p.dev or trajs.dtype is not torch.float32:
+            trajs = trajs.to(p.dev, dtype=torch.float32)
+        shape = trajs.shape
+        if len(shape) != 3 or shape[1] != p.T:
             # learn_mp_params_from_trajs asserts trajs.shape[:-1] == times.shape (uni_bspline.py:487)
-            raise AssertionError(f"trajectory shape {tuple(trajs.shape)} does not match [B, {self.times.numel()}, "
-                                 f"num_dof] time grid")
-        B, T, Din = trajs.shape
-        if Din < self.num_dof and (self.joint_indices + self.gripper_indices):
-            top = max(self.joint_indices + self.gripper_indices)
-            if top >= Din:
-                raise IndexError(f"index {top} is out of bounds for dimension 2 with size {Din}")
-        if trajs.stride(2) != 1 and trajs.numel():
+            raise AssertionError(f"trajectory shape {tuple(shape)} does not match [B, {p.T}, num_dof] time grid")
+        B, T, Din = shape
+        if Din < p.min_din:
+            raise IndexError(f"index {p.min_din - 1} is out of bounds for dimension 2 with size {Din}")
+        st = trajs.stride()
+        if st[2] != 1 and B * T * Din:
             trajs = trajs.contiguous()
-        _, proj = self._constants(dev)
-        src, _ = self._dof_maps(dev)
-        D, N = self.num_dof, self.num_basis
-        params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
-        tokens = None
-        wmn = wmx = None
-        if tokens_offset is not None:
-            tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
-            wmn, wmx = self._bounds(dev)
-        _lib.run("beast_encode_f32", trajs.data_ptr(), B, T, trajs.stride(0), trajs.stride(1), trajs.stride(2),
-                 Din, D, self.joint_dof, src.data_ptr(), proj.data_ptr(), N, _lib.ptr(wmn), _lib.ptr(wmx),
-                 self.vocab_size, tokens_offset or 0, params.data_ptr(), _lib.ptr(tokens), _lib.stream_of(dev))
+            st = trajs.stride()
+        DN = self.num_dof * self.num_basis
+        params = torch.empty((B, DN), dtype=torch.float32, device=p.dev)
+        if tokens_offset is None:
+            tokens, p_tok, p_wmn, p_wmx = None, None, None, None
+        else:
+            tokens = torch.empty((B, DN), dtype=torch.int64, device=p.dev)
+            p_tok, p_wmn, p_wmx = tokens.data_ptr(), p.p_wmn, p.p_wmx
+        rc = p.enc(trajs.data_ptr(), B, T, st[0], st[1], st[2], Din, self.num_dof, self.joint_dof, p.p_src,
+                   p.p_proj, self.num_basis, p_wmn, p_wmx, self.vocab_size, tokens_offset or 0, params.data_ptr(),
+                   p_tok, _lib.raw_stream(p.idx))
+        if rc:
+            _lib.check(rc, "beast_encode_f32")
         return params, tokens
 
     # ===============================================
@@ -360,9 +409,7 @@ class BEASTBsplineTokenizer(TokenizerBase):
     @torch.no_grad()
     def compute_weights(self, demos):
         """Fitted params [B, num_dof*num_basis] in (d n) order (reference :344-360)."""
-        dev = self._dev()
-        demos = demos.to(dev, dtype=torch.float32)
-        params, _ = self._fit(demos, None, dev)
+        params, _ = self._fit(demos, None, self._plan())
         return params
 
     @torch.no_grad()
@@ -394,20 +441,22 @@ class BEASTBsplineTokenizer(TokenizerBase):
     #           - tokenizer encoding -
     # ===============================================
 
-    @torch.no_grad()
     def encode(self, trajs, update_bounds=False, *, respect_llm_vocab_size=True):
-        """(tokens int64 [B, num_basis*num_dof], params_dict) -- reference :399-428."""
-        dev = self._dev()
-        trajs = trajs.to(dev, dtype=torch.float32)
-        offset = self._offset(respect_llm_vocab_size)
+        """(tokens int64 [B, num_basis*num_dof], params_dict) -- reference :399-428.
+
+        No autograd graph is recorded: the outputs are written by the kernel into fresh
+        tensors (the reference runs under ``torch.no_grad`` equivalently)."""
+        p = self._plan()
+        offset = (self.llm_vocab_size - self.vocab_size
+                  if respect_llm_vocab_size and self.llm_vocab_size is not None else 0)
         if update_bounds:
-            params, _ = self._fit(trajs, None, dev)
-            self.update_weights_bounds_per_batch(params)
-            tokens = self._quantize(params, offset, dev, mode=0)
+            with torch.no_grad():
+                params, _ = self._fit(trajs, None, p)
+                self.update_weights_bounds_per_batch(params)
+                tokens = self._quantize(params, offset, p.dev, mode=0)
         else:
-            params, tokens = self._fit(trajs, offset, dev)
-        params_dict = {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
-        return tokens, params_dict
+            params, tokens = self._fit(trajs, offset, p)
+        return tokens, {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
 
     def _quantize(self, params: torch.Tensor, offset: int, dev: torch.device, mode: int):
         B = params.shape[0]
@@ -427,12 +476,11 @@ class BEASTBsplineTokenizer(TokenizerBase):
     @torch.no_grad()
     def encode_continuous(self, trajs, update_bounds=False):
         """Normalised params in [-1, 1], (t d) order (reference :430-450)."""
-        dev = self._dev()
-        trajs = trajs.to(dev, dtype=torch.float32)
-        params, _ = self._fit(trajs, None, dev)
+        p = self._plan()
+        params, _ = self._fit(trajs, None, p)
         if update_bounds:
             self.update_weights_bounds_per_batch(params)
-        tokens = self._quantize(params, 0, dev, mode=1)
+        tokens = self._quantize(params, 0, p.dev, mode=1)
         params_dict = {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
         return tokens, params_dict
 
@@ -466,38 +514,38 @@ class BEASTBsplineTokenizer(TokenizerBase):
         return self.reconstruct_traj(tokens, times=times, **kwargs)
 
     def _token_rows(self, tokens, dev):
-        tokens = tokens.to(dev)
-        if tokens.dim() == 3:
+        if tokens.device != dev:
+            tokens = tokens.to(dev)
+        nd = tokens.dim()
+        if nd == 3:
             tokens = tokens.reshape(tokens.shape[0], -1)
-        elif tokens.dim() != 2:
+        elif nd != 2:
             raise ValueError(f"Unexpected token shape {tokens.shape}")
         if tokens.shape[1] != self.num_basis * self.num_dof:
             raise ValueError(f"Token dimension {tokens.shape[1]} does not match expected "
                              f"{self.num_basis * self.num_dof}.")
-        if tokens.dtype != torch.int64:
+        if tokens.dtype is not torch.int64:
             tokens = tokens.to(torch.int64)
-        return tokens.contiguous()
+        return tokens if tokens.is_contiguous() else tokens.contiguous()
 
-    @torch.no_grad()
     def decode(self, tokens, *, respect_llm_vocab_size=True):
         """Dequantised params [B, num_dof*num_basis] in (d n) order (reference :483-496)."""
-        dev = self._dev()
-        tokens = self._token_rows(tokens, dev)
+        p = self._plan()
+        tokens = self._token_rows(tokens, p.dev)
         B = tokens.shape[0]
-        D, N = self.num_dof, self.num_basis
-        wmn, wmx = self._bounds(dev)
-        params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
-        _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, self.joint_dof, N, self.vocab_size,
-                 self._offset(respect_llm_vocab_size), wmn.data_ptr(), wmx.data_ptr(), None, 0, 0, None, D, None,
-                 0, None, params.data_ptr(), None, None, _lib.stream_of(dev))
+        params = torch.empty((B, self.num_dof * self.num_basis), dtype=torch.float32, device=p.dev)
+        rc = p.rec(tokens.data_ptr(), B, self.num_dof, self.joint_dof, self.num_basis, self.vocab_size,
+                   self._offset(respect_llm_vocab_size), p.p_wmn, p.p_wmx, None, 0, 0, None, self.num_dof, None,
+                   0, None, params.data_ptr(), None, None, _lib.raw_stream(p.idx))
+        if rc:
+            _lib.check(rc, "beast_reconstruct_f32")
         return params
 
-    def _basis_for(self, times, B: int, dev: torch.device):
-        """(basis ptr tensor, batch stride, T_out) for reconstruct; default grid is cached."""
-        N = self.num_basis
+    def _basis_for(self, times, B: int, p: _Plan):
+        """(basis tensor or None, basis ptr, batch stride, T_out) for reconstruct; the default grid is cached."""
         if times is None:
-            phi, _ = self._constants(dev)
-            return phi, 0, phi.shape[1]
+            return None, p.p_phi, 0, p.T
+        N, dev = self.num_basis, p.dev
         t = times.to(dev, dtype=torch.float32)
         if t.dim() == 2 and t.shape[0] == B and (B == 1 or torch.equal(t, t[:1].expand_as(t))):
             t = t[0]
@@ -505,50 +553,49 @@ class BEASTBsplineTokenizer(TokenizerBase):
             Tn = t.numel()
             phi = torch.zeros((2, Tn, N), dtype=torch.float32, device=dev)
             phi[: self._basis.n_kinds] = self._basis.basis_at(t)
-            return phi, 0, Tn
+            return phi, phi.data_ptr(), 0, Tn
         if t.dim() != 2 or t.shape[0] != B:
             raise ValueError(f"times must be [T] or [B, T]; got {tuple(t.shape)} for B={B}")
         Tn = t.shape[1]
         phi_k = self._basis.basis_at(t)                       # [kinds, B, T, N]
         phi = torch.zeros((B, 2, Tn, N), dtype=torch.float32, device=dev)
         phi[:, : self._basis.n_kinds] = phi_k.permute(1, 0, 2, 3)
-        return phi, 2 * Tn * N, Tn
+        return phi, phi.data_ptr(), 2 * Tn * N, Tn
 
-    def _reconstruct(self, tokens, ntokens, times, init_p, respect_llm_vocab_size, dev):
+    def _reconstruct(self, tokens, ntokens, times, init_p, respect_llm_vocab_size, p: _Plan):
         src = tokens if tokens is not None else ntokens
         B = src.shape[0]
-        D, N = self.num_dof, self.num_basis
-        wmn, wmx = self._bounds(dev)
-        phi, basis_sb, Tn = self._basis_for(times, B, dev)
-        _, dst = self._dof_maps(dev)
-        pos = torch.empty((B, Tn, D), dtype=torch.float32, device=dev)
-        ip = ip_src = None
-        if self.init_pos and init_p is not None and self.joint_dof > 0:
-            ip = torch.as_tensor(init_p).to(dev, dtype=torch.float32)
+        D = self.num_dof
+        phi, p_phi, basis_sb, Tn = self._basis_for(times, B, p)
+        pos = torch.empty((B, Tn, D), dtype=torch.float32, device=p.dev)
+        ip, ip_sb, ip_src = None, 0, None
+        if init_p is not None and self.init_pos and self.joint_dof > 0:
+            ip = torch.as_tensor(init_p).to(p.dev, dtype=torch.float32)
             if ip.dim() != 2 or ip.shape[0] != B:
                 raise ValueError(f"init_p must be [B, num_dof]; got {tuple(ip.shape)}")
             if ip.stride(1) != 1:
                 ip = ip.contiguous()
-            ip_src = dst[: self.joint_dof]
+            ip_sb, ip_src = ip.stride(0), p.p_dst      # joint DoFs come first in the dof map
         offset = self._offset(respect_llm_vocab_size) if tokens is not None else 0
-        _lib.run("beast_reconstruct_f32", _lib.ptr(tokens), B, D, self.joint_dof, N, self.vocab_size, offset,
-                 wmn.data_ptr(), wmx.data_ptr(), phi.data_ptr(), basis_sb, Tn, dst.data_ptr(), D, _lib.ptr(ip),
-                 ip.stride(0) if ip is not None else 0, _lib.ptr(ip_src), None, pos.data_ptr(), _lib.ptr(ntokens),
-                 _lib.stream_of(dev))
+        rc = p.rec(None if tokens is None else tokens.data_ptr(), B, D, self.joint_dof, self.num_basis,
+                   self.vocab_size, offset, p.p_wmn, p.p_wmx, p_phi, basis_sb, Tn, p.p_dst, D,
+                   None if ip is None else ip.data_ptr(), ip_sb, ip_src, None, pos.data_ptr(),
+                   None if ntokens is None else ntokens.data_ptr(), _lib.raw_stream(p.idx))
+        if rc:
+            _lib.check(rc, "beast_reconstruct_f32")
         return pos
 
-    @torch.no_grad()
     def reconstruct_traj(self, tokens, times=None, **kwargs):
         """Positions [B, T, num_dof] from tokens (reference :498-536); kwargs: init_p [B, num_dof]."""
-        dev = self._dev()
-        tokens = self._token_rows(tokens, dev)
-        return self._reconstruct(tokens, None, times, kwargs.get("init_p"), True, dev)
+        p = self._plan()
+        tokens = self._token_rows(tokens, p.dev)
+        return self._reconstruct(tokens, None, times, kwargs.get("init_p"), True, p)
 
     @torch.no_grad()
     def reconstruct_traj_continuous(self, params, times=None, **kwargs):
         """Positions from normalised params in (t d) order (reference :538-582)."""
-        dev = self._dev()
-        params = params.to(dev)
+        p = self._plan()
+        params = params.to(p.dev)
         if len(params.shape) == 3:
             params = params.reshape(params.shape[0], -1)
         if params.shape[-1] != self.num_basis * self.num_dof:
@@ -556,7 +603,7 @@ class BEASTBsplineTokenizer(TokenizerBase):
                 f"Token dimension {params.shape[-1]} does not match expected {self.num_basis * self.num_dof}."
             )
         params = params.to(torch.float32).contiguous()
-        return self._reconstruct(None, params, times, kwargs.get("init_p"), False, dev)
+        return self._reconstruct(None, params, times, kwargs.get("init_p"), False, p)
 
     # ===============================================
     #           - tokenizer evaluation -

@@ -2,7 +2,7 @@
 
 The reference rebuilds the basis for every call (uni_bspline.py:539, :160); here
 the basis Phi [2][T][N] (kind 0 = joint degree p, kind 1 = gripper degree 0) and
-the ridge projection P [2][N][T] (float64) are evaluated ON THE GPU by
+the ridge projection P [2][16][Tp] (float64, and its fp32 image for the kernel) are evaluated ON THE GPU by
 ``beast_bspline_basis_f32`` / ``beast_bspline_projection_f64`` once per time grid
 and cached; the per-batch kernels only read them.
 
@@ -62,8 +62,9 @@ class DeviceBasis:
                      kv.numel(), self.degrees[k], self.num_basis, out[k].data_ptr(), s)
         return out
 
-    def constants(self, times: torch.Tensor, version: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-        """(Phi [2][T][N] fp32, P [2][16][Tp] fp64 zero-padded) for a 1-D grid, cached per (device, version, T)."""
+    def constants(self, times: torch.Tensor, version: int = 0) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(Phi [2][T][N] fp32, P [2][16][Tp] fp64 zero-padded, P in fp32) for a 1-D grid,
+        cached per (device, version, T).  The encode kernel reads the fp32 image of P."""
         key = (times.device, version, times.numel())
         hit = self._cache.get(key)
         if hit is not None:
@@ -76,8 +77,9 @@ class DeviceBasis:
         s = _lib.stream_of(times.device)
         for k in range(self.n_kinds):
             _lib.run("beast_bspline_projection_f64", phi[k].data_ptr(), T, N, self.reg, proj[k].data_ptr(), s)
-        self._cache[key] = (phi, proj)
-        return phi, proj
+        hit = (phi, proj, proj.to(torch.float32))
+        self._cache[key] = hit
+        return hit
 
     def clear(self, device: Optional[torch.device] = None) -> None:
         self._cache = {k: v for k, v in self._cache.items() if device is not None and k[0] != device}

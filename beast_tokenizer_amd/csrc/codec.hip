@@ -56,11 +56,10 @@ __device__ __forceinline__ void burst16(uint4* __restrict__ dst, const uint4* __
     uint4 r[MAXK];
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) r[k] = src[min(base + k * NTHREADS + (int)threadIdx.x, n16 - 1)];
+    // unconditional stores: a lane past the end rewrites element n16-1 with its own value,
+    // so the compiler cannot sink the loads into per-element branches (one round trip)
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
-      const int i = base + k * NTHREADS + (int)threadIdx.x;
-      if (i < n16) dst[i] = r[k];
-    }
+    for (int k = 0; k < MAXK; ++k) dst[min(base + k * NTHREADS + (int)threadIdx.x, n16 - 1)] = r[k];
   }
 }
 
@@ -71,10 +70,7 @@ __device__ __forceinline__ void burst4(uint32_t* __restrict__ dst, const uint32_
 #pragma unroll
     for (int k = 0; k < MAXK; ++k) r[k] = src[min(base + k * NTHREADS + (int)threadIdx.x, n - 1)];
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k) {
-      const int i = base + k * NTHREADS + (int)threadIdx.x;
-      if (i < n) dst[i] = r[k];
-    }
+    for (int k = 0; k < MAXK; ++k) dst[min(base + k * NTHREADS + (int)threadIdx.x, n - 1)] = r[k];
   }
 }
 
@@ -104,6 +100,30 @@ __device__ __forceinline__ void store_out(float* __restrict__ dst, const float* 
     for (int i = (n4 << 2) + threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
   } else {
     for (int i = threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
+  }
+}
+
+// LDS-DMA (global_load_lds): HBM -> LDS with no VGPR round trip, so every load of a stage
+// is in flight at once and one vmcnt wait (the next __syncthreads) retires them all.  A
+// wave-instruction writes 64 consecutive slots from a wave-uniform base: destinations are
+// padded to whole wave-instructions, sources past the end are clamped to the last element.
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(void* lds, const void* g, int n16) {
+  const int tid = threadIdx.x, wb = tid & ~63;
+  for (int base = 0; base < n16; base += NTHREADS) {
+    if (base + wb < n16)
+      __builtin_amdgcn_global_load_lds(static_cast<const uint4*>(g) + min(base + tid, n16 - 1),
+                                       (lds_void*)(static_cast<uint4*>(lds) + base + wb), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void dma4(void* lds, const void* g, int n) {
+  const int tid = threadIdx.x, wb = tid & ~63;
+  for (int base = 0; base < n; base += NTHREADS) {
+    if (base + wb < n)
+      __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(g) + min(base + tid, n - 1),
+                                       (lds_void*)(static_cast<uint32_t*>(lds) + base + wb), 4, 0, 0);
   }
 }
 
@@ -149,7 +169,7 @@ struct EncArgs {
   int64_t B, sb, st, sd, ntiles;
   int row_elems, vocab, phases;
   const int32_t* dof_src;
-  const double* proj;  // [2][16][Tp]
+  const float* proj;   // [kinds][16][Tp] fp32 rounding of the fp64 ridge projection
   const float* w_min;
   const float* w_max;
   int64_t tok_offset;
@@ -159,21 +179,21 @@ struct EncArgs {
 };
 
 struct EncSmem {
-  int P, Y, pb, wlo, whi, wsc, kmap, lcol, total;
+  int P, Y, pb, wlo, whi, kmap, lcol, total;
 };
 
+// Every buffer an LDS-DMA fills is padded to whole wave-instructions (64 lanes x 16 B).
 template <int TBT>
 __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N, int nkinds) {
   EncSmem s;
   int o = 0;
-  s.P = o;    o += round_up(nkinds * 16 * Tp * 4, 16);  // fp32 copy of the [16][Tp] projection
-  s.Y = o;    o += round_up(TBT * T * Dl * 4, 16);
+  s.P = o;    o += round_up(nkinds * 16 * Tp * 4, 1024);   // fp32 [16][Tp] projection per kind
+  s.Y = o;    o += round_up(TBT * T * Dl * 4, 1024);
   s.pb = o;   o += round_up(TBT * D * N * 4, 16);
-  s.wlo = o;  o += round_up(D * N * 4, 16);
-  s.whi = o;  o += round_up(D * N * 4, 16);
-  s.wsc = o;  o += round_up(D * N * 4, 16);
+  s.wlo = o;  o += round_up(D * N * 4, 256);
+  s.whi = o;  o += round_up(D * N * 4, 256);
   s.kmap = o; o += round_up(D * N * 2, 16);
-  s.lcol = o; o += round_up(D * 4, 16);
+  s.lcol = o; o += round_up(D * 4, 256);
   s.total = o;
   return s;
 }
@@ -191,51 +211,27 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
-  float* wsc = reinterpret_cast<float*>(smem + L.wsc);
   uint16_t* kmap = reinterpret_cast<uint16_t*>(smem + L.kmap);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x;
   const bool quant = a.tokens_out != nullptr;
+  const int tile_elems = T * a.row_elems;   // FAST: one trajectory, contiguous, % 4 == 0
 
-  // ---- constants, once per workgroup: one round trip for all of them
-  {
-    float lo[4], hi[4];
-    int lc = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = min(tid + i * NTHREADS, DN - 1);
-      lo[i] = quant ? a.w_min[k] : 0.0f;
-      hi[i] = quant ? a.w_max[k] : 0.0f;
-    }
-    if (tid < D) lc = a.dof_src[tid];
-    {   // f64 projection -> fp32 LDS copy (all loads issued before the stores)
-      const int tot = nkinds * 16 * Tp;
-      for (int base = 0; base < tot; base += 8 * NTHREADS) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = a.proj[min(base + u * NTHREADS + tid, tot - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = base + u * NTHREADS + tid;
-          if (i < tot) P[i] = (float)v[u];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = tid + i * NTHREADS;
-      if (k < DN) {
-        wlo[k] = lo[i];
-        whi[k] = hi[i];
-        const float s = __fsub_rn(hi[i], lo[i]);
-        wsc[k] = (s < 1e-8f) ? 1e-8f : s;   // torch.clamp(max - min, min=1e-8), NaN kept
-      }
-    }
-    if (tid < D) lcol[tid] = FAST ? min(max(lc, 0), a.row_elems - 1) : tid;
-    for (int r = tid; r < per; r += NTHREADS) {   // (n d) slot -> (d n) index
-      const int n = r / D, d = r - n * D;
-      kmap[r] = (uint16_t)(d * N + n);
-    }
+  // ---- prologue: the first tile and every constant go HBM -> LDS by DMA in one round trip
+  if (FAST && (a.phases & 1) && blockIdx.x < a.ntiles) {
+    const int64_t b0 = (int64_t)blockIdx.x * TBT;
+    const int nb = (int)min<int64_t>(TBT, a.B - b0);
+    dma16(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
+  }
+  dma16(P, a.proj, nkinds * 4 * Tp);
+  if (quant) {
+    dma4(wlo, a.w_min, DN);
+    dma4(whi, a.w_max, DN);
+  }
+  dma4(lcol, a.dof_src, D);
+  for (int r = tid; r < per; r += NTHREADS) {   // (n d) slot -> (d n) index
+    const int n = r / D, d = r - n * D;
+    kmap[r] = (uint16_t)(d * N + n);
   }
 
   const int wave = tid >> 6, lane = tid & 63;
@@ -246,10 +242,10 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
     const int64_t b0 = tile * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
 
-    // ---- stage the trajectory tile (HBM -> LDS)
+    // ---- the trajectory tile lands in LDS (the first one is already in flight)
     if (a.phases & 1) {
       if (FAST) {
-        burst<(TBT * 4 * 50 * 14 + 4095) / 4096>(Y, a.traj + b0 * a.sb, nb * T * a.row_elems * 4);
+        if (tile != blockIdx.x) dma16(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
       } else {
         const int pt = T * D;
         for (int e = tid; e < nb * pt; e += NTHREADS) {
@@ -260,7 +256,7 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
         }
       }
     }
-    __syncthreads();
+    __syncthreads();   // waits for the DMA (vmcnt) and the LDS stores
 
     // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f32 MFMA 16x16x4; A = P, B = y).
     //      A wave owns two column tiles per pass (two independent chains), operands
@@ -272,10 +268,12 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
       tile_col<TBT>(g, min(q0 + NWAVES, g.nq - 1), lr, j1, d1, k1, ok1);
       ok0 = ok0 && j0 < nb;
       ok1 = ok1 && j1 < nb && (q0 + NWAVES < g.nq);
+      const int c0 = FAST ? min(max(lcol[d0], 0), Dl - 1) : d0;
+      const int c1 = FAST ? min(max(lcol[d1], 0), Dl - 1) : d1;
       const float* pa0 = P + (k0 * 16 + lr) * Tp + lk;
       const float* pa1 = P + (k1 * 16 + lr) * Tp + lk;
-      const float* yc0 = Y + j0 * T * Dl + lcol[d0];
-      const float* yc1 = Y + j1 * T * Dl + lcol[d1];
+      const float* yc0 = Y + j0 * T * Dl + c0;
+      const float* yc1 = Y + j1 * T * Dl + c1;
       const float* yb0 = yc0 + lk * Dl;
       const float* yb1 = yc1 + lk * Dl;
       float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -317,7 +315,10 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
           const uint32_t e = min(2 * e2 + h, total - 1);
           const uint32_t j = fdiv(e, g.fd_per);
           const int k = kmap[e - j * per];
-          v[h] = beast::quantize_scaled(pb[j * DN + k], wlo[k], whi[k], wsc[k], vm1) + a.tok_offset;
+          const float lo = wlo[k], hi = whi[k];
+          float sc = __fsub_rn(hi, lo);
+          sc = (sc < 1e-8f) ? 1e-8f : sc;   // torch.clamp(max - min, min=1e-8), NaN kept
+          v[h] = beast::quantize_scaled(pb[j * DN + k], lo, hi, sc, vm1) + a.tok_offset;
         }
         if (vec && 2 * e2 + 1 < total) {
           *reinterpret_cast<longlong2*>(tout + 2 * e2) = make_longlong2(v[0], v[1]);
@@ -335,7 +336,7 @@ struct RecArgs {
   const long long* tokens;
   const float* ntokens;
   int64_t B, ntiles, tok_offset, basis_sb, init_p_sb;
-  int vocab, Tout, ndo, phases, lut_n;
+  int vocab, Tout, ndo, phases, lut_n, tbt;
   const float* w_min;
   const float* w_max;
   const float* basis;      // [2][Tout][N] (shared) or per trajectory with stride basis_sb
@@ -351,10 +352,20 @@ struct RecArgs {
 constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divided once
 
 struct RecSmem {
-  int phi, pb, tok, wlo, whi, wrg, lut, pmap, kq, kpb, dst, col2d, out, total;
+  int phi, pb, tok, wlo, whi, lut, pmap, kq, kpb, dst, col2d, out, total;
   int Np4, RTR;   // padded basis width, padded output rows
   bool stage;
 };
+
+// token tile [nb][per] (int64, or fp32 normalised tokens) HBM -> LDS by DMA
+__device__ __forceinline__ void stage_tokens(const RecArgs& a, void* lds, int64_t b0, int per) {
+  const int nb = (int)min<int64_t>(a.B - b0, 1 << 30);
+  const void* src = a.ntokens ? static_cast<const void*>(a.ntokens + b0 * per)
+                              : static_cast<const void*>(a.tokens + b0 * per);
+  const int bytes = min(nb, a.tbt) * per * (a.ntokens ? 4 : 8);
+  if ((bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) dma16(lds, src, bytes >> 4);
+  else dma4(lds, src, bytes >> 2);
+}
 
 // KS > 0: shared basis on MFMA (K-steps of 4 basis functions); KS == 0: per-row basis on VALU
 template <int TBT, int KS>
@@ -366,15 +377,14 @@ __host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, int
   int o = 0;
   s.phi = o;   o += KS ? round_up(nkinds * s.RTR * s.Np4 * 4, 16) : 0;
   s.pb = o;    o += round_up(TBT * D * s.Np4 * 4, 16);
-  s.tok = o;   o += round_up(TBT * per * 8, 16);
-  s.wlo = o;   o += round_up(per * 4, 16);
-  s.whi = o;   o += round_up(per * 4, 16);
-  s.wrg = o;   o += round_up(per * 4, 16);
+  s.tok = o;   o += round_up(TBT * per * 8, 1024);   // DMA destinations: whole wave-instructions
+  s.wlo = o;   o += round_up(per * 4, 256);
+  s.whi = o;   o += round_up(per * 4, 256);
   s.lut = o;   o += round_up(lut_n * 4, 16);
   s.pmap = o;  o += round_up(per * 2, 16);   // (n d) slot -> W offset d*Np4 + n
   s.kq = o;    o += round_up(per * 2, 16);   // (n d) slot -> (d n) index d*N + n
   s.kpb = o;   o += round_up(per * 2, 16);   // (d n) index -> W offset
-  s.dst = o;   o += round_up(D * 4, 16);
+  s.dst = o;   o += round_up(D * 4, 256);
   s.col2d = o; o += round_up(ndo * 4, 16);
   const int outb = round_up(TBT * s.RTR * ndo * 4, 16);
   s.stage = KS ? true : (o + outb) <= 96 * 1024;
@@ -397,7 +407,6 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
-  float* wrg = reinterpret_cast<float*>(smem + L.wrg);
   float* lut = reinterpret_cast<float*>(smem + L.lut);
   uint16_t* pmap = reinterpret_cast<uint16_t*>(smem + L.pmap);
   uint16_t* kq = reinterpret_cast<uint16_t*>(smem + L.kq);
@@ -408,64 +417,49 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
   const int tid = threadIdx.x;
   const float vm1 = (float)(a.vocab - 1);
 
-  // ---- constants, once per workgroup
-  {
-    float lo[4], hi[4];
+  // ---- prologue: the first token tile, the bounds and the DoF map by DMA, the
+  //      padded basis by register staging -- all in flight together (one round trip)
+  if ((a.phases & 1) && blockIdx.x < a.ntiles) stage_tokens(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
+  dma4(wlo, a.w_min, per);
+  dma4(whi, a.w_max, per);
+  if (pos) dma4(dst, a.dof_dst, D);
+  if (KS && pos) {   // Phi zero-padded to [kinds][RTR][Np4]: clamped loads, then unconditional stores
+    const int tot = nkinds * RTR * Np4;
+    const int tn = RTR * Np4;
+    for (int base = 0; base < tot; base += 8 * NTHREADS) {
+      float v[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = min(tid + i * NTHREADS, per - 1);
-      lo[i] = a.w_min[k];
-      hi[i] = a.w_max[k];
-    }
-    int dd = 0;
-    if (pos && tid < D) dd = a.dof_dst[tid];
-    if (KS && pos) {   // Phi zero-padded to [kinds][RTR][Np4]: clamped loads, then select
-      const int tot = nkinds * RTR * Np4;
-      for (int base = 0; base < tot; base += 8 * NTHREADS) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = min(base + u * NTHREADS + tid, tot - 1);
-          const int k = i / (RTR * Np4), r = i - k * RTR * Np4, t = r / Np4, n = r - t * Np4;
-          const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
-          v[u] = (t < Tout && n < N) ? x : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int i = base + u * NTHREADS + tid;
-          if (i < tot) phi[i] = v[u];
-        }
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(base + u * NTHREADS + tid, tot - 1);
+        const int k = i >= tn ? 1 : 0, r = i - k * tn, t = r / Np4, n = r - t * Np4;
+        const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
+        // bit-mask select: x stays used on every path, so the load is not sunk into a branch
+        const uint32_t keep = 0u - (uint32_t)((t < Tout) & (n < N));
+        v[u] = __uint_as_float(__float_as_uint(x) & keep);
       }
-    }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = tid + i * NTHREADS;
-      if (k < per) {
-        wlo[k] = lo[i];
-        whi[k] = hi[i];
-        wrg[k] = __fsub_rn(hi[i], lo[i]);   // (max_val - min_val), beast/utils.py:24
-      }
+      for (int u = 0; u < 8; ++u) phi[min(base + u * NTHREADS + tid, tot - 1)] = v[u];
     }
-    for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
-    for (int r = tid; r < per; r += NTHREADS) {
-      const int n = r / D, d = r - n * D;
-      pmap[r] = (uint16_t)(d * Np4 + n);
-      kq[r] = (uint16_t)(d * N + n);
-      const int d2 = r / N, n2 = r - d2 * N;
-      kpb[r] = (uint16_t)(d2 * Np4 + n2);
-    }
-    for (int e = tid; e < TBT * D * (Np4 - N); e += NTHREADS) {   // zero W pad columns once
-      const int row = e / (Np4 - N), n = N + (e - row * (Np4 - N));
-      pb[row * Np4 + n] = 0.0f;
-    }
-    if (pos) {
-      for (int c = tid; c < ndo; c += NTHREADS) col2d[c] = -1;
-      if (tid < D) dst[tid] = dd;
-      __syncthreads();
-      if (tid < D) {
-        if (dd >= 0 && dd < ndo) col2d[dd] = tid;
-        else dst[tid] = 0;   // out-of-range destination: precondition violated; keep stores in bounds
-      }
+  }
+  for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
+  for (int r = tid; r < per; r += NTHREADS) {
+    const int n = r / D, d = r - n * D;
+    pmap[r] = (uint16_t)(d * Np4 + n);
+    kq[r] = (uint16_t)(d * N + n);
+    const int d2 = r / N, n2 = r - d2 * N;
+    kpb[r] = (uint16_t)(d2 * Np4 + n2);
+  }
+  for (int e = tid; e < TBT * D * (Np4 - N); e += NTHREADS) {   // zero W pad columns once
+    const int row = e / (Np4 - N), n = N + (e - row * (Np4 - N));
+    pb[row * Np4 + n] = 0.0f;
+  }
+  if (pos && KS == 0) {   // per-row basis path: output column -> DoF (after the DMA of dst)
+    __syncthreads();
+    for (int c = tid; c < ndo; c += NTHREADS) col2d[c] = -1;
+    __syncthreads();
+    if (tid < D) {
+      const int dd = dst[tid];
+      if (dd >= 0 && dd < ndo) col2d[dd] = tid;
     }
   }
 
@@ -476,11 +470,8 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
     const int64_t b0 = tile * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
 
-    // ---- stage the token tile (HBM -> LDS)
-    if (a.phases & 1) {
-      if (a.ntokens) burst<(TBT * 140 * 4 + 4095) / 4096>(smem + L.tok, a.ntokens + b0 * per, nb * per * 4);
-      else burst<(TBT * 140 * 8 + 4095) / 4096>(smem + L.tok, a.tokens + b0 * per, nb * per * 8);
-    }
+    // ---- the token tile lands in LDS (the first one is already in flight)
+    if ((a.phases & 1) && tile != blockIdx.x) stage_tokens(a, smem + L.tok, b0, per);
     __syncthreads();
 
     // ---- decode (H6): (n d) tokens -> W[j][d][n], bit-exact discrete_to_continuous
@@ -497,7 +488,8 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
         } else {
           const long long t = tin[e] - a.tok_offset;
           const float nrm = (t >= 0 && t < a.lut_n) ? lut[t] : __fdiv_rn((float)t, vm1);
-          v = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, wrg[k]), wlo[k]), wlo[k], whi[k]);
+          const float lo = wlo[k], hi = whi[k];   // (max_val - min_val), beast/utils.py:24
+          v = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi, lo)), lo), lo, hi);
         }
         pb[j * D * Np4 + po] = v;
       }
@@ -535,7 +527,7 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) w[ks] = Wc[4 * ks];
         const float* Ph = phi + (kind * RTR + lr) * Np4 + lk;
-        float* oc = ob + (j * RTR + lk * 4) * ndo + dst[d];
+        float* oc = ob + (j * RTR + lk * 4) * ndo + min(max(dst[d], 0), ndo - 1);
         for (int rt = 0; rt < RTR / 16; rt += 2) {
           float a0[KS], a1[KS];
 #pragma unroll
@@ -629,7 +621,7 @@ int64_t grid_for(int64_t ntiles, int lds_bytes) {
 }
 
 template <int TBT>
-int launch_encode(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t s) {
+int launch_encode_t(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t s) {
   a.g = make_geom<TBT>(D, nj, N, T);
   a.ntiles = (a.B + TBT - 1) / TBT;
   const int Dl = fast ? a.row_elems : D;
@@ -640,6 +632,29 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t
   else hipLaunchKernelGGL((k_encode<TBT, false>), dim3(grid), dim3(NTHREADS), L.total, s, a);
   BEAST_LAUNCHED("k_encode");
   return BEAST_OK;
+}
+
+// Tile size: the largest of 8/4/2/1 trajectories whose rows fit 32 KB of LDS
+// (BEAST_ENC_TBT overrides, for measurements).
+int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
+  const int64_t traj_bytes = (int64_t)T * a.row_elems * 4;
+  const bool contiguous = a.sd == 1 && a.st == a.row_elems && a.sb == (int64_t)T * a.row_elems &&
+                          (((uintptr_t)a.traj) & 15) == 0 && ((int64_t)T * a.row_elems) % 4 == 0;
+  static const int forced = [] {
+    const char* e = getenv("BEAST_ENC_TBT");
+    return e ? atoi(e) : 0;
+  }();
+  int tbt = 8;
+  while (tbt > 1 && tbt * traj_bytes > 32 * 1024) tbt >>= 1;
+  const bool fast = contiguous && tbt * traj_bytes <= 32 * 1024;
+  if (!fast) tbt = 8;
+  if (forced == 1 || forced == 2 || forced == 4 || (forced == 8 && fast)) tbt = std::min(tbt, forced);
+  switch (tbt) {
+    case 1: return launch_encode_t<1>(a, T, D, nj, N, fast, s);
+    case 2: return launch_encode_t<2>(a, T, D, nj, N, fast, s);
+    case 4: return launch_encode_t<4>(a, T, D, nj, N, fast, s);
+    default: return launch_encode_t<8>(a, T, D, nj, N, fast, s);
+  }
 }
 
 template <int TBT, int KS>
@@ -656,6 +671,7 @@ template <int TBT>
 int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t s) {
   a.g = make_geom<TBT>(D, nj, N, 1);
   a.ntiles = (a.B + TBT - 1) / TBT;
+  a.tbt = TBT;
   a.fd_row = make_fd((uint32_t)(a.Tout * a.ndo));
   a.lut_n = (a.ntokens == nullptr && a.vocab <= LUT_MAX) ? a.vocab : 0;
   const bool pos = a.pos_out != nullptr;
@@ -675,7 +691,7 @@ int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t
 
 // =================================================================== C-ABI ==
 extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st, int64_t sd,
-                                int row_elems, int D, int n_joint, const int32_t* dof_src, const double* proj,
+                                int row_elems, int D, int n_joint, const int32_t* dof_src, const float* proj,
                                 int N, const float* w_min, const float* w_max, int vocab, int64_t tok_offset,
                                 float* params_out, int64_t* tokens_out, void* stream) {
   BEAST_REQUIRE(traj && dof_src && proj, "beast_encode_f32: null input pointer");
@@ -691,8 +707,7 @@ extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb,
   a.traj = traj; a.B = B; a.sb = sb; a.st = st; a.sd = sd; a.row_elems = row_elems; a.vocab = vocab;
   a.phases = debug_phases(); a.dof_src = dof_src; a.proj = proj; a.w_min = w_min; a.w_max = w_max;
   a.tok_offset = tok_offset; a.params_out = params_out; a.tokens_out = reinterpret_cast<long long*>(tokens_out);
-  const bool fast8 = (sd == 1 && st == row_elems && sb == (int64_t)T * row_elems && 8 * T * row_elems * 4 <= 64 * 1024);
-  return launch_encode<8>(a, T, D, n_joint, N, fast8, beast::as_stream(stream));
+  return launch_encode(a, T, D, n_joint, N, beast::as_stream(stream));
 }
 
 extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, int n_joint, int N, int vocab,

@@ -11,7 +11,7 @@ is the max over ranks.  rank 0 prints ONE JSON line.
 
 Extra objects in that line:
   roofline      dominant kernel: algorithmic bytes / its average launch duration
-                (HIP events on the kernel's stream, one bracketed launch at a time)
+                (HIP events on the kernel's stream around back-to-back launches)
   cpu_baseline  the oracle's restatement of the reference op sequence (oracle/
                 beast_oracle.py, bitwise equal to the reference in the build
                 container) timed on this host's cores on a bounded sample
@@ -58,20 +58,23 @@ def parse():
     return ap.parse_args()
 
 
-def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 50) -> float:
-    """Average duration of one launch: each launch is bracketed by events on the
-    kernel's stream, queued behind a short sleep so launch overhead is excluded."""
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(reps)]
+def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 100, rounds: int = 5) -> float:
+    """Average duration of one launch in a back-to-back stream of ``reps`` launches,
+    bracketed by HIP events on the kernel's own stream and queued behind a short
+    sleep so host launch cost is hidden (the rocprofv3 per-kernel average plus the
+    inter-kernel gap).  Median over ``rounds``."""
+    per = []
     with torch.cuda.stream(stream):
-        for i in range(reps):
-            torch.cuda._sleep(20000)
-            starts[i].record(stream)
-            launch()
-            ends[i].record(stream)
-    stream.synchronize()
-    ts = sorted(s.elapsed_time(e) * 1e3 for s, e in zip(starts, ends))
-    return float(np.mean(ts[: max(1, int(0.9 * reps))]))  # trim the slowest 10%
+        for _ in range(rounds):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(200000)
+            s.record(stream)
+            for _ in range(reps):
+                launch()
+            e.record(stream)
+            stream.synchronize()
+            per.append(s.elapsed_time(e) * 1e3 / reps)
+    return float(np.median(per))
 
 
 def cpu_baseline(tok_bounds, seconds: float):
@@ -197,13 +200,12 @@ def main():
 
     # ---- dominant-kernel roofline, measured live on the kernel's stream
     stream = torch.cuda.current_stream(dev)
-    _, proj = tok._constants(dev)
+    phi, _, proj = tok._constants(dev)
     src, dst = tok._dof_maps(dev)
     wmn, wmx = tok._bounds(dev)
     params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
     tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
     pos = torch.empty((B, T, D), dtype=torch.float32, device=dev)
-    phi, _ = tok._constants(dev)
     sp = stream.cuda_stream
 
     def launch_enc():
@@ -244,7 +246,7 @@ def main():
             "metric": "trajectories/sec encode+reconstruct (B=4096,T=50,DoF=14)",
             "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32 in/out, f64 fit accumulate, int64 tokens",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 (fp32 MFMA fit, int64 tokens)",
             "data": "synthetic (seeded splitmix64 sinusoids, beast_tokenizer_amd/synthetic.py)",
             "config": {"workload": "BEASTBsplineTokenizer encode->reconstruct_traj, num_dof=14 num_basis=10 "
                                    "seq_len=50 vocab=256 degree_p=4", "global_batch": B * world,

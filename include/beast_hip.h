@@ -67,14 +67,15 @@ int beast_bspline_projection_f64(const float* basis, int T, int N, double reg, d
  * (beast/utils.py:4-17) + rearrange + LLM offset, as ONE fused kernel.
  *   traj[b*sb + t*st + dof_src[d]*sd]  fp32 input, element strides
  *   row_elems   size of the input's last dim (for the contiguous fast path)
- *   proj        [2][16][Tp] float64 zero-padded projections (kind 0 joint, kind 1
- *               gripper), as written by beast_bspline_projection_f64
+ *   proj        [2][16][Tp] fp32 zero-padded projections (kind 0 joint, kind 1
+ *               gripper): the round-to-nearest fp32 image of the float64 output of
+ *               beast_bspline_projection_f64, converted once per time grid
  *   params_out  [B][D*N] fp32 unclamped fit (params_dict['params']); nullable
  *   tokens_out  [B][N*D] int64 = round_half_even(clamp01((clamp(p)-wmin)/max(wmax-wmin,1e-8))*(vocab-1))
  *               + tok_offset; nullable.  vocab <= 0 disables quantisation.
  * Constraints: N <= 16, T <= 256, D <= 64. */
 int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st, int64_t sd, int row_elems,
-                     int D, int n_joint, const int32_t* dof_src, const double* proj, int N,
+                     int D, int n_joint, const int32_t* dof_src, const float* proj, int N,
                      const float* w_min, const float* w_max, int vocab, int64_t tok_offset,
                      float* params_out, int64_t* tokens_out, void* stream);
 

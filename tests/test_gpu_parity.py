@@ -68,8 +68,9 @@ def check_token_flips(tok_gpu, tok_ref, x, g, name, max_flips):
 def test_basis_bitexact(name, golden, gpu_device):
     g = golden[name]
     tok = make_tok(name, g, gpu_device)
-    phi, proj = tok._constants(gpu_device)
+    phi, proj, proj32 = tok._constants(gpu_device)
     assert np.array_equal(phi[0].cpu().numpy(), g["phi_joint"])
+    assert np.array_equal(proj32.cpu().numpy(), proj.cpu().numpy().astype(np.float32))
     if "phi_grip" in g:
         assert np.array_equal(phi[1].cpu().numpy(), g["phi_grip"])
     P = O.projection_f64(g["phi_joint"])

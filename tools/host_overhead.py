@@ -15,8 +15,6 @@ dev = torch.device("cuda", 0)
 tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
 x = torch.from_numpy(synth_trajectories(4096, 50, 14, seed=0)).to(dev)
 out = {}
-for name, fn in [("encode", lambda: tok.encode(x)), ("reconstruct", None), ("step", None)]:
-    pass
 tokens, _ = tok.encode(x)
 
 
@@ -33,9 +31,9 @@ def t(fn, n=2000):
     return host * 1e6, wall * 1e6
 
 
-out["encode_host_us, wall_us"] = t(lambda: tok.encode(x))
+out["encode"] = t(lambda: tok.encode(x))
 out["reconstruct"] = t(lambda: tok.reconstruct_traj(tokens))
 out["step"] = t(lambda: tok.reconstruct_traj(tok.encode(x)[0]))
 out["empty_alloc"] = t(lambda: (torch.empty((4096, 140), dtype=torch.int64, device=dev),
                                 torch.empty((4096, 140), device=dev)))
-print(json.dumps(out))
+print(json.dumps({k: {"host_us": round(h, 2), "wall_us": round(w, 2)} for k, (h, w) in out.items()}))

@@ -25,8 +25,7 @@ def one():
         x = torch.from_numpy(synth_trajectories(min(B, 65536), T, D, seed=0)).to(dev)
         if B > 65536:
             x = x.repeat(B // 65536, 1, 1)
-        _, proj = tok._constants(dev)
-        phi, _ = tok._constants(dev)
+        phi, _, proj = tok._constants(dev)
         src, dst = tok._dof_maps(dev)
         wmn, wmx = tok._bounds(dev)
         params = torch.empty((B, D * N), device=dev)
