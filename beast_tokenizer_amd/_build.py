@@ -27,7 +27,7 @@ CXXFLAGS = [
     # bit-exact quantise / dequantise / basis: no FMA contraction, IEEE fp32 division
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
-]
+] + [f"-D{d}" for d in os.environ.get("BEAST_DEFINES", "").split()]
 
 
 def _hipcc() -> str:

@@ -21,6 +21,7 @@ BEAST_E_HIP = -2
 BEAST_E_UNSUPPORTED = -3
 BEAST_E_WORKSPACE = -4
 ABI_VERSION = 1
+OPT_GENERIC_KERNELS = 1
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 
@@ -28,6 +29,7 @@ _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.
 SIGNATURES = {
     "beast_abi_version": (_i32, []),
     "beast_last_error": (C.c_char_p, []),
+    "beast_set_option": (_i32, [_i32, _i32]),
     "beast_bspline_basis_f32": (_i32, [_vp, _i64, _f32, _f32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "beast_bspline_projection_f64": (_i32, [_vp, _i32, _i32, _f64, _vp, _vp]),
     "beast_encode_f32": (_i32, [_vp, _i64, _i32, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp,

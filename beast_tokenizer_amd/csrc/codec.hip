@@ -30,7 +30,7 @@ constexpr int NWAVES = NTHREADS / 64;
 constexpr int MAX_T = 256;
 constexpr int MAX_N = 16;
 constexpr int MAX_D = 64;
-constexpr int TILES = 4;  // independent MFMA accumulation chains per wave
+constexpr int ECH = 4;    // encode: K-steps per LDS-operand chunk
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
@@ -127,11 +127,24 @@ __device__ __forceinline__ void dma4(void* lds, const void* g, int n) {
   }
 }
 
+// In-kernel cycle stamps (tools/stamps builds this file with -DBEAST_STAMPS; the product
+// library compiles them out): s_memtime of lane 0 of every wave of workgroup 0 at the
+// phase boundaries of its first tile.
+#ifdef BEAST_STAMPS
+__device__ unsigned long long g_stamps[2][NWAVES][16];
+#define STAMP(k, i)                                                                              \
+  do {                                                                                           \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_stamps[k][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(k, i) do { } while (0)
+#endif
+
 // -------------------------------------------------------------- geometry --
 struct Geom {
   int D, nj, N, T, Tp, per;   // per = N * D
   int nq0, nq;                // column tiles of kind 0, of both kinds
-  FastDiv fd_nj, fd_ng, fd_per, fd_N, fd_nq;
+  FastDiv fd_nj, fd_ng, fd_per, fd_N, fd_D, fd_nq;
 };
 
 template <int TBT>
@@ -145,22 +158,54 @@ inline Geom make_geom(int D, int nj, int N, int T) {
   g.fd_ng = make_fd(std::max(ng, 1));
   g.fd_per = make_fd(g.per);
   g.fd_N = make_fd(N);
+  g.fd_D = make_fd(D);
   g.fd_nq = make_fd(std::max(g.nq, 1));
   return g;
 }
 
-// MFMA column (trajectory j, DoF d) of tile q for lane column lc; valid = inside the tile set.
-template <int TBT>
-__device__ __forceinline__ void tile_col(const Geom& g, int q, int lc, int& j, int& d, int& kind, bool& valid) {
-  const int k0 = q < g.nq0 ? 0 : 1;
-  const int dk = k0 ? g.D - g.nj : g.nj;
-  const int c = (q - (k0 ? g.nq0 : 0)) * 16 + lc;
+// Compile-time problem shape.  A zero field is read from the runtime Geom instead; the
+// BEAST defaults (N = 10 basis functions, T = 50 steps, 7 or 14 DoF with or without the
+// two gripper DoF) get fully specialised kernels in which every index is a constant.
+template <int SD, int SNJ, int SN, int ST, int SDL>
+struct Shape {
+  static constexpr int D = SD, NJ = SNJ, N = SN, T = ST, DL = SDL;
+  static constexpr bool fixed = SD > 0;
+};
+using DynShape = Shape<0, 0, 0, 0, 0>;
+
+template <class S>
+struct Dims {   // the shape, constant-folded where S fixes it
+  int D, nj, ng, N, T, Tp, per;
+  __device__ __forceinline__ Dims(const Geom& g)
+      : D(S::D ? S::D : g.D), nj(S::fixed ? S::NJ : g.nj), ng(D - nj), N(S::N ? S::N : g.N),
+        T(S::T ? S::T : g.T), Tp(S::T ? round_up(S::T, 4) : g.Tp), per(N * D) {}
+};
+
+template <class S>
+__device__ __forceinline__ uint32_t div_by(uint32_t x, int dconst, const FastDiv& f) {
+  return S::fixed ? x / (uint32_t)dconst : fdiv(x, f);
+}
+
+// MFMA column (trajectory j, DoF d) of tile q (wave-uniform) for lane column lc; valid =
+// inside the tile set.
+template <int TBT, class S>
+__device__ __forceinline__ void tile_col(const Geom& g, const Dims<S>& m, int q, int lc, int& j, int& d, int& kind,
+                                         bool& valid) {
+  const int nq0 = (TBT * m.nj + 15) / 16;
+  const int k0 = q < nq0 ? 0 : 1;
+  const int dk = k0 ? m.ng : m.nj;
+  const int c = (q - (k0 ? nq0 : 0)) * 16 + lc;
   valid = c < TBT * dk;
   const uint32_t cc = valid ? c : TBT * dk - 1;
-  const uint32_t jj = fdiv(cc, k0 ? g.fd_ng : g.fd_nj);
+  const uint32_t jj = k0 ? div_by<S>(cc, m.ng > 0 ? m.ng : 1, g.fd_ng) : div_by<S>(cc, m.nj > 0 ? m.nj : 1, g.fd_nj);
   j = (int)jj;
-  d = (int)(cc - jj * dk) + (k0 ? g.nj : 0);
+  d = (int)(cc - jj * dk) + (k0 ? m.nj : 0);
   kind = k0;
+}
+
+template <int TBT, class S>
+__device__ __forceinline__ int n_coltiles(const Dims<S>& m) {
+  return (TBT * m.nj + 15) / 16 + (TBT * m.ng + 15) / 16;
 }
 
 // ----------------------------------------------------------------- encode --
@@ -179,7 +224,7 @@ struct EncArgs {
 };
 
 struct EncSmem {
-  int P, Y, pb, wlo, whi, kmap, lcol, total;
+  int P, Y, pb, tq, wlo, whi, lcol, total;
 };
 
 // Every buffer an LDS-DMA fills is padded to whole wave-instructions (64 lanes x 16 B).
@@ -187,54 +232,58 @@ template <int TBT>
 __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N, int nkinds) {
   EncSmem s;
   int o = 0;
-  s.P = o;    o += round_up(nkinds * 16 * Tp * 4, 1024);   // fp32 [16][Tp] projection per kind
+  // DMA destinations padded to whole wave-instructions, plus slack for the MFMA loop's
+  // one-step-ahead operand reads past the last row (never used)
+  s.P = o;    o += round_up(nkinds * 16 * Tp * 4 + 64 * ECH, 1024);   // fp32 [16][Tp] projection per kind
   s.Y = o;    o += round_up(TBT * T * Dl * 4, 1024);
-  s.pb = o;   o += round_up(TBT * D * N * 4, 16);
+  s.pb = o;   o += round_up(TBT * D * N * 4, 16);        // params, (d n) per trajectory
+  s.tq = o;   o += round_up(TBT * D * N * 4, 16);        // token bins (int32), (n d) per trajectory
   s.wlo = o;  o += round_up(D * N * 4, 256);
   s.whi = o;  o += round_up(D * N * 4, 256);
-  s.kmap = o; o += round_up(D * N * 2, 16);
   s.lcol = o; o += round_up(D * 4, 256);
   s.total = o;
   return s;
 }
 
-template <int TBT, bool FAST>
+template <int TBT, bool FAST, class S>
 __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Geom& g = a.g;
-  const int D = g.D, N = g.N, T = g.T, Tp = g.Tp, per = g.per, DN = D * N;
-  const int Dl = FAST ? a.row_elems : D;
-  const int nkinds = (g.nj < D) ? 2 : 1;
+  const Dims<S> m(g);
+  const int D = m.D, N = m.N, T = m.T, Tp = m.Tp, per = m.per, DN = D * N;
+  const int Dl = FAST ? (S::DL ? S::DL : a.row_elems) : D;
+  const int nkinds = (m.nj < D) ? 2 : 1;
+  const int nq = n_coltiles<TBT>(m);
   const EncSmem L = enc_smem<TBT>(T, Tp, Dl, D, N, nkinds);
   float* P = reinterpret_cast<float*>(smem + L.P);
   float* Y = reinterpret_cast<float*>(smem + L.Y);
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
-  uint16_t* kmap = reinterpret_cast<uint16_t*>(smem + L.kmap);
+  int* tq = reinterpret_cast<int*>(smem + L.tq);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x;
   const bool quant = a.tokens_out != nullptr;
   const int tile_elems = T * a.row_elems;   // FAST: one trajectory, contiguous, % 4 == 0
 
+  STAMP(0, 0);
   // ---- prologue: the first tile and every constant go HBM -> LDS by DMA in one round trip
   if (FAST && (a.phases & 1) && blockIdx.x < a.ntiles) {
     const int64_t b0 = (int64_t)blockIdx.x * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
     dma16(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
   }
+  STAMP(0, 9);
   dma16(P, a.proj, nkinds * 4 * Tp);
+  STAMP(0, 10);
   if (quant) {
     dma4(wlo, a.w_min, DN);
     dma4(whi, a.w_max, DN);
   }
   dma4(lcol, a.dof_src, D);
-  for (int r = tid; r < per; r += NTHREADS) {   // (n d) slot -> (d n) index
-    const int n = r / D, d = r - n * D;
-    kmap[r] = (uint16_t)(d * N + n);
-  }
+  STAMP(0, 11);
 
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int lr = lane & 15, lk = lane >> 4;
   const float vm1 = (float)(a.vocab - 1);
 
@@ -256,79 +305,115 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
         }
       }
     }
+    if (tile == blockIdx.x) STAMP(0, 1);
     __syncthreads();   // waits for the DMA (vmcnt) and the LDS stores
+    if (tile == blockIdx.x) STAMP(0, 2);
+    if (tile == blockIdx.x + gridDim.x) STAMP(0, 12);
 
     // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f32 MFMA 16x16x4; A = P, B = y).
     //      A wave owns two column tiles per pass (two independent chains), operands
     //      pointer-stepped through LDS; rows t >= T (tail step) meet a zero A column.
-    for (int q0 = wave; (a.phases & 2) && q0 < g.nq; q0 += NWAVES * 2) {
+    for (int q0 = wave; (a.phases & 2) && q0 < nq; q0 += NWAVES * 2) {
       int j0, d0, k0, j1, d1, k1;
       bool ok0, ok1;
-      tile_col<TBT>(g, q0, lr, j0, d0, k0, ok0);
-      tile_col<TBT>(g, min(q0 + NWAVES, g.nq - 1), lr, j1, d1, k1, ok1);
+      tile_col<TBT>(g, m, q0, lr, j0, d0, k0, ok0);
+      tile_col<TBT>(g, m, min(q0 + NWAVES, nq - 1), lr, j1, d1, k1, ok1);
       ok0 = ok0 && j0 < nb;
-      ok1 = ok1 && j1 < nb && (q0 + NWAVES < g.nq);
+      ok1 = ok1 && j1 < nb && (q0 + NWAVES < nq);
       const int c0 = FAST ? min(max(lcol[d0], 0), Dl - 1) : d0;
       const int c1 = FAST ? min(max(lcol[d1], 0), Dl - 1) : d1;
+      // K-steps in chunks of ECH: every LDS operand of a chunk is read before its MFMAs and
+      // the next chunk's reads are issued before them too (one LDS round trip per chunk);
+      // even / odd steps accumulate separately (two chains per tile).  Step s covers rows
+      // t = 4s + lane/16, clamped to T - 1 (the zero-padded P columns meet them).
+      const int nst = (T + 3) >> 2;
+      const bool two = q0 + NWAVES < nq;   // wave-uniform: a second column tile this pass
       const float* pa0 = P + (k0 * 16 + lr) * Tp + lk;
       const float* pa1 = P + (k1 * 16 + lr) * Tp + lk;
       const float* yc0 = Y + j0 * T * Dl + c0;
       const float* yc1 = Y + j1 * T * Dl + c1;
-      const float* yb0 = yc0 + lk * Dl;
-      const float* yb1 = yc1 + lk * Dl;
-      float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-      int s = 0;
-#pragma unroll 4
-      for (; s + 4 <= T; s += 4) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[s], *yb0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[s], *yb1, acc1, 0, 0, 0);
-        yb0 += 4 * Dl;
-        yb1 += 4 * Dl;
+      float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+      float xa[ECH], ya[ECH], xb[ECH], yb[ECH];
+#pragma unroll
+      for (int i = 0; i < ECH; ++i) {
+        const int row = min(4 * i + lk, T - 1) * Dl;
+        xa[i] = pa0[4 * i]; ya[i] = yc0[row]; xb[i] = pa1[4 * i]; yb[i] = yc1[row];
       }
-      if (s < T) {   // wave-uniform tail (T % 4 != 0)
-        const int row = min(s + lk, T - 1) * Dl;
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa0[s], yc0[row], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(pa1[s], yc1[row], acc1, 0, 0, 0);
+      for (int c = 0; c < nst; c += ECH) {
+        float nxa[ECH], nya[ECH], nxb[ECH], nyb[ECH];
+#pragma unroll
+        for (int i = 0; i < ECH; ++i) {   // next chunk (reads past the end land in LDS slack, unused)
+          const int st = c + ECH + i, row = min(4 * st + lk, T - 1) * Dl;
+          nxa[i] = pa0[4 * st]; nya[i] = yc0[row]; nxb[i] = pa1[4 * st]; nyb[i] = yc1[row];
+        }
+#pragma unroll
+        for (int i = 0; i < ECH; ++i) {
+          if (c + i < nst) {   // wave-uniform
+            if (i & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[i], ya[i], acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[i], ya[i], acc0, 0, 0, 0);
+            if (two) {
+              if (i & 1) acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i], yb[i], acc3, 0, 0, 0);
+              else acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[i], yb[i], acc2, 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < ECH; ++i) { xa[i] = nxa[i]; ya[i] = nya[i]; xb[i] = nxb[i]; yb[i] = nyb[i]; }
       }
-      // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc0[r] = __fadd_rn(acc0[r], acc1[r]);
+        acc2[r] = __fadd_rn(acc2[r], acc3[r]);
+      }
+      // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r.  Each lane writes its params
+      // ((d n) image) and quantises them into the token bins ((n d) image) in place.
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = lk * 4 + r;
         if (n < N) {
-          if (ok0) pb[j0 * DN + d0 * N + n] = acc0[r];
-          if (ok1) pb[j1 * DN + d1 * N + n] = acc1[r];
+          if (ok0) {
+            pb[j0 * DN + d0 * N + n] = acc0[r];
+            if (quant) tq[j0 * per + n * D + d0] = beast::quantize_bin_fast(acc0[r], wlo[d0 * N + n], whi[d0 * N + n], vm1);
+          }
+          if (ok1) {
+            pb[j1 * DN + d1 * N + n] = acc2[r];
+            if (quant) tq[j1 * per + n * D + d1] = beast::quantize_bin_fast(acc2[r], wlo[d1 * N + n], whi[d1 * N + n], vm1);
+          }
         }
       }
     }
+    if (tile == blockIdx.x) STAMP(0, 3);
+    if (tile == blockIdx.x + gridDim.x) STAMP(0, 13);
     __syncthreads();
+    if (tile == blockIdx.x) STAMP(0, 4);
 
     // ---- epilogue: params (d n) and tokens (n d), both contiguous per tile
     if (a.params_out != nullptr && (a.phases & 4)) store_out(a.params_out + b0 * DN, pb, nb * DN);
-    if (quant && (a.phases & 8)) {
+    if (tile == blockIdx.x) STAMP(0, 5);
+    if (quant && (a.phases & 8)) {   // int32 bins -> int64 tokens + offset, 2 x 16 B per 4 tokens
       const int total = nb * per;
       long long* tout = a.tokens_out + b0 * per;
-      const bool vec = ((((uintptr_t)tout) & 15) == 0);
-      for (int e2 = tid; 2 * e2 < total; e2 += NTHREADS) {
-        long long v[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t e = min(2 * e2 + h, total - 1);
-          const uint32_t j = fdiv(e, g.fd_per);
-          const int k = kmap[e - j * per];
-          const float lo = wlo[k], hi = whi[k];
-          float sc = __fsub_rn(hi, lo);
-          sc = (sc < 1e-8f) ? 1e-8f : sc;   // torch.clamp(max - min, min=1e-8), NaN kept
-          v[h] = beast::quantize_scaled(pb[j * DN + k], lo, hi, sc, vm1) + a.tok_offset;
+      const unsigned long long off = (unsigned long long)a.tok_offset;
+      int done = 0;
+      if ((((uintptr_t)tout) & 15) == 0) {
+        const int n4 = total >> 2;
+        for (int i = tid; i < n4; i += NTHREADS) {
+          const int4 b = reinterpret_cast<const int4*>(tq)[i];
+          longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
+          o2[0] = make_longlong2(beast::widen_bin(b.x, off), beast::widen_bin(b.y, off));
+          o2[1] = make_longlong2(beast::widen_bin(b.z, off), beast::widen_bin(b.w, off));
         }
-        if (vec && 2 * e2 + 1 < total) {
-          *reinterpret_cast<longlong2*>(tout + 2 * e2) = make_longlong2(v[0], v[1]);
-        } else {
-          tout[2 * e2] = v[0];
-          if (2 * e2 + 1 < total) tout[2 * e2 + 1] = v[1];
-        }
+        done = n4 << 2;
       }
+      for (int e = done + tid; e < total; e += NTHREADS) tout[e] = beast::widen_bin(tq[e], off);
     }
+    if (tile == blockIdx.x) STAMP(0, 6);
+    if (tile == blockIdx.x + gridDim.x) STAMP(0, 14);
   }
+#ifdef BEAST_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(0, 7);
+#endif
 }
 
 // ------------------------------------------------------------ reconstruct --
@@ -350,42 +435,54 @@ struct RecArgs {
 };
 
 constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divided once
-
-struct RecSmem {
-  int phi, pb, tok, wlo, whi, lut, pmap, kq, kpb, dst, col2d, out, total;
-  int Np4, RTR;   // padded basis width, padded output rows
-  bool stage;
-};
+constexpr int RT_REG = 4;       // row tiles (64 output rows) whose basis operands live in registers
 
 // token tile [nb][per] (int64, or fp32 normalised tokens) HBM -> LDS by DMA
 __device__ __forceinline__ void stage_tokens(const RecArgs& a, void* lds, int64_t b0, int per) {
-  const int nb = (int)min<int64_t>(a.B - b0, 1 << 30);
+  const int nb = (int)min<int64_t>(a.B - b0, a.tbt);
   const void* src = a.ntokens ? static_cast<const void*>(a.ntokens + b0 * per)
                               : static_cast<const void*>(a.tokens + b0 * per);
-  const int bytes = min(nb, a.tbt) * per * (a.ntokens ? 4 : 8);
+  const int bytes = nb * per * (a.ntokens ? 4 : 8);
   if ((bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) dma16(lds, src, bytes >> 4);
   else dma4(lds, src, bytes >> 2);
 }
 
-// KS > 0: shared basis on MFMA (K-steps of 4 basis functions); KS == 0: per-row basis on VALU
-template <int TBT, int KS>
+// W[j][d][n] from the staged tile: bit-exact discrete_to_continuous (beast/utils.py:20-25)
+// or, for normalised tokens, denormalize_tensor's intent (utils.py:38-44).
+__device__ __forceinline__ float rec_weight(const RecArgs& a, const unsigned char* tokl, int e, int k,
+                                            const float* wlo, const float* whi, const float* lut, float vm1) {
+  const float lo = wlo[k], hi = whi[k];
+  if (a.ntokens) return beast::denormalize_one(reinterpret_cast<const float*>(tokl)[e], lo, hi);
+  const long long t = reinterpret_cast<const long long*>(tokl)[e] - a.tok_offset;
+  const float nrm = (t >= 0 && t < a.lut_n) ? lut[t] : __fdiv_rn((float)t, vm1);
+  return beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi, lo)), lo), lo, hi);
+}
+
+struct RecSmem {
+  int phi, tok, wlo, whi, lut, dst, out, pb, pmap, col2d, total;
+  int Np4, RTR;   // padded basis width, padded output rows
+  bool stage;
+};
+
+// Shared basis (KS > 0, MFMA): the basis operands are in registers (RT = RT_REG, T_out <= 64)
+// or in LDS (RT = 0).  Per-row basis (KS == 0, VALU): W in LDS, rows of the basis from HBM.
+template <int TBT, int KS, int RT>
 __host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, int nkinds, int lut_n) {
   RecSmem s;
   const int per = N * D;
   s.Np4 = KS ? 4 * KS : round_up(N, 4);
-  s.RTR = KS ? round_up(Tout, 32) : Tout;   // even number of 16-row tiles
+  s.RTR = KS ? round_up(Tout, 64) : Tout;   // row tiles in groups of four
   int o = 0;
-  s.phi = o;   o += KS ? round_up(nkinds * s.RTR * s.Np4 * 4, 16) : 0;
-  s.pb = o;    o += round_up(TBT * D * s.Np4 * 4, 16);
+  // basis in LDS: RT == 0 the zero-padded [kinds][RTR][Np4] image; RT > 0 the raw [kinds][Tout][N] (DMA)
+  s.phi = o;   o += KS ? (RT == 0 ? round_up(nkinds * s.RTR * s.Np4 * 4, 16) : round_up(nkinds * Tout * N * 4, 1024)) : 0;
   s.tok = o;   o += round_up(TBT * per * 8, 1024);   // DMA destinations: whole wave-instructions
   s.wlo = o;   o += round_up(per * 4, 256);
   s.whi = o;   o += round_up(per * 4, 256);
   s.lut = o;   o += round_up(lut_n * 4, 16);
-  s.pmap = o;  o += round_up(per * 2, 16);   // (n d) slot -> W offset d*Np4 + n
-  s.kq = o;    o += round_up(per * 2, 16);   // (n d) slot -> (d n) index d*N + n
-  s.kpb = o;   o += round_up(per * 2, 16);   // (d n) index -> W offset
   s.dst = o;   o += round_up(D * 4, 256);
-  s.col2d = o; o += round_up(ndo * 4, 16);
+  s.pb = o;    o += KS ? 0 : round_up(TBT * D * s.Np4 * 4, 16);
+  s.pmap = o;  o += KS ? 0 : round_up(per * 2, 16);   // (n d) slot -> W offset d*Np4 + n
+  s.col2d = o; o += KS ? 0 : round_up(ndo * 4, 16);
   const int outb = round_up(TBT * s.RTR * ndo * 4, 16);
   s.stage = KS ? true : (o + outb) <= 96 * 1024;
   s.out = o;   o += s.stage ? outb : 0;
@@ -393,39 +490,84 @@ __host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, int
   return s;
 }
 
-template <int TBT, int KS>
+// decode-only output (params_out, (d n) order) straight from the staged tokens
+__device__ __forceinline__ void rec_params_out(const RecArgs& a, const unsigned char* tokl, int64_t b0, int nb,
+                                               const float* wlo, const float* whi, const float* lut, float vm1) {
+  const Geom& g = a.g;
+  const int per = g.per, D = g.D, N = g.N;
+  float* pout = a.params_out + b0 * per;
+  for (int e = threadIdx.x; e < nb * per; e += NTHREADS) {
+    const uint32_t j = fdiv(e, g.fd_per);
+    const int k = e - j * per;                 // (d n) index
+    const uint32_t d = fdiv(k, g.fd_N);
+    const int n = k - d * N;
+    pout[e] = rec_weight(a, tokl, j * per + n * D + d, k, wlo, whi, lut, vm1);
+  }
+}
+
+// ob rows [0, Tout) of each trajectory -> one contiguous HBM tile
+template <class S>
+__device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const float* ob, int nb, int RTR) {
+  const int Tout = S::T ? S::T : a.Tout, ndo = S::DL ? S::DL : a.ndo;
+  const int rowlen = Tout * ndo;
+  if ((rowlen & 3) == 0 && ((RTR * ndo) & 3) == 0 && ((((uintptr_t)gout) & 15) == 0)) {
+    const int n4 = nb * rowlen / 4;
+    for (int i = threadIdx.x; i < n4; i += NTHREADS) {
+      const uint32_t e = 4 * i;
+      const uint32_t j = div_by<S>(e, rowlen, a.fd_row);
+      reinterpret_cast<float4*>(gout)[i] = *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen));
+    }
+  } else {
+    for (int e = threadIdx.x; e < nb * rowlen; e += NTHREADS) {
+      const uint32_t j = div_by<S>(e, rowlen, a.fd_row);
+      gout[e] = ob[j * RTR * ndo + (e - j * rowlen)];
+    }
+  }
+}
+
+template <int TBT, int KS, int RT, class S>
 __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
+  static_assert(KS > 0, "shared-basis kernel");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Geom& g = a.g;
-  const int D = g.D, N = g.N, nj = g.nj, per = g.per;
-  const int Tout = a.Tout, ndo = a.ndo;
+  const Dims<S> m(g);
+  const int D = m.D, N = m.N, nj = m.nj, per = m.per;
+  const int Tout = S::T ? S::T : a.Tout, ndo = S::DL ? S::DL : a.ndo;
   const int nkinds = (nj < D) ? 2 : 1;
-  const bool pos = a.pos_out != nullptr;
-  const RecSmem L = rec_smem<TBT, KS>(Tout, D, N, ndo, nkinds, a.lut_n);
-  const int Np4 = L.Np4, RTR = L.RTR;
+  const int nq = n_coltiles<TBT>(m);
+  const RecSmem L = rec_smem<TBT, KS, RT>(Tout, D, N, ndo, nkinds, a.lut_n);
+  constexpr int Np4 = 4 * KS;
+  const int RTR = L.RTR;
   float* phi = reinterpret_cast<float*>(smem + L.phi);
-  float* pb = reinterpret_cast<float*>(smem + L.pb);
+  const unsigned char* tokl = smem + L.tok;
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
   float* lut = reinterpret_cast<float*>(smem + L.lut);
-  uint16_t* pmap = reinterpret_cast<uint16_t*>(smem + L.pmap);
-  uint16_t* kq = reinterpret_cast<uint16_t*>(smem + L.kq);
-  uint16_t* kpb = reinterpret_cast<uint16_t*>(smem + L.kpb);
   int* dst = reinterpret_cast<int*>(smem + L.dst);
-  int* col2d = reinterpret_cast<int*>(smem + L.col2d);
   float* ob = reinterpret_cast<float*>(smem + L.out);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int lr = lane & 15, lk = lane >> 4;
   const float vm1 = (float)(a.vocab - 1);
 
-  // ---- prologue: the first token tile, the bounds and the DoF map by DMA, the
-  //      padded basis by register staging -- all in flight together (one round trip)
+  STAMP(1, 0);
+  // ---- prologue: the first token tile, the bounds and the DoF map by DMA; the basis
+  //      operands (registers or LDS) by clamped loads -- all in flight together
   if ((a.phases & 1) && blockIdx.x < a.ntiles) stage_tokens(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
+  STAMP(1, 9);
   dma4(wlo, a.w_min, per);
   dma4(whi, a.w_max, per);
-  if (pos) dma4(dst, a.dof_dst, D);
-  if (KS && pos) {   // Phi zero-padded to [kinds][RTR][Np4]: clamped loads, then unconditional stores
-    const int tot = nkinds * RTR * Np4;
-    const int tn = RTR * Np4;
+  dma4(dst, a.dof_dst, D);
+  STAMP(1, 10);
+  // A operand of MFMA row tile rt, K-step ks: Phi_kind[rt*16 + lr][n], n = lane/16 * KS + ks,
+  // zero outside [Tout) x [N).  RT > 0: the raw basis [kinds][Tout][N] is DMA'd to LDS with
+  // the first token tile and the operands are read into registers once, after it lands.
+  float phr[2][RT > 0 ? RT : 1][KS];
+  if constexpr (RT > 0) {
+    const int pbytes = nkinds * Tout * N * 4;
+    if ((pbytes & 15) == 0 && (((uintptr_t)a.basis) & 15) == 0) dma16(phi, a.basis, pbytes >> 4);
+    else dma4(phi, a.basis, pbytes >> 2);
+  } else {
+    const int tot = nkinds * RTR * Np4, tn = RTR * Np4;
     for (int base = 0; base < tot; base += 8 * NTHREADS) {
       float v[8];
 #pragma unroll
@@ -433,7 +575,6 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
         const int i = min(base + u * NTHREADS + tid, tot - 1);
         const int k = i >= tn ? 1 : 0, r = i - k * tn, t = r / Np4, n = r - t * Np4;
         const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
-        // bit-mask select: x stays used on every path, so the load is not sunk into a branch
         const uint32_t keep = 0u - (uint32_t)((t < Tout) & (n < N));
         v[u] = __uint_as_float(__float_as_uint(x) & keep);
       }
@@ -441,19 +582,141 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
       for (int u = 0; u < 8; ++u) phi[min(base + u * NTHREADS + tid, tot - 1)] = v[u];
     }
   }
+  STAMP(1, 11);
+  for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
+  STAMP(1, 12);
+
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * TBT;
+    const int nb = (int)min<int64_t>(TBT, a.B - b0);
+
+    if ((a.phases & 1) && tile != blockIdx.x) stage_tokens(a, smem + L.tok, b0, per);
+    if (tile == blockIdx.x) STAMP(1, 1);
+    __syncthreads();   // tokens (DMA), bounds, DoF map, LDS basis and LUT are in place
+    if (tile == blockIdx.x) STAMP(1, 2);
+    if constexpr (RT > 0) {
+      if (tile == blockIdx.x) {
+#pragma unroll
+        for (int kd = 0; kd < 2; ++kd)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              const int t = rt * 16 + lr, n = lk * KS + ks;
+              const float x = phi[(min(kd, nkinds - 1) * Tout + min(t, Tout - 1)) * N + min(n, N - 1)];
+              phr[kd][rt][ks] = (t < Tout && n < N && kd < nkinds) ? x : 0.0f;
+            }
+      }
+    }
+    if (a.params_out != nullptr) rec_params_out(a, tokl, b0, nb, wlo, whi, lut, vm1);
+
+    // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W).
+    //      A wave owns a column tile (j, d) and dequantises its own B operand (K-step ks
+    //      holds n = 4*ks + lane/16) straight from the token tile; the basis operands
+    //      are reused across the wave's column tiles; rows past Tout land in ob's padding.
+    for (int q = wave; (a.phases & 2) && q < nq; q += NWAVES) {
+      int j, d, kind;
+      bool ok;
+      tile_col<TBT>(g, m, q, lr, j, d, kind, ok);
+      ok = ok && j < nb;
+      float w[KS];   // B operand, K-step ks: W[j][d][n], n = lane/16 * KS + ks
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int n = min(lk * KS + ks, N - 1);
+        const float v = rec_weight(a, tokl, j * per + n * D + d, d * N + n, wlo, whi, lut, vm1);
+        w[ks] = (ok && lk * KS + ks < N) ? v : 0.0f;
+      }
+      if (a.init_p != nullptr && lk == 0 && ok && d < nj)   // coefficient n = 0 of the joint DoFs <- init_p
+        w[0] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];   // (reference :505-510)
+      float* oc = ob + (j * RTR + lk * 4) * ndo + min(max(dst[d], 0), ndo - 1);
+      if constexpr (RT > 0) {
+        float4_t acc[RT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int i = 0; i < RT; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(kind ? phr[1][i][ks] : phr[0][i][ks], w[ks], acc[i], 0,
+                                                          0, 0);
+        // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
+        if (ok) {
+#pragma unroll
+          for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) oc[(i * 16 + r) * ndo] = acc[i][r];
+        }
+      } else {
+        const float* Ph = phi + (kind * RTR + lr) * Np4 + lk * KS;
+        for (int rt = 0; rt < RTR / 16; rt += 4) {   // four row tiles: four independent chains
+          float av[4][KS];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) av[i][ks] = Ph[((rt + i) * 16) * Np4 + ks];
+          float4_t acc[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][ks], w[ks], acc[i], 0, 0, 0);
+          if (ok) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) oc[((rt + i) * 16 + r) * ndo] = acc[i][r];
+          }
+        }
+      }
+    }
+    if (tile == blockIdx.x) STAMP(1, 5);
+    __syncthreads();
+    if (tile == blockIdx.x) STAMP(1, 6);
+    if (a.phases & 4) rec_store<S>(a, a.pos_out + b0 * (int64_t)Tout * ndo, ob, nb, RTR);
+    if (tile == blockIdx.x) STAMP(1, 7);
+  }
+#ifdef BEAST_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(1, 8);
+#endif
+}
+
+// Per-trajectory basis rows (custom times per row, KS == 0): decode W into LDS, then a
+// sequential fma over n per output (the MFMA chain's order) on the VALU; also the
+// decode-only path when no positions are requested.
+template <int TBT>
+__global__ __launch_bounds__(NTHREADS) void k_reconstruct_rows(RecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Geom& g = a.g;
+  const int D = g.D, N = g.N, nj = g.nj, per = g.per;
+  const int Tout = a.Tout, ndo = a.ndo;
+  const bool pos = a.pos_out != nullptr;
+  const RecSmem L = rec_smem<TBT, 0, 0>(Tout, D, N, ndo, (nj < D) ? 2 : 1, a.lut_n);
+  const int Np4 = L.Np4;
+  const unsigned char* tokl = smem + L.tok;
+  float* pb = reinterpret_cast<float*>(smem + L.pb);
+  float* wlo = reinterpret_cast<float*>(smem + L.wlo);
+  float* whi = reinterpret_cast<float*>(smem + L.whi);
+  float* lut = reinterpret_cast<float*>(smem + L.lut);
+  uint16_t* pmap = reinterpret_cast<uint16_t*>(smem + L.pmap);
+  int* dst = reinterpret_cast<int*>(smem + L.dst);
+  int* col2d = reinterpret_cast<int*>(smem + L.col2d);
+  float* ob = reinterpret_cast<float*>(smem + L.out);
+  const int tid = threadIdx.x;
+  const float vm1 = (float)(a.vocab - 1);
+
+  if (blockIdx.x < a.ntiles) stage_tokens(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
+  dma4(wlo, a.w_min, per);
+  dma4(whi, a.w_max, per);
+  if (pos) dma4(dst, a.dof_dst, D);
   for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
   for (int r = tid; r < per; r += NTHREADS) {
     const int n = r / D, d = r - n * D;
     pmap[r] = (uint16_t)(d * Np4 + n);
-    kq[r] = (uint16_t)(d * N + n);
-    const int d2 = r / N, n2 = r - d2 * N;
-    kpb[r] = (uint16_t)(d2 * Np4 + n2);
   }
-  for (int e = tid; e < TBT * D * (Np4 - N); e += NTHREADS) {   // zero W pad columns once
-    const int row = e / (Np4 - N), n = N + (e - row * (Np4 - N));
-    pb[row * Np4 + n] = 0.0f;
-  }
-  if (pos && KS == 0) {   // per-row basis path: output column -> DoF (after the DMA of dst)
+  if (pos) {   // output column -> DoF (after the DMA of dst)
     __syncthreads();
     for (int c = tid; c < ndo; c += NTHREADS) col2d[c] = -1;
     __syncthreads();
@@ -463,131 +726,43 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
     }
   }
 
-  const int wave = tid >> 6, lane = tid & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-
   for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int64_t b0 = tile * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
-
-    // ---- the token tile lands in LDS (the first one is already in flight)
-    if ((a.phases & 1) && tile != blockIdx.x) stage_tokens(a, smem + L.tok, b0, per);
+    if (tile != blockIdx.x) stage_tokens(a, smem + L.tok, b0, per);
     __syncthreads();
-
-    // ---- decode (H6): (n d) tokens -> W[j][d][n], bit-exact discrete_to_continuous
-    if (a.phases & 16) {
-      const long long* tin = reinterpret_cast<const long long*>(smem + L.tok);
-      const float* fin = reinterpret_cast<const float*>(smem + L.tok);
-      for (int e = tid; e < nb * per; e += NTHREADS) {
-        const uint32_t j = fdiv(e, g.fd_per);
-        const int r = e - j * per;
-        const int po = pmap[r], k = kq[r];
-        float v;
-        if (a.ntokens) {
-          v = beast::denormalize_one(fin[e], wlo[k], whi[k]);
-        } else {
-          const long long t = tin[e] - a.tok_offset;
-          const float nrm = (t >= 0 && t < a.lut_n) ? lut[t] : __fdiv_rn((float)t, vm1);
-          const float lo = wlo[k], hi = whi[k];   // (max_val - min_val), beast/utils.py:24
-          v = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi, lo)), lo), lo, hi);
-        }
-        pb[j * D * Np4 + po] = v;
-      }
-    }
-    __syncthreads();
-    if (a.params_out != nullptr) {
-      float* pout = a.params_out + b0 * per;
-      for (int e = tid; e < nb * per; e += NTHREADS) {
-        const uint32_t j = fdiv(e, g.fd_per);
-        pout[e] = pb[j * D * Np4 + kpb[e - j * per]];
-      }
-    }
+    if (a.params_out != nullptr) rec_params_out(a, tokl, b0, nb, wlo, whi, lut, vm1);
     if (!pos) continue;
+    for (int e = tid; e < nb * per; e += NTHREADS) {   // (n d) tokens -> W[j][d][n]
+      const uint32_t j = fdiv(e, g.fd_per);
+      const int r = e - j * per;
+      const uint32_t n = fdiv(r, g.fd_D);
+      const int d = r - n * D;
+      pb[j * D * Np4 + pmap[r]] = rec_weight(a, tokl, e, d * N + n, wlo, whi, lut, vm1);
+    }
+    __syncthreads();
     if (a.init_p != nullptr) {   // coefficient 0 of the joint DoFs <- init_p (reference :505-510)
-      __syncthreads();
       for (int e = tid; e < nb * nj; e += NTHREADS) {
         const int j = e / nj, d = e - j * nj;
         pb[(j * D + d) * Np4] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];
       }
       __syncthreads();
     }
-
     float* gout = a.pos_out + b0 * (int64_t)Tout * ndo;
-    if constexpr (KS > 0) {
-      // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W).
-      //      A wave owns a column tile: W stays in registers while it walks pairs of row
-      //      tiles (two independent chains); rows past Tout land in ob's padding.
-      for (int q = wave; (a.phases & 2) && q < g.nq; q += NWAVES) {
-        int j, d, kind;
-        bool ok;
-        tile_col<TBT>(g, q, lr, j, d, kind, ok);
-        ok = ok && j < nb;
-        float w[KS];
-        const float* Wc = pb + (j * D + d) * Np4 + lk;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) w[ks] = Wc[4 * ks];
-        const float* Ph = phi + (kind * RTR + lr) * Np4 + lk;
-        float* oc = ob + (j * RTR + lk * 4) * ndo + min(max(dst[d], 0), ndo - 1);
-        for (int rt = 0; rt < RTR / 16; rt += 2) {
-          float a0[KS], a1[KS];
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-            a0[ks] = Ph[(rt * 16) * Np4 + 4 * ks];
-            a1[ks] = Ph[(rt * 16 + 16) * Np4 + 4 * ks];
-          }
-          float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[ks], w[ks], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[ks], w[ks], acc1, 0, 0, 0);
-          }
-          // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
-          if (ok) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              oc[(rt * 16 + r) * ndo] = acc0[r];
-              oc[(rt * 16 + 16 + r) * ndo] = acc1[r];
-            }
-          }
-        }
+    for (int e = tid; e < nb * Tout * ndo; e += NTHREADS) {
+      const int j = e / (Tout * ndo), r = e - j * Tout * ndo, t = r / ndo, c = r - t * ndo;
+      const int d = col2d[c];
+      float acc = 0.0f;
+      if (d >= 0) {
+        const int kind = (d < nj) ? 0 : 1;
+        const float* Phr = a.basis + (b0 + j) * a.basis_sb + (int64_t)kind * Tout * N + (int64_t)t * N;
+        const float* Wr = pb + (j * D + d) * Np4;
+        for (int n = 0; n < N; ++n) acc = fmaf(Phr[n], Wr[n], acc);
       }
-      __syncthreads();
-      if (a.phases & 4) {   // ob rows [0, Tout) of each trajectory -> contiguous HBM tile
-        const int rowlen = Tout * ndo;
-        if ((rowlen & 3) == 0 && ((RTR * ndo) & 3) == 0 && ((((uintptr_t)gout) & 15) == 0)) {
-          const int n4 = nb * rowlen / 4;
-          for (int i = tid; i < n4; i += NTHREADS) {
-            const uint32_t e = 4 * i;
-            const uint32_t j = fdiv(e, a.fd_row);
-            reinterpret_cast<float4*>(gout)[i] =
-                *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen));
-          }
-        } else {
-          for (int e = tid; e < nb * rowlen; e += NTHREADS) {
-            const uint32_t j = fdiv(e, a.fd_row);
-            gout[e] = ob[j * RTR * ndo + (e - j * rowlen)];
-          }
-        }
-      }
-    } else {
-      // per-trajectory basis (custom times per row): sequential fma over n, the MFMA chain's order
-      for (int e = tid; (a.phases & 2) && e < nb * Tout * ndo; e += NTHREADS) {
-        const int j = e / (Tout * ndo), r = e - j * Tout * ndo, t = r / ndo, c = r - t * ndo;
-        const int d = col2d[c];
-        float acc = 0.0f;
-        if (d >= 0) {
-          const int kind = (d < nj) ? 0 : 1;
-          const float* Phr = a.basis + (b0 + j) * a.basis_sb + (int64_t)kind * Tout * N + (int64_t)t * N;
-          const float* Wr = pb + (j * D + d) * Np4;
-          for (int n = 0; n < N; ++n) acc = fmaf(Phr[n], Wr[n], acc);
-        }
-        if (L.stage) ob[e] = acc; else gout[e] = acc;
-      }
-      if (L.stage && (a.phases & 4)) {
-        __syncthreads();
-        store_out(gout, ob, nb * Tout * ndo);
-      }
+      if (L.stage) ob[e] = acc; else gout[e] = acc;
     }
+    __syncthreads();
+    if (L.stage) store_out(gout, ob, nb * Tout * ndo);   // (per-row path: DynShape)
   }
 }
 
@@ -620,7 +795,11 @@ int64_t grid_for(int64_t ntiles, int lds_bytes) {
   return std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cu_count() * per_cu * 2));
 }
 
-template <int TBT>
+// Diagnostic / test knob (beast_set_option): run the runtime-shape kernels even where a
+// specialised one exists.
+bool g_generic_only = false;
+
+template <int TBT, class S>
 int launch_encode_t(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t s) {
   a.g = make_geom<TBT>(D, nj, N, T);
   a.ntiles = (a.B + TBT - 1) / TBT;
@@ -628,14 +807,15 @@ int launch_encode_t(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream
   const EncSmem L = enc_smem<TBT>(T, a.g.Tp, Dl, D, N, nj < D ? 2 : 1);
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "encode tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
-  if (fast) hipLaunchKernelGGL((k_encode<TBT, true>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else hipLaunchKernelGGL((k_encode<TBT, false>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  if (fast) hipLaunchKernelGGL((k_encode<TBT, true, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  else hipLaunchKernelGGL((k_encode<TBT, false, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
   BEAST_LAUNCHED("k_encode");
   return BEAST_OK;
 }
 
 // Tile size: the largest of 8/4/2/1 trajectories whose rows fit 32 KB of LDS
-// (BEAST_ENC_TBT overrides, for measurements).
+// (BEAST_ENC_TBT overrides, for measurements).  The BEAST default shapes (T = 50,
+// N = 10, D = 14 with 0 or 2 gripper DoF, D = 7) run fully specialised kernels.
 int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   const int64_t traj_bytes = (int64_t)T * a.row_elems * 4;
   const bool contiguous = a.sd == 1 && a.st == a.row_elems && a.sb == (int64_t)T * a.row_elems &&
@@ -649,22 +829,38 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   const bool fast = contiguous && tbt * traj_bytes <= 32 * 1024;
   if (!fast) tbt = 8;
   if (forced == 1 || forced == 2 || forced == 4 || (forced == 8 && fast)) tbt = std::min(tbt, forced);
+  if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
+    if (D == 14 && nj == 14) return launch_encode_t<8, Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, true, s);
+    if (D == 14 && nj == 12) return launch_encode_t<8, Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, true, s);
+    if (D == 7 && nj == 7) return launch_encode_t<8, Shape<7, 7, 10, 50, 7>>(a, T, D, nj, N, true, s);
+  }
   switch (tbt) {
-    case 1: return launch_encode_t<1>(a, T, D, nj, N, fast, s);
-    case 2: return launch_encode_t<2>(a, T, D, nj, N, fast, s);
-    case 4: return launch_encode_t<4>(a, T, D, nj, N, fast, s);
-    default: return launch_encode_t<8>(a, T, D, nj, N, fast, s);
+    case 1: return launch_encode_t<1, DynShape>(a, T, D, nj, N, fast, s);
+    case 2: return launch_encode_t<2, DynShape>(a, T, D, nj, N, fast, s);
+    case 4: return launch_encode_t<4, DynShape>(a, T, D, nj, N, fast, s);
+    default: return launch_encode_t<8, DynShape>(a, T, D, nj, N, fast, s);
   }
 }
 
-template <int TBT, int KS>
+template <int TBT, int KS, int RT, class S = DynShape>
 int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
-  const RecSmem L = rec_smem<TBT, KS>(a.Tout, D, a.g.N, a.ndo, nj < D ? 2 : 1, a.lut_n);
+  const RecSmem L = rec_smem<TBT, KS, RT>(a.Tout, D, a.g.N, a.ndo, nj < D ? 2 : 1, a.lut_n);
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
-  hipLaunchKernelGGL((k_reconstruct<TBT, KS>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  if constexpr (KS == 0) hipLaunchKernelGGL((k_reconstruct_rows<TBT>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  else hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
   BEAST_LAUNCHED("k_reconstruct");
   return BEAST_OK;
+}
+
+template <int TBT, int RT>
+int launch_rec_mfma(RecArgs a, int D, int nj, int N, hipStream_t s) {
+  switch ((N + 3) / 4) {
+    case 1: return launch_rec_ks<TBT, 1, RT>(a, D, nj, s);
+    case 2: return launch_rec_ks<TBT, 2, RT>(a, D, nj, s);
+    case 3: return launch_rec_ks<TBT, 3, RT>(a, D, nj, s);
+    default: return launch_rec_ks<TBT, 4, RT>(a, D, nj, s);
+  }
 }
 
 template <int TBT>
@@ -675,15 +871,18 @@ int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t
   a.fd_row = make_fd((uint32_t)(a.Tout * a.ndo));
   a.lut_n = (a.ntokens == nullptr && a.vocab <= LUT_MAX) ? a.vocab : 0;
   const bool pos = a.pos_out != nullptr;
-  // MFMA path needs the shared basis and the padded output tile in LDS
-  const bool mfma = shared && pos && rec_smem<TBT, 4>(a.Tout, D, N, a.ndo, 2, a.lut_n).total <= 112 * 1024;
-  if (!mfma) return launch_rec_ks<TBT, 0>(a, D, nj, s);
-  switch ((N + 3) / 4) {
-    case 1: return launch_rec_ks<TBT, 1>(a, D, nj, s);
-    case 2: return launch_rec_ks<TBT, 2>(a, D, nj, s);
-    case 3: return launch_rec_ks<TBT, 3>(a, D, nj, s);
-    default: return launch_rec_ks<TBT, 4>(a, D, nj, s);
+  // MFMA path: shared basis, positions requested, the padded output tile fits LDS
+  const bool mfma = shared && pos && rec_smem<TBT, 4, 0>(a.Tout, D, N, a.ndo, 2, a.lut_n).total <= 112 * 1024;
+  if (!mfma) return launch_rec_ks<TBT, 0, 0>(a, D, nj, s);
+  if (a.Tout <= 16 * RT_REG) {
+    if (!g_generic_only && N == 10 && a.Tout == 50 && a.ndo == D) {
+      if (D == 14 && nj == 14) return launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14>>(a, D, nj, s);
+      if (D == 14 && nj == 12) return launch_rec_ks<TBT, 3, RT_REG, Shape<14, 12, 10, 50, 14>>(a, D, nj, s);
+      if (D == 7 && nj == 7) return launch_rec_ks<TBT, 3, RT_REG, Shape<7, 7, 10, 50, 7>>(a, D, nj, s);
+    }
+    return launch_rec_mfma<TBT, RT_REG>(a, D, nj, N, s);
   }
+  return launch_rec_mfma<TBT, 0>(a, D, nj, N, s);
 }
 
 
@@ -734,4 +933,16 @@ extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, in
   a.dof_dst = dof_dst; a.init_p = init_p; a.init_p_src = init_p_src; a.params_out = params_out; a.pos_out = pos_out;
   const bool shared = (basis_sb == 0);
   return launch_reconstruct<8>(a, D, n_joint, N, shared, beast::as_stream(stream));
+}
+
+#ifdef BEAST_STAMPS
+extern "C" int beast_stamps_read(unsigned long long* out) {   // [2][NWAVES][16]
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
+
+extern "C" int beast_set_option(int option, int value) {
+  BEAST_REQUIRE(option == BEAST_OPT_GENERIC_KERNELS, "unknown option %d", option);
+  g_generic_only = value != 0;
+  return BEAST_OK;
 }

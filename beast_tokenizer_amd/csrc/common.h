@@ -51,6 +51,38 @@ __device__ __forceinline__ long long quantize_scaled(float p, float lo, float hi
   return (long long)r;
 }
 
+// quantize_one as a bin index: the same ops, int32 result, INT32_MIN for NaN (widened
+// to ATen's INT64_MIN by the caller).
+__device__ __forceinline__ int quantize_bin(float p, float lo, float hi, float vm1) {
+  const float x = clamp_t(p, lo, hi);
+  float s = __fsub_rn(hi, lo);
+  s = (s < 1e-8f) ? 1e-8f : s;
+  float u = __fdiv_rn(__fsub_rn(x, lo), s);
+  u = (u < 0.0f) ? 0.0f : u;
+  u = (1.0f < u) ? 1.0f : u;
+  const float r = rintf(__fmul_rn(u, vm1));
+  return (r != r) ? (int)0x80000000 : (int)r;
+}
+
+// quantize_bin through a reciprocal: va = (x - lo) * (vm1 * rcp(s)) is within 3.6e-7 * vm1
+// of the exactly-rounded chain's u * vm1, so whenever va is farther than 2^-20 * vm1 from
+// a rounding boundary (k + 0.5) both round to the same bin; otherwise -- and for NaN /
+// inf -- the exact chain decides.  Bit-identical to quantize_bin for every input.
+__device__ __forceinline__ int quantize_bin_fast(float p, float lo, float hi, float vm1) {
+  const float x = clamp_t(p, lo, hi);
+  float s = __fsub_rn(hi, lo);
+  s = (s < 1e-8f) ? 1e-8f : s;
+  const float va = __fmul_rn(__fsub_rn(x, lo), __fmul_rn(vm1, __builtin_amdgcn_rcpf(s)));
+  const float f = __fsub_rn(va, floorf(va));
+  if (fabsf(__fsub_rn(f, 0.5f)) > 9.5367431640625e-7f * vm1) return (int)rintf(fminf(va, vm1));
+  return quantize_bin(p, lo, hi, vm1);
+}
+
+__device__ __forceinline__ long long widen_bin(int bin, unsigned long long offset) {
+  const unsigned long long v = (bin == (int)0x80000000) ? 0x8000000000000000ULL : (unsigned long long)(long long)bin;
+  return (long long)(v + offset);   // two's-complement wrap, as ATen's int64 add
+}
+
 // beast/utils.py:23-25, one element: int64 -> fp32, div, mul, add, clamp.
 __device__ __forceinline__ float dequantize_one(long long tok, float lo, float hi, float vm1) {
   float n = __fdiv_rn((float)tok, vm1);

@@ -42,6 +42,13 @@ extern "C" {
 int beast_abi_version(void);
 const char* beast_last_error(void);
 
+/* Process-wide tuning / test options.  BEAST_OPT_GENERIC_KERNELS = 1 makes encode and
+ * reconstruct use their runtime-shape kernels even where a shape-specialised kernel
+ * exists (the BEAST defaults T = 50, N = 10, D = 7 / 14); results are identical.
+ * Not thread-safe with concurrent launches. */
+#define BEAST_OPT_GENERIC_KERNELS 1
+int beast_set_option(int option, int value);
+
 /* ---------------------------------------------------------------- H1/H2 ---
  * Replaces UniBSplineBasis.basis (MP_lite_PyTorch/mp_pytorch/basis_gn/
  * uni_bspline_basis.py:59-113) with LinearPhaseGenerator.phase

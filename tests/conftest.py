@@ -45,3 +45,13 @@ def gpu_device():
     from beast_tokenizer_amd import _lib
     _lib.load()
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(params=["specialised", "generic"])
+def kernel_mode(request):
+    """Run a parity test on the shape-specialised kernels and on the runtime-shape ones."""
+    from beast_tokenizer_amd import _lib
+    lib = _lib.load()
+    lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 1 if request.param == "generic" else 0)
+    yield request.param
+    lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0)

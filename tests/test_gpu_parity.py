@@ -80,7 +80,7 @@ def test_basis_bitexact(name, golden, gpu_device):
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_encode_params_and_tokens(name, golden, gpu_device):
+def test_encode_params_and_tokens(name, golden, gpu_device, kernel_mode):
     g = golden[name]
     tok = make_tok(name, g, gpu_device)
     x = g["x"]
@@ -127,7 +127,7 @@ def test_quantize_bitexact_on_reference_params(name, golden, gpu_device):
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_decode_bitexact(name, golden, gpu_device):
+def test_decode_bitexact(name, golden, gpu_device, kernel_mode):
     g = golden[name]
     tok = make_tok(name, g, gpu_device)
     dec = tok.decode(torch.from_numpy(g["tokens"])).cpu().numpy()
@@ -148,7 +148,7 @@ def _close_pos(a, b):
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
-def test_reconstruct(name, golden, gpu_device):
+def test_reconstruct(name, golden, gpu_device, kernel_mode):
     g = golden[name]
     tok = make_tok(name, g, gpu_device)
     toks = torch.from_numpy(g["tokens"])
@@ -187,7 +187,7 @@ def test_reconstruct_per_row_times(name, golden, gpu_device):
 
 
 @pytest.mark.parametrize("name", ["k2", "k3"])
-def test_flip_census_4096(name, gpu_device):
+def test_flip_census_4096(name, gpu_device, kernel_mode):
     """Full BASELINE size: tokens vs the reference's, every flip a rounding tie."""
     z = load_npz(f"tokens4096_{name}.npz")
     gi = CONFIGS[name]["gripper_indices"] or []
@@ -199,6 +199,59 @@ def test_flip_census_4096(name, gpu_device):
     tokens, _ = tok.encode(torch.from_numpy(x))
     n = check_token_flips(tokens.cpu().numpy(), z["tokens"].astype(np.int64), x, g, name, max_flips=60)
     print(f"{name}: {n} tie flips of {tokens.numel()} tokens")
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_specialised_kernels_equal_generic(name, gpu_device):
+    """The shape-specialised encode / reconstruct kernels compute exactly what the
+    runtime-shape kernels compute (same operation order): bitwise-equal outputs."""
+    from beast_tokenizer_amd import _lib
+    lib = _lib.load()
+    gi = CONFIGS[name]["gripper_indices"] or []
+    g = dict(load_npz(f"bspline_{name}.npz"))
+    tok = make_tok(name, g, gpu_device)
+    x = torch.from_numpy(synth_trajectories(1000, 50, CONFIGS[name]["num_dof"], seed=3, gripper_indices=gi))
+    outs = []
+    for generic in (0, 1):
+        lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, generic)
+        try:
+            t, pd = tok.encode(x)
+            pos = tok.reconstruct_traj(t)
+            outs.append((t.cpu().numpy(), pd["params"].cpu().numpy(), pos.cpu().numpy()))
+        finally:
+            lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("vocab", [256, 1024, 4096])
+def test_encode_quantiser_exact_near_ties(vocab, gpu_device, kernel_mode):
+    """The encode kernel's in-lane quantiser (reciprocal fast path + exact fallback) must
+    equal continuous_to_discrete on its own params bit for bit.  Trajectories are built
+    as y = Phi w with w on or next to rounding ties (k + 0.5) of the bins, plus NaN /
+    inf / degenerate-range columns."""
+    rng = np.random.default_rng(vocab)
+    B, T, D, N = 2048, 50, 7, 10
+    tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=vocab, device=str(gpu_device))
+    lo = rng.uniform(-2, 0, size=D * N).astype(np.float32)
+    hi = (lo + rng.uniform(0.5, 3, size=D * N)).astype(np.float32)
+    hi[3] = lo[3]                                   # degenerate range: scale clamps to 1e-8
+    tok.load_state_dict({"w_min": lo.tolist(), "w_max": hi.tolist()})
+    # targets on ties: u * (vocab - 1) = k + 0.5 (+ a few ulps either way)
+    k = rng.integers(0, vocab - 1, size=(B, D * N))
+    u = (k + 0.5 + rng.choice([0, 1e-7, -1e-7, 3e-6, -3e-6], size=k.shape)) / (vocab - 1)
+    w = (lo + u * (hi - lo)).astype(np.float64)                     # [B, (d n)]
+    phi = O.basis(O.times_grid(2 * np.pi, T), np.float32(2 * np.pi), 4, N).astype(np.float64)   # [T, N]
+    y = np.einsum("tn,bdn->btd", phi, w.reshape(B, D, N)).astype(np.float32)
+    y[5, 7, 2] = np.nan                             # NaN params for DoF 2 of trajectory 5
+    y[9, :, 4] = np.inf                             # inf / NaN params for DoF 4 of trajectory 9
+    tokens, pd = tok.encode(torch.from_numpy(y))
+    params = pd["params"].cpu().numpy()
+    want = O.continuous_to_discrete(O._clamp_t(params, lo, hi), lo, hi, vocab)
+    want = want.reshape(B, D, N).transpose(0, 2, 1).reshape(B, N * D)
+    assert np.array_equal(tokens.cpu().numpy(), want)
+    near = np.abs(O.normalized_units(params, lo, hi, vocab) % 1.0 - 0.5) < 1e-4
+    assert near.sum() > B   # the fast path's fallback really was exercised
 
 
 @pytest.mark.parametrize("name", ["k2", "k3"])

@@ -44,3 +44,31 @@ out = {
     "no_grad_ctx": t(lambda: torch.no_grad().__enter__()),
 }
 print(json.dumps(out))
+
+# ---- the tokenizer's own path, piece by piece (B=4096, D=14)
+from beast_tokenizer_amd import BEASTBsplineTokenizer  # noqa: E402
+tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
+x = torch.randn(4096, 50, 14, device=dev)
+pl = tok._plan()
+params = torch.empty((4096, 140), device=dev)
+tokens = torch.empty((4096, 140), dtype=torch.int64, device=dev)
+xp, pp, tp = x.data_ptr(), params.data_ptr(), tokens.data_ptr()
+
+
+def enc_call():
+    pl.enc(xp, 4096, 50, 700, 14, 1, 14, 14, 14, pl.p_src, pl.p_proj, 10, pl.p_wmn, pl.p_wmx, 256, 0, pp, tp,
+           torch._C._cuda_getCurrentRawStream(0))
+
+
+tok_rows, _ = tok.encode(x)
+out2 = {
+    "enc_ctypes_plus_launch": t(enc_call, 5000),
+    "plan_lookup": t(lambda: tok._plan()),
+    "dev_lookup": t(lambda: tok._dev()),
+    "fit": t(lambda: tok._fit(x, 0, pl), 5000),
+    "encode": t(lambda: tok.encode(x), 5000),
+    "token_rows": t(lambda: tok._token_rows(tok_rows, pl.dev)),
+    "reconstruct_traj": t(lambda: tok.reconstruct_traj(tok_rows), 5000),
+}
+torch.cuda.synchronize()
+print(json.dumps(out2))

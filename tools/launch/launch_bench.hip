@@ -1,0 +1,81 @@
+// Host cost of one kernel launch by different HIP entry points (tools only).
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+struct Args { char pad[224]; };
+
+__global__ void k_spin(long long cycles) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < cycles) {}
+}
+
+__global__ void k_noop(Args a) {
+  if (a.pad[0] == 123 && threadIdx.x == 9999) a.pad[1] = 0;
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+template <class F>
+double host_us(F f, int n) {
+  for (int i = 0; i < 200; ++i) f();
+  hipDeviceSynchronize();
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n; ++i) f();
+  auto t1 = std::chrono::steady_clock::now();
+  hipDeviceSynchronize();
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / n;
+}
+
+int main() {
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  Args a;
+  memset(&a, 0, sizeof(a));
+  const int n = 20000;
+  printf("{\"hipLaunchKernelGGL_512\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a); }, n));
+  printf("\"hipLaunchKernelGGL_1\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s, a); }, n));
+  printf("\"hipLaunchKernelGGL_512_dynlds\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 40000, s, a); }, n));
+  void* args[] = {&a};
+  printf("\"hipLaunchKernel\": %.3f, ", host_us([&] { hipLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s); }, n));
+  hipFunction_t f;
+  CK(hipGetFuncBySymbol(&f, (const void*)k_noop));
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  printf("\"hipModuleLaunchKernel_extra\": %.3f, ", host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, nullptr, cfg); }, n));
+  printf("\"hipModuleLaunchKernel_params\": %.3f, ", host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, args, nullptr); }, n));
+  printf("\"hipExtLaunchKernel\": %.3f, ", host_us([&] { hipExtLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s, nullptr, nullptr, 0); }, n));
+  // null stream
+  printf("\"GGL_null_stream\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, 0, a); }, n));
+  // graph of 2 kernels
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a);
+  CK(hipStreamEndCapture(s, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  printf("\"graph2_launch\": %.3f, ", host_us([&] { hipGraphLaunch(ge, s); }, n));
+  // device-side throughput of back-to-back launches
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
+  hipEventRecord(e0, s);
+  for (int i = 0; i < 2000; ++i) hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a);
+  hipEventRecord(e1, s);
+  hipEventSynchronize(e1);
+  float ms; hipEventElapsedTime(&ms, e0, e1);
+  printf("\"gpu_us_per_noop_512\": %.3f, ", ms * 1000 / 2000);
+  // queue pre-filled behind a spin: the GPU's own per-kernel cadence
+  for (int grid : {1, 512, 2048}) {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 200000000LL);
+    hipEventRecord(e0, s);
+    for (int i = 0; i < 1000; ++i) hipLaunchKernelGGL(k_noop, dim3(grid), dim3(256), 0, s, a);
+    hipEventRecord(e1, s);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("\"gpu_us_per_noop_queued_grid%d\": %.3f, ", grid, ms * 1000 / 1000);
+  }
+  printf("\"end\": 0}\n");
+  return 0;
+}

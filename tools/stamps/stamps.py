@@ -1,0 +1,88 @@
+"""Phase timeline of workgroup 0 of k_encode / k_reconstruct from in-kernel s_memtime
+stamps (a -DBEAST_STAMPS build of csrc/, this tool only; the product compiles them out).
+
+    python tools/stamps/stamps.py [B ...]
+"""
+import ctypes as C
+import glob
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+NW = 4   # waves per workgroup (NTHREADS / 64 in csrc/codec.hip)
+ENC = ["start", "issued", "landed", "mfma_done", "pb_ready", "params_stored", "tokens_stored", "drained", "-",
+       "y_dma", "p_dma", "small_dma", "t2_landed", "t2_mfma_done", "t2_tokens_stored"]
+REC = ["start", "issued", "landed", "decoded", "w_ready", "mfma_done", "ob_ready", "stored", "drained",
+       "tok_dma", "small_dma", "phi_loads", "lut"]
+
+
+def build():
+    from beast_tokenizer_amd import _build
+    so = os.path.join(HERE, "libbeast_stamps.so")
+    objs = []
+    for src in glob.glob(os.path.join(REPO, "beast_tokenizer_amd", "csrc", "*.hip")):
+        o = os.path.join(HERE, os.path.basename(src) + ".o")
+        subprocess.run([_build._hipcc(), *_build.CXXFLAGS, "-DBEAST_STAMPS", "-c", src, "-o", o], check=True)
+        objs.append(o)
+    subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-o", so, *objs], check=True)
+    return so
+
+
+def main():
+    import torch
+    from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib
+    from beast_tokenizer_amd.synthetic import synth_trajectories
+    lib = C.CDLL(build())
+    for name, (res, args) in _lib.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    lib.beast_stamps_read.argtypes = [C.c_void_p]
+    dev = torch.device("cuda", 0)
+    tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
+    p = tok._plan()
+    stamps = (C.c_ulonglong * (2 * NW * 16))()
+    lib.beast_stamps_read(stamps)
+    sizes = [int(v) for v in sys.argv[1:]] or [4096, 1048576]
+    s = torch._C._cuda_getCurrentRawStream(0)
+    out = {}
+    for B in sizes:
+        x = torch.from_numpy(synth_trajectories(min(B, 65536), 50, 14, seed=0)).to(dev)
+        if B > 65536:
+            x = x.repeat(B // 65536, 1, 1)
+        params = torch.empty((B, 140), device=dev)
+        tokens = torch.empty((B, 140), dtype=torch.int64, device=dev)
+        pos = torch.empty((B, 50, 14), device=dev)
+
+        def enc():
+            return lib.beast_encode_f32(x.data_ptr(), B, 50, 700, 14, 1, 14, 14, 14, p.p_src, p.p_proj, 10, p.p_wmn,
+                                        p.p_wmx, 256, 0, params.data_ptr(), tokens.data_ptr(), s)
+
+        def enc_params_only():
+            return lib.beast_encode_f32(x.data_ptr(), B, 50, 700, 14, 1, 14, 14, 14, p.p_src, p.p_proj, 10, p.p_wmn,
+                                        p.p_wmx, 256, 0, params.data_ptr(), None, s)
+
+        def rec():
+            return lib.beast_reconstruct_f32(tokens.data_ptr(), B, 14, 14, 10, 256, 0, p.p_wmn, p.p_wmx, p.p_phi, 0,
+                                             50, p.p_dst, 14, None, 0, None, None, pos.data_ptr(), None, s)
+        res = {}
+        for kname, fn, names, k in (("encode", enc, ENC, 0), ("encode_params_only", enc_params_only, ENC, 0),
+                                    ("reconstruct", rec, REC, 1)):
+            for _ in range(20):           # warm: code, constants and the tile in L2 as in back-to-back use
+                assert fn() == 0
+            torch.cuda.synchronize()
+            assert lib.beast_stamps_read(stamps) == 0
+            v = [stamps[(k * NW + w) * 16: (k * NW + w) * 16 + 16] for w in range(NW)]
+            t0 = min(v[w][0] for w in range(NW))
+            res[kname] = {names[i]: [int(v[w][i] - t0) if v[w][i] >= t0 else None for w in range(NW)]
+                          for i in range(len(names)) if names[i] != "-"}
+        out[B] = res
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
