@@ -230,7 +230,8 @@ def main():
             pmc = json.load(f)
         traffic = pmc.get(kname, {}).get("hbm_bytes_per_launch")
     roof = {"bound": "hbm", "kernel": kname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK, "traffic": traffic, "algo_bytes_per_launch": kbytes,
+            "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
+            "algo_bytes_per_launch": kbytes,
             "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
 
     bpe = None
