@@ -113,27 +113,82 @@ class GpuBpeOps:
         _lib.run("beast_bpe_pretok_emit", tokens.data_ptr(), seq_off.data_ptr(), S, mn, lut_d.data_ptr(),
                  lut_d.numel(), woff.data_ptr(), soff.data_ptr(), b2i.data_ptr(), sym.data_ptr(), wstart.data_ptr(),
                  wlen.data_ptr(), s)
-        return {"sym": sym, "wstart": wstart, "wlen": wlen, "n_words": nw, "n_syms": ns}
+        return {"sym": sym, "wstart": wstart, "wlen": wlen, "wcount": None, "n_words": nw, "n_syms": ns}
+
+    def dedup(self, words):
+        """Distinct words of >= 2 symbols x their counts (HF trains on word counts)."""
+        n = words["n_words"]
+        dev, s = self.device, self.stream
+        ws = torch.empty(_lib.load().beast_bpe_dedup_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        m = max(n, 1)
+        ow = torch.empty(m, dtype=torch.int32, device=dev)
+        ol = torch.empty(m, dtype=torch.int32, device=dev)
+        oc = torch.empty(m, dtype=torch.int32, device=dev)
+        on = torch.empty(1, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_dedup_words", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                 n, ws.data_ptr(), ws.numel(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), on.data_ptr(), s)
+        nu = self._read_i64(on, 1)[0]
+        del ws
+        # contiguous, length-ordered copy of the distinct words (coalesced merge scans)
+        ws = torch.empty(_lib.load().beast_bpe_repack_workspace_bytes(nu), dtype=torch.uint8, device=dev)
+        m = max(nu, 1)
+        sym2 = torch.empty(max(words["n_syms"], 1), dtype=torch.int16, device=dev)
+        w2, l2, c2 = (torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3))
+        _lib.run("beast_bpe_repack_words", words["sym"].data_ptr(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), nu,
+                 ws.data_ptr(), ws.numel(), sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), c2.data_ptr(),
+                 on.data_ptr(), s)
+        ns = self._read_i64(on, 1)[0]
+        del ws, ow, ol, oc
+        sym2 = sym2[:max(ns, 1)].clone()
+        sig = torch.empty(m, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_word_signatures", sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), nu, sig.data_ptr(), s)
+        return dict(words, sym=sym2, wstart=w2, wlen=l2, wcount=c2, sig=sig, n_words=nu, n_distinct=nu,
+                    n_syms_distinct=ns)
+
+    def compact(self, words):
+        """Drop words with < 2 symbols left (they can no longer merge)."""
+        n = words["n_words"]
+        if n == 0:
+            return words
+        dev = self.device
+        ow = torch.empty(n, dtype=torch.int32, device=dev)
+        ol = torch.empty(n, dtype=torch.int32, device=dev)
+        oc = torch.empty(n, dtype=torch.int32, device=dev)
+        on = torch.empty(1, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_compact_words", words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                 _lib.ptr(words["wcount"]), n, ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), on.data_ptr(), self.stream)
+        m = self._read_i64(on, 1)[0]
+        out = dict(words, wstart=ow[:max(m, 1)], wlen=ol[:max(m, 1)], wcount=oc[:max(m, 1)], n_words=m)
+        if words.get("sig") is not None:
+            out["sig"] = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+            _lib.run("beast_bpe_word_signatures", words["sym"].data_ptr(), out["wstart"].data_ptr(),
+                     out["wlen"].data_ptr(), m, out["sig"].data_ptr(), self.stream)
+        return out
 
     def count_pairs(self, words, Vt: int) -> torch.Tensor:
         table = torch.zeros(Vt * Vt, dtype=torch.int32, device=self.device)
         _lib.run("beast_bpe_count_pairs", words["sym"].data_ptr(), words["wstart"].data_ptr(),
-                 words["wlen"].data_ptr(), None, words["n_words"], table.data_ptr(), Vt, self.stream)
+                 words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")), words["n_words"], table.data_ptr(), Vt,
+                 self.stream)
         return table
 
     def new_state(self, Vt: int, tlen: np.ndarray):
-        self._res = torch.zeros(1, dtype=torch.int64, device=self.device)
+        nb = _lib.load().beast_bpe_argmax_workspace_bytes(Vt)
+        self._argws = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=self.device)
+        self._calls = 0
         self._deltas = torch.zeros(4 * Vt, dtype=torch.int32, device=self.device)
         self._tlen = torch.from_numpy(tlen.astype(np.int32)).to(self.device)
 
     def argmax(self, table: torch.Tensor, Vt: int, vcur: int) -> int:
-        _lib.run("beast_bpe_argmax", table.data_ptr(), Vt, vcur, self._res.data_ptr(), self.stream)
-        return self._read_i64(self._res, 1)[0] & 0xFFFFFFFFFFFFFFFF
+        k = self._calls
+        self._calls += 1
+        _lib.run("beast_bpe_argmax", table.data_ptr(), Vt, vcur, self._argws.data_ptr(), k, self.stream)
+        return self._read_i64(self._argws[2 + (k & 1):], 1)[0] & 0xFFFFFFFFFFFFFFFF
 
     def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int) -> torch.Tensor:
         _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
-                 None, words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len, self._deltas.data_ptr(), Vt,
-                 self.stream)
+                 _lib.ptr(words.get("wcount")), words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len,
+                 self._deltas.data_ptr(), Vt, _lib.ptr(words.get("sig")), self.stream)
         return self._deltas
 
     def apply(self, table: torch.Tensor, deltas: torch.Tensor, Vt: int, a: int, b: int, nid: int) -> None:
@@ -167,7 +222,7 @@ def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special
 def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
-              mn_mx: Optional[Tuple[int, int]] = None) -> BPEResult:
+              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0) -> BPEResult:
     """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard)."""
     import time
     t0 = time.perf_counter()
@@ -199,6 +254,9 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         raise NotImplementedError(f"dense pair table needs Vt <= 32768 (got {Vt})")
     lut = class_lut(n_cp)
     words = ops.pretokenize(tokens, seq_off, mn, lut, byte2id)
+    n_words, n_syms = words["n_words"], words["n_syms"]
+    if hasattr(ops, "dedup"):
+        words = ops.dedup(words)
     table = ops.count_pairs(words, Vt)
     reduce(table, "sum")
     tlen = np.zeros(Vt, dtype=np.int64)
@@ -225,9 +283,12 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         deltas = ops.merge(words, a, b, nid, max_len, Vt)
         reduce(deltas, "sum")
         ops.apply(table, deltas, Vt, a, b, nid)
+        if compact_every and len(merges) % compact_every == 0 and hasattr(ops, "compact"):
+            words = ops.compact(words)
     t2 = time.perf_counter()
-    stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": words["n_words"],
-             "n_syms": words["n_syms"], "Vt": Vt}
+    stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
+             "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
+             "Vt": Vt}
     return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
 
 

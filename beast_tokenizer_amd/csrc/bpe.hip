@@ -12,7 +12,9 @@
 //                            in place; HF's pair-count changes are accumulated in
 //                            LDS-privatised delta vectors [4][Vt] and flushed once
 //                            per workgroup
-//   k_apply                  table += deltas, retire the merged pair
+//   k_apply                  table += deltas; zero the merged pair (retired)
+//   k_dedup_*                distinct words x counts (HF trains on word counts)
+//   k_compact_words          drop words that can no longer merge (< 2 symbols)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -243,32 +245,58 @@ __global__ void k_count_pairs(const uint16_t* __restrict__ sym, const uint32_t* 
 
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
-__global__ void k_argmax(const uint32_t* __restrict__ table, int Vt, int vcur, unsigned long long* __restrict__ res) {
+// ARG_TPR threads per row, 8 entries each (two 16-B loads in flight per thread, no
+// division); each workgroup folds its best into ws[2 + parity] with one atomicMax only when
+// it beats the value already there.  Result slots alternate between calls: call k writes
+// slot k & 1 and zeroes the other for call k + 1 (ws[1] = call counter), so no memset.
+constexpr int ARG_TPR = 256;
+__global__ __launch_bounds__(256) void k_argmax(const uint32_t* __restrict__ table, int Vt, int vcur,
+                                                unsigned long long* __restrict__ ws, int parity) {
   __shared__ unsigned long long sh[4];
+  const int x = blockIdx.x;
+  const uint32_t* row = table + (size_t)x * Vt;
   unsigned long long best = 0;
-  const int64_t total = (int64_t)vcur * vcur;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int x = (int)(e / vcur), y = (int)(e % vcur);
-    const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
-    const uint32_t c = table[idx];
-    if (c) best = umax64(best, ((unsigned long long)c << 32) | (unsigned long long)(~idx));
+  if (blockIdx.x == 0 && threadIdx.x == 0) ws[2 + (parity ^ 1)] = 0ull;
+  for (int y0 = threadIdx.x * 8; y0 < vcur; y0 += ARG_TPR * 8) {
+    uint32_t c[8];
+    if (((Vt & 3) == 0) && y0 + 8 <= vcur) {
+      const uint4 u0 = *reinterpret_cast<const uint4*>(row + y0);
+      const uint4 u1 = *reinterpret_cast<const uint4*>(row + y0 + 4);
+      c[0] = u0.x; c[1] = u0.y; c[2] = u0.z; c[3] = u0.w; c[4] = u1.x; c[5] = u1.y; c[6] = u1.z; c[7] = u1.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] = y0 + k < vcur ? row[y0 + k] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)(y0 + k);
+      if (c[k]) best = umax64(best, ((unsigned long long)c[k] << 32) | (unsigned long long)(~idx));
+    }
   }
   for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) best = umax64(best, sh[k]);
-    if (best) atomicMax(res, best);
+    for (int k = 1; k < 4; ++k) best = umax64(best, sh[k]);
+    unsigned long long* slot = ws + 2 + parity;
+    if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
   }
 }
 
 // ------------------------------------------------------------------ merge --
 // LDS-privatised deltas when 4*Vt int32 fit in 64 KiB, else global atomics.
+// Deltas go to LDS (LDS = true, 4*Vt int32 <= 64 KiB) and are flushed once per workgroup
+// into deltas[] with contiguous atomics (multi-GPU: all-reduced, then beast_bpe_apply).
+// (A last-workgroup-applies variant was measured slower: every workgroup's device-scope
+// fence writes back its XCD's L2.)
+__device__ __forceinline__ unsigned long long sig_bit(uint32_t x) { return 1ull << (x & 63u); }
+
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
-                                               int64_t nw, int a, int b, int nid, const uint32_t* __restrict__ tlen,
-                                               int max_len, int32_t* __restrict__ deltas, int Vt) {
+                                               int64_t nw, int a, int b, int nid, uint32_t* __restrict__ tlen,
+                                               int max_len, int32_t* __restrict__ deltas, int Vt,
+                                               unsigned long long* __restrict__ sig) {
   extern __shared__ __attribute__((aligned(16))) int32_t dl[];
   __shared__ int touched;
   int32_t* dv = LDS ? dl : deltas;
@@ -283,14 +311,22 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   int32_t* rowB = dv + 2 * Vt;
   int32_t* rowN = dv + 3 * Vt;
   bool any = false;
+  const unsigned long long need = sig_bit(a) | sig_bit(b);
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    // the word's symbol signature (64-bit Bloom mask) rules out most words without
+    // touching their symbols
+    if (sig != nullptr && (sig[w] & need) != need) continue;
     const uint32_t L = wlen[w];
     if (L < 2) continue;
     uint16_t* s = sym + wstart[w];
     // read-only probe first: most words do not contain the pair
     bool hit = false;
-    for (uint32_t i = 0; i + 1 < L; ++i)
-      if (s[i] == a && s[i + 1] == b) { hit = true; break; }
+    uint32_t prev = s[0];
+    for (uint32_t i = 1; i < L && !hit; ++i) {
+      const uint32_t cur = s[i];
+      hit = (prev == (uint32_t)a) & (cur == (uint32_t)b);
+      prev = cur;
+    }
     if (!hit) continue;
     any = true;
     const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
@@ -316,11 +352,16 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
       }
     }
     wlen[w] = o;
+    if (sig != nullptr) {
+      unsigned long long g = 0;
+      for (uint32_t i = 0; i < o; ++i) g |= sig_bit(s[i]);
+      sig[w] = g;
+    }
   }
   if (LDS) {
     if (any) touched = 1;
     __syncthreads();
-    if (touched)
+    if (touched)   // contiguous atomics (one cache line per 32 entries)
       for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) {
         const int32_t v = dl[i];
         if (v) atomicAdd(&deltas[i], v);
@@ -328,24 +369,219 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   }
 }
 
-__global__ void k_apply(uint32_t* __restrict__ table, int32_t* __restrict__ deltas, int Vt, int a, int b, int nid,
-                        uint32_t* __restrict__ tlen) {
-  for (int x = threadIdx.x; x < Vt; x += blockDim.x) {
-    int32_t v;
-    if ((v = deltas[x])) atomicAdd(&table[(size_t)x * Vt + a], (uint32_t)v);
-    if ((v = deltas[Vt + x])) atomicAdd(&table[(size_t)x * Vt + nid], (uint32_t)v);
-    if ((v = deltas[2 * Vt + x])) atomicAdd(&table[(size_t)b * Vt + x], (uint32_t)v);
-    if ((v = deltas[3 * Vt + x])) atomicAdd(&table[(size_t)nid * Vt + x], (uint32_t)v);
-    deltas[x] = 0;
-    deltas[Vt + x] = 0;
-    deltas[2 * Vt + x] = 0;
-    deltas[3 * Vt + x] = 0;
+// table += deltas, deltas = 0, table[a][b] = 0, tlen[new] = tlen[a] + tlen[b].  Only the
+// thread of x == a can touch (a, b) (through (x, a) or (b, x) when a == b, both negative),
+// so it retires the pair after its own adds: no fence, one launch.
+__global__ __launch_bounds__(256) void k_apply(uint32_t* __restrict__ table, int32_t* __restrict__ deltas, int Vt,
+                                               int a, int b, int nid, uint32_t* __restrict__ tlen) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= Vt) return;
+  int32_t v;
+  if ((v = deltas[x])) atomicAdd(&table[(size_t)x * Vt + a], (uint32_t)v);
+  if ((v = deltas[Vt + x])) atomicAdd(&table[(size_t)x * Vt + nid], (uint32_t)v);
+  if ((v = deltas[2 * Vt + x])) atomicAdd(&table[(size_t)b * Vt + x], (uint32_t)v);
+  if ((v = deltas[3 * Vt + x])) atomicAdd(&table[(size_t)nid * Vt + x], (uint32_t)v);
+  deltas[x] = 0;
+  deltas[Vt + x] = 0;
+  deltas[2 * Vt + x] = 0;
+  deltas[3 * Vt + x] = 0;
+  if (x == a) {
+    atomicExch(&table[(size_t)a * Vt + b], 0u);   // merged pair retired (never re-picked)
+    tlen[nid] = tlen[a] + tlen[b];
   }
-  __threadfence();
+}
+
+// ------------------------------------------------------------ word dedup --
+// HF trains on distinct words x their counts: words of >= 2 symbols are inserted into an
+// open-addressing table keyed by (32-bit hash tag, representative index); a candidate
+// whose tag matches is compared symbol by symbol with the representative, so collisions
+// never merge different words.  The winner of an empty slot appends itself to the
+// distinct list; every occurrence adds 1 to the slot's count.
+__device__ __forceinline__ uint64_t word_hash(const uint16_t* s, uint32_t L) {
+  uint64_t h = 0xcbf29ce484222325ull ^ (uint64_t)L;
+  for (uint32_t i = 0; i < L; ++i) h = (h ^ s[i]) * 0x100000001b3ull;
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  return h;
+}
+
+struct DedupWs {
+  unsigned long long* keys;   // [cap]
+  uint32_t* cnt;              // [cap]
+  uint32_t* rep;              // [n] distinct -> representative word
+  uint32_t* slot;             // [n] distinct -> table slot
+  unsigned long long* nu;     // distinct count
+  uint64_t cap;
+};
+
+__host__ __device__ inline uint64_t dedup_cap(int64_t n) {
+  uint64_t c = 1024;
+  while (c < (uint64_t)n * 2) c <<= 1;
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                      const uint32_t* __restrict__ wlen, int64_t nw, DedupWs ws) {
+  const uint64_t mask = ws.cap - 1;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t L = wlen[w];
+    if (L < 2) continue;
+    const uint16_t* s = sym + wstart[w];
+    const uint64_t h = word_hash(s, L);
+    const unsigned long long mine = ((h >> 32) << 32) | (unsigned long long)(uint32_t)(w + 1);
+    uint64_t k = h & mask;
+    while (true) {
+      unsigned long long v = ws.keys[k];
+      if (v == 0ull) {
+        v = atomicCAS(&ws.keys[k], 0ull, mine);
+        if (v == 0ull) {   // new distinct word
+          atomicAdd(&ws.cnt[k], 1u);
+          const unsigned long long u = atomicAdd(ws.nu, 1ull);
+          ws.rep[u] = (uint32_t)w;
+          ws.slot[u] = (uint32_t)k;
+          break;
+        }
+      }
+      if ((v >> 32) == (h >> 32)) {
+        const uint32_t r = (uint32_t)(v & 0xFFFFFFFFull) - 1u;
+        bool eq = wlen[r] == L;
+        if (eq) {
+          const uint16_t* t = sym + wstart[r];
+          for (uint32_t i = 0; i < L && eq; ++i) eq = t[i] == s[i];
+        }
+        if (eq) {
+          atomicAdd(&ws.cnt[k], 1u);
+          break;
+        }
+      }
+      k = (k + 1) & mask;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict__ wstart,
+                                                      const uint32_t* __restrict__ wlen, DedupWs ws,
+                                                      uint32_t* __restrict__ ow, uint32_t* __restrict__ ol,
+                                                      uint32_t* __restrict__ oc, int64_t* __restrict__ out_n) {
+  const int64_t nu = (int64_t)*ws.nu;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out_n = nu;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nu; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = ws.rep[i];
+    ow[i] = wstart[r];
+    ol[i] = wlen[r];
+    oc[i] = ws.cnt[ws.slot[i]];
+  }
+}
+
+// keep the words that can still merge (>= 2 symbols); one atomic per wave
+__global__ __launch_bounds__(256) void k_compact_words(const uint32_t* __restrict__ wstart,
+                                                       const uint32_t* __restrict__ wlen,
+                                                       const uint32_t* __restrict__ wcount, int64_t nw,
+                                                       uint32_t* __restrict__ ow, uint32_t* __restrict__ ol,
+                                                       uint32_t* __restrict__ oc, unsigned long long* __restrict__ n) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nw; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = base + threadIdx.x;
+    const bool keep = w < nw && wlen[w] >= 2;
+    const unsigned long long m = __ballot(keep);
+    unsigned long long off = 0;
+    if (lane == 0 && m) off = atomicAdd(n, (unsigned long long)__popcll(m));
+    off = __shfl(off, 0);
+    if (keep) {
+      const unsigned long long pos = off + __popcll(m & ((1ull << lane) - 1ull));
+      ow[pos] = wstart[w];
+      ol[pos] = wlen[w];
+      oc[pos] = wcount ? wcount[w] : 1u;
+    }
+  }
+}
+
+// ------------------------------------------------------------ word repack --
+// Distinct words copied into one contiguous symbol array ordered by length (bucket
+// min(L, 255)): a wave's words are neighbours in memory and of similar length, so the
+// merge scan is coalesced and its per-thread loops stay in step.
+constexpr int RP_WPB = 2048;   // words per workgroup in the bucket scatter
+
+__global__ __launch_bounds__(256) void k_len_hist(const uint32_t* __restrict__ wlen, int64_t nw,
+                                                  uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&h[min(wlen[w], 255u)], 1u);
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_bucket_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t v[256];
+  v[threadIdx.x] = hist[threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicExch(&table[(size_t)a * Vt + b], 0u);   // merged pair retired (HF never re-picks it)
-    tlen[nid] = tlen[a] + tlen[b];
+    uint32_t acc = 0;
+    for (int i = 0; i < 256; ++i) { const uint32_t c = v[i]; v[i] = acc; acc += c; }
+  }
+  __syncthreads();
+  cursor[threadIdx.x] = v[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_len_scatter(const uint32_t* __restrict__ wlen, int64_t nw,
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[256], base[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t w0 = (int64_t)blockIdx.x * RP_WPB;
+  uint32_t bk[RP_WPB / 256], rk[RP_WPB / 256];
+#pragma unroll
+  for (int k = 0; k < RP_WPB / 256; ++k) {
+    const int64_t w = w0 + k * 256 + threadIdx.x;
+    bk[k] = w < nw ? min(wlen[w], 255u) : 0u;
+    rk[k] = w < nw ? atomicAdd(&h[bk[k]], 1u) : 0u;
+  }
+  __syncthreads();
+  base[threadIdx.x] = h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < RP_WPB / 256; ++k) {
+    const int64_t w = w0 + k * 256 + threadIdx.x;
+    if (w < nw) order[base[bk[k]] + rk[k]] = (uint32_t)w;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gather_lens(const uint32_t* __restrict__ order, const uint32_t* __restrict__ wlen,
+                                                     const uint32_t* __restrict__ wcount, int64_t nw,
+                                                     int64_t* __restrict__ lens, uint32_t* __restrict__ ol,
+                                                     uint32_t* __restrict__ oc) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = order[i];
+    lens[i] = wlen[w];
+    ol[i] = wlen[w];
+    oc[i] = wcount ? wcount[w] : 1u;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__ order, const uint16_t* __restrict__ sym,
+                                                    const uint32_t* __restrict__ wstart, const uint32_t* __restrict__ wlen,
+                                                    const int64_t* __restrict__ offs, int64_t nw,
+                                                    uint16_t* __restrict__ osym, uint32_t* __restrict__ ow,
+                                                    int64_t* __restrict__ out_nsym) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = order[i], L = wlen[w];
+    const uint16_t* src = sym + wstart[w];
+    uint16_t* dst = osym + offs[i];
+    for (uint32_t k = 0; k < L; ++k) dst[k] = src[k];
+    ow[i] = (uint32_t)offs[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out_nsym = offs[nw];
+}
+
+__global__ __launch_bounds__(256) void k_word_sig(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                  const uint32_t* __restrict__ wlen, int64_t nw,
+                                                  unsigned long long* __restrict__ sig) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t* s = sym + wstart[w];
+    unsigned long long g = 0;
+    for (uint32_t i = 0, L = wlen[w]; i < L; ++i) g |= sig_bit(s[i]);
+    sig[w] = g;
   }
 }
 
@@ -429,20 +665,30 @@ extern "C" int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart
   return BEAST_OK;
 }
 
-extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* result, void* stream) {
-  BEAST_REQUIRE(table && result && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
-  hipStream_t s = beast::as_stream(stream);
-  BEAST_HIP(hipMemsetAsync(result, 0, sizeof(uint64_t), s), "argmax memset");
-  const int64_t total = (int64_t)vcur * vcur;
-  hipLaunchKernelGGL(k_argmax, dim3(grid_for(total, 256 * 8, 2048)), dim3(256), 0, s, table, Vt, vcur,
-                     reinterpret_cast<unsigned long long*>(result));
+extern "C" size_t beast_bpe_argmax_workspace_bytes(int Vt) { (void)Vt; return 4 * 8; }
+
+extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int call, void* stream) {
+  BEAST_REQUIRE(table && ws && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
+  BEAST_REQUIRE(call >= 0, "beast_bpe_argmax: call index must be >= 0");
+  hipLaunchKernelGGL(k_argmax, dim3(vcur), dim3(ARG_TPR), 0, beast::as_stream(stream), table, Vt, vcur,
+                     reinterpret_cast<unsigned long long*>(ws), call & 1);
   BEAST_LAUNCHED("k_argmax");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                                         int64_t n_words, uint64_t* sig, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && sig && n_words >= 0, "beast_bpe_word_signatures: bad args");
+  if (n_words == 0) return BEAST_OK;
+  hipLaunchKernelGGL(k_word_sig, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, beast::as_stream(stream), sym,
+                     wstart, wlen, n_words, reinterpret_cast<unsigned long long*>(sig));
+  BEAST_LAUNCHED("k_word_sig");
   return BEAST_OK;
 }
 
 extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                                int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
-                               int32_t* deltas, int Vt, void* stream) {
+                               int32_t* deltas, int Vt, uint64_t* sig, void* stream) {
   BEAST_REQUIRE(sym && wstart && wlen && tlen && deltas, "beast_bpe_merge: null pointer");
   BEAST_REQUIRE(a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt && Vt <= 65535,
                 "beast_bpe_merge: ids out of range (a=%d b=%d new=%d Vt=%d)", a, b, new_id, Vt);
@@ -450,12 +696,13 @@ extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* 
   hipStream_t s = beast::as_stream(stream);
   const int grid = grid_for(n_words, 256, 2048);
   const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
   if (lds <= 64 * 1024)
     hipLaunchKernelGGL(k_merge<true>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       tlen, max_token_length, deltas, Vt);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg);
   else
     hipLaunchKernelGGL(k_merge<false>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       tlen, max_token_length, deltas, Vt);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg);
   BEAST_LAUNCHED("k_merge");
   return BEAST_OK;
 }
@@ -464,7 +711,105 @@ extern "C" int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, 
                                void* stream) {
   BEAST_REQUIRE(table && deltas && tlen && a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt,
                 "beast_bpe_apply: bad args");
-  hipLaunchKernelGGL(k_apply, dim3(1), dim3(1024), 0, beast::as_stream(stream), table, deltas, Vt, a, b, new_id, tlen);
+  hipLaunchKernelGGL(k_apply, dim3((Vt + 255) / 256), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, a, b,
+                     new_id, tlen);
   BEAST_LAUNCHED("k_apply");
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_dedup_workspace_bytes(int64_t n_words) {
+  const uint64_t cap = dedup_cap(n_words > 0 ? n_words : 1);
+  return (size_t)(cap * 12 + (uint64_t)(n_words > 0 ? n_words : 1) * 8 + 64);
+}
+
+extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                                     int64_t n_words, void* workspace, size_t ws_bytes, uint32_t* out_wstart,
+                                     uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_n, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && workspace && out_wstart && out_wlen && out_wcount && out_n,
+                "beast_bpe_dedup_words: null pointer");
+  BEAST_REQUIRE(n_words >= 0 && n_words < (int64_t(1) << 32) - 1, "beast_bpe_dedup_words: bad n_words");
+  BEAST_REQUIRE_CODE(ws_bytes >= beast_bpe_dedup_workspace_bytes(n_words), BEAST_E_WORKSPACE,
+                     "dedup workspace %zu < %zu", ws_bytes, beast_bpe_dedup_workspace_bytes(n_words));
+  hipStream_t s = beast::as_stream(stream);
+  const int64_t n = n_words > 0 ? n_words : 1;
+  DedupWs ws;
+  ws.cap = dedup_cap(n);
+  char* p = static_cast<char*>(workspace);
+  ws.keys = reinterpret_cast<unsigned long long*>(p);  p += ws.cap * 8;
+  ws.cnt = reinterpret_cast<uint32_t*>(p);              p += ws.cap * 4;
+  ws.rep = reinterpret_cast<uint32_t*>(p);              p += n * 4;
+  ws.slot = reinterpret_cast<uint32_t*>(p);             p += n * 4;
+  ws.nu = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
+  BEAST_HIP(hipMemsetAsync(workspace, 0, ws.cap * 12, s), "dedup memset");
+  BEAST_HIP(hipMemsetAsync(ws.nu, 0, 8, s), "dedup memset");
+  if (n_words > 0) {
+    hipLaunchKernelGGL(k_dedup_insert, dim3(grid_for(n_words, 256, 16384)), dim3(256), 0, s, sym, wstart, wlen,
+                       n_words, ws);
+    BEAST_LAUNCHED("k_dedup_insert");
+  }
+  hipLaunchKernelGGL(k_dedup_gather, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, wstart, wlen, ws, out_wstart,
+                     out_wlen, out_wcount, out_n);
+  BEAST_LAUNCHED("k_dedup_gather");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_compact_words(const uint32_t* wstart, const uint32_t* wlen, const uint32_t* wcount,
+                                       int64_t n_words, uint32_t* out_wstart, uint32_t* out_wlen,
+                                       uint32_t* out_wcount, int64_t* out_n, void* stream) {
+  BEAST_REQUIRE(wstart && wlen && out_wstart && out_wlen && out_wcount && out_n,
+                "beast_bpe_compact_words: null pointer");
+  BEAST_REQUIRE(n_words >= 0, "beast_bpe_compact_words: bad n_words");
+  hipStream_t s = beast::as_stream(stream);
+  BEAST_HIP(hipMemsetAsync(out_n, 0, 8, s), "compact memset");
+  if (n_words > 0) {
+    hipLaunchKernelGGL(k_compact_words, dim3(grid_for(n_words, 256, 16384)), dim3(256), 0, s, wstart, wlen, wcount,
+                       n_words, out_wstart, out_wlen, out_wcount, reinterpret_cast<unsigned long long*>(out_n));
+    BEAST_LAUNCHED("k_compact_words");
+  }
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_repack_workspace_bytes(int64_t n_words) {
+  const int64_t n = n_words > 0 ? n_words : 1;
+  return (size_t)(2 * 256 * 4 + n * 4 + n * 8 + (n + 1) * 8 + 64) + beast_scan_workspace_bytes(n);
+}
+
+extern "C" int beast_bpe_repack_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                                      const uint32_t* wcount, int64_t n_words, void* workspace, size_t ws_bytes,
+                                      uint16_t* out_sym, uint32_t* out_wstart, uint32_t* out_wlen,
+                                      uint32_t* out_wcount, int64_t* out_nsym, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && workspace && out_sym && out_wstart && out_wlen && out_wcount && out_nsym,
+                "beast_bpe_repack_words: null pointer");
+  BEAST_REQUIRE(n_words >= 0 && n_words < (int64_t(1) << 31), "beast_bpe_repack_words: bad n_words");
+  BEAST_REQUIRE_CODE(ws_bytes >= beast_bpe_repack_workspace_bytes(n_words), BEAST_E_WORKSPACE,
+                     "repack workspace %zu < %zu", ws_bytes, beast_bpe_repack_workspace_bytes(n_words));
+  hipStream_t s = beast::as_stream(stream);
+  const int64_t n = n_words > 0 ? n_words : 1;
+  char* p = static_cast<char*>(workspace);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(p);   p += 256 * 4;
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(p); p += 256 * 4;
+  uint32_t* order = reinterpret_cast<uint32_t*>(p);  p += n * 4;
+  p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
+  int64_t* lens = reinterpret_cast<int64_t*>(p);     p += n * 8;
+  int64_t* offs = reinterpret_cast<int64_t*>(p);     p += (n + 1) * 8;
+  int64_t* sws = reinterpret_cast<int64_t*>(p);
+  BEAST_HIP(hipMemsetAsync(hist, 0, 256 * 4, s), "repack memset");
+  if (n_words == 0) {
+    BEAST_HIP(hipMemsetAsync(out_nsym, 0, 8, s), "repack memset");
+    return BEAST_OK;
+  }
+  const int g = grid_for(n_words, 256, 8192);
+  hipLaunchKernelGGL(k_len_hist, dim3(g), dim3(256), 0, s, wlen, n_words, hist);
+  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, s, hist, cursor);
+  hipLaunchKernelGGL(k_len_scatter, dim3((n_words + RP_WPB - 1) / RP_WPB), dim3(256), 0, s, wlen, n_words, cursor, order);
+  hipLaunchKernelGGL(k_gather_lens, dim3(g), dim3(256), 0, s, order, wlen, wcount, n_words, lens, out_wlen,
+                     out_wcount);
+  BEAST_LAUNCHED("k_gather_lens");
+  int rc = scan_rec(lens, offs, n_words, sws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(64), 0, s, lens, offs, n_words);
+  hipLaunchKernelGGL(k_copy_words, dim3(g), dim3(256), 0, s, order, sym, wstart, wlen, offs, n_words, out_sym,
+                     out_wstart, out_nsym);
+  BEAST_LAUNCHED("k_copy_words");
   return BEAST_OK;
 }

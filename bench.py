@@ -127,7 +127,8 @@ def bpe_bench(tok, dev, args, world, rank, reduce):
            "value": res.stats["n_merges"] / el, "unit": "merges/s", "merges": res.stats["n_merges"],
            "seconds": el, "trajectories": per_rank * world, "vocab_size": args.bpe_vocab,
            "setup_s": res.stats["setup_s"], "merge_loop_s": res.stats["merge_loop_s"],
-           "words": res.stats["n_words"], "symbols": res.stats["n_syms"]}
+           "words": res.stats["n_words"], "symbols": res.stats["n_syms"],
+           "distinct_words": res.stats.get("n_distinct"), "live_words_at_end": res.stats.get("n_live_end")}
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = hf_bpe_baseline(allrows[:20000].cpu().numpy(), args.bpe_vocab, res)
     return out

@@ -165,18 +165,52 @@ int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off, int64_t n_
 /* pair table [Vt][Vt] uint32 += word count for each adjacent pair (BpeTrainer::count_pairs). */
 int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
                           const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream);
-/* result = max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)); zeroes *result first. */
-int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* result, void* stream);
+/* max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)) (0 if the table is empty)
+ * into ws[2 + (call & 1)], where call = 0, 1, 2, ... numbers the calls on this workspace
+ * (each call zeroes the other slot for the next one: no memset per call).
+ * ws: beast_bpe_argmax_workspace_bytes(Vt), zero-filled once before call 0. */
+size_t beast_bpe_argmax_workspace_bytes(int Vt);
+int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int call, void* stream);
 /* Merge (a,b)->new_id in every word, left to right, non-overlapping (HF Word::merge);
- * accumulate HF's pair-count changes into deltas[4][Vt] int32:
- * [0]: (x,a)  [1]: (x,new)  [2]: (b,y)  [3]: (new,y). */
+ * HF's pair-count changes, per word times wcount (NULL = 1):
+ * [0]: (x,a)  [1]: (x,new)  [2]: (b,y)  [3]: (new,y).
+ * are accumulated into deltas[4][Vt] int32 (multi-GPU: all-reduce them, then
+ * beast_bpe_apply).  sig: see beast_bpe_word_signatures (nullable). */
 int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                     int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
-                    int32_t* deltas, int Vt, void* stream);
+                    int32_t* deltas, int Vt, uint64_t* sig, void* stream);
+/* sig[w] = OR of 1 << (symbol & 63) over word w (a Bloom mask of its symbols).  Passed to
+ * beast_bpe_merge (nullable), it lets the merge skip words that cannot contain the pair
+ * without reading their symbols; the merge keeps it current for the words it rewrites. */
+int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                              uint64_t* sig, void* stream);
 /* table += deltas (then deltas = 0), table[a][b] = 0 (merged pair retired),
  * tlen[new_id] = tlen[a] + tlen[b]. */
 int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, int b, int new_id, uint32_t* tlen,
                     void* stream);
+/* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
+ * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
+ * different words); out_* get one entry per distinct word (its first-seen copy in sym),
+ * out_wcount its multiplicity, *out_n (device int64) the number of distinct words.
+ * Output order is unspecified (training results do not depend on it).  Words of 0 or 1
+ * symbols are dropped (they hold no pair). out_* sized n_words. */
+size_t beast_bpe_dedup_workspace_bytes(int64_t n_words);
+int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                          void* workspace, size_t ws_bytes, uint32_t* out_wstart, uint32_t* out_wlen,
+                          uint32_t* out_wcount, int64_t* out_n, void* stream);
+/* Copy words into one contiguous symbol array ordered by length (min(L, 255) buckets,
+ * order inside a bucket unspecified): out_sym capacity >= sum of wlen (e.g. the corpus
+ * symbol count); *out_nsym (device int64) = symbols written. wcount may be NULL. */
+size_t beast_bpe_repack_workspace_bytes(int64_t n_words);
+int beast_bpe_repack_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, const uint32_t* wcount,
+                           int64_t n_words, void* workspace, size_t ws_bytes, uint16_t* out_sym,
+                           uint32_t* out_wstart, uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_nsym,
+                           void* stream);
+/* Keep the words that still have >= 2 symbols (order unspecified); *out_n device int64.
+ * wcount may be NULL (count 1). */
+int beast_bpe_compact_words(const uint32_t* wstart, const uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
+                            uint32_t* out_wstart, uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_n,
+                            void* stream);
 
 #ifdef __cplusplus
 }

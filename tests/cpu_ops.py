@@ -41,13 +41,24 @@ class NumpyBpeOps:
             text = "".join(map(chr, (t[off[s]:off[s + 1]] - mn).astype(int)))
             for piece in bpe_oracle.pretokenize(text):
                 words.append([int(byte2id[b]) for b in piece.encode("utf-8")])
-        return {"words": words, "n_words": len(words), "n_syms": sum(map(len, words))}
+        return {"words": words, "counts": [1] * len(words), "n_words": len(words), "n_syms": sum(map(len, words))}
+
+    def dedup(self, words):
+        from collections import Counter
+        c = Counter(tuple(w) for w in words["words"] if len(w) >= 2)
+        ws = [list(k) for k in c]
+        return dict(words, words=ws, counts=[c[tuple(w)] for w in ws], n_words=len(ws), n_distinct=len(ws))
+
+    def compact(self, words):
+        keep = [i for i, w in enumerate(words["words"]) if len(w) >= 2]
+        return dict(words, words=[words["words"][i] for i in keep], counts=[words["counts"][i] for i in keep],
+                    n_words=len(keep))
 
     def count_pairs(self, words, Vt):
         table = np.zeros(Vt * Vt, dtype=np.int64)
-        for w in words["words"]:
+        for w, n in zip(words["words"], words["counts"]):
             for x, y in zip(w, w[1:]):
-                table[x * Vt + y] += 1
+                table[x * Vt + y] += n
         return torch.from_numpy(table.astype(np.int32))
 
     def new_state(self, Vt, tlen):
@@ -65,19 +76,19 @@ class NumpyBpeOps:
     def merge(self, words, a, b, nid, max_len, Vt):
         d = np.zeros((4, Vt), dtype=np.int64)
         nl = self.tlen[a] + self.tlen[b]
-        for w in words["words"]:
+        for w, n in zip(words["words"], words["counts"]):
             i = 0
             while i < len(w):
                 if w[i] == a and i + 1 < len(w) and w[i + 1] == b:
                     if i > 0:
-                        d[0, w[i - 1]] -= 1
+                        d[0, w[i - 1]] -= n
                         if self.tlen[w[i - 1]] + nl < max_len:
-                            d[1, w[i - 1]] += 1
+                            d[1, w[i - 1]] += n
                     w[i:i + 2] = [nid]
                     if i < len(w) - 1:
-                        d[2, w[i + 1]] -= 1
+                        d[2, w[i + 1]] -= n
                         if self.tlen[w[i + 1]] + nl < max_len:
-                            d[3, w[i + 1]] += 1
+                            d[3, w[i + 1]] += n
                 i += 1
         self.deltas = torch.from_numpy(d.reshape(-1).astype(np.int32))
         return self.deltas

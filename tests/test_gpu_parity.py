@@ -398,6 +398,49 @@ def test_bpe_pretok_words_match_hf(gpu_device):
     assert got == pieces
 
 
+def test_bpe_dedup_and_compact_match_counter(gpu_device):
+    """Distinct words x counts equal a Counter over the pre-tokenised words (>= 2 symbols);
+    compaction keeps exactly the words that can still merge."""
+    from collections import Counter
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, fixed_rows_to_device
+    from beast_tokenizer_amd.pretok import class_lut
+    rng = np.random.default_rng(11)
+    base = rng.integers(0, 300, size=9)
+    arr = base[rng.integers(0, 9, size=(3000, 40))]
+    arr[::7] = rng.integers(0, 300, size=(arr[::7].shape[0], 40))
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    present = np.zeros(300, dtype=bool)
+    present[np.unique(arr)] = True
+    _, _, byte2id = build_alphabet(present, [chr(i) for i in range(300)], [])
+    ops = GpuBpeOps(gpu_device)
+    w = ops.pretokenize(flat, off, 0, class_lut(300), byte2id)
+
+    def words_of(d):
+        sym = d["sym"].cpu().numpy().view(np.uint16)
+        ws, wl = d["wstart"].cpu().numpy(), d["wlen"].cpu().numpy()
+        return [tuple(sym[a:a + n]) for a, n in zip(ws[: d["n_words"]], wl[: d["n_words"]])]
+    want = Counter(x for x in words_of(w) if len(x) >= 2)
+    u = ops.dedup(w)
+    got = dict(zip(words_of(u), u["wcount"].cpu().numpy()[: u["n_words"]].tolist()))
+    assert len(got) == u["n_words"] == len(want)
+    assert got == dict(want)
+    lens = u["wlen"].cpu().numpy()[: u["n_words"]]
+    assert np.all(np.diff(np.minimum(lens, 255)) >= 0)                     # length-ordered
+    ws = u["wstart"].cpu().numpy()[: u["n_words"]]
+    assert np.array_equal(ws[1:], ws[:-1] + lens[:-1])                      # contiguous
+    # shorten some words to length 1 / 0 and compact
+    wl = u["wlen"].clone()
+    wl[::3] = 1
+    wl[1::5] = 0
+    u2 = dict(u, wlen=wl)
+    c = ops.compact(u2)
+    keep = [(a, n, k) for a, n, k in zip(u["wstart"].cpu().tolist(), wl.cpu().tolist(), u["wcount"].cpu().tolist())
+            if n >= 2]
+    got_c = sorted(zip(c["wstart"].cpu().tolist()[: c["n_words"]], c["wlen"].cpu().tolist()[: c["n_words"]],
+                       c["wcount"].cpu().tolist()[: c["n_words"]]))
+    assert got_c == sorted(keep)
+
+
 def test_bpe_tokenizer_end_to_end(gpu_device):
     g = load_npz("bspline_k2.npz")
     tok = make_tok("k2", g, gpu_device, cls=BEASTBsplineBPETokenizer, bpe_vocab_size=512)

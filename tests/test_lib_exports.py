@@ -63,7 +63,7 @@ def test_abi_version():
                           None)),
     ("beast_reconstruct_f32", (None, 4, 14, 14, 10, 256, 0, None, None, None, 0, 50, None, 14, None, 0, None,
                                None, None, None, None)),
-    ("beast_bpe_argmax", (None, 300, 300, None, None)),
+    ("beast_bpe_argmax", (None, 300, 300, None, 0, None)),
 ])
 def test_null_pointers_are_rejected_before_any_hip_call(name, args):
     rc = getattr(_lib.load(), name)(*args)
