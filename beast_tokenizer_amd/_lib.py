@@ -56,9 +56,12 @@ SIGNATURES = {
     "beast_bpe_count_pairs": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp]),
     "beast_bpe_argmax_workspace_bytes": (_sz, [_i32]),
     "beast_bpe_argmax": (_i32, [_vp, _i32, _i32, _vp, _i32, _vp]),
-    "beast_bpe_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp]),
+    "beast_bpe_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i64,
+                               _vp]),
+    "beast_bpe_index_workspace_bytes": (_sz, [_i32, _i64]),
+    "beast_bpe_build_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _sz, _vp]),
     "beast_bpe_word_signatures": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
-    "beast_bpe_apply": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "beast_bpe_apply_argmax": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),

@@ -146,7 +146,9 @@ class GpuBpeOps:
                     n_syms_distinct=ns)
 
     def compact(self, words):
-        """Drop words with < 2 symbols left (they can no longer merge)."""
+        """Drop words with < 2 symbols left (they can no longer merge).  Word indices change,
+        so the inverted index is dropped (merges then visit every word)."""
+        self._index = None
         n = words["n_words"]
         if n == 0:
             return words
@@ -172,6 +174,14 @@ class GpuBpeOps:
                  self.stream)
         return table
 
+    def build_index(self, words, Vt: int):
+        """Inverted symbol -> word index with room for the merges' appends."""
+        cap = int(words.get("n_syms_distinct", words["n_syms"])) + Vt + 2 * int(words["n_words"]) + 1024
+        nb = _lib.load().beast_bpe_index_workspace_bytes(Vt, cap)
+        self._index = torch.empty((nb + 3) // 4, dtype=torch.int32, device=self.device)
+        _lib.run("beast_bpe_build_index", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                 words["n_words"], Vt, self._index.data_ptr(), nb, self.stream)
+
     def new_state(self, Vt: int, tlen: np.ndarray):
         nb = _lib.load().beast_bpe_argmax_workspace_bytes(Vt)
         self._argws = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=self.device)
@@ -185,15 +195,22 @@ class GpuBpeOps:
         _lib.run("beast_bpe_argmax", table.data_ptr(), Vt, vcur, self._argws.data_ptr(), k, self.stream)
         return self._read_i64(self._argws[2 + (k & 1):], 1)[0] & 0xFFFFFFFFFFFFFFFF
 
-    def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int) -> torch.Tensor:
+    def apply_argmax(self, table: torch.Tensor, deltas: torch.Tensor, Vt: int, vcur: int, a: int, b: int, nid: int,
+                     reused: bool) -> int:
+        """table += deltas, retire (a, b), then the next argmax -- one launch."""
+        k = self._calls
+        self._calls += 1
+        _lib.run("beast_bpe_apply_argmax", table.data_ptr(), deltas.data_ptr(), Vt, vcur, a, b, nid,
+                 self._tlen.data_ptr(), _lib.ptr(getattr(self, "_index", None)), int(reused),
+                 self._argws.data_ptr(), k, self.stream)
+        return self._read_i64(self._argws[2 + (k & 1):], 1)[0] & 0xFFFFFFFFFFFFFFFF
+
+    def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int, count: int = 1 << 62) -> torch.Tensor:
         _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
                  _lib.ptr(words.get("wcount")), words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len,
-                 self._deltas.data_ptr(), Vt, _lib.ptr(words.get("sig")), self.stream)
+                 self._deltas.data_ptr(), Vt, _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)),
+                 int(count), self.stream)
         return self._deltas
-
-    def apply(self, table: torch.Tensor, deltas: torch.Tensor, Vt: int, a: int, b: int, nid: int) -> None:
-        _lib.run("beast_bpe_apply", table.data_ptr(), deltas.data_ptr(), Vt, a, b, nid, self._tlen.data_ptr(),
-                 self.stream)
 
 
 def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special_tokens: Sequence[str]):
@@ -222,7 +239,7 @@ def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special
 def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
-              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0) -> BPEResult:
+              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False) -> BPEResult:
     """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard)."""
     import time
     t0 = time.perf_counter()
@@ -263,11 +280,13 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     for i, s in enumerate(id2str):
         tlen[i] = len(s.encode("utf-8"))
     ops.new_state(Vt, tlen)
+    if use_index and hasattr(ops, "build_index"):
+        ops.build_index(words, Vt)
     max_len = int(max_token_length) if max_token_length is not None else 2 ** 31 - 1
     merges: List[Tuple[str, str]] = []
     t1 = time.perf_counter()
+    key = ops.argmax(table, Vt, len(id2str))
     while len(id2str) < vocab_size:
-        key = ops.argmax(table, Vt, len(id2str))
         count = key >> 32
         if count < 1 or count < min_frequency:
             break
@@ -275,14 +294,18 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         a, b = divmod(idx, Vt)
         new_tok = id2str[a] + id2str[b]
         nid = str2id.get(new_tok)
+        reused = nid is not None
         if nid is None:
             nid = len(id2str)
             str2id[new_tok] = nid
             id2str.append(new_tok)
         merges.append((id2str[a], id2str[b]))
-        deltas = ops.merge(words, a, b, nid, max_len, Vt)
+        deltas = ops.merge(words, a, b, nid, max_len, Vt, count)
         reduce(deltas, "sum")
-        ops.apply(table, deltas, Vt, a, b, nid)
+        if len(id2str) >= vocab_size:          # last merge: apply without searching again
+            ops.apply_argmax(table, deltas, Vt, len(id2str), a, b, nid, reused)
+            break
+        key = ops.apply_argmax(table, deltas, Vt, len(id2str), a, b, nid, reused)
         if compact_every and len(merges) % compact_every == 0 and hasattr(ops, "compact"):
             words = ops.compact(words)
     t2 = time.perf_counter()

@@ -12,7 +12,8 @@
 //                            in place; HF's pair-count changes are accumulated in
 //                            LDS-privatised delta vectors [4][Vt] and flushed once
 //                            per workgroup
-//   k_apply                  table += deltas; zero the merged pair (retired)
+//   k_apply_argmax           table += deltas, retire the merged pair, then the argmax
+//                            (incremental: only changed rows are rescanned)
 //   k_dedup_*                distinct words x counts (HF trains on word counts)
 //   k_compact_words          drop words that can no longer merge (< 2 symbols)
 #include <hip/hip_runtime.h>
@@ -245,60 +246,135 @@ __global__ void k_count_pairs(const uint16_t* __restrict__ sym, const uint32_t* 
 
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
-// ARG_TPR threads per row, 8 entries each (two 16-B loads in flight per thread, no
-// division); each workgroup folds its best into ws[2 + parity] with one atomicMax only when
-// it beats the value already there.  Result slots alternate between calls: call k writes
-// slot k & 1 and zeroes the other for call k + 1 (ws[1] = call counter), so no memset.
-constexpr int ARG_TPR = 256;
-__global__ __launch_bounds__(256) void k_argmax(const uint32_t* __restrict__ table, int Vt, int vcur,
-                                                unsigned long long* __restrict__ ws, int parity) {
-  __shared__ unsigned long long sh[4];
-  const int x = blockIdx.x;
-  const uint32_t* row = table + (size_t)x * Vt;
-  unsigned long long best = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) ws[2 + (parity ^ 1)] = 0ull;
-  for (int y0 = threadIdx.x * 8; y0 < vcur; y0 += ARG_TPR * 8) {
-    uint32_t c[8];
-    if (((Vt & 3) == 0) && y0 + 8 <= vcur) {
-      const uint4 u0 = *reinterpret_cast<const uint4*>(row + y0);
-      const uint4 u1 = *reinterpret_cast<const uint4*>(row + y0 + 4);
-      c[0] = u0.x; c[1] = u0.y; c[2] = u0.z; c[3] = u0.w; c[4] = u1.x; c[5] = u1.y; c[6] = u1.z; c[7] = u1.w;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) c[k] = y0 + k < vcur ? row[y0 + k] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)(y0 + k);
-      if (c[k]) best = umax64(best, ((unsigned long long)c[k] << 32) | (unsigned long long)(~idx));
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < 4; ++k) best = umax64(best, sh[k]);
-    unsigned long long* slot = ws + 2 + parity;
-    if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
-  }
+// Incremental argmax.  ws layout (u64): [2 + parity] result slots, [4, 4+Vt) the best key of
+// each row, then u32 clean[Vt] (0 = never scanned: the zero-filled workspace starts
+// all-dirty).  Call k writes slot k & 1 and zeroes the other for call k + 1 (no memset).
+struct ArgWs {
+  unsigned long long* slot;   // [2]
+  unsigned long long* rowbest;
+  uint32_t* clean;
+};
+__host__ __device__ inline ArgWs argws_view(void* ws, int Vt) {
+  ArgWs v;
+  unsigned long long* p = static_cast<unsigned long long*>(ws);
+  v.slot = p + 2;
+  v.rowbest = p + 4;
+  v.clean = reinterpret_cast<uint32_t*>(p + 4 + Vt);
+  return v;
 }
 
 // ------------------------------------------------------------------ merge --
-// LDS-privatised deltas when 4*Vt int32 fit in 64 KiB, else global atomics.
-// Deltas go to LDS (LDS = true, 4*Vt int32 <= 64 KiB) and are flushed once per workgroup
-// into deltas[] with contiguous atomics (multi-GPU: all-reduced, then beast_bpe_apply).
-// (A last-workgroup-applies variant was measured slower: every workgroup's device-scope
-// fence writes back its XCD's L2.)
 __device__ __forceinline__ unsigned long long sig_bit(uint32_t x) { return 1ull << (x & 63u); }
 
+// Inverted index symbol -> distinct words that may contain it (HF's where_to_update, on
+// the GPU).  Built once from the distinct words; the merge creating token `new` appends
+// the words it rewrote to a pool and k_apply_argmax turns that range into new's list.
+// A list that cannot be exact (pool full, or `new` re-used an existing id) is INEXACT and
+// merges involving it fall back to scanning every word.  Stale entries (a word that no
+// longer holds the symbol) are harmless: the probe finds no pair there.
+constexpr uint32_t IDX_INEXACT = 0xFFFFFFFFu;
+constexpr int64_t MERGE_LDS_MIN_COUNT = 1 << 16;
+constexpr int MERGE_UNROLL = 4;
+struct WordIndex {
+  uint32_t* start;   // [Vt]
+  uint32_t* len;     // [Vt]
+  uint32_t* ctl;     // [0] pool top, [1] mark (top after the previous apply), [2] capacity
+  uint32_t* pool;    // [capacity]
+};
+
+__host__ __device__ inline WordIndex index_view(void* ws, int Vt) {
+  WordIndex ix;
+  char* p = static_cast<char*>(ws);
+  ix.start = reinterpret_cast<uint32_t*>(p);
+  ix.len = ix.start + Vt;
+  ix.ctl = ix.len + Vt;
+  ix.pool = ix.ctl + 4;
+  return ix;
+}
+
+// One thread per word; words are short, so the distinct-symbol test is a backward scan.
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_index_words(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                     const uint32_t* __restrict__ wlen, int64_t nw, WordIndex ix,
+                                                     uint32_t* __restrict__ cursor) {
+  if (FILL && ix.ctl[3]) return;   // overflowed: the index is unused
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    const uint16_t* s = sym + wstart[w];
+    const uint32_t L = wlen[w];
+    for (uint32_t i = 0; i < L; ++i) {
+      const uint32_t x = s[i];
+      bool seen = false;
+      for (uint32_t k = 0; k < i && !seen; ++k) seen = s[k] == x;
+      if (seen) continue;
+      if (FILL) ix.pool[atomicAdd(&cursor[x], 1u)] = (uint32_t)w;
+      else atomicAdd(&ix.len[x], 1u);
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_index_scan(WordIndex ix, int Vt, uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t part[1024];
+  const int per = (Vt + 1023) / 1024, t = threadIdx.x;
+  uint32_t acc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int x = t * per + k;
+    if (x < Vt) acc += ix.len[x];
+  }
+  part[t] = acc;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {   // inclusive Hillis-Steele scan of the partial sums
+    const uint32_t v = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const uint32_t total = part[1023];
+  const bool fits = (uint64_t)total + (uint64_t)Vt <= (uint64_t)ix.ctl[2];   // cursor scratch sits past the lists
+  uint32_t run = t ? part[t - 1] : 0u;
+  for (int k = 0; k < per; ++k) {
+    const int x = t * per + k;
+    if (x < Vt) {
+      ix.start[x] = run;
+      cursor[x] = run;
+      run += ix.len[x];
+      if (!fits) ix.len[x] = IDX_INEXACT;   // pool too small: no lists, merges scan every word
+    }
+  }
+  if (t == 1023) {
+    ix.ctl[0] = fits ? total : ix.ctl[2];
+    ix.ctl[1] = ix.ctl[0];
+    ix.ctl[3] = fits ? 0u : 1u;
+  }
+}
+
+
+// Deltas go to LDS (LDS = true, 4*Vt int32 <= 64 KiB) and are flushed once per workgroup
+// into deltas[] with contiguous atomics (multi-GPU: all-reduced, then k_apply_argmax).
+// (A last-workgroup-applies variant was measured slower: every workgroup's device-scope
+// fence writes back its XCD's L2.)  Candidate words: the shorter exact index list of a
+// and b, else every word (pre-filtered by the Bloom signature).
 template <bool LDS>
 __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
                                                int64_t nw, int a, int b, int nid, uint32_t* __restrict__ tlen,
                                                int max_len, int32_t* __restrict__ deltas, int Vt,
-                                               unsigned long long* __restrict__ sig) {
+                                               unsigned long long* __restrict__ sig, WordIndex ix, bool use_ix) {
   extern __shared__ __attribute__((aligned(16))) int32_t dl[];
   __shared__ int touched;
+  const uint32_t* cand = nullptr;
+  int64_t ncand = nw;
+  if (use_ix) {
+    const uint32_t la = ix.len[a], lb = ix.len[b];
+    if (la != IDX_INEXACT || lb != IDX_INEXACT) {
+      const bool pa = la != IDX_INEXACT && (lb == IDX_INEXACT || la <= lb);
+      const int64_t n = pa ? la : lb;
+      if (n * 8 < nw) {   // indirect (uncoalesced) visits only pay for short lists
+        ncand = n;
+        cand = ix.pool + (pa ? ix.start[a] : ix.start[b]);
+      }
+    }
+  }
+  if ((int64_t)blockIdx.x * blockDim.x >= ncand) return;   // block-uniform: nothing to do
   int32_t* dv = LDS ? dl : deltas;
   if (LDS) {
     for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) dl[i] = 0;
@@ -312,19 +388,36 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   int32_t* rowN = dv + 3 * Vt;
   bool any = false;
   const unsigned long long need = sig_bit(a) | sig_bit(b);
-  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < ncand; i0 += MERGE_UNROLL * G) {
+   // MERGE_UNROLL candidates per pass: their signature loads are all in flight together
+   unsigned long long sg[MERGE_UNROLL];
+   int64_t ws[MERGE_UNROLL];
+#pragma unroll
+   for (int u = 0; u < MERGE_UNROLL; ++u) {
+     const int64_t i = min(i0 + u * G, ncand - 1);
+     ws[u] = cand ? (int64_t)cand[i] : i;
+   }
+#pragma unroll
+   for (int u = 0; u < MERGE_UNROLL; ++u) sg[u] = sig != nullptr ? sig[ws[u]] : need;
+   for (int u = 0; u < MERGE_UNROLL; ++u) {
+    if (i0 + u * G >= ncand) break;
+    const int64_t w = ws[u];
     // the word's symbol signature (64-bit Bloom mask) rules out most words without
     // touching their symbols
-    if (sig != nullptr && (sig[w] & need) != need) continue;
+    if ((sg[u] & need) != need) continue;
     const uint32_t L = wlen[w];
     if (L < 2) continue;
     uint16_t* s = sym + wstart[w];
-    // read-only probe first: most words do not contain the pair
+    // read-only probe first: most words do not contain the pair.  No early exit: the
+    // loads do not wait on the compares, so they stream (long words are frequent
+    // signature false positives)
     bool hit = false;
     uint32_t prev = s[0];
-    for (uint32_t i = 1; i < L && !hit; ++i) {
-      const uint32_t cur = s[i];
-      hit = (prev == (uint32_t)a) & (cur == (uint32_t)b);
+#pragma unroll 8
+    for (uint32_t k = 1; k < L; ++k) {
+      const uint32_t cur = s[k];
+      hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
       prev = cur;
     }
     if (!hit) continue;
@@ -354,9 +447,14 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
     wlen[w] = o;
     if (sig != nullptr) {
       unsigned long long g = 0;
-      for (uint32_t i = 0; i < o; ++i) g |= sig_bit(s[i]);
+      for (uint32_t k = 0; k < o; ++k) g |= sig_bit(s[k]);
       sig[w] = g;
     }
+    if (use_ix) {   // w now holds `new`: it goes on new's list
+      const uint32_t pos = atomicAdd(&ix.ctl[0], 1u);
+      if (pos < ix.ctl[2]) ix.pool[pos] = (uint32_t)w;
+    }
+   }
   }
   if (LDS) {
     if (any) touched = 1;
@@ -369,25 +467,92 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   }
 }
 
-// table += deltas, deltas = 0, table[a][b] = 0, tlen[new] = tlen[a] + tlen[b].  Only the
-// thread of x == a can touch (a, b) (through (x, a) or (b, x) when a == b, both negative),
-// so it retires the pair after its own adds: no fence, one launch.
-__global__ __launch_bounds__(256) void k_apply(uint32_t* __restrict__ table, int32_t* __restrict__ deltas, int Vt,
-                                               int a, int b, int nid, uint32_t* __restrict__ tlen) {
-  const int x = blockIdx.x * 256 + threadIdx.x;
-  if (x >= Vt) return;
-  int32_t v;
-  if ((v = deltas[x])) atomicAdd(&table[(size_t)x * Vt + a], (uint32_t)v);
-  if ((v = deltas[Vt + x])) atomicAdd(&table[(size_t)x * Vt + nid], (uint32_t)v);
-  if ((v = deltas[2 * Vt + x])) atomicAdd(&table[(size_t)b * Vt + x], (uint32_t)v);
-  if ((v = deltas[3 * Vt + x])) atomicAdd(&table[(size_t)nid * Vt + x], (uint32_t)v);
-  deltas[x] = 0;
-  deltas[Vt + x] = 0;
-  deltas[2 * Vt + x] = 0;
-  deltas[3 * Vt + x] = 0;
-  if (x == a) {
-    atomicExch(&table[(size_t)a * Vt + b], 0u);   // merged pair retired (never re-picked)
-    tlen[nid] = tlen[a] + tlen[b];
+// Fused apply + argmax, one workgroup per row x (the apply touches only entries of rows it
+// owns: (x, a) and (x, new) for every x, rows b and new entirely).  When `apply`:
+// table += deltas for row x, deltas consumed are zeroed, row a's (a, b) is retired after its
+// own adds (the only deltas that can reach (a, b) are row a's, when a == b), tlen[new] set.
+// A row rescans only if it changed (or was never scanned); then each workgroup folds its
+// row's best into the result slot.
+__global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ table, int32_t* __restrict__ deltas,
+                                                      int Vt, int vcur, ArgWs aw, int parity, int apply, int a, int b,
+                                                      int nid, uint32_t* __restrict__ tlen, WordIndex ix, bool use_ix,
+                                                      bool reused) {
+  __shared__ unsigned long long sh[4];
+  __shared__ int changed;
+  const int x = blockIdx.x;
+  uint32_t* row = table + (size_t)x * Vt;
+  if (x == 0 && threadIdx.x == 0) aw.slot[parity ^ 1] = 0ull;
+  if (threadIdx.x == 0) changed = 0;
+  __syncthreads();
+  if (apply) {
+    if (threadIdx.x == 0) {
+      int32_t v;
+      if ((v = deltas[x])) { row[a] += (uint32_t)v; deltas[x] = 0; changed = 1; }
+      if ((v = deltas[Vt + x])) { row[nid] += (uint32_t)v; deltas[Vt + x] = 0; changed = 1; }
+    }
+    __syncthreads();   // row[a] / row[nid] before the row-wide adds below (x == b or x == nid)
+    if (x == b || x == nid) {
+      int any = 0;
+      for (int y = threadIdx.x; y < Vt; y += 256) {
+        int32_t v;
+        if (x == b && (v = deltas[2 * Vt + y])) { row[y] += (uint32_t)v; deltas[2 * Vt + y] = 0; any = 1; }
+        if (x == nid && (v = deltas[3 * Vt + y])) { row[y] += (uint32_t)v; deltas[3 * Vt + y] = 0; any = 1; }
+      }
+      if (any) changed = 1;
+    }
+    __syncthreads();
+    if (x == a && threadIdx.x == 0) {
+      row[b] = 0u;   // merged pair retired (never re-picked)
+      tlen[nid] = tlen[a] + tlen[b];
+      changed = 1;
+      if (use_ix) {   // the pool range appended by the merge becomes new's word list
+        const uint32_t top = ix.ctl[0], mark = ix.ctl[1], cap = ix.ctl[2];
+        if (reused || top > cap) {
+          ix.len[nid] = IDX_INEXACT;
+        } else {
+          ix.start[nid] = mark;
+          ix.len[nid] = top - mark;
+        }
+        const uint32_t t = top > cap ? cap : top;
+        ix.ctl[0] = t;
+        ix.ctl[1] = t;
+      }
+    }
+    __syncthreads();
+  }
+  if (x >= vcur) return;
+  unsigned long long best = 0;
+  if (aw.clean[x] && !changed) {
+    best = aw.rowbest[x];
+  } else {
+    for (int y0 = threadIdx.x * 8; y0 < vcur; y0 += 256 * 8) {
+      uint32_t c[8];
+      if (((Vt & 3) == 0) && y0 + 8 <= vcur) {
+        const uint4 u0 = *reinterpret_cast<const uint4*>(row + y0);
+        const uint4 u1 = *reinterpret_cast<const uint4*>(row + y0 + 4);
+        c[0] = u0.x; c[1] = u0.y; c[2] = u0.z; c[3] = u0.w; c[4] = u1.x; c[5] = u1.y; c[6] = u1.z; c[7] = u1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = y0 + k < vcur ? row[y0 + k] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)(y0 + k);
+        if (c[k]) best = umax64(best, ((unsigned long long)c[k] << 32) | (unsigned long long)(~idx));
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
+    __syncthreads();
+    best = umax64(umax64(sh[0], sh[1]), umax64(sh[2], sh[3]));
+    if (threadIdx.x == 0) {
+      aw.rowbest[x] = best;
+      aw.clean[x] = 1u;
+    }
+  }
+  if (threadIdx.x == 0 && best) {
+    unsigned long long* slot = aw.slot + parity;
+    if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
   }
 }
 
@@ -665,14 +830,66 @@ extern "C" int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart
   return BEAST_OK;
 }
 
-extern "C" size_t beast_bpe_argmax_workspace_bytes(int Vt) { (void)Vt; return 4 * 8; }
+extern "C" size_t beast_bpe_argmax_workspace_bytes(int Vt) { return (size_t)(4 + (int64_t)Vt) * 8 + (size_t)Vt * 4; }
 
 extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int call, void* stream) {
   BEAST_REQUIRE(table && ws && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
   BEAST_REQUIRE(call >= 0, "beast_bpe_argmax: call index must be >= 0");
-  hipLaunchKernelGGL(k_argmax, dim3(vcur), dim3(ARG_TPR), 0, beast::as_stream(stream), table, Vt, vcur,
-                     reinterpret_cast<unsigned long long*>(ws), call & 1);
-  BEAST_LAUNCHED("k_argmax");
+  hipLaunchKernelGGL(k_apply_argmax, dim3(vcur), dim3(256), 0, beast::as_stream(stream), const_cast<uint32_t*>(table),
+                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false);
+  BEAST_LAUNCHED("k_apply_argmax");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, int a, int b, int new_id,
+                                      uint32_t* tlen, void* index, int new_id_reused, uint64_t* ws, int call,
+                                      void* stream) {
+  BEAST_REQUIRE(table && deltas && tlen && ws && vcur >= 1 && vcur <= Vt && call >= 0,
+                "beast_bpe_apply_argmax: bad args");
+  BEAST_REQUIRE(a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt,
+                "beast_bpe_apply_argmax: ids out of range");
+  const WordIndex ix = index ? index_view(index, Vt) : WordIndex{};
+  // every row that can change must run: rows < vcur, and a / b / new_id
+  const int rows = std::max(vcur, std::max(a, std::max(b, new_id)) + 1);
+  hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, vcur,
+                     argws_view(ws, Vt), call & 1, 1, a, b, new_id, tlen, ix, index != nullptr, new_id_reused != 0);
+  BEAST_LAUNCHED("k_apply_argmax");
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_index_workspace_bytes(int Vt, int64_t pool_capacity) {
+  return (size_t)(2 * (int64_t)Vt + 4 + pool_capacity) * 4;
+}
+
+extern "C" int beast_bpe_build_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                                     int Vt, void* index, size_t index_bytes, void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && index && n_words >= 0 && Vt >= 1 && Vt <= 65535,
+                "beast_bpe_build_index: bad args");
+  const size_t head = (size_t)(2 * (int64_t)Vt + 4) * 4;
+  BEAST_REQUIRE_CODE(index_bytes >= head + 4, BEAST_E_WORKSPACE, "index workspace too small");
+  const int64_t cap = (int64_t)(index_bytes - head) / 4;
+  BEAST_REQUIRE(cap < (int64_t)IDX_INEXACT, "index pool too large");
+  hipStream_t s = beast::as_stream(stream);
+  WordIndex ix = index_view(index, Vt);
+  uint32_t* cursor = ix.pool;   // scratch: the first Vt pool slots are rewritten by the fill
+  BEAST_REQUIRE_CODE(cap >= Vt, BEAST_E_WORKSPACE, "index pool smaller than the vocabulary");
+  BEAST_HIP(hipMemsetAsync(index, 0, head, s), "index memset");
+  const uint32_t capv = (uint32_t)cap;
+  BEAST_HIP(hipMemcpyAsync(ix.ctl + 2, &capv, 4, hipMemcpyHostToDevice, s), "index cap");
+  if (n_words > 0) {
+    hipLaunchKernelGGL(k_index_words<false>, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, s, sym, wstart, wlen,
+                       n_words, ix, cursor);
+    BEAST_LAUNCHED("k_index_words");
+  }
+  // cursor lives in a separate scratch region: reuse the (not yet filled) tail of the pool
+  uint32_t* cur2 = ix.pool + (cap - Vt);
+  hipLaunchKernelGGL(k_index_scan, dim3(1), dim3(1024), 0, s, ix, Vt, cur2);
+  BEAST_LAUNCHED("k_index_scan");
+  if (n_words > 0) {
+    hipLaunchKernelGGL(k_index_words<true>, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, s, sym, wstart, wlen,
+                       n_words, ix, cur2);
+    BEAST_LAUNCHED("k_index_words");
+  }
   return BEAST_OK;
 }
 
@@ -688,7 +905,8 @@ extern "C" int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* ws
 
 extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                                int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
-                               int32_t* deltas, int Vt, uint64_t* sig, void* stream) {
+                               int32_t* deltas, int Vt, uint64_t* sig, void* index, int64_t pair_count,
+                               void* stream) {
   BEAST_REQUIRE(sym && wstart && wlen && tlen && deltas, "beast_bpe_merge: null pointer");
   BEAST_REQUIRE(a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt && Vt <= 65535,
                 "beast_bpe_merge: ids out of range (a=%d b=%d new=%d Vt=%d)", a, b, new_id, Vt);
@@ -697,25 +915,19 @@ extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* 
   const int grid = grid_for(n_words, 256, 2048);
   const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
   unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
-  if (lds <= 64 * 1024)
+  const WordIndex ix = index ? index_view(index, Vt) : WordIndex{};
+  // LDS-privatised deltas only for frequent pairs: a rare pair touches few words, and the
+  // per-workgroup LDS clear / flush would dominate (global atomics then)
+  if (lds <= 64 * 1024 && pair_count >= MERGE_LDS_MIN_COUNT)
     hipLaunchKernelGGL(k_merge<true>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr);
   else
     hipLaunchKernelGGL(k_merge<false>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr);
   BEAST_LAUNCHED("k_merge");
   return BEAST_OK;
 }
 
-extern "C" int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, int b, int new_id, uint32_t* tlen,
-                               void* stream) {
-  BEAST_REQUIRE(table && deltas && tlen && a >= 0 && a < Vt && b >= 0 && b < Vt && new_id >= 0 && new_id < Vt,
-                "beast_bpe_apply: bad args");
-  hipLaunchKernelGGL(k_apply, dim3((Vt + 255) / 256), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, a, b,
-                     new_id, tlen);
-  BEAST_LAUNCHED("k_apply");
-  return BEAST_OK;
-}
 
 extern "C" size_t beast_bpe_dedup_workspace_bytes(int64_t n_words) {
   const uint64_t cap = dedup_cap(n_words > 0 ? n_words : 1);

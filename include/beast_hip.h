@@ -167,7 +167,9 @@ int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uin
                           const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream);
 /* max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)) (0 if the table is empty)
  * into ws[2 + (call & 1)], where call = 0, 1, 2, ... numbers the calls on this workspace
- * (each call zeroes the other slot for the next one: no memset per call).
+ * (each call zeroes the other slot for the next one: no memset per call).  Incremental:
+ * ws caches each row's best; a row is rescanned only when beast_bpe_apply_argmax changed it
+ * -- any other table write needs a fresh zero-filled ws.
  * ws: beast_bpe_argmax_workspace_bytes(Vt), zero-filled once before call 0. */
 size_t beast_bpe_argmax_workspace_bytes(int Vt);
 int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int call, void* stream);
@@ -175,19 +177,31 @@ int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int 
  * HF's pair-count changes, per word times wcount (NULL = 1):
  * [0]: (x,a)  [1]: (x,new)  [2]: (b,y)  [3]: (new,y).
  * are accumulated into deltas[4][Vt] int32 (multi-GPU: all-reduce them, then
- * beast_bpe_apply).  sig: see beast_bpe_word_signatures (nullable). */
+ * beast_bpe_apply_argmax).  sig: see beast_bpe_word_signatures (nullable).  pair_count: the pair's
+ * count from beast_bpe_argmax (a hint choosing LDS-privatised or direct delta atomics). */
 int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                     int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
-                    int32_t* deltas, int Vt, uint64_t* sig, void* stream);
+                    int32_t* deltas, int Vt, uint64_t* sig, void* index, int64_t pair_count, void* stream);
+/* Inverted index symbol -> words (HF's where_to_update): the merge visits only the words on
+ * the shorter list of a and b, and appends the words it rewrote as the list of new_id
+ * (committed by beast_bpe_apply_argmax).  index: beast_bpe_index_workspace_bytes(Vt, capacity) with
+ * capacity >= (symbols of the words) + Vt + room for appends; when it runs out, lists become
+ * unknown and merges fall back to visiting every word (results never change).  Nullable. */
+size_t beast_bpe_index_workspace_bytes(int Vt, int64_t pool_capacity);
+int beast_bpe_build_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                          int Vt, void* index, size_t index_bytes, void* stream);
 /* sig[w] = OR of 1 << (symbol & 63) over word w (a Bloom mask of its symbols).  Passed to
  * beast_bpe_merge (nullable), it lets the merge skip words that cannot contain the pair
  * without reading their symbols; the merge keeps it current for the words it rewrites. */
 int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
                               uint64_t* sig, void* stream);
-/* table += deltas (then deltas = 0), table[a][b] = 0 (merged pair retired),
- * tlen[new_id] = tlen[a] + tlen[b]. */
-int beast_bpe_apply(uint32_t* table, int32_t* deltas, int Vt, int a, int b, int new_id, uint32_t* tlen,
-                    void* stream);
+/* The step after a merge, fused with the next argmax: table += deltas (deltas consumed are
+ * zeroed), table[a][b] = 0 (merged pair retired), tlen[new_id] = tlen[a] + tlen[b], with an
+ * index commit new_id's word list (new_id_reused != 0: new_id already existed, its list
+ * becomes unknown); then the argmax of beast_bpe_argmax (same ws, next call index) over
+ * x, y < vcur (vcur counting new_id). */
+int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, int a, int b, int new_id,
+                           uint32_t* tlen, void* index, int new_id_reused, uint64_t* ws, int call, void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

@@ -73,7 +73,7 @@ class NumpyBpeOps:
         x, y = np.argwhere(tb == c)[0]           # row-major first = smallest (x, y)
         return (c << 32) | (0xFFFFFFFF - (int(x) * Vt + int(y)))
 
-    def merge(self, words, a, b, nid, max_len, Vt):
+    def merge(self, words, a, b, nid, max_len, Vt, count=0):
         d = np.zeros((4, Vt), dtype=np.int64)
         nl = self.tlen[a] + self.tlen[b]
         for w, n in zip(words["words"], words["counts"]):
@@ -92,6 +92,10 @@ class NumpyBpeOps:
                 i += 1
         self.deltas = torch.from_numpy(d.reshape(-1).astype(np.int32))
         return self.deltas
+
+    def apply_argmax(self, table, deltas, Vt, vcur, a, b, nid, reused=False):
+        self.apply(table, deltas, Vt, a, b, nid)
+        return self.argmax(table, Vt, vcur)
 
     def apply(self, table, deltas, Vt, a, b, nid):
         tb = table.numpy().reshape(Vt, Vt)

@@ -379,6 +379,35 @@ def test_bpe_train_matches_hf(case, bpe_golden, gpu_device):
     assert st.tokenizer.decode(ids) == text
 
 
+@pytest.mark.parametrize("index_mode", ["index", "tiny_pool", "no_index", "compact"])
+@pytest.mark.parametrize("case", ["skew/2048", "rand256/700", "traj_k3/2048"])
+def test_bpe_merge_paths_match_hf(case, index_mode, bpe_golden, gpu_device):
+    """The merge loop's fallbacks give HF's merges too: an index pool that overflows (lists
+    unknown -> every word visited), no index at all, and periodic compaction."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+    ref, corpora = bpe_golden
+    cname, vs = case.split("/")
+    arr = corpora[cname]
+
+    class Ops(GpuBpeOps):
+        def build_index(self, words, Vt):
+            if index_mode == "index":
+                return GpuBpeOps.build_index(self, words, Vt)
+            if index_mode == "no_index":
+                self._index = None
+                return
+            nb = _lib.load().beast_bpe_index_workspace_bytes(Vt, Vt + 64)
+            self._index = torch.empty((nb + 3) // 4, dtype=torch.int32, device=self.device)
+            _lib.run("beast_bpe_build_index", words["sym"].data_ptr(), words["wstart"].data_ptr(),
+                     words["wlen"].data_ptr(), words["n_words"], Vt, self._index.data_ptr(), nb, self.stream)
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    res = train_bpe(flat, off, int(vs), ops=Ops(gpu_device) if index_mode != "compact" else None,
+                    compact_every=3 if index_mode == "compact" else 0, use_index=index_mode != "compact")
+    assert res.vocab == ref[case]["vocab"]
+    assert [list(m) for m in res.merges] == ref[case]["merges"]
+
+
 def test_bpe_pretok_words_match_hf(gpu_device):
     from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, sequences_to_device
     from beast_tokenizer_amd.pretok import bytes_to_unicode, class_lut
