@@ -37,8 +37,29 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP extension cannot be built")
 
 
+FAST_SRC = os.path.join(CSRC, "fastpath.cpp")
+FAST_DIR = os.path.join(PKG, "_fastpath")
+FAST_NAME = "beast_fastpath"
+
+
 def _sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def fastpath_so() -> str:
+    return os.path.join(FAST_DIR, FAST_NAME + ".so")
+
+
+def build_fastpath(force: bool = False, verbose: bool = False) -> str:
+    """The host-side C++ fast path (csrc/fastpath.cpp, ATen only, no device code), built
+    in-tree with torch.utils.cpp_extension so it travels with the repo."""
+    so = fastpath_so()
+    if not force and os.path.exists(so) and os.path.getmtime(so) >= os.path.getmtime(FAST_SRC):
+        return so
+    from torch.utils.cpp_extension import load
+    os.makedirs(FAST_DIR, exist_ok=True)
+    load(name=FAST_NAME, sources=[FAST_SRC], build_directory=FAST_DIR, extra_cflags=["-O3"], verbose=verbose)
+    return so
 
 
 def _deps():
@@ -87,4 +108,5 @@ if __name__ == "__main__":
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     print(build(force=a.force, verbose=a.verbose))
+    print(build_fastpath(force=a.force, verbose=a.verbose))
     sys.exit(0)

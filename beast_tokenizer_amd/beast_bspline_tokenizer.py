@@ -62,6 +62,26 @@ class _MPInfo:
                 f"tau={self.tau:.6g})")
 
 
+_FAST = None
+
+
+def _fastpath():
+    """The in-tree C++ host fast path (csrc/fastpath.cpp) if it was built, else None."""
+    global _FAST
+    if _FAST is None:
+        import importlib.util
+        import os
+        from . import _build
+        so = _build.fastpath_so()
+        _FAST = False
+        if os.path.exists(so):
+            spec = importlib.util.spec_from_file_location(_build.FAST_NAME, so)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _FAST = mod
+    return _FAST or None
+
+
 class _Plan:
     """Launch state of the hot path on one device: the cached constants (basis Phi,
     fp32 projection P, DoF maps) and the bound tensors, kept as raw pointers so a
@@ -69,7 +89,7 @@ class _Plan:
     bound tensors change (in-place updates of ``w_min`` / ``w_max`` keep it valid)."""
 
     __slots__ = ("dev", "idx", "version", "wmin", "wmax", "keep", "T", "min_din",
-                 "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec")
+                 "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec", "fast")
 
     def __init__(self, tok: "BEASTBsplineTokenizer", dev: torch.device):
         lib = _lib.load()
@@ -86,6 +106,15 @@ class _Plan:
         self.p_src, self.p_dst = src.data_ptr(), dst.data_ptr()
         self.p_wmn, self.p_wmx = wmn.data_ptr(), wmx.data_ptr()
         self.enc, self.rec = lib.beast_encode_f32, lib.beast_reconstruct_f32
+        fp = _fastpath()
+        self.fast = None
+        if fp is not None:
+            import ctypes
+            addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value   # noqa: E731
+            self.fast = fp.make_plan(addr(lib.beast_encode_f32), addr(lib.beast_reconstruct_f32),
+                                     addr(lib.beast_last_error), dev.index, tok.num_dof, tok.joint_dof,
+                                     tok.num_basis, self.T, tok.vocab_size, self.min_din, self.p_src, self.p_proj,
+                                     self.p_wmn, self.p_wmx, self.p_phi, self.p_dst)
 
     def cacheable(self) -> bool:
         # bounds living elsewhere were copied to the device: do not reuse the copy
@@ -449,6 +478,10 @@ class BEASTBsplineTokenizer(TokenizerBase):
         p = self._plan()
         offset = (self.llm_vocab_size - self.vocab_size
                   if respect_llm_vocab_size and self.llm_vocab_size is not None else 0)
+        if not update_bounds and p.fast is not None:
+            r = p.fast.encode(trajs, offset, torch._C._cuda_getCurrentRawStream(p.idx))
+            if r is not None:
+                return r[0], {"params": r[1], "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
         if update_bounds:
             with torch.no_grad():
                 params, _ = self._fit(trajs, None, p)
@@ -588,6 +621,10 @@ class BEASTBsplineTokenizer(TokenizerBase):
     def reconstruct_traj(self, tokens, times=None, **kwargs):
         """Positions [B, T, num_dof] from tokens (reference :498-536); kwargs: init_p [B, num_dof]."""
         p = self._plan()
+        if times is None and p.fast is not None and kwargs.get("init_p") is None:
+            r = p.fast.reconstruct(tokens, self._offset(True), torch._C._cuda_getCurrentRawStream(p.idx))
+            if r is not None:
+                return r
         tokens = self._token_rows(tokens, p.dev)
         return self._reconstruct(tokens, None, times, kwargs.get("init_p"), True, p)
 

@@ -1,0 +1,98 @@
+// Host fast path for BEASTBsplineTokenizer.encode / reconstruct_traj (default time grid).
+//
+// Host-side C++ only: the same C-ABI entry points the ctypes binding calls
+// (beast_encode_f32 / beast_reconstruct_f32 in libbeast_hip.so, passed in as function
+// pointers so this module does not link the library), with the output tensors allocated by
+// ATen instead of through Python.  It saves the per-call Python cost of two torch.empty and
+// the ctypes argument marshalling (the B=4096 step is host-bound).  Anything
+// unusual (non-contiguous input, wrong device / dtype / shape) returns None and the caller
+// takes the general Python path, which raises the reference's exception types.
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace {
+
+typedef int (*enc_fn_t)(const float*, int64_t, int, int64_t, int64_t, int64_t, int, int, int, const int32_t*,
+                        const float*, int, const float*, const float*, int, int64_t, float*, int64_t*, void*);
+typedef int (*rec_fn_t)(const int64_t*, int64_t, int, int, int, int, int64_t, const float*, const float*,
+                        const float*, int64_t, int, const int32_t*, int, const float*, int64_t, const int32_t*, float*,
+                        float*, const float*, void*);
+typedef const char* (*err_fn_t)(void);
+
+struct Plan {
+  enc_fn_t enc = nullptr;
+  rec_fn_t rec = nullptr;
+  err_fn_t err = nullptr;
+  int64_t device = 0;
+  int64_t D = 0, nj = 0, N = 0, T = 0, V = 0, min_din = 0;
+  int64_t p_src = 0, p_proj = 0, p_wmn = 0, p_wmx = 0, p_phi = 0, p_dst = 0;
+
+  void fail(int rc, const char* what) const {
+    std::string m = std::string(what) + ": " + (err ? err() : "error") + " (code " + std::to_string(rc) + ")";
+    throw std::runtime_error(m);
+  }
+
+  // (tokens int64 [B, N*D] + offset, params fp32 [B, D*N]) or None
+  py::object encode(const at::Tensor& x, int64_t offset, int64_t stream) const {
+    if (!x.is_cuda() || x.get_device() != device || x.scalar_type() != at::kFloat || x.dim() != 3 ||
+        x.size(1) != T || x.size(2) < min_din || x.stride(2) != 1)
+      return py::none();
+    const int64_t B = x.size(0);
+    const int64_t DN = D * N;
+    at::Tensor params = at::empty({B, DN}, x.options());
+    at::Tensor tokens = at::empty({B, DN}, x.options().dtype(at::kLong));
+    const int rc = enc(x.data_ptr<float>(), B, (int)T, x.stride(0), x.stride(1), x.stride(2), (int)x.size(2), (int)D,
+                       (int)nj, reinterpret_cast<const int32_t*>(p_src), reinterpret_cast<const float*>(p_proj),
+                       (int)N, reinterpret_cast<const float*>(p_wmn), reinterpret_cast<const float*>(p_wmx), (int)V,
+                       offset, params.data_ptr<float>(), tokens.data_ptr<int64_t>(),
+                       reinterpret_cast<void*>(stream));
+    if (rc) fail(rc, "beast_encode_f32");
+    return py::make_tuple(tokens, params);
+  }
+
+  // positions fp32 [B, T, D] from int64 tokens [B, N*D] (or [B, N, D]) or None
+  py::object reconstruct(const at::Tensor& tok, int64_t offset, int64_t stream) const {
+    if (!tok.is_cuda() || tok.get_device() != device || tok.scalar_type() != at::kLong || !tok.is_contiguous())
+      return py::none();
+    const int64_t DN = D * N;
+    int64_t B;
+    if (tok.dim() == 2 && tok.size(1) == DN) B = tok.size(0);
+    else if (tok.dim() == 3 && tok.size(1) * tok.size(2) == DN) B = tok.size(0);
+    else return py::none();
+    at::Tensor pos = at::empty({B, T, D}, tok.options().dtype(at::kFloat));
+    const int rc = rec(tok.data_ptr<int64_t>(), B, (int)D, (int)nj, (int)N, (int)V, offset,
+                       reinterpret_cast<const float*>(p_wmn), reinterpret_cast<const float*>(p_wmx),
+                       reinterpret_cast<const float*>(p_phi), 0, (int)T, reinterpret_cast<const int32_t*>(p_dst),
+                       (int)D, nullptr, 0, nullptr, nullptr, pos.data_ptr<float>(), nullptr,
+                       reinterpret_cast<void*>(stream));
+    if (rc) fail(rc, "beast_reconstruct_f32");
+    return py::cast(pos);
+  }
+};
+
+Plan make_plan(int64_t enc, int64_t rec, int64_t err, int64_t device, int64_t D, int64_t nj, int64_t N, int64_t T,
+               int64_t V, int64_t min_din, int64_t p_src, int64_t p_proj, int64_t p_wmn, int64_t p_wmx, int64_t p_phi,
+               int64_t p_dst) {
+  Plan p;
+  p.enc = reinterpret_cast<enc_fn_t>(enc);
+  p.rec = reinterpret_cast<rec_fn_t>(rec);
+  p.err = reinterpret_cast<err_fn_t>(err);
+  p.device = device;
+  p.D = D; p.nj = nj; p.N = N; p.T = T; p.V = V; p.min_din = min_din;
+  p.p_src = p_src; p.p_proj = p_proj; p.p_wmn = p_wmn; p.p_wmx = p_wmx; p.p_phi = p_phi; p.p_dst = p_dst;
+  if (!p.enc || !p.rec || !p.err) throw std::invalid_argument("null entry point");
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "host fast path of the BEAST encode / reconstruct calls (see csrc/fastpath.cpp)";
+  py::class_<Plan>(m, "Plan")
+      .def("encode", &Plan::encode, py::arg("x"), py::arg("offset"), py::arg("stream"))
+      .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"));
+  m.def("make_plan", &make_plan);
+}

@@ -224,6 +224,36 @@ def test_specialised_kernels_equal_generic(name, gpu_device):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_host_fastpath_equals_python_path(name, gpu_device):
+    """The C++ host fast path (csrc/fastpath.cpp) is built, in use, and returns exactly what
+    the Python/ctypes path returns; inputs it does not take fall through to that path."""
+    gi = CONFIGS[name]["gripper_indices"] or []
+    g = dict(load_npz(f"bspline_{name}.npz"))
+    tok = make_tok(name, g, gpu_device, llm_vocab_size=32000)
+    p = tok._plan()
+    assert p.fast is not None, "fast path not built / not loaded"
+    x = torch.from_numpy(synth_trajectories(777, 50, CONFIGS[name]["num_dof"], seed=4, gripper_indices=gi))
+    xd = x.to(gpu_device)
+    t1, d1 = tok.encode(xd)
+    r1 = tok.reconstruct_traj(t1)
+    fast = p.fast
+    p.fast = None
+    try:
+        t2, d2 = tok.encode(xd)
+        r2 = tok.reconstruct_traj(t2)
+    finally:
+        p.fast = fast
+    assert torch.equal(t1, t2) and torch.equal(d1["params"], d2["params"]) and torch.equal(r1, r2)
+    # fall-through cases: host input, strided input, 3-D int32 tokens
+    t3, _ = tok.encode(x)
+    assert torch.equal(t3, t1)
+    t4, _ = tok.encode(torch.cat([xd, xd], dim=2)[..., : xd.shape[2]])
+    assert torch.equal(t4, t1)
+    r5 = tok.reconstruct_traj(t1.reshape(777, 10, -1).to(torch.int32))
+    assert torch.equal(r5, r1)
+
+
 @pytest.mark.parametrize("vocab", [256, 1024, 4096])
 def test_encode_quantiser_exact_near_ties(vocab, gpu_device, kernel_mode):
     """The encode kernel's in-lane quantiser (reciprocal fast path + exact fallback) must
