@@ -23,7 +23,7 @@ OBJDIR = os.path.join(PKG, "csrc", "build")
 
 ARCH = os.environ.get("BEAST_OFFLOAD_ARCH", "gfx950")
 CXXFLAGS = [
-    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+    f"--offload-arch={ARCH}", os.environ.get("BEAST_OPT", "-O3"), "-std=c++17", "-fPIC",
     # bit-exact quantise / dequantise / basis: no FMA contraction, IEEE fp32 division
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",

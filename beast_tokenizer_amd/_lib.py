@@ -22,6 +22,7 @@ BEAST_E_UNSUPPORTED = -3
 BEAST_E_WORKSPACE = -4
 ABI_VERSION = 1
 OPT_GENERIC_KERNELS = 1
+OPT_BLOCK_WAVES = 2
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 

@@ -91,15 +91,16 @@ __device__ __forceinline__ void burst(void* __restrict__ dst, const void* __rest
 }
 
 // LDS -> global, float count
+template <int NT = NTHREADS>
 __device__ __forceinline__ void store_out(float* __restrict__ dst, const float* __restrict__ src, int count) {
   if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
     const int n4 = count >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (int i = threadIdx.x; i < n4; i += NTHREADS) d4[i] = s4[i];
-    for (int i = (n4 << 2) + threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
+    for (int i = threadIdx.x; i < n4; i += NT) d4[i] = s4[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < count; i += NT) dst[i] = src[i];
   } else {
-    for (int i = threadIdx.x; i < count; i += NTHREADS) dst[i] = src[i];
+    for (int i = threadIdx.x; i < count; i += NT) dst[i] = src[i];
   }
 }
 
@@ -109,18 +110,20 @@ __device__ __forceinline__ void store_out(float* __restrict__ dst, const float* 
 // padded to whole wave-instructions, sources past the end are clamped to the last element.
 typedef __attribute__((address_space(3))) void lds_void;
 
+template <int NT = NTHREADS>
 __device__ __forceinline__ void dma16(void* lds, const void* g, int n16) {
   const int tid = threadIdx.x, wb = tid & ~63;
-  for (int base = 0; base < n16; base += NTHREADS) {
+  for (int base = 0; base < n16; base += NT) {
     if (base + wb < n16)
       __builtin_amdgcn_global_load_lds(static_cast<const uint4*>(g) + min(base + tid, n16 - 1),
                                        (lds_void*)(static_cast<uint4*>(lds) + base + wb), 16, 0, 0);
   }
 }
 
+template <int NT = NTHREADS>
 __device__ __forceinline__ void dma4(void* lds, const void* g, int n) {
   const int tid = threadIdx.x, wb = tid & ~63;
-  for (int base = 0; base < n; base += NTHREADS) {
+  for (int base = 0; base < n; base += NT) {
     if (base + wb < n)
       __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(g) + min(base + tid, n - 1),
                                        (lds_void*)(static_cast<uint32_t*>(lds) + base + wb), 4, 0, 0);
@@ -131,13 +134,26 @@ __device__ __forceinline__ void dma4(void* lds, const void* g, int n) {
 // library compiles them out): s_memtime of lane 0 of every wave of workgroup 0 at the
 // phase boundaries of its first tile.
 #ifdef BEAST_STAMPS
-__device__ unsigned long long g_stamps[2][NWAVES][16];
+__device__ unsigned long long g_stamps[2][8][16];
 #define STAMP(k, i)                                                                              \
   do {                                                                                           \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_stamps[k][threadIdx.x >> 6][i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// Per-workgroup lifetime (first 4096 workgroups): s_memrealtime (100 MHz, chip-wide) at
+// entry and after the drain, and HW_ID / XCC_ID of the wave.
+__device__ unsigned long long g_bstamps[2][4096][4];
+#define BSTAMP(k, i)                                                                             \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                                                 \
+      g_bstamps[k][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();                            \
+      if (i == 0)                                                                                \
+        g_bstamps[k][blockIdx.x][2] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF814) << 32) | \
+                                      (unsigned)__builtin_amdgcn_s_getreg(0xF804);               \
+    }                                                                                            \
+  } while (0)
 #else
 #define STAMP(k, i) do { } while (0)
+#define BSTAMP(k, i) do { } while (0)
 #endif
 
 // -------------------------------------------------------------- geometry --
@@ -166,9 +182,10 @@ inline Geom make_geom(int D, int nj, int N, int T) {
 // Compile-time problem shape.  A zero field is read from the runtime Geom instead; the
 // BEAST defaults (N = 10 basis functions, T = 50 steps, 7 or 14 DoF with or without the
 // two gripper DoF) get fully specialised kernels in which every index is a constant.
-template <int SD, int SNJ, int SN, int ST, int SDL>
+template <int SD, int SNJ, int SN, int ST, int SDL, int SW = NWAVES>
 struct Shape {
   static constexpr int D = SD, NJ = SNJ, N = SN, T = ST, DL = SDL;
+  static constexpr int W = SW;   // waves per workgroup: one per MFMA column tile of a full tile
   static constexpr bool fixed = SD > 0;
 };
 using DynShape = Shape<0, 0, 0, 0, 0>;
@@ -224,7 +241,7 @@ struct EncArgs {
 };
 
 struct EncSmem {
-  int P, Y, pb, tq, wlo, whi, lcol, total;
+  int P, Y, pb, kq, wlo, whi, lcol, total;
 };
 
 // Every buffer an LDS-DMA fills is padded to whole wave-instructions (64 lanes x 16 B).
@@ -237,7 +254,7 @@ __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N,
   s.P = o;    o += round_up(nkinds * 16 * Tp * 4 + 64 * ECH, 1024);   // fp32 [16][Tp] projection per kind
   s.Y = o;    o += round_up(TBT * T * Dl * 4, 1024);
   s.pb = o;   o += round_up(TBT * D * N * 4, 16);        // params, (d n) per trajectory
-  s.tq = o;   o += round_up(TBT * D * N * 4, 16);        // token bins (int32), (n d) per trajectory
+  s.kq = o;   o += round_up(D * N * 4, 16);              // quantiser scale per (d n) column
   s.wlo = o;  o += round_up(D * N * 4, 256);
   s.whi = o;  o += round_up(D * N * 4, 256);
   s.lcol = o; o += round_up(D * 4, 256);
@@ -246,8 +263,9 @@ __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N,
 }
 
 template <int TBT, bool FAST, class S>
-__global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
+__global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NW = S::W, NT = NW * 64;
   const Geom& g = a.g;
   const Dims<S> m(g);
   const int D = m.D, N = m.N, T = m.T, Tp = m.Tp, per = m.per, DN = D * N;
@@ -260,27 +278,28 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
-  int* tq = reinterpret_cast<int*>(smem + L.tq);
+  float* kq = reinterpret_cast<float*>(smem + L.kq);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x;
   const bool quant = a.tokens_out != nullptr;
   const int tile_elems = T * a.row_elems;   // FAST: one trajectory, contiguous, % 4 == 0
 
   STAMP(0, 0);
+  BSTAMP(0, 0);
   // ---- prologue: the first tile and every constant go HBM -> LDS by DMA in one round trip
   if (FAST && (a.phases & 1) && blockIdx.x < a.ntiles) {
     const int64_t b0 = (int64_t)blockIdx.x * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
-    dma16(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
+    dma16<NT>(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
   }
   STAMP(0, 9);
-  dma16(P, a.proj, nkinds * 4 * Tp);
+  dma16<NT>(P, a.proj, nkinds * 4 * Tp);
   STAMP(0, 10);
   if (quant) {
-    dma4(wlo, a.w_min, DN);
-    dma4(whi, a.w_max, DN);
+    dma4<NT>(wlo, a.w_min, DN);
+    dma4<NT>(whi, a.w_max, DN);
   }
-  dma4(lcol, a.dof_src, D);
+  dma4<NT>(lcol, a.dof_src, D);
   STAMP(0, 11);
 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -294,10 +313,10 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
     // ---- the trajectory tile lands in LDS (the first one is already in flight)
     if (a.phases & 1) {
       if (FAST) {
-        if (tile != blockIdx.x) dma16(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
+        if (tile != blockIdx.x) dma16<NT>(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
       } else {
         const int pt = T * D;
-        for (int e = tid; e < nb * pt; e += NTHREADS) {
+        for (int e = tid; e < nb * pt; e += NT) {
           const int j = e / pt, r = e - j * pt, t = r / D, d = r - t * D;
           const int col = a.dof_src[d];
           Y[e] = (col >= 0 && col < a.row_elems)
@@ -309,17 +328,19 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
     __syncthreads();   // waits for the DMA (vmcnt) and the LDS stores
     if (tile == blockIdx.x) STAMP(0, 2);
     if (tile == blockIdx.x + gridDim.x) STAMP(0, 12);
+    if (quant && tile == blockIdx.x)   // bounds landed with the first tile; read after the next barrier
+      for (int i = tid; i < DN; i += NT) kq[i] = beast::quantize_scale(wlo[i], whi[i], vm1);
 
     // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f32 MFMA 16x16x4; A = P, B = y).
     //      A wave owns two column tiles per pass (two independent chains), operands
     //      pointer-stepped through LDS; rows t >= T (tail step) meet a zero A column.
-    for (int q0 = wave; (a.phases & 2) && q0 < nq; q0 += NWAVES * 2) {
+    for (int q0 = wave; (a.phases & 2) && q0 < nq; q0 += NW * 2) {
       int j0, d0, k0, j1, d1, k1;
       bool ok0, ok1;
       tile_col<TBT>(g, m, q0, lr, j0, d0, k0, ok0);
-      tile_col<TBT>(g, m, min(q0 + NWAVES, nq - 1), lr, j1, d1, k1, ok1);
+      tile_col<TBT>(g, m, min(q0 + NW, nq - 1), lr, j1, d1, k1, ok1);
       ok0 = ok0 && j0 < nb;
-      ok1 = ok1 && j1 < nb && (q0 + NWAVES < nq);
+      ok1 = ok1 && j1 < nb && (q0 + NW < nq);
       const int c0 = FAST ? min(max(lcol[d0], 0), Dl - 1) : d0;
       const int c1 = FAST ? min(max(lcol[d1], 0), Dl - 1) : d1;
       // K-steps in chunks of ECH: every LDS operand of a chunk is read before its MFMAs and
@@ -327,7 +348,7 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
       // even / odd steps accumulate separately (two chains per tile).  Step s covers rows
       // t = 4s + lane/16, clamped to T - 1 (the zero-padded P columns meet them).
       const int nst = (T + 3) >> 2;
-      const bool two = q0 + NWAVES < nq;   // wave-uniform: a second column tile this pass
+      const bool two = q0 + NW < nq;   // wave-uniform: a second column tile this pass
       const float* pa0 = P + (k0 * 16 + lr) * Tp + lk;
       const float* pa1 = P + (k1 * 16 + lr) * Tp + lk;
       const float* yc0 = Y + j0 * T * Dl + c0;
@@ -366,19 +387,14 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
         acc2[r] = __fadd_rn(acc2[r], acc3[r]);
       }
       // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r.  Each lane writes its params
-      // ((d n) image) and quantises them into the token bins ((n d) image) in place.
+      // into the (d n) image; quantisation happens in the epilogue, spread over every thread.
+      if (tile == blockIdx.x && q0 == wave) STAMP(0, 8);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = lk * 4 + r;
         if (n < N) {
-          if (ok0) {
-            pb[j0 * DN + d0 * N + n] = acc0[r];
-            if (quant) tq[j0 * per + n * D + d0] = beast::quantize_bin_fast(acc0[r], wlo[d0 * N + n], whi[d0 * N + n], vm1);
-          }
-          if (ok1) {
-            pb[j1 * DN + d1 * N + n] = acc2[r];
-            if (quant) tq[j1 * per + n * D + d1] = beast::quantize_bin_fast(acc2[r], wlo[d1 * N + n], whi[d1 * N + n], vm1);
-          }
+          if (ok0) pb[j0 * DN + d0 * N + n] = acc0[r];
+          if (ok1) pb[j1 * DN + d1 * N + n] = acc2[r];
         }
       }
     }
@@ -388,24 +404,48 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
     if (tile == blockIdx.x) STAMP(0, 4);
 
     // ---- epilogue: params (d n) and tokens (n d), both contiguous per tile
-    if (a.params_out != nullptr && (a.phases & 4)) store_out(a.params_out + b0 * DN, pb, nb * DN);
+    if (a.params_out != nullptr && (a.phases & 4)) store_out<NT>(a.params_out + b0 * DN, pb, nb * DN);
     if (tile == blockIdx.x) STAMP(0, 5);
-    if (quant && (a.phases & 8)) {   // int32 bins -> int64 tokens + offset, 2 x 16 B per 4 tokens
+    if (quant && (a.phases & 8)) {
+      // tokens in (n d) order: each thread quantises 4 consecutive tokens from the (d n)
+      // params image (fast bins; the exactly-rounded chain only where one lies near a
+      // rounding boundary), widens them to int64 + offset and stores 2 x 16 B.
       const int total = nb * per;
       long long* tout = a.tokens_out + b0 * per;
       const unsigned long long off = (unsigned long long)a.tok_offset;
+      auto col_of = [&](int e, int& pj) {   // token e of the tile -> (d n) column, trajectory
+        const int j = (int)div_by<S>((uint32_t)e, per, g.fd_per);
+        const int r = e - j * per;
+        const int n = (int)div_by<S>((uint32_t)r, D, g.fd_D);
+        pj = j * DN;
+        return (r - n * D) * N + n;
+      };
       int done = 0;
       if ((((uintptr_t)tout) & 15) == 0) {
         const int n4 = total >> 2;
-        for (int i = tid; i < n4; i += NTHREADS) {
-          const int4 b = reinterpret_cast<const int4*>(tq)[i];
+        for (int i = tid; i < n4; i += NT) {
+          int bin[4], c[4], pj[4];
+          bool ex = false;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            c[u] = col_of(4 * i + u, pj[u]);
+            bin[u] = beast::quantize_bin_k(pb[pj[u] + c[u]], wlo[c[u]], whi[c[u]], kq[c[u]], vm1, ex);
+          }
+          if (ex) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pb[pj[u] + c[u]], wlo[c[u]], whi[c[u]], vm1);
+          }
           longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
-          o2[0] = make_longlong2(beast::widen_bin(b.x, off), beast::widen_bin(b.y, off));
-          o2[1] = make_longlong2(beast::widen_bin(b.z, off), beast::widen_bin(b.w, off));
+          o2[0] = make_longlong2(beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
+          o2[1] = make_longlong2(beast::widen_bin(bin[2], off), beast::widen_bin(bin[3], off));
         }
         done = n4 << 2;
       }
-      for (int e = done + tid; e < total; e += NTHREADS) tout[e] = beast::widen_bin(tq[e], off);
+      for (int e = done + tid; e < total; e += NT) {
+        int pj;
+        const int c = col_of(e, pj);
+        tout[e] = beast::widen_bin(beast::quantize_bin(pb[pj + c], wlo[c], whi[c], vm1), off);
+      }
     }
     if (tile == blockIdx.x) STAMP(0, 6);
     if (tile == blockIdx.x + gridDim.x) STAMP(0, 14);
@@ -413,6 +453,7 @@ __global__ __launch_bounds__(NTHREADS) void k_encode(EncArgs a) {
 #ifdef BEAST_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(0, 7);
+  BSTAMP(0, 1);
 #endif
 }
 
@@ -438,13 +479,14 @@ constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divide
 constexpr int RT_REG = 4;       // row tiles (64 output rows) whose basis operands live in registers
 
 // token tile [nb][per] (int64, or fp32 normalised tokens) HBM -> LDS by DMA
+template <int NT = NTHREADS>
 __device__ __forceinline__ void stage_tokens(const RecArgs& a, void* lds, int64_t b0, int per) {
   const int nb = (int)min<int64_t>(a.B - b0, a.tbt);
   const void* src = a.ntokens ? static_cast<const void*>(a.ntokens + b0 * per)
                               : static_cast<const void*>(a.tokens + b0 * per);
   const int bytes = nb * per * (a.ntokens ? 4 : 8);
-  if ((bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) dma16(lds, src, bytes >> 4);
-  else dma4(lds, src, bytes >> 2);
+  if ((bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) dma16<NT>(lds, src, bytes >> 4);
+  else dma4<NT>(lds, src, bytes >> 2);
 }
 
 // W[j][d][n] from the staged tile: bit-exact discrete_to_continuous (beast/utils.py:20-25)
@@ -491,12 +533,13 @@ __host__ __device__ inline RecSmem rec_smem(int Tout, int D, int N, int ndo, int
 }
 
 // decode-only output (params_out, (d n) order) straight from the staged tokens
+template <int NT = NTHREADS>
 __device__ __forceinline__ void rec_params_out(const RecArgs& a, const unsigned char* tokl, int64_t b0, int nb,
                                                const float* wlo, const float* whi, const float* lut, float vm1) {
   const Geom& g = a.g;
   const int per = g.per, D = g.D, N = g.N;
   float* pout = a.params_out + b0 * per;
-  for (int e = threadIdx.x; e < nb * per; e += NTHREADS) {
+  for (int e = threadIdx.x; e < nb * per; e += NT) {
     const uint32_t j = fdiv(e, g.fd_per);
     const int k = e - j * per;                 // (d n) index
     const uint32_t d = fdiv(k, g.fd_N);
@@ -512,13 +555,13 @@ __device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const f
   const int rowlen = Tout * ndo;
   if ((rowlen & 3) == 0 && ((RTR * ndo) & 3) == 0 && ((((uintptr_t)gout) & 15) == 0)) {
     const int n4 = nb * rowlen / 4;
-    for (int i = threadIdx.x; i < n4; i += NTHREADS) {
+    for (int i = threadIdx.x; i < n4; i += S::W * 64) {
       const uint32_t e = 4 * i;
       const uint32_t j = div_by<S>(e, rowlen, a.fd_row);
       reinterpret_cast<float4*>(gout)[i] = *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen));
     }
   } else {
-    for (int e = threadIdx.x; e < nb * rowlen; e += NTHREADS) {
+    for (int e = threadIdx.x; e < nb * rowlen; e += S::W * 64) {
       const uint32_t j = div_by<S>(e, rowlen, a.fd_row);
       gout[e] = ob[j * RTR * ndo + (e - j * rowlen)];
     }
@@ -526,9 +569,10 @@ __device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const f
 }
 
 template <int TBT, int KS, int RT, class S>
-__global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
+__global__ __launch_bounds__(S::W * 64) void k_reconstruct(RecArgs a) {
   static_assert(KS > 0, "shared-basis kernel");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NW = S::W, NT = NW * 64;
   const Geom& g = a.g;
   const Dims<S> m(g);
   const int D = m.D, N = m.N, nj = m.nj, per = m.per;
@@ -550,13 +594,14 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
   const float vm1 = (float)(a.vocab - 1);
 
   STAMP(1, 0);
+  BSTAMP(1, 0);
   // ---- prologue: the first token tile, the bounds and the DoF map by DMA; the basis
   //      operands (registers or LDS) by clamped loads -- all in flight together
-  if ((a.phases & 1) && blockIdx.x < a.ntiles) stage_tokens(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
+  if ((a.phases & 1) && blockIdx.x < a.ntiles) stage_tokens<NT>(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
   STAMP(1, 9);
-  dma4(wlo, a.w_min, per);
-  dma4(whi, a.w_max, per);
-  dma4(dst, a.dof_dst, D);
+  dma4<NT>(wlo, a.w_min, per);
+  dma4<NT>(whi, a.w_max, per);
+  dma4<NT>(dst, a.dof_dst, D);
   STAMP(1, 10);
   // A operand of MFMA row tile rt, K-step ks: Phi_kind[rt*16 + lr][n], n = lane/16 * KS + ks,
   // zero outside [Tout) x [N).  RT > 0: the raw basis [kinds][Tout][N] is DMA'd to LDS with
@@ -564,33 +609,33 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
   float phr[2][RT > 0 ? RT : 1][KS];
   if constexpr (RT > 0) {
     const int pbytes = nkinds * Tout * N * 4;
-    if ((pbytes & 15) == 0 && (((uintptr_t)a.basis) & 15) == 0) dma16(phi, a.basis, pbytes >> 4);
-    else dma4(phi, a.basis, pbytes >> 2);
+    if ((pbytes & 15) == 0 && (((uintptr_t)a.basis) & 15) == 0) dma16<NT>(phi, a.basis, pbytes >> 4);
+    else dma4<NT>(phi, a.basis, pbytes >> 2);
   } else {
     const int tot = nkinds * RTR * Np4, tn = RTR * Np4;
-    for (int base = 0; base < tot; base += 8 * NTHREADS) {
+    for (int base = 0; base < tot; base += 8 * NT) {
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int i = min(base + u * NTHREADS + tid, tot - 1);
+        const int i = min(base + u * NT + tid, tot - 1);
         const int k = i >= tn ? 1 : 0, r = i - k * tn, t = r / Np4, n = r - t * Np4;
         const float x = a.basis[(int64_t)k * Tout * N + min(t, Tout - 1) * N + min(n, N - 1)];
         const uint32_t keep = 0u - (uint32_t)((t < Tout) & (n < N));
         v[u] = __uint_as_float(__float_as_uint(x) & keep);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) phi[min(base + u * NTHREADS + tid, tot - 1)] = v[u];
+      for (int u = 0; u < 8; ++u) phi[min(base + u * NT + tid, tot - 1)] = v[u];
     }
   }
   STAMP(1, 11);
-  for (int t = tid; t < a.lut_n; t += NTHREADS) lut[t] = __fdiv_rn((float)t, vm1);
+  for (int t = tid; t < a.lut_n; t += NT) lut[t] = __fdiv_rn((float)t, vm1);
   STAMP(1, 12);
 
   for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int64_t b0 = tile * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
 
-    if ((a.phases & 1) && tile != blockIdx.x) stage_tokens(a, smem + L.tok, b0, per);
+    if ((a.phases & 1) && tile != blockIdx.x) stage_tokens<NT>(a, smem + L.tok, b0, per);
     if (tile == blockIdx.x) STAMP(1, 1);
     __syncthreads();   // tokens (DMA), bounds, DoF map, LDS basis and LUT are in place
     if (tile == blockIdx.x) STAMP(1, 2);
@@ -608,13 +653,13 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
             }
       }
     }
-    if (a.params_out != nullptr) rec_params_out(a, tokl, b0, nb, wlo, whi, lut, vm1);
+    if (a.params_out != nullptr) rec_params_out<NT>(a, tokl, b0, nb, wlo, whi, lut, vm1);
 
     // ---- pos[j][t][dst(d)] = sum_n Phi_kind[t][n] W[j][d][n]  (f32 MFMA 16x16x4; A = Phi, B = W).
     //      A wave owns a column tile (j, d) and dequantises its own B operand (K-step ks
     //      holds n = 4*ks + lane/16) straight from the token tile; the basis operands
     //      are reused across the wave's column tiles; rows past Tout land in ob's padding.
-    for (int q = wave; (a.phases & 2) && q < nq; q += NWAVES) {
+    for (int q = wave; (a.phases & 2) && q < nq; q += NW) {
       int j, d, kind;
       bool ok;
       tile_col<TBT>(g, m, q, lr, j, d, kind, ok);
@@ -680,6 +725,7 @@ __global__ __launch_bounds__(NTHREADS) void k_reconstruct(RecArgs a) {
 #ifdef BEAST_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(1, 8);
+  BSTAMP(1, 1);
 #endif
 }
 
@@ -790,14 +836,36 @@ int cu_count() {
   return n;
 }
 
+// Diagnostic knob: BEAST_DEBUG_GRID_CAP=<n> caps the codec grids (tools/stamps uses it to
+// give each workgroup a second tile, i.e. to time a tile with warm instruction cache).
+int64_t debug_grid_cap() {
+  static const int64_t v = [] {
+    const char* e = getenv("BEAST_DEBUG_GRID_CAP");
+    return e ? std::max<int64_t>(1, atoll(e)) : INT64_MAX;
+  }();
+  return v;
+}
+
 int64_t grid_for(int64_t ntiles, int lds_bytes) {
   const int per_cu = std::max(1, std::min(8, (160 * 1024) / std::max(lds_bytes, 1)));
-  return std::max<int64_t>(1, std::min<int64_t>(ntiles, (int64_t)cu_count() * per_cu * 2));
+  const int64_t g = std::min<int64_t>(ntiles, (int64_t)cu_count() * per_cu * 2);
+  return std::max<int64_t>(1, std::min(g, debug_grid_cap()));
 }
 
 // Diagnostic / test knob (beast_set_option): run the runtime-shape kernels even where a
 // specialised one exists.
 bool g_generic_only = false;
+
+// Specialised 14-DoF kernels come in two widths.  A batch that gives every CU at most two
+// tiles is latency-bound: 7 waves, one MFMA column tile each, shorten a workgroup's critical
+// path.  Larger batches want more tiles in flight per CU: 4 waves (two column tiles each)
+// fit 4 workgroups per CU where 7-wave ones fit 2.  beast_set_option(BEAST_OPT_BLOCK_WAVES,
+// 4 | 7) forces one (tests, measurements); 0 = by batch size.
+int g_block_waves = 0;
+bool wide_blocks(int64_t ntiles) {
+  if (g_block_waves == 4 || g_block_waves == 7) return g_block_waves == 7;
+  return ntiles <= 2 * (int64_t)cu_count();
+}
 
 template <int TBT, class S>
 int launch_encode_t(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream_t s) {
@@ -807,8 +875,8 @@ int launch_encode_t(EncArgs a, int T, int D, int nj, int N, bool fast, hipStream
   const EncSmem L = enc_smem<TBT>(T, a.g.Tp, Dl, D, N, nj < D ? 2 : 1);
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "encode tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
-  if (fast) hipLaunchKernelGGL((k_encode<TBT, true, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else hipLaunchKernelGGL((k_encode<TBT, false, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  if (fast) hipLaunchKernelGGL((k_encode<TBT, true, S>), dim3(grid), dim3(S::W * 64), L.total, s, a);
+  else hipLaunchKernelGGL((k_encode<TBT, false, S>), dim3(grid), dim3(S::W * 64), L.total, s, a);
   BEAST_LAUNCHED("k_encode");
   return BEAST_OK;
 }
@@ -830,8 +898,13 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   if (!fast) tbt = 8;
   if (forced == 1 || forced == 2 || forced == 4 || (forced == 8 && fast)) tbt = std::min(tbt, forced);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
-    if (D == 14 && nj == 14) return launch_encode_t<8, Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, true, s);
-    if (D == 14 && nj == 12) return launch_encode_t<8, Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, true, s);
+    const bool wide = wide_blocks((a.B + 7) / 8);
+    if (D == 14 && nj == 14)
+      return wide ? launch_encode_t<8, Shape<14, 14, 10, 50, 14, 7>>(a, T, D, nj, N, true, s)
+                  : launch_encode_t<8, Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, true, s);
+    if (D == 14 && nj == 12)
+      return wide ? launch_encode_t<8, Shape<14, 12, 10, 50, 14, 7>>(a, T, D, nj, N, true, s)
+                  : launch_encode_t<8, Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, true, s);
     if (D == 7 && nj == 7) return launch_encode_t<8, Shape<7, 7, 10, 50, 7>>(a, T, D, nj, N, true, s);
   }
   switch (tbt) {
@@ -848,7 +921,7 @@ int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
   if constexpr (KS == 0) hipLaunchKernelGGL((k_reconstruct_rows<TBT>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(NTHREADS), L.total, s, a);
+  else hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(S::W * 64), L.total, s, a);
   BEAST_LAUNCHED("k_reconstruct");
   return BEAST_OK;
 }
@@ -876,8 +949,13 @@ int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t
   if (!mfma) return launch_rec_ks<TBT, 0, 0>(a, D, nj, s);
   if (a.Tout <= 16 * RT_REG) {
     if (!g_generic_only && N == 10 && a.Tout == 50 && a.ndo == D) {
-      if (D == 14 && nj == 14) return launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14>>(a, D, nj, s);
-      if (D == 14 && nj == 12) return launch_rec_ks<TBT, 3, RT_REG, Shape<14, 12, 10, 50, 14>>(a, D, nj, s);
+      const bool wide = wide_blocks(a.ntiles);
+      if (D == 14 && nj == 14)
+        return wide ? launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14, 7>>(a, D, nj, s)
+                    : launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14>>(a, D, nj, s);
+      if (D == 14 && nj == 12)
+        return wide ? launch_rec_ks<TBT, 3, RT_REG, Shape<14, 12, 10, 50, 14, 7>>(a, D, nj, s)
+                    : launch_rec_ks<TBT, 3, RT_REG, Shape<14, 12, 10, 50, 14>>(a, D, nj, s);
       if (D == 7 && nj == 7) return launch_rec_ks<TBT, 3, RT_REG, Shape<7, 7, 10, 50, 7>>(a, D, nj, s);
     }
     return launch_rec_mfma<TBT, RT_REG>(a, D, nj, N, s);
@@ -936,13 +1014,25 @@ extern "C" int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, in
 }
 
 #ifdef BEAST_STAMPS
-extern "C" int beast_stamps_read(unsigned long long* out) {   // [2][NWAVES][16]
+extern "C" int beast_stamps_read(unsigned long long* out) {   // [2][8][16]
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -2;
+}
+
+extern "C" int beast_bstamps_read(unsigned long long* out) {   // [2][4096][4]
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(g_bstamps)) == hipSuccess ? 0 : -2;
 }
 #endif
 
 extern "C" int beast_set_option(int option, int value) {
-  BEAST_REQUIRE(option == BEAST_OPT_GENERIC_KERNELS, "unknown option %d", option);
-  g_generic_only = value != 0;
-  return BEAST_OK;
+  if (option == BEAST_OPT_GENERIC_KERNELS) {
+    g_generic_only = value != 0;
+    return BEAST_OK;
+  }
+  if (option == BEAST_OPT_BLOCK_WAVES) {
+    BEAST_REQUIRE(value == 0 || value == 4 || value == 7, "BEAST_OPT_BLOCK_WAVES: %d is not 0, 4 or 7", value);
+    g_block_waves = value;
+    return BEAST_OK;
+  }
+  BEAST_REQUIRE(false, "unknown option %d", option);
+  return BEAST_E_INVALID;
 }

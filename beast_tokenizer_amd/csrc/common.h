@@ -78,6 +78,25 @@ __device__ __forceinline__ int quantize_bin_fast(float p, float lo, float hi, fl
   return quantize_bin(p, lo, hi, vm1);
 }
 
+// quantize_bin_fast with the scale precomputed per (DoF, basis) column,
+// k = vm1 * rcp(max(hi - lo, 1e-8)) (NaN bounds give a NaN k): returns the fast bin and sets
+// `exact` when quantize_bin must decide instead (within 2^-20 * vm1 of a rounding boundary,
+// or a NaN / inf on the way).  med3 is clamp_t for lo <= hi; inverted bounds give va <= 0
+// -> bin 0, as the exact chain's clamp of u to [0, 1] does.
+__device__ __forceinline__ int quantize_bin_k(float p, float lo, float hi, float k, float vm1, bool& exact) {
+  const float x = __builtin_amdgcn_fmed3f(p, lo, hi);
+  const float va = __fmul_rn(__fsub_rn(x, lo), k);
+  const float f = __builtin_amdgcn_fractf(va);
+  exact = exact || !(fabsf(__fsub_rn(f, 0.5f)) > 9.5367431640625e-7f * vm1) || (p != p);
+  return (int)rintf(fminf(fmaxf(va, 0.0f), vm1));
+}
+
+__device__ __forceinline__ float quantize_scale(float lo, float hi, float vm1) {
+  float s = __fsub_rn(hi, lo);
+  s = (s < 1e-8f) ? 1e-8f : s;
+  return __fmul_rn(vm1, __builtin_amdgcn_rcpf(s));
+}
+
 __device__ __forceinline__ long long widen_bin(int bin, unsigned long long offset) {
   const unsigned long long v = (bin == (int)0x80000000) ? 0x8000000000000000ULL : (unsigned long long)(long long)bin;
   return (long long)(v + offset);   // two's-complement wrap, as ATen's int64 add

@@ -45,8 +45,11 @@ const char* beast_last_error(void);
 /* Process-wide tuning / test options.  BEAST_OPT_GENERIC_KERNELS = 1 makes encode and
  * reconstruct use their runtime-shape kernels even where a shape-specialised kernel
  * exists (the BEAST defaults T = 50, N = 10, D = 7 / 14); results are identical.
+ * BEAST_OPT_BLOCK_WAVES = 4 or 7 forces the workgroup width of the specialised 14-DoF
+ * kernels (0 = chosen by batch size); results are identical.
  * Not thread-safe with concurrent launches. */
 #define BEAST_OPT_GENERIC_KERNELS 1
+#define BEAST_OPT_BLOCK_WAVES 2
 int beast_set_option(int option, int value);
 
 /* ---------------------------------------------------------------- H1/H2 ---

@@ -47,11 +47,22 @@ def gpu_device():
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(params=["specialised", "generic"])
-def kernel_mode(request):
-    """Run a parity test on the shape-specialised kernels and on the runtime-shape ones."""
+KERNEL_MODES = {"specialised": (0, 0), "specialised_w4": (0, 4), "specialised_w7": (0, 7), "generic": (1, 0)}
+
+
+def set_kernel_mode(mode):
+    """(runtime-shape kernels?, forced workgroup width) for the encode / reconstruct launches."""
     from beast_tokenizer_amd import _lib
     lib = _lib.load()
-    lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 1 if request.param == "generic" else 0)
+    generic, waves = KERNEL_MODES[mode]
+    lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, generic)
+    lib.beast_set_option(_lib.OPT_BLOCK_WAVES, waves)
+
+
+@pytest.fixture(params=["specialised", "specialised_w4", "generic"])
+def kernel_mode(request):
+    """Run a parity test on the shape-specialised kernels (the width the batch size picks,
+    and the 4-wave width large batches use) and on the runtime-shape ones."""
+    set_kernel_mode(request.param)
     yield request.param
-    lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0)
+    set_kernel_mode("specialised")

@@ -203,25 +203,25 @@ def test_flip_census_4096(name, gpu_device, kernel_mode):
 
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_specialised_kernels_equal_generic(name, gpu_device):
-    """The shape-specialised encode / reconstruct kernels compute exactly what the
-    runtime-shape kernels compute (same operation order): bitwise-equal outputs."""
-    from beast_tokenizer_amd import _lib
-    lib = _lib.load()
+    """The shape-specialised encode / reconstruct kernels (both workgroup widths) compute
+    exactly what the runtime-shape kernels compute (same operation order): bitwise-equal."""
+    from conftest import set_kernel_mode
     gi = CONFIGS[name]["gripper_indices"] or []
     g = dict(load_npz(f"bspline_{name}.npz"))
     tok = make_tok(name, g, gpu_device)
     x = torch.from_numpy(synth_trajectories(1000, 50, CONFIGS[name]["num_dof"], seed=3, gripper_indices=gi))
     outs = []
-    for generic in (0, 1):
-        lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, generic)
+    for mode in ("generic", "specialised_w4", "specialised_w7", "specialised"):
+        set_kernel_mode(mode)
         try:
             t, pd = tok.encode(x)
             pos = tok.reconstruct_traj(t)
             outs.append((t.cpu().numpy(), pd["params"].cpu().numpy(), pos.cpu().numpy()))
         finally:
-            lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0)
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
+            set_kernel_mode("specialised")
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
@@ -259,13 +259,15 @@ def test_encode_quantiser_exact_near_ties(vocab, gpu_device, kernel_mode):
     """The encode kernel's in-lane quantiser (reciprocal fast path + exact fallback) must
     equal continuous_to_discrete on its own params bit for bit.  Trajectories are built
     as y = Phi w with w on or next to rounding ties (k + 0.5) of the bins, plus NaN /
-    inf / degenerate-range columns."""
+    inf / degenerate-range / inverted-bound / NaN-bound columns."""
     rng = np.random.default_rng(vocab)
     B, T, D, N = 2048, 50, 7, 10
     tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=vocab, device=str(gpu_device))
     lo = rng.uniform(-2, 0, size=D * N).astype(np.float32)
     hi = (lo + rng.uniform(0.5, 3, size=D * N)).astype(np.float32)
     hi[3] = lo[3]                                   # degenerate range: scale clamps to 1e-8
+    hi[5] = lo[5] - 0.7                             # inverted bounds: every bin is 0
+    hi[12] = np.nan                                 # NaN bound: clamp gives NaN
     tok.load_state_dict({"w_min": lo.tolist(), "w_max": hi.tolist()})
     # targets on ties: u * (vocab - 1) = k + 0.5 (+ a few ulps either way)
     k = rng.integers(0, vocab - 1, size=(B, D * N))

@@ -67,6 +67,8 @@ out2 = {
     "dev_lookup": t(lambda: tok._dev()),
     "fit": t(lambda: tok._fit(x, 0, pl), 5000),
     "encode": t(lambda: tok.encode(x), 5000),
+    "fast_encode_only": t(lambda: pl.fast.encode(x, 0, 0), 5000),
+    "fast_reconstruct_only": t(lambda: pl.fast.reconstruct(tok_rows, 0, 0), 5000),
     "token_rows": t(lambda: tok._token_rows(tok_rows, pl.dev)),
     "reconstruct_traj": t(lambda: tok.reconstruct_traj(tok_rows), 5000),
 }

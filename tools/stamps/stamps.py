@@ -14,8 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
-NW = 4   # waves per workgroup (NTHREADS / 64 in csrc/codec.hip)
-ENC = ["start", "issued", "landed", "mfma_done", "pb_ready", "params_stored", "tokens_stored", "drained", "-",
+NW = 8   # stamp slots per kernel (waves per workgroup <= 8 in csrc/codec.hip)
+ENC = ["start", "issued", "landed", "mfma_done", "pb_ready", "params_stored", "tokens_stored", "drained", "acc_ready",
        "y_dma", "p_dma", "small_dma", "t2_landed", "t2_mfma_done", "t2_tokens_stored"]
 REC = ["start", "issued", "landed", "decoded", "w_ready", "mfma_done", "ob_ready", "stored", "drained",
        "tok_dma", "small_dma", "phi_loads", "lut"]
@@ -33,6 +33,34 @@ def build():
     return so
 
 
+def grid_of(B):
+    return (B + 7) // 8 if "BEAST_DEBUG_GRID_CAP" not in os.environ else min((B + 7) // 8, int(os.environ["BEAST_DEBUG_GRID_CAP"]))
+
+
+def block_summary(bst, k, nblk):
+    """Workgroup lifetimes from s_memrealtime (10 ns ticks): dispatch spread, durations,
+    and the spread per XCC (HW_REG_XCC_ID) / CU."""
+    import numpy as np
+    a = np.array(bst[k * 4096 * 4:(k + 1) * 4096 * 4], dtype=np.uint64).reshape(4096, 4)[:nblk]
+    st, en = a[:, 0].astype(np.int64), a[:, 1].astype(np.int64)
+    ok = (st > 0) & (en >= st)
+    st, en, hw = st[ok], en[ok], a[ok, 2]
+    t0 = st.min()
+    xcc = (hw >> np.uint64(32)).astype(np.int64) & 0xF
+    cu = (hw.astype(np.int64) >> 8) & 0xF
+    se = (hw.astype(np.int64) >> 13) & 0x7
+    dur = (en - st) * 10
+    def q(x):
+        return [int(np.percentile(x, p)) for p in (0, 10, 50, 90, 100)]
+    out = {"n": int(ok.sum()), "start_ns_pct_0_10_50_90_100": q((st - t0) * 10),
+           "end_ns_pct": q((en - t0) * 10), "dur_ns_pct": q(dur),
+           "per_xcc_blocks": [int((xcc == x).sum()) for x in range(8)],
+           "per_xcc_last_end_ns": [int(((en[xcc == x] - t0) * 10).max()) if (xcc == x).any() else None
+                                   for x in range(8)],
+           "distinct_cu": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist()))))}
+    return out
+
+
 def main():
     import torch
     from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib
@@ -42,6 +70,8 @@ def main():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
     lib.beast_stamps_read.argtypes = [C.c_void_p]
+    lib.beast_bstamps_read.argtypes = [C.c_void_p]
+    bst = (C.c_ulonglong * (2 * 4096 * 4))()
     dev = torch.device("cuda", 0)
     tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
     p = tok._plan()
@@ -77,9 +107,12 @@ def main():
             torch.cuda.synchronize()
             assert lib.beast_stamps_read(stamps) == 0
             v = [stamps[(k * NW + w) * 16: (k * NW + w) * 16 + 16] for w in range(NW)]
-            t0 = min(v[w][0] for w in range(NW))
-            res[kname] = {names[i]: [int(v[w][i] - t0) if v[w][i] >= t0 else None for w in range(NW)]
+            ws = [w for w in range(NW) if v[w][0]]   # waves that exist in this kernel
+            t0 = min(v[w][0] for w in ws)
+            res[kname] = {names[i]: [int(v[w][i] - t0) if v[w][i] >= t0 else None for w in ws]
                           for i in range(len(names)) if names[i] != "-"}
+            assert lib.beast_bstamps_read(bst) == 0
+            res[kname]["blocks"] = block_summary(bst, k, min(4096, grid_of(B)))
         out[B] = res
     print(json.dumps(out, indent=1))
 
