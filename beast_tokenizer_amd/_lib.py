@@ -68,6 +68,13 @@ SIGNATURES = {
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_repack_words": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_compact_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "beast_bpe_mergemap_log2cap": (_i32, [_i32]),
+    "beast_bpe_mergemap_bytes": (_sz, [_i32]),
+    "beast_bpe_mergemap_build": (_i32, [_vp, _vp, _vp, _i32, _vp, _sz, _vp]),
+    "beast_bpe_encode_lds_bytes": (_sz, [_i32, _i32]),
+    "beast_bpe_encode_rows": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
+                                     _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "beast_bpe_decode_rows": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
 }
 
 _lock = threading.Lock()

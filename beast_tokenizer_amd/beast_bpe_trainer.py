@@ -43,9 +43,14 @@ class FIGBPEState:
     max_token: int
 
 
-def tokenizer_from_result(res: BPEResult) -> ByteLevelBPETokenizer:
-    """Wrap GPU-trained vocab / merges in the HF object the reference returns."""
-    return ByteLevelBPETokenizer(vocab=dict(res.vocab), merges=list(res.merges))
+def tokenizer_from_result(res: BPEResult, special_tokens: Sequence[str] = ()) -> ByteLevelBPETokenizer:
+    """Wrap GPU-trained vocab / merges in the HF object the reference returns; the trainer's
+    special tokens become added special tokens with their vocab ids, as HF's trainer leaves
+    them (Tokenizer::train_from_iterator adds trainer.special_tokens)."""
+    tok = ByteLevelBPETokenizer(vocab=dict(res.vocab), merges=list(res.merges))
+    if special_tokens:
+        tok.add_special_tokens(list(special_tokens))
+    return tok
 
 
 def _default_device() -> torch.device:
@@ -94,7 +99,7 @@ class FIGBPE:
                         special_tokens=self.special_tokens, max_token_length=self.max_token_length,
                         initial_alphabet=alphabet, reduce=self._reducer())
         self.last_result = res
-        tokenizer = tokenizer_from_result(res)
+        tokenizer = tokenizer_from_result(res, self.special_tokens)
         self.tokenizer = tokenizer
         self.min_token = res.min_token
         self.max_token = res.max_token
@@ -114,7 +119,7 @@ class FIGBPE:
                         special_tokens=self.special_tokens, max_token_length=self.max_token_length,
                         initial_alphabet=list(alphabet), reduce=self._reducer(), mn_mx=(0, hi))
         self.last_result = res
-        return tokenizer_from_result(res)
+        return tokenizer_from_result(res, self.special_tokens)
 
     def fit_from_sequences(self, sequences: Iterable[ArrayLike]) -> FIGBPEState:
         """Reference :76-98: global min/max shift, alphabet chr(0..max-min), train."""

@@ -2,9 +2,10 @@
 
 B-spline tokenizer plus a byte-level BPE over its bins.  ``fit_from_trajectories``
 encodes on the GPU and trains the BPE with the HIP trainer (beast_bpe_trainer.FIGBPE);
-the trained model is an HF ``ByteLevelBPETokenizer`` exactly like the reference's,
-so per-sequence BPE encode / decode (not yet on the GPU) and
-the on-disk format (``bpe_tokenizer/{vocab.json,merges.txt,tokenizer.json}``) match.
+the trained model is an HF ``ByteLevelBPETokenizer`` exactly like the reference's, so
+the on-disk format (``bpe_tokenizer/{vocab.json,merges.txt,tokenizer.json}``) matches.
+Per-row BPE encode / decode run on the GPU from that model's
+tables (bpe_codec.py, csrc/bpe_codec.hip), one launch per batch.
 """
 from __future__ import annotations
 
@@ -174,73 +175,56 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
             return [np.asarray(values)]
         return [np.asarray(row) for row in values]  # type: ignore[arg-type]
 
-    def _discrete_to_bpe(self, discrete_tokens: TokenLike) -> List[List[int]]:
-        """Reference :175-198 (HF BPE model of the GPU-trained merges)."""
+    def _gpu_bpe(self):
+        """Device image of the trained HF model (csrc/bpe_codec.hip), rebuilt when the model
+        object or its vocabulary changes."""
+        from .bpe_codec import GpuBpeModel
         tokenizer = self._require_bpe()
-        result: List[List[int]] = []
-        for seq in self._as_sequence_list(discrete_tokens):
-            flattened = np.asarray(seq).reshape(-1).astype(int)
-            shifted = flattened - self.bpe_min_token
-            if (shifted < 0).any():
-                raise ValueError(
-                    "Discrete tokens contain values smaller than the configured BPE minimum token."
-                )
-            if self.bpe_max_token is not None:
-                max_allowed = self.bpe_max_token - self.bpe_min_token
-                if (shifted > max_allowed).any():
-                    raise ValueError(
-                        "Discrete tokens contain values greater than the configured BPE maximum token. "
-                        "Either retrain the BPE tokenizer with a wider range or disable BPE for this run."
-                    )
-            text = "".join(map(chr, shifted))
-            result.append(tokenizer.encode(text, add_special_tokens=False).ids)
-        return result
+        dev = self._dev()
+        key = (id(tokenizer), str(dev), tokenizer.get_vocab_size(with_added_tokens=True))
+        if getattr(self, "_bpe_gpu_key", None) != key:
+            self._bpe_gpu = GpuBpeModel(tokenizer, dev)
+            self._bpe_gpu_key = key
+            self._bpe_gpu_owner = tokenizer   # keeps id(tokenizer) from being reused
+        return self._bpe_gpu
+
+    def _discrete_to_bpe(self, discrete_tokens: TokenLike) -> List[List[int]]:
+        """Reference :175-198, every row in one GPU launch (csrc/bpe_codec.hip k_bpe_encode):
+        same ids as HF's per-row ``encode(text, add_special_tokens=False)``, same errors."""
+        from .bpe_codec import rows_from_sequences, rows_from_tensor
+        model = self._gpu_bpe()
+        dev = model.device
+        max_span = None if self.bpe_max_token is None else self.bpe_max_token - self.bpe_min_token
+        if isinstance(discrete_tokens, torch.Tensor) and discrete_tokens.ndim in (1, 2):
+            rows = discrete_tokens if discrete_tokens.ndim == 2 else discrete_tokens[None]
+            flat, off, width = rows_from_tensor(rows, dev)
+        else:
+            seqs = [np.asarray(s).reshape(-1).astype(np.int64) for s in self._as_sequence_list(discrete_tokens)]
+            flat, off, width = rows_from_sequences(seqs, dev)
+        return model.encode_to_lists(flat, off, width, self.bpe_min_token, max_span)
 
     def _bpe_to_discrete(self, tokens: Iterable[TokenLike]) -> torch.Tensor:
-        """Reference :200-247."""
-        tokenizer = self._require_bpe()
-        if isinstance(tokens, torch.Tensor):
-            if tokens.ndim == 1:
-                token_sequences = [tokens]
-            elif tokens.ndim == 2:
-                token_sequences = [row for row in tokens]
-            else:
-                raise ValueError("Expected tensor with 1 or 2 dimensions for BPE tokens.")
-        elif isinstance(tokens, np.ndarray):
-            if tokens.ndim == 1:
-                token_sequences = [tokens]
-            elif tokens.ndim == 2:
-                token_sequences = [row for row in tokens]
-            else:
-                raise ValueError("Expected numpy array with 1 or 2 dimensions for BPE tokens.")
-        elif isinstance(tokens, Sequence) and tokens and isinstance(tokens[0], numbers.Integral):
-            token_sequences = [tokens]
+        """Reference :200-247, every row in one GPU launch (k_bpe_decode): HF's
+        ``decode(ids, skip_special_tokens=True)``, ``ord + min``, the same checks and errors."""
+        from .bpe_codec import ids_as_i32, rows_from_sequences, rows_from_tensor
+        model = self._gpu_bpe()
+        dev = model.device
+        if isinstance(tokens, (torch.Tensor, np.ndarray)):
+            if tokens.ndim not in (1, 2):
+                kind = "tensor" if isinstance(tokens, torch.Tensor) else "numpy array"
+                raise ValueError(f"Expected {kind} with 1 or 2 dimensions for BPE tokens.")
+            t = torch.as_tensor(tokens)
+            rows = t if t.ndim == 2 else t[None]
+            flat, off, _ = rows_from_tensor(ids_as_i32(rows.to(dev)), dev, dtype=torch.int32)
         else:
-            token_sequences = tokens
-
-        sequences: List[np.ndarray] = []
-        unk_id = tokenizer.token_to_id("<unk>")
-        for token in token_sequences:
-            if isinstance(token, torch.Tensor):
-                token_list = [int(t) for t in token.detach().cpu().tolist()]
-            elif isinstance(token, np.ndarray):
-                token_list = [int(t) for t in token.tolist()]
+            if isinstance(tokens, Sequence) and tokens and isinstance(tokens[0], numbers.Integral):
+                seqs = [tokens]
             else:
-                token_list = [int(t) for t in token]
-            if unk_id is not None and unk_id in token_list:
-                raise ValueError(
-                    "BPE sequence contains <unk> tokens. This usually means that the discrete "
-                    "BEAST tokens went out of the range seen during BPE training. Consider "
-                    "retraining the BPE tokenizer with a wider token range or disable BPE."
-                )
-            text = tokenizer.decode(token_list, skip_special_tokens=True)
-            decoded = np.array(list(map(ord, text)), dtype=np.int64) + self.bpe_min_token
-            if decoded.size != self.sequence_length:
-                raise ValueError(
-                    f"Decoded sequence has length {decoded.size}, expected {self.sequence_length}."
-                )
-            sequences.append(decoded)
-        return torch.tensor(np.stack(sequences), dtype=torch.long, device=self.device)
+                seqs = list(tokens)
+            seqs = [ids_as_i32(s.detach().cpu().numpy() if isinstance(s, torch.Tensor) else
+                               np.asarray(s, dtype=np.int64)).reshape(-1) for s in seqs]
+            flat, off, _ = rows_from_sequences(seqs, dev, dtype=np.int32)
+        return model.decode_checked(flat, off, self.sequence_length, self.bpe_min_token)
 
     # ===============================================
     #               - BEAST overriden -

@@ -65,3 +65,49 @@ def batches(total: int, batch: int, **kw) -> Iterable[np.ndarray]:
     """Yield consecutive slices of one synthetic stream (same as one big call)."""
     for s in range(0, total, batch):
         yield synth_trajectories(min(batch, total - s), start=s, **kw)
+
+
+# splitmix64 in int64 torch arithmetic (multiplication wraps; logical shifts are masked)
+def _i64(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def _srl(z, k: int):
+    import torch
+    return (z >> k) & torch.tensor((1 << (64 - k)) - 1, dtype=torch.int64, device=z.device)
+
+
+def _splitmix64_t(x):
+    z = x + _i64(int(_GOLDEN))
+    z = (z ^ _srl(z, 30)) * _i64(int(_M1))
+    z = (z ^ _srl(z, 27)) * _i64(int(_M2))
+    return z ^ _srl(z, 31)
+
+
+def synth_trajectories_device(batch: int, seq_len: int = 50, num_dof: int = 14, seed: int = 0,
+                              gripper_indices: Sequence[int] = (), start: int = 0, device="cuda"):
+    """:func:`synth_trajectories` evaluated with torch on ``device`` (same splitmix64 stream,
+    float64 arithmetic, fp32 result) -- for benches whose inputs are too large to build on
+    the host.  Equal to the numpy generator up to the last-ulp behaviour of the device's
+    float64 ``sin``/``log``."""
+    import torch
+    dev = torch.device(device)
+    b = torch.arange(start, start + batch, dtype=torch.int64, device=dev)[:, None]
+    d = torch.arange(num_dof, dtype=torch.int64, device=dev)[None, :]
+    key = _i64((seed * 0xD1B54A32D192ED03) & ((1 << 64) - 1)) ^ (b * num_dof + d)
+    u, state = [], key
+    for _ in range(6):
+        state = _splitmix64_t(state)
+        u.append((_srl(state, 11).to(torch.float64) + 0.5) * (1.0 / 9007199254740992.0))
+    two_pi = 2.0 * np.pi
+    a = torch.sqrt(-2.0 * torch.log(u[0])) * torch.cos(two_pi * u[1])
+    f = 0.5 + 3.0 * u[2]
+    phi = two_pi * u[3]
+    c = 0.1 * torch.sqrt(-2.0 * torch.log(u[4])) * torch.cos(two_pi * u[5])
+    t = torch.linspace(0.0, 1.0, seq_len, dtype=torch.float64, device=dev)[None, :, None]
+    arg = two_pi * f[:, None, :] * t + phi[:, None, :]
+    x = a[:, None, :] * torch.sin(arg) + c[:, None, :]
+    if len(gripper_indices):
+        gi = torch.as_tensor(list(gripper_indices), dtype=torch.int64, device=dev)
+        x[:, :, gi] = torch.sign(torch.sin(arg[:, :, gi]))
+    return x.to(torch.float32)

@@ -15,6 +15,9 @@ Extra objects in that line:
   cpu_baseline  the oracle's restatement of the reference op sequence (oracle/
                 beast_oracle.py, bitwise equal to the reference in the build
                 container) timed on this host's cores on a bounded sample
+  fit           fit_parameters (config K4: 1e6 trajectories, sharded over ranks with the
+                quantile histograms all-reduced) in trajectories/s, with the reference
+                op sequence + np.quantile timed on a bounded host sample
   bpe           BEASTBsplineBPETokenizer-style BPE training (vocab 2048) on GPU,
                 merges/s, with HF tokenizers (the reference's BPE) timed on a
                 bounded sample of the same corpus on the host
@@ -34,12 +37,13 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib  # noqa: E402
-from beast_tokenizer_amd.synthetic import synth_trajectories  # noqa: E402
+from beast_tokenizer_amd.synthetic import synth_trajectories, synth_trajectories_device  # noqa: E402
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 T, D, N, V = 50, 14, 10, 256
 ENC_BYTES = T * D * 4 + N * D * 8 + D * N * 4    # read traj, write int64 tokens + fp32 params
 REC_BYTES = N * D * 8 + T * D * 4                # read tokens, write positions
+FIT_BYTES = T * D * 4 + D * N * 4 * (1 + 4)      # read traj; params written once, read/written per radix pass
 
 
 def parse():
@@ -50,6 +54,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-bpe", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-fit", action="store_true")
+    ap.add_argument("--fit-trajs", type=int, default=1000000, help="fit_parameters corpus (all ranks)")
     ap.add_argument("--bpe-seqs", type=int, default=500000, help="BPE corpus (trajectories, all ranks)")
     ap.add_argument("--bpe-vocab", type=int, default=2048)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -102,6 +108,73 @@ def cpu_baseline(tok_bounds, seconds: float):
                       f"torch.linalg.solve), {el:.1f}s"}
 
 
+def fit_bench(dev, args, world, rank):
+    """Config K4: fit_parameters over --fit-trajs trajectories (batches of 4096, resident in HBM),
+    each rank its contiguous shard; with world > 1 the radix-select histograms are all-reduced
+    (RCCL), so every rank ends with the bounds of the union."""
+    per_rank = args.fit_trajs // world
+    x = synth_trajectories_device(per_rank, T, D, seed=11, start=rank * per_rank, device=dev)
+    loader = [{"actions": x[s:s + 4096]} for s in range(0, per_rank, 4096)]
+    ftok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, device=str(dev))
+    pg = True if world > 1 else None
+    ftok.fit_parameters(loader[:4], verbose=False, process_group=pg)          # warm-up
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(3):
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ftok.fit_parameters(loader, verbose=False, process_group=pg)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], device=dev)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            el = float(tt.item())
+        times.append(el)
+    el = float(np.median(times))
+    # stage split on this rank: the batched fits alone
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in loader:
+        ftok.compute_weights(b["actions"])
+    torch.cuda.synchronize()
+    t_fit = time.perf_counter() - t0
+    n = per_rank * world
+    out = {"metric": "fit_parameters trajectories/s (K4: w_min/w_max = exact 1%/99% column quantiles)",
+           "value": n / el, "unit": "trajectories/s", "trajectories": n, "batch": 4096, "seconds": el,
+           "fit_batches_s": t_fit, "quantile_s": max(el - t_fit, 0.0),
+           "algo_bytes_per_traj": FIT_BYTES, "achieved_GBps": FIT_BYTES * n / el / 1e9 / world,
+           "hbm_frac": FIT_BYTES * n / el / world / HBM_PEAK,
+           "w_min_checksum": float(ftok.w_min.double().sum()), "w_max_checksum": float(ftok.w_max.double().sum())}
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_fit_baseline(args.cpu_seconds / 2)
+    del x, loader
+    return out
+
+
+def cpu_fit_baseline(seconds: float):
+    """Reference fit_parameters on the host: per-batch fit through the reference op sequence
+    (oracle/beast_oracle.py:fit_reference_ops) then np.quantile(q=0.01/0.99, axis=0)."""
+    from oracle import beast_oracle as O
+    t = O.times_grid(2 * np.pi, T)
+    pj = O.basis(t, np.float32(2 * np.pi), 4, N)
+    Bc = 512
+    xs = synth_trajectories(Bc, T, D, seed=11)
+    O.fit_reference_ops(xs, pj)
+    params, n, t0 = [], 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        params.append(O.fit_reference_ops(xs, pj).reshape(Bc, -1))
+        n += Bc
+    allp = np.concatenate(params)
+    np.quantile(allp, [0.01, 0.99], axis=0)
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "trajectories/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} trajectories in batches of {Bc}: oracle/beast_oracle.py fit_reference_ops "
+                      f"(block-diagonal bmm + torch.linalg.solve) + np.quantile, {el:.1f}s"}
+
+
 def bpe_bench(tok, dev, args, world, rank, reduce):
     from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
     per_rank = args.bpe_seqs // world
@@ -131,6 +204,69 @@ def bpe_bench(tok, dev, args, world, rank, reduce):
            "distinct_words": res.stats.get("n_distinct"), "live_words_at_end": res.stats.get("n_live_end")}
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = hf_bpe_baseline(allrows[:20000].cpu().numpy(), args.bpe_vocab, res)
+    out["codec"] = bpe_codec_bench(res, allrows[:args.batch], dev, args)
+    return out
+
+
+def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
+    """Per-row BPE inference with the trained model: the reference's
+    _discrete_to_bpe / _bpe_to_discrete loops (beast_bspline_bpe_tokenizer.py:175-247) as one
+    k_bpe_encode / k_bpe_decode launch per batch.  Kernel rows/s from HIP events over
+    back-to-back launches on the kernel's stream; API rows/s include the host list build."""
+    from beast_tokenizer_amd.beast_bpe_trainer import tokenizer_from_result
+    from beast_tokenizer_amd.bpe_codec import GpuBpeModel, rows_from_tensor
+    hf = tokenizer_from_result(res)
+    model = GpuBpeModel(hf, dev)
+    lo, span = res.min_token, res.max_token - res.min_token
+    flat, off, width = rows_from_tensor(rows, dev)
+    R = rows.shape[0]
+    stream = torch.cuda.current_stream(dev)
+    out = {}
+    enc = {}
+
+    def launch_enc():
+        enc["r"] = model.encode_rows(flat, off, width, lo, span)
+    t_enc = kernel_time_us(launch_enc, stream, reps=20, rounds=3)
+    ids, lens, _ = enc["r"]
+    lens_np = lens.cpu().numpy()
+    n_ids = int(lens_np.sum())
+    # flat ids for decode
+    mask = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]
+    dflat = ids[mask].contiguous()
+    doff = torch.zeros(R + 1, dtype=torch.int64, device=dev)
+    doff[1:] = torch.cumsum(lens.to(torch.int64), 0)
+    dec = {}
+
+    def launch_dec():
+        dec["r"] = model.decode_rows(dflat, doff, width, lo)
+    t_dec = kernel_time_us(launch_dec, stream, reps=20, rounds=3)
+    assert torch.equal(dec["r"][0], rows), "BPE decode(encode(rows)) != rows"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lists = model.encode_to_lists(flat, off, width, lo, span)
+    t_api_enc = time.perf_counter() - t0
+    out.update({"rows": R, "ids_per_row": n_ids / R,
+                "encode_kernel_us": t_enc, "encode_rows_per_s_kernel": R / (t_enc * 1e-6),
+                "decode_kernel_us": t_dec, "decode_rows_per_s_kernel": R / (t_dec * 1e-6),
+                "encode_api_rows_per_s": R / t_api_enc,
+                "encode_kernel_GBps": (R * width * 8 + n_ids * 4) / (t_enc * 1e-6) / 1e9,
+                "decode_kernel_GBps": (n_ids * 4 + R * width * 8) / (t_dec * 1e-6) / 1e9})
+    if not args.no_cpu:
+        # the reference's per-row HF loop on a bounded sample
+        host = rows.cpu().numpy() - lo
+        n = min(R, 2048)
+        t0 = time.perf_counter()
+        ref = [hf.encode("".join(map(chr, r)), add_special_tokens=False).ids for r in host[:n]]
+        t_cpu = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for r in ref:
+            hf.decode(r, skip_special_tokens=True)
+        t_cpu_dec = time.perf_counter() - t0
+        assert ref == lists[:n], "GPU BPE encode != HF"
+        out["cpu_baseline"] = {"encode_rows_per_s": n / t_cpu, "decode_rows_per_s": n / t_cpu_dec,
+                               "kind": "reference", "cores": 1,
+                               "sample": f"HF tokenizers per-row encode/decode loop "
+                                         f"(beast_bspline_bpe_tokenizer.py:175-247) over {n} rows"}
     return out
 
 
@@ -235,6 +371,10 @@ def main():
             "algo_bytes_per_launch": kbytes,
             "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
 
+    fitb = None
+    if not args.no_fit:
+        fitb = fit_bench(dev, args, world, rank)
+
     bpe = None
     if not args.no_bpe:
         bpe = bpe_bench(tok, dev, args, world, rank, reduce)
@@ -253,7 +393,7 @@ def main():
             "config": {"workload": "BEASTBsplineTokenizer encode->reconstruct_traj, num_dof=14 num_basis=10 "
                                    "seq_len=50 vocab=256 degree_p=4", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "bpe": bpe,
+            "roofline": roof, "cpu_baseline": cpu, "fit": fitb, "bpe": bpe,
         }
         if cpu and cpu.get("value"):
             line["gpu_over_cpu"] = value / cpu["value"]

@@ -229,6 +229,46 @@ int beast_bpe_compact_words(const uint32_t* wstart, const uint32_t* wlen, const 
                             uint32_t* out_wstart, uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_n,
                             void* stream);
 
+/* ------------------------------------------------------- §8f rank 1: BPE codec ---
+ * Per-row BPE inference with a trained byte-level model, replacing
+ * beast/beast_bspline_bpe_tokenizer.py:175-198 (_discrete_to_bpe: per row
+ * tokenizer.encode("".join(map(chr, row - min)), add_special_tokens=False).ids) and
+ * :200-247 (_bpe_to_discrete: tokenizer.decode(ids, skip_special_tokens=True), ord + min).
+ * HF tokenizers semantics: AddedVocabulary split on special tokens (leftmost-longest),
+ * ByteLevel pre-tokeniser, BPE::merge_word / Word::merge_all (rank, pos) min-heap,
+ * ByteLevel decoder + String::from_utf8_lossy.
+ *
+ * Merge map: (a, b) -> (rank, new_id), open addressing in device memory; merges in rank
+ * order (a pair listed twice keeps its last rank, as HF's HashMap collect). ids < 65536. */
+int beast_bpe_mergemap_log2cap(int n_merges);
+size_t beast_bpe_mergemap_bytes(int n_merges);
+int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* merge_b, const int32_t* merge_new,
+                             int n_merges, void* map, size_t map_bytes, void* stream);
+/* Encode rows tok[row_off[r] .. row_off[r+1]) (int64 bins).  Shifted code point
+ * v = tok - min_tok; status[r]: 0 ok, 1 some v < 0, 2 some v > max_span (max_span >= 0),
+ * 3 v > 0x10FFFF, 4 surrogate, 5 v >= lut_n (no class), 6 row longer than max_row_cps /
+ * max_row_syms.  byte2id[256]: vocab id of each byte-level char, -1 if absent (dropped, or
+ * unk_id (fused when fuse_unk) if the model has an unk token).  Special tokens:
+ * spec_cps[n_spec][64] code points, spec_len, spec_id.  Output: out_ids[r][0 .. out_len[r])
+ * (row stride out_stride >= max_row_syms).  LDS per row: beast_bpe_encode_lds_bytes
+ * (must be <= 64 KiB, else BEAST_E_UNSUPPORTED). */
+size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms);
+int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
+                          int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
+                          const void* map, int n_merges, const int32_t* spec_cps, const int32_t* spec_len,
+                          const int32_t* spec_id, int n_spec, int unk_id, int fuse_unk, int max_row_cps,
+                          int max_row_syms, int32_t* out_ids, int64_t out_stride, int32_t* out_len,
+                          int32_t* status, void* stream);
+/* Decode rows ids[row_off[r] .. row_off[r+1]).  tok_off[n_vocab+1] / tok_bytes: each id's
+ * ByteLevel-decoded bytes; tok_skip[id] = 1 for special tokens (skip_special_tokens) and
+ * unassigned ids.  out[r][0 .. min(count, L)) = code point + min_tok; out_count[r] = code
+ * points decoded (the caller checks == L); status[r] bit 0: the row holds unk_id, bit 1: it
+ * holds an id < -1 (the caller's mark for a value that is not a u32).  Id -1 is skipped. */
+int beast_bpe_decode_rows(const int32_t* ids, const int64_t* row_off, int64_t n_rows, const int32_t* tok_off,
+                          const uint8_t* tok_bytes, const uint8_t* tok_skip, int n_vocab, int unk_id,
+                          int64_t min_tok, int L, int64_t* out, int32_t* out_count, int32_t* status,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -210,3 +210,117 @@ def train_sequences(seqs, vocab_size: int, min_frequency: int = 2):
     hi = int(max(int(s.max()) for s in seqs))
     strings = ["".join(map(chr, (s - lo).astype(int))) for s in seqs]
     return train(strings, [chr(i) for i in range(hi - lo + 1)], vocab_size, min_frequency)
+
+
+# ------------------------------------------------------------ BPE inference ----
+# Restates what the reference calls per row (beast/beast_bspline_bpe_tokenizer.py:175-247):
+# HF tokenizers 0.22.2 Tokenizer::encode(text, add_special_tokens=False) for a trained
+# ByteLevelBPETokenizer -- AddedVocabulary split on special tokens (aho-corasick,
+# MatchKind::LeftmostLongest), ByteLevel pre-tokeniser, models/bpe/model.rs merge_word and
+# models/bpe/word.rs merge_all (BinaryHeap of Merge{pos, rank, new_id} ordered by (rank, pos),
+# expired entries skipped) -- and Tokenizer::decode(ids, skip_special_tokens=True) with the
+# ByteLevel decoder (pre_tokenizers/byte_level.rs decode_chain: per token the byte-level
+# chars' bytes, or the token's own UTF-8 if a char is not a byte-level char) and
+# String::from_utf8_lossy.  Pinned against HF outputs in tests/golden/bpe_codec.json.
+import heapq  # noqa: E402
+
+U2B = {c: b for b, c in B2U.items()}
+
+
+class BpeModel:
+    """vocab / merges / special tokens of a trained byte-level BPE model."""
+
+    def __init__(self, vocab: Dict[str, int], merges: Sequence[Sequence[str]], specials: Sequence[Tuple[str, int]] = (),
+                 unk_token=None, fuse_unk=False):
+        self.vocab = dict(vocab)
+        self.merge_map: Dict[Tuple[int, int], Tuple[int, int]] = {}
+        for rank, (a, b) in enumerate(merges):     # HashMap collect: a repeated pair keeps its last rank
+            self.merge_map[(vocab[a], vocab[b])] = (rank, vocab[a + b])
+        self.specials = list(specials)
+        self.unk_id = vocab[unk_token] if unk_token is not None else None
+        self.fuse_unk = fuse_unk
+        self.id2tok = {i: s for s, i in vocab.items()}
+        for s, i in self.specials:
+            self.id2tok[i] = s
+
+    def _merge_word(self, piece: str) -> List[int]:
+        syms: List[int] = []
+        pending = None
+        for ch in byte_level(piece):
+            i = self.vocab.get(ch)
+            if i is not None:
+                if pending is not None:
+                    syms.append(pending); pending = None
+                syms.append(i)
+            elif self.unk_id is not None:
+                if pending is not None and not self.fuse_unk:
+                    syms.append(pending)
+                pending = self.unk_id
+        if pending is not None:
+            syms.append(pending)
+        n = len(syms)
+        c = syms[:]
+        alive = [True] * n
+        prv = list(range(-1, n - 1))
+        nxt = list(range(1, n)) + [-1]
+        heap = []
+        for i in range(n - 1):
+            m = self.merge_map.get((c[i], c[i + 1]))
+            if m is not None:
+                heapq.heappush(heap, (m[0], i, m[1]))
+        while heap:
+            rank, pos, new_id = heapq.heappop(heap)
+            if not alive[pos] or nxt[pos] == -1:
+                continue
+            nx = nxt[pos]
+            m = self.merge_map.get((c[pos], c[nx]))
+            if m is None or m[1] != new_id:
+                continue
+            c[pos] = new_id
+            alive[nx] = False
+            nxt[pos] = nxt[nx]
+            if nxt[nx] != -1:
+                prv[nxt[nx]] = pos
+            if prv[pos] >= 0:
+                m = self.merge_map.get((c[prv[pos]], new_id))
+                if m is not None:
+                    heapq.heappush(heap, (m[0], prv[pos], m[1]))
+            if nxt[pos] != -1:
+                m = self.merge_map.get((new_id, c[nxt[pos]]))
+                if m is not None:
+                    heapq.heappush(heap, (m[0], pos, m[1]))
+        return [c[i] for i in range(n) if alive[i]]
+
+    def encode(self, text: str) -> List[int]:
+        out: List[int] = []
+        i, seg, n = 0, 0, len(text)
+        while i <= n:
+            best = None
+            if i < n:
+                for s, sid in self.specials:
+                    if text.startswith(s, i) and (best is None or len(s) > len(best[0])):
+                        best = (s, sid)
+            if best is not None or i == n:
+                for piece in pretokenize(text[seg:i]):
+                    out.extend(self._merge_word(piece))
+                if i == n:
+                    break
+                out.append(best[1])
+                i += len(best[0])
+                seg = i
+            else:
+                i += 1
+        return out
+
+    def decode(self, ids: Sequence[int]) -> str:
+        special = {s for s, _ in self.specials}
+        buf = bytearray()
+        for i in ids:
+            t = self.id2tok.get(int(i))
+            if t is None or t in special:
+                continue
+            if all(ch in U2B for ch in t):
+                buf.extend(U2B[ch] for ch in t)
+            else:
+                buf.extend(t.encode("utf-8"))
+        return buf.decode("utf-8", errors="replace")

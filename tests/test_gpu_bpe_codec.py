@@ -1,0 +1,144 @@
+"""GPU BPE encode / decode (csrc/bpe_codec.hip) == HF tokenizers per row.
+
+The reference runs, per row (beast/beast_bspline_bpe_tokenizer.py:175-247),
+``tokenizer.encode(text, add_special_tokens=False).ids`` and
+``tokenizer.decode(ids, skip_special_tokens=True)``.  Bar: bit-exact ids and code points,
+on the HF-captured vectors of tests/golden/bpe_codec.json and live against HF itself
+(installed on the GPU box) on larger random corpora.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_json, load_npz
+
+pytestmark = pytest.mark.gpu
+
+from beast_tokenizer_amd import BEASTBsplineBPETokenizer  # noqa: E402
+from beast_tokenizer_amd.bpe_codec import GpuBpeModel, ids_as_i32, rows_from_sequences  # noqa: E402
+
+CODEC = load_json("bpe_codec.json")
+HF = load_json("bpe_hf.json")
+
+
+def hf_tokenizer(spec):
+    from tokenizers import ByteLevelBPETokenizer
+    m = spec["model"]
+    if "ref" in m:
+        r = HF[m["ref"]]
+        return ByteLevelBPETokenizer(vocab=r["vocab"], merges=[tuple(x) for x in r["merges"]])
+    tok = ByteLevelBPETokenizer(vocab=m["vocab"], merges=[tuple(x) for x in m["merges"]])
+    if m["specials"]:
+        tok.add_special_tokens([s for s, _ in sorted(m["specials"], key=lambda t: t[1])])
+    return tok
+
+
+def encode_rows(model, rows, dev, max_span=None):
+    seqs = [np.asarray(r, dtype=np.int64) for r in rows]
+    flat, off, width = rows_from_sequences(seqs, dev)
+    ids, lens, status = model.encode_rows(flat, off, width, 0, max_span)
+    ids, lens, status = ids.cpu().numpy(), lens.cpu().numpy(), status.cpu().numpy()
+    return [ids[i, :lens[i]].tolist() for i in range(len(seqs))], status
+
+
+def decode_rows(model, id_rows, dev, L):
+    seqs = [ids_as_i32(np.asarray(r, dtype=np.int64)).reshape(-1) for r in id_rows]
+    flat, off, _ = rows_from_sequences(seqs, dev, dtype=np.int32)
+    out, counts, status = model.decode_rows(flat, off, L, 0)
+    out, counts = out.cpu().numpy(), counts.cpu().numpy()
+    return [out[i, :counts[i]].tolist() for i in range(len(seqs))], counts, status.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", sorted(CODEC))
+def test_encode_matches_hf_golden(case, gpu_device):
+    spec = CODEC[case]
+    model = GpuBpeModel(hf_tokenizer(spec), gpu_device)
+    rows = [cps for cps, _ in spec["encode"]]
+    got, status = encode_rows(model, rows, gpu_device)
+    assert not status.any()
+    assert got == [ids for _, ids in spec["encode"]]
+
+
+@pytest.mark.parametrize("case", sorted(CODEC))
+def test_decode_matches_hf_golden(case, gpu_device):
+    spec = CODEC[case]
+    model = GpuBpeModel(hf_tokenizer(spec), gpu_device)
+    want = [cps for _, cps in spec["decode"]]
+    L = max(len(w) for w in want) + 1
+    got, counts, status = decode_rows(model, [ids for ids, _ in spec["decode"]], gpu_device, L)
+    assert counts.tolist() == [len(w) for w in want]
+    assert got == want
+
+
+@pytest.mark.parametrize("span,rows,width,vocab", [(255, 3000, 140, 2048), (700, 1500, 60, 1500),
+                                                    (3000, 800, 50, 4000), (127, 2000, 140, 800)])
+def test_codec_matches_live_hf(span, rows, width, vocab, gpu_device):
+    """Train with HF (the reference's trainer), then every row of a fresh corpus -- including
+    bins never seen in training -- encodes and decodes exactly as HF does."""
+    from tokenizers import ByteLevelBPETokenizer
+    from tokenizers.trainers import BpeTrainer
+    rng = np.random.default_rng(span)
+    centre = rng.integers(0, span + 1, size=(rows, 1))
+    train = np.clip(centre + np.round(rng.normal(0, span / 12, size=(rows, width))), 0, span).astype(np.int64)
+    tok = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=vocab, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(span + 1)], max_token_length=10000)
+    tok._tokenizer.train_from_iterator(["".join(map(chr, r)) for r in train], trainer=tr)
+    test = np.clip(centre + np.round(rng.normal(0, span / 8, size=(rows, width))), 0, span).astype(np.int64)
+    model = GpuBpeModel(tok, gpu_device)
+    got, status = encode_rows(model, list(test), gpu_device, max_span=span)
+    assert not status.any()
+    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
+    assert got == want
+    dec, counts, _ = decode_rows(model, want, gpu_device, width)
+    assert (counts == width).all()
+    assert np.array_equal(np.array(dec), test)
+    # garbage ids decode like HF's lossy UTF-8 (count and code points)
+    V = tok.get_vocab_size()
+    garbage = [rng.integers(0, V + 10, size=int(rng.integers(0, 3 * width))).tolist() for _ in range(300)]
+    want_g = [[ord(c) for c in tok.decode(g, skip_special_tokens=True)] for g in garbage]
+    Lg = max(len(w) for w in want_g) + 1
+    got_g, counts_g, _ = decode_rows(model, garbage, gpu_device, Lg)
+    assert got_g == want_g
+
+
+def test_bpe_tokenizer_api_and_errors(gpu_device):
+    """BEASTBsplineBPETokenizer encode / decode through the GPU codec: HF's ids, the
+    reference's exceptions (beast_bspline_bpe_tokenizer.py:181-192, :221-243)."""
+    from beast_tokenizer_amd.synthetic import synth_trajectories
+    g = load_npz("bspline_k2.npz")
+    tok = BEASTBsplineBPETokenizer(num_dof=14, bpe_vocab_size=700, device=str(gpu_device))
+    tok.w_min.copy_(torch.from_numpy(g["w_min"]))
+    tok.w_max.copy_(torch.from_numpy(g["w_max"]))
+    batches = [torch.from_numpy(synth_trajectories(1024, 50, 14, seed=21, start=1024 * i)) for i in range(2)]
+    st = tok.fit_from_trajectories(batches, show_progress=False)
+    x = torch.from_numpy(synth_trajectories(257, 50, 14, seed=22)).to(gpu_device)
+    ids, _, mp = tok.encode(x, return_mp_tokens=True)
+    hf = st.tokenizer
+    lo = tok.bpe_min_token
+    rows = mp.cpu().numpy() - lo
+    want = [hf.encode("".join(map(chr, r)), add_special_tokens=False).ids for r in rows]
+    assert ids == want
+    # list / ndarray / 1-D inputs
+    assert tok._discrete_to_bpe(list(mp.cpu().numpy()[:5])) == want[:5]
+    assert tok._discrete_to_bpe(mp[3]) == [want[3]]
+    assert tok._discrete_to_bpe([int(v) for v in mp[4].tolist()]) == [want[4]]
+    back = tok.bpe_to_mp_tokens(ids)
+    assert torch.equal(back.cpu(), mp.cpu())
+    # padded 2-D id tensors decode too (pads must be ids that decode to nothing: none here)
+    assert torch.equal(tok.bpe_to_mp_tokens(ids[:1]).cpu(), mp[:1].cpu())
+    with pytest.raises(ValueError, match="smaller than the configured BPE minimum"):
+        tok._discrete_to_bpe(mp - (lo + 1))
+    if tok.bpe_max_token is not None:
+        bad = mp.clone()
+        bad[7, 3] = tok.bpe_max_token + 1
+        with pytest.raises(ValueError, match="greater than the configured BPE maximum"):
+            tok._discrete_to_bpe(bad)
+    with pytest.raises(ValueError, match="Decoded sequence has length"):
+        tok.bpe_to_mp_tokens([ids[0][:-1]])
+    with pytest.raises(OverflowError):
+        tok.bpe_to_mp_tokens([[-5] + ids[0]])
+    with pytest.raises(ValueError, match="1 or 2 dimensions"):
+        tok.bpe_to_mp_tokens(torch.zeros((1, 1, 1), dtype=torch.int64))

@@ -185,3 +185,24 @@ def test_bpe_hf_semantics_random_small():
         model = json.loads(bpe._tokenizer.to_str())["model"]
         v, m = BO.train(strings, [chr(i) for i in range(hi - lo + 1)], vs)
         assert v == model["vocab"] and [list(x) for x in m] == model["merges"], trial
+
+
+# ------------------------------------------------------- BPE encode / decode ----
+def _codec_model(case, spec, hf):
+    m = spec["model"]
+    if "ref" in m:
+        r = hf[m["ref"]]
+        return BO.BpeModel(r["vocab"], r["merges"])
+    return BO.BpeModel(m["vocab"], m["merges"], [tuple(s) for s in m["specials"]])
+
+
+@pytest.mark.parametrize("case", sorted(load_json("bpe_codec.json").keys()))
+def test_bpe_codec_oracle_matches_hf_golden(case):
+    """oracle/bpe_oracle.py BpeModel.encode / decode == HF tokenizers 0.22.2 per-row encode /
+    decode (beast/beast_bspline_bpe_tokenizer.py:175-247) on the captured vectors."""
+    spec = load_json("bpe_codec.json")[case]
+    om = _codec_model(case, spec, load_json("bpe_hf.json"))
+    for cps, ids in spec["encode"]:
+        assert om.encode("".join(map(chr, cps))) == ids
+    for ids, cps in spec["decode"]:
+        assert [ord(c) for c in om.decode(ids)] == cps
