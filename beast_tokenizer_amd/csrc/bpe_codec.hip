@@ -6,17 +6,23 @@
 // split, ByteLevel pre-tokeniser, BPE::merge_word + Word::merge_all, ByteLevel decoder,
 // String::from_utf8_lossy).
 //
-//   k_mergemap_build   open-addressing (a, b) -> (rank, new_id) table in HBM; a pair listed
-//                      twice keeps its LAST rank (HF collects the merges into a HashMap)
-//   k_bpe_encode       one 64-lane workgroup per row, everything of the row in LDS:
+//   k_mergemap_build   open-addressing (a, b) -> (rank, new_id) table + rank -> new_id;
+//                      a pair listed twice keeps its LAST rank (HF collects the merges
+//                      into a HashMap)
+//   k_bpe_encode       one wave per row, 4 rows per workgroup in flight, grid-stride over
+//                      rows; the merge map is staged once per workgroup into LDS when it
+//                      fits (<= 8192 slots, <= 4096 merges), so every lookup of the merge loop is an LDS
+//                      probe, not a dependent HBM/L2 round trip.  Per row, all in LDS:
 //                        lanes: code points, range checks, classes, UTF-8 symbol offsets
 //                        lane 0: special-token split (leftmost-longest) + GPT-2 regex walk
-//                        lanes: byte -> vocab id, one word per lane: HF's merge_all with
-//                        its (rank, pos) min-heap in LDS (stale entries skipped exactly as
-//                        HF does, so the result is HF's even when two merges share an id)
+//                        lanes: byte -> vocab id; one word per lane: HF's merge_all with
+//                        its (rank, pos) min-heap (stale entries skipped exactly as HF
+//                        does, so the result is HF's even when two merges share an id)
 //                        lanes: scan of per-word counts, ids written to the padded output
-//   k_bpe_decode       one thread per row: token bytes streamed through Rust's lossy UTF-8
-//                      decoder (maximal-subpart U+FFFD), code points + min written out
+//   k_bpe_decode       one wave per row: lanes gather their ids' bytes into LDS at
+//                      scanned offsets; valid UTF-8 (the normal case) decodes lane-
+//                      parallel (one lane per lead byte); anything else goes through
+//                      Rust's lossy decoder (maximal-subpart U+FFFD) on lane 0
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -25,25 +31,54 @@ namespace {
 
 constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;
 constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
-constexpr int ENC_T = 64;           // one wave per row
+constexpr int WAVES = 4;            // rows in flight per workgroup
+constexpr int BLOCK = 64 * WAVES;
 constexpr int MAX_SPECIAL = 64, MAX_SPECIAL_LEN = 64;
+constexpr int LDS_MAP_MAX_LOG2 = 13;   // stage maps of <= 8192 slots (64 KiB + rank table)
+constexpr size_t LDS_BUDGET = 160 * 1024;   // gfx950: one workgroup may declare all 160 KiB
 
 // encode status per row (host maps them to the reference's exceptions)
 constexpr int ST_OK = 0, ST_BELOW_MIN = 1, ST_ABOVE_MAX = 2, ST_NOT_UNICODE = 3, ST_SURROGATE = 4,
               ST_NO_CLASS = 5, ST_TOO_LONG = 6;
 
+#ifdef BPE_STAMPS
+// tools/codec_stamps.py only (the product compiles these out): s_memtime at phase
+// boundaries of row 0
+__device__ unsigned long long g_bpe_stamps[16];
+#define BPE_STAMP(k) do { if (r == 0 && lane == 0) g_bpe_stamps[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BPE_STAMP(k) do { } while (0)
+#endif
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// ------------------------------------------------------------- merge map --
+// layout: keys u32[cap] | vals u32[cap] ((rank + 1) << 16 | new_id, 0 = unset) | rank2new u16[n]
+struct MergeMap {
+  const uint32_t* keys;
+  const uint32_t* vals;
+  const uint16_t* rank2new;
+  int log2cap;
+};
+
 __device__ __forceinline__ uint32_t mm_hash(uint32_t key, int log2cap) {
   return (key * 0x9E3779B1u) >> (32 - log2cap);
 }
 
-__global__ void k_mergemap_clear(uint32_t* __restrict__ keys, unsigned long long* __restrict__ vals, int cap) {
+__global__ void k_mergemap_clear(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap) { keys[i] = EMPTY_KEY; vals[i] = 0ull; }
+  if (i < cap) { keys[i] = EMPTY_KEY; vals[i] = 0u; }
 }
 
 __global__ void k_mergemap_build(const int32_t* __restrict__ ma, const int32_t* __restrict__ mb,
                                  const int32_t* __restrict__ mnew, int n, uint32_t* __restrict__ keys,
-                                 unsigned long long* __restrict__ vals, int log2cap) {
+                                 uint32_t* __restrict__ vals, uint16_t* __restrict__ rank2new, int log2cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = ((uint32_t)ma[i] << 16) | (uint32_t)mb[i];
@@ -54,22 +89,22 @@ __global__ void k_mergemap_build(const int32_t* __restrict__ ma, const int32_t* 
     if (prev == EMPTY_KEY || prev == key) break;
     h = (h + 1) & mask;
   }
-  // later rank wins; the value is (rank + 1) << 32 | new_id so that 0 means "unset"
-  atomicMax(&vals[h], ((unsigned long long)(uint32_t)(i + 1) << 32) | (uint32_t)mnew[i]);
+  atomicMax(&vals[h], ((uint32_t)(i + 1) << 16) | (uint32_t)mnew[i]);   // later rank wins
+  rank2new[i] = (uint16_t)mnew[i];
 }
 
-// (rank << 16 | new_id) of pair (a, b), or -1.  rank < 2^31, new_id < 2^16.
-__device__ __forceinline__ long long mm_find(const uint32_t* __restrict__ keys,
-                                             const unsigned long long* __restrict__ vals, int log2cap,
-                                             int a, int b) {
+// rank of pair (a, b), or -1; *new_id set when found
+template <class Map>
+__device__ __forceinline__ int mm_find(const Map& m, int a, int b, int& new_id) {
   const uint32_t key = ((uint32_t)a << 16) | (uint32_t)b;
-  const uint32_t mask = (1u << log2cap) - 1u;
-  uint32_t h = mm_hash(key, log2cap);
+  const uint32_t mask = (1u << m.log2cap) - 1u;
+  uint32_t h = mm_hash(key, m.log2cap);
   while (true) {
-    const uint32_t k = keys[h];
+    const uint32_t k = m.keys[h];
     if (k == key) {
-      const unsigned long long v = vals[h];
-      return (long long)((((v >> 32) - 1ull) << 16) | (v & 0xFFFFull));
+      const uint32_t v = m.vals[h];
+      new_id = (int)(v & 0xFFFFu);
+      return (int)(v >> 16) - 1;
     }
     if (k == EMPTY_KEY) return -1;
     h = (h + 1) & mask;
@@ -86,78 +121,81 @@ __device__ __forceinline__ int utf8_byte(int cp, int q) {
 }
 
 // ---------------------------------------------------------------- heap --
-// min-heap of u64 keys (rank << 32 | pos << 16 | new_id) in LDS, one per word
-__device__ __forceinline__ void heap_push(unsigned long long* h, int& n, unsigned long long v) {
+// min-heap of u32 keys (rank << 16 | pos) in LDS, one per word: HF's Merge order (rank, pos)
+__device__ __forceinline__ void heap_push(uint32_t* h, int& n, uint32_t v) {
   int i = n++;
   while (i > 0) {
     const int p = (i - 1) >> 1;
-    if (h[p] <= v) break;
-    h[i] = h[p];
+    const uint32_t hp = h[p];
+    if (hp <= v) break;
+    h[i] = hp;
     i = p;
   }
   h[i] = v;
 }
 
-__device__ __forceinline__ unsigned long long heap_pop(unsigned long long* h, int& n) {
-  const unsigned long long top = h[0];
-  const unsigned long long v = h[--n];
+__device__ __forceinline__ uint32_t heap_pop(uint32_t* h, int& n) {
+  const uint32_t top = h[0];
+  const uint32_t v = h[--n];
   int i = 0;
   while (true) {
     int c = 2 * i + 1;
     if (c >= n) break;
-    if (c + 1 < n && h[c + 1] < h[c]) ++c;
-    if (v <= h[c]) break;
-    h[i] = h[c];
+    uint32_t hc = h[c];
+    if (c + 1 < n) {
+      const uint32_t h1 = h[c + 1];
+      if (h1 < hc) { hc = h1; ++c; }
+    }
+    if (v <= hc) break;
+    h[i] = hc;
     i = c;
   }
   if (n > 0) h[i] = v;
   return top;
 }
 
+// ------------------------------------------------------------- encode --
 struct EncLds {
+  uint32_t* heap;     // [3 S]
+  int32_t* c;         // [S] symbol ids (-1: none)
   int32_t* cps;       // [Lc] shifted code points
   int32_t* symoff;    // [Lc + 1] first byte symbol of each code point
   int32_t* wcp;       // [Lc + 1] word boundaries (code point index)
   int32_t* wspec;     // [Lc] special-token id of a word, or -1
   int32_t* wcnt;      // [Lc] final symbols per word, then their output offsets
-  uint8_t* cls;       // [Lc]
-  int32_t* c;         // [S] symbol ids (-1: none)
   int16_t* prv;       // [S]
   int16_t* nxt;       // [S]
-  unsigned long long* heap;  // [3 S]
+  uint8_t* cls;       // [Lc]
   int32_t* misc;      // [4]: n_words
 };
 
-__host__ __device__ inline size_t enc_align(size_t x) { return (x + 15) & ~size_t(15); }
-
-__host__ __device__ inline size_t enc_lds_bytes(int Lc, int S) {
-  size_t b = 0;
-  b += enc_align(sizeof(int32_t) * Lc);            // cps
-  b += enc_align(sizeof(int32_t) * (Lc + 1)) * 2;  // symoff, wcp
-  b += enc_align(sizeof(int32_t) * Lc) * 2;        // wspec, wcnt
-  b += enc_align(Lc);                              // cls
-  b += enc_align(sizeof(int32_t) * S);             // c
-  b += enc_align(sizeof(int16_t) * S) * 2;         // prv, nxt
-  b += enc_align(sizeof(unsigned long long) * 3 * (size_t)S);
-  b += 16;                                         // misc
-  return b;
+__host__ __device__ inline size_t enc_row_bytes(int Lc, int S) {
+  return al16(sizeof(uint32_t) * 3 * (size_t)S) + al16(sizeof(int32_t) * S) + al16(sizeof(int32_t) * Lc) +
+         2 * al16(sizeof(int32_t) * (Lc + 1)) + 2 * al16(sizeof(int32_t) * Lc) + 2 * al16(sizeof(int16_t) * S) +
+         al16(Lc) + 16;
 }
 
 __device__ inline EncLds enc_carve(char* p, int Lc, int S) {
   EncLds L;
-  auto take = [&](size_t bytes) { char* r = p; p += enc_align(bytes); return r; };
-  L.heap = (unsigned long long*)take(sizeof(unsigned long long) * 3 * (size_t)S);
+  auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
+  L.heap = (uint32_t*)take(sizeof(uint32_t) * 3 * (size_t)S);
+  L.c = (int32_t*)take(sizeof(int32_t) * S);
   L.cps = (int32_t*)take(sizeof(int32_t) * Lc);
   L.symoff = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
   L.wcp = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
   L.wspec = (int32_t*)take(sizeof(int32_t) * Lc);
   L.wcnt = (int32_t*)take(sizeof(int32_t) * Lc);
-  L.c = (int32_t*)take(sizeof(int32_t) * S);
   L.prv = (int16_t*)take(sizeof(int16_t) * S);
   L.nxt = (int16_t*)take(sizeof(int16_t) * S);
   L.cls = (uint8_t*)take(Lc);
   L.misc = (int32_t*)take(16);
   return L;
+}
+
+// bytes of the staged merge map (0 if it stays in HBM)
+__host__ __device__ inline size_t map_lds_bytes(int log2cap, int n_merges) {
+  if (log2cap > LDS_MAP_MAX_LOG2) return 0;
+  return al16(sizeof(uint32_t) * 2 * ((size_t)1 << log2cap)) + al16(sizeof(uint16_t) * (size_t)n_merges);
 }
 
 struct EncArgs {
@@ -169,9 +207,9 @@ struct EncArgs {
   const uint8_t* lut;
   int lut_n;
   const int32_t* byte2id;     // [256], -1: byte-level char not in the vocab
-  const uint32_t* mm_keys;
-  const unsigned long long* mm_vals;
-  int mm_log2cap;
+  MergeMap map;               // in HBM
+  int n_merges;
+  int map_in_lds;             // host choice: k_bpe_encode<true> stages the map
   const int32_t* spec_cps;    // [n_spec][MAX_SPECIAL_LEN]
   const int32_t* spec_len;
   const int32_t* spec_id;
@@ -211,32 +249,39 @@ __device__ __forceinline__ int regex_word(const int32_t* cps, const uint8_t* cls
   return j;
 }
 
-__global__ __launch_bounds__(ENC_T) void k_bpe_encode(EncArgs a) {
-  extern __shared__ __align__(16) char lds_raw[];
-  const int64_t r = blockIdx.x;
-  if (r >= a.n_rows) return;
-  const int lane = threadIdx.x;
-  EncLds L = enc_carve(lds_raw, a.Lc, a.S);
+__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  total = __shfl(x, 63);
+  return x - v;
+}
+
+template <class Map>
+__device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r, int lane) {
+  BPE_STAMP(0);
   const int64_t r0 = a.row_off[r];
   const int n = (int)(a.row_off[r + 1] - r0);
   if (n > a.Lc) {
     if (lane == 0) { a.status[r] = ST_TOO_LONG; a.out_len[r] = 0; }
     return;
   }
-
   // 1. code points, range checks (reference :181-192 order: below-min first), classes
   int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
-  for (int i = lane; i < n; i += ENC_T) {
+  for (int i = lane; i < n; i += 64) {
     const long long v = a.tok[r0 + i] - a.min_tok;
     below |= v < 0;
     above |= (a.max_span >= 0 && v > a.max_span);
     notuni |= v > 0x10FFFF;
     surr |= (v >= 0xD800 && v <= 0xDFFF);
     nocls |= v >= a.lut_n;
-    const int cp = (int)(v < 0 ? 0 : v > 0x10FFFF ? 0 : v);
+    const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
     L.cps[i] = cp;
     L.cls[i] = (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
   }
+  BPE_STAMP(1);
   int st = ST_OK;
   if (__any(below)) st = ST_BELOW_MIN;
   else if (__any(above)) st = ST_ABOVE_MAX;
@@ -247,29 +292,54 @@ __global__ __launch_bounds__(ENC_T) void k_bpe_encode(EncArgs a) {
     if (lane == 0) { a.status[r] = st; a.out_len[r] = 0; }
     return;
   }
-  // UTF-8 symbol offsets: wave scan in chunks of 64 code points
+  // UTF-8 symbol offsets
   int carry = 0;
-  for (int base = 0; base < n; base += ENC_T) {
+  for (int base = 0; base < n; base += 64) {
     const int i = base + lane;
+    int tot;
     const int len = (i < n) ? utf8_len(L.cps[i]) : 0;
-    int x = len;
-    for (int o = 1; o < ENC_T; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (i < n) L.symoff[i] = carry + x - len;
-    carry += __shfl(x, ENC_T - 1);
+    const int ex = wave_excl_scan(len, lane, tot);
+    if (i < n) L.symoff[i] = carry + ex;
+    carry += tot;
   }
   if (lane == 0) L.symoff[n] = carry;
-  const int nsym = carry;
-  if (nsym > a.S) {   // host sizes S from the code-point bound; guard anyway
+  if (carry > a.S) {   // host sizes S from the code-point bound; guard anyway
     if (lane == 0) { a.status[r] = ST_TOO_LONG; a.out_len[r] = 0; }
     return;
   }
-  __syncthreads();
+  wave_sync();
 
-  // 2. lane 0: AddedVocabulary split (leftmost-longest special token), then the regex walk
-  if (lane == 0) {
+  BPE_STAMP(2);
+  // 2. word boundaries.  No special tokens: every lane evaluates the regex from each of its
+  //    positions (end of a word starting there) in parallel, then lane 0 only follows the
+  //    chain 0 -> e[0] -> ...  With special tokens: lane 0 runs AddedVocabulary's split
+  //    (leftmost-longest) and the regex walk per segment.
+  if (a.n_spec == 0) {
+#ifndef BPE_SERIAL_PRETOK
+    int32_t* e = L.wcnt;   // scratch until step 4
+    for (int i = lane; i < n; i += 64) e[i] = regex_word(L.cps, L.cls, i, n);
+    wave_sync();
+    if (lane == 0) {
+      int nw = 0, p = 0;
+      while (p < n) {
+        L.wcp[nw] = p; L.wspec[nw] = -1; ++nw;
+        p = e[p];
+      }
+      L.wcp[nw] = n;
+      L.misc[0] = nw;
+    }
+#else
+    if (lane == 0) {
+      int nw = 0, p = 0;
+      while (p < n) {
+        L.wcp[nw] = p; L.wspec[nw] = -1; ++nw;
+        p = regex_word(L.cps, L.cls, p, n);
+      }
+      L.wcp[nw] = n;
+      L.misc[0] = nw;
+    }
+#endif
+  } else if (lane == 0) {
     int nw = 0, seg = 0, i = 0;
     while (i <= n) {
       int mlen = 0, mid = -1;
@@ -284,7 +354,6 @@ __global__ __launch_bounds__(ENC_T) void k_bpe_encode(EncArgs a) {
         }
       }
       if (mlen > 0 || i == n) {
-        // pre-tokenise the plain segment [seg, i)
         int p = seg;
         while (p < i) {
           const int j = regex_word(L.cps, L.cls, p, i);
@@ -302,16 +371,18 @@ __global__ __launch_bounds__(ENC_T) void k_bpe_encode(EncArgs a) {
     L.wcp[nw] = n;
     L.misc[0] = nw;
   }
+  BPE_STAMP(3);
   // 3. byte symbols as vocab ids
-  for (int i = lane; i < n; i += ENC_T) {
+  for (int i = lane; i < n; i += 64) {
     const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
     for (int q = 0; q < len; ++q) L.c[o + q] = a.byte2id[utf8_byte(cp, q)];
   }
-  __syncthreads();
+  wave_sync();
   const int nw = L.misc[0];
 
+  BPE_STAMP(4);
   // 4. one word per lane: BPE::merge_word + Word::merge_all
-  for (int w = lane; w < nw; w += ENC_T) {
+  for (int w = lane; w < nw; w += 64) {
     const int sb = L.symoff[L.wcp[w]], se = L.symoff[L.wcp[w + 1]];
     if (L.wspec[w] >= 0) {
       L.c[sb] = L.wspec[w];
@@ -337,70 +408,108 @@ __global__ __launch_bounds__(ENC_T) void k_bpe_encode(EncArgs a) {
       if (last >= 0) L.nxt[last] = (int16_t)s;
       last = s;
     }
-    unsigned long long* hp = L.heap + 3 * (size_t)sb;
+    uint32_t* hp = L.heap + 3 * (size_t)sb;
     int hn = 0;
     for (int s = sb; s < se; ++s) {
       if (L.c[s] < 0 || L.nxt[s] < 0) continue;
-      const long long m = mm_find(a.mm_keys, a.mm_vals, a.mm_log2cap, L.c[s], L.c[L.nxt[s]]);
-      if (m >= 0)
-        heap_push(hp, hn, ((unsigned long long)(m >> 16) << 32) | ((unsigned long long)(s - sb) << 16) |
-                              (unsigned long long)(m & 0xFFFF));
+      int nid;
+      const int rk = mm_find(mm, L.c[s], L.c[L.nxt[s]], nid);
+      if (rk >= 0) heap_push(hp, hn, ((uint32_t)rk << 16) | (uint32_t)(s - sb));
     }
+    int cnt = 0;
+    for (int s = sb; s < se; ++s) cnt += (L.c[s] >= 0);
+#ifdef BPE_SKIP_MERGE
+    hn = 0;
+#endif
     while (hn > 0) {
-      const unsigned long long top = heap_pop(hp, hn);
-      const int pos = sb + (int)((top >> 16) & 0xFFFF);
-      const int new_id = (int)(top & 0xFFFF);
+      const uint32_t top = heap_pop(hp, hn);
+      const int pos = sb + (int)(top & 0xFFFFu);
+      const int trank = (int)(top >> 16);
       if (L.c[pos] < 0) continue;             // merged into its left neighbour
       const int nx = L.nxt[pos];
       if (nx < 0) continue;                   // last symbol
-      const long long m = mm_find(a.mm_keys, a.mm_vals, a.mm_log2cap, L.c[pos], L.c[nx]);
-      if (m < 0 || (int)(m & 0xFFFF) != new_id) continue;  // expired entry
+      int new_id;
+      const int rk = mm_find(mm, L.c[pos], L.c[nx], new_id);
+      if (rk < 0) continue;
+      if (rk != trank && mm.rank2new[trank] != new_id) continue;   // expired entry
       L.c[pos] = new_id;
       L.c[nx] = -1;
+      --cnt;
       const int nn = L.nxt[nx];
       L.nxt[pos] = (int16_t)nn;
       if (nn >= 0) L.prv[nn] = (int16_t)pos;
       const int pv = L.prv[pos];
       if (pv >= 0) {
-        const long long mp = mm_find(a.mm_keys, a.mm_vals, a.mm_log2cap, L.c[pv], new_id);
-        if (mp >= 0)
-          heap_push(hp, hn, ((unsigned long long)(mp >> 16) << 32) | ((unsigned long long)(pv - sb) << 16) |
-                                (unsigned long long)(mp & 0xFFFF));
+        int nid;
+        const int rp = mm_find(mm, L.c[pv], new_id, nid);
+        if (rp >= 0) heap_push(hp, hn, ((uint32_t)rp << 16) | (uint32_t)(pv - sb));
       }
       if (nn >= 0) {
-        const long long mn = mm_find(a.mm_keys, a.mm_vals, a.mm_log2cap, new_id, L.c[nn]);
-        if (mn >= 0)
-          heap_push(hp, hn, ((unsigned long long)(mn >> 16) << 32) | ((unsigned long long)(pos - sb) << 16) |
-                                (unsigned long long)(mn & 0xFFFF));
+        int nid;
+        const int rn = mm_find(mm, new_id, L.c[nn], nid);
+        if (rn >= 0) heap_push(hp, hn, ((uint32_t)rn << 16) | (uint32_t)(pos - sb));
       }
     }
-    int cnt = 0;
-    for (int s = sb; s < se; ++s) cnt += (L.c[s] >= 0);
     L.wcnt[w] = cnt;
   }
-  __syncthreads();
+  wave_sync();
+  BPE_STAMP(5);
   // 5. word offsets (wave scan), ids in order
   carry = 0;
-  for (int base = 0; base < nw; base += ENC_T) {
+  for (int base = 0; base < nw; base += 64) {
     const int w = base + lane;
+    int tot;
     const int v = (w < nw) ? L.wcnt[w] : 0;
-    int x = v;
-    for (int o = 1; o < ENC_T; o <<= 1) {
-      const int y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    if (w < nw) L.wcnt[w] = carry + x - v;
-    carry += __shfl(x, ENC_T - 1);
+    const int ex = wave_excl_scan(v, lane, tot);
+    if (w < nw) L.wcnt[w] = carry + ex;
+    carry += tot;
   }
-  __syncthreads();
+  wave_sync();
   int32_t* out = a.out_ids + r * a.out_stride;
-  for (int w = lane; w < nw; w += ENC_T) {
+  for (int w = lane; w < nw; w += 64) {
     const int sb = L.symoff[L.wcp[w]], se = L.symoff[L.wcp[w + 1]];
     int o = L.wcnt[w];
     for (int s = sb; s < se; ++s)
       if (L.c[s] >= 0) out[o++] = L.c[s];
   }
   if (lane == 0) { a.out_len[r] = carry; a.status[r] = ST_OK; }
+  BPE_STAMP(6);
+}
+
+// the merge map staged in LDS: offsets from the dynamic LDS base, so every probe is a ds_read
+struct LdsMap {
+  const uint32_t* keys;
+  const uint32_t* vals;
+  const uint16_t* rank2new;
+  int log2cap;
+};
+
+template <bool MAP_LDS>
+__global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
+  extern __shared__ __align__(16) char lds_raw[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  size_t row_base = 0;
+  LdsMap lm;
+  if constexpr (MAP_LDS) {
+    const int cap = 1 << a.map.log2cap;
+    uint32_t* k = reinterpret_cast<uint32_t*>(lds_raw);
+    uint32_t* v = k + cap;
+    uint16_t* r2n = reinterpret_cast<uint16_t*>(lds_raw + al16(sizeof(uint32_t) * 2 * (size_t)cap));
+    for (int i = threadIdx.x; i < cap; i += BLOCK) { k[i] = a.map.keys[i]; v[i] = a.map.vals[i]; }
+    for (int i = threadIdx.x; i < a.n_merges; i += BLOCK) r2n[i] = a.map.rank2new[i];
+    lm.keys = k; lm.vals = v; lm.rank2new = r2n; lm.log2cap = a.map.log2cap;
+    row_base = map_lds_bytes(a.map.log2cap, a.n_merges);
+    __syncthreads();
+  }
+#ifdef BPE_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_bpe_stamps[8] = __builtin_amdgcn_s_memtime();
+#endif
+  EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S), a.Lc, a.S);
+  for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
+    if constexpr (MAP_LDS) encode_row(a, lm, L, r, lane);
+    else encode_row(a, a.map, L, r, lane);
+    wave_sync();
+  }
 }
 
 // ---------------------------------------------------------------- decode --
@@ -415,83 +524,171 @@ struct DecArgs {
   int unk_id;                 // id of "<unk>", -1: none
   long long min_tok;
   int L;                      // expected code points per row (output row width)
+  int bcap;                   // LDS byte buffer per wave
   long long* out;             // [n_rows][L]
   int32_t* out_count;         // decoded code points per row
   int32_t* status;            // bit 0: the row holds the <unk> id; bit 1: an id < -1 (not a u32)
 };
 
-struct ByteStream {
-  const int32_t* ids;
-  int64_t ni, ti;    // id index, byte index within that id
-  int32_t bo, be;    // current id's byte range
-  const DecArgs* a;
-  __device__ bool next_token() {
-    while (ti < ni) {
-      const int id = ids[ti++];
-      if (id < 0 || id >= a->n_vocab || a->tok_skip[id]) continue;
-      bo = a->tok_off[id];
-      be = a->tok_off[id + 1];
-      if (bo < be) return true;
-    }
-    return false;
-  }
-  __device__ int get() {  // next byte or -1
-    if (bo >= be && !next_token()) return -1;
-    return a->tok_bytes[bo++];
-  }
-};
+__device__ __forceinline__ bool cont(int b) { return (b & 0xC0) == 0x80; }
 
-__global__ __launch_bounds__(256) void k_bpe_decode(DecArgs a) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r >= a.n_rows) return;
+// One step of Rust's lossy UTF-8 decoder (core::str::lossy::Utf8Chunks) on b0 with the
+// next bytes b1..b3 (0 past the end): code point (0xFFFD on error) and bytes consumed.
+__device__ __forceinline__ int utf8_step(int b0, int b1, int b2, int b3, int& used) {
+  if (b0 < 0x80) { used = 1; return b0; }
+  if (b0 >= 0xC2 && b0 <= 0xDF) {
+    if (cont(b1)) { used = 2; return ((b0 & 0x1F) << 6) | (b1 & 0x3F); }
+    used = 1; return 0xFFFD;
+  }
+  if (b0 >= 0xE0 && b0 <= 0xEF) {
+    const bool ok1 = (b0 == 0xE0) ? (b1 >= 0xA0 && b1 <= 0xBF) : (b0 == 0xED) ? (b1 >= 0x80 && b1 <= 0x9F)
+                                                                              : (b1 >= 0x80 && b1 <= 0xBF);
+    if (!ok1) { used = 1; return 0xFFFD; }
+    if (!cont(b2)) { used = 2; return 0xFFFD; }
+    used = 3; return ((b0 & 0x0F) << 12) | ((b1 & 0x3F) << 6) | (b2 & 0x3F);
+  }
+  if (b0 >= 0xF0 && b0 <= 0xF4) {
+    const bool ok1 = (b0 == 0xF0) ? (b1 >= 0x90 && b1 <= 0xBF) : (b0 == 0xF4) ? (b1 >= 0x80 && b1 <= 0x8F)
+                                                                              : (b1 >= 0x80 && b1 <= 0xBF);
+    if (!ok1) { used = 1; return 0xFFFD; }
+    if (!cont(b2)) { used = 2; return 0xFFFD; }
+    if (!cont(b3)) { used = 3; return 0xFFFD; }
+    used = 4; return ((b0 & 0x07) << 18) | ((b1 & 0x3F) << 12) | ((b2 & 0x3F) << 6) | (b3 & 0x3F);
+  }
+  used = 1; return 0xFFFD;
+}
+
+// serial lossy decode of a byte source (get(i) for i < nb); returns the code point count
+template <class Get>
+__device__ int decode_serial(Get get, int64_t nb, long long* out, int L, long long min_tok) {
+  int cnt = 0;
+  int64_t i = 0;
+  while (i < nb) {
+    const int b0 = get(i);
+    const int b1 = i + 1 < nb ? get(i + 1) : 0, b2 = i + 2 < nb ? get(i + 2) : 0, b3 = i + 3 < nb ? get(i + 3) : 0;
+    int used;
+    const int cp = utf8_step(b0, b1, b2, b3, used);
+    if (cnt < L) out[cnt] = (long long)cp + min_tok;
+    ++cnt;
+    i += used;
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ int tok_len(const DecArgs& a, int id) {
+  if (id < 0 || id >= a.n_vocab || a.tok_skip[id]) return 0;
+  return a.tok_off[id + 1] - a.tok_off[id];
+}
+
+__device__ void decode_row(const DecArgs& a, uint8_t* buf, int64_t r, int lane) {
   const int64_t i0 = a.row_off[r], i1 = a.row_off[r + 1];
+  const int n = (int)(i1 - i0);
+  long long* out = a.out + r * (int64_t)a.L;
   int unk = 0, ovf = 0;
-  for (int64_t i = i0; i < i1; ++i) {
-    const int id = a.ids[i];
+  // gather bytes into LDS at scanned offsets
+  int64_t nb = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const int id = (i < n) ? a.ids[i0 + i] : -1;
     unk |= (a.unk_id >= 0 && id == a.unk_id);
     ovf |= (id < -1);
-  }
-  a.status[r] = unk | (ovf << 1);
-  ByteStream bs{a.ids + i0, i1 - i0, 0, 0, 0, &a};
-  int buf[4], nb = 0, cnt = 0;
-  long long* out = a.out + r * (int64_t)a.L;
-  while (true) {
-    while (nb < 4) {
-      const int b = bs.get();
-      if (b < 0) break;
-      buf[nb++] = b;
+    const int len = tok_len(a, id);
+    int tot;
+    const int ex = wave_excl_scan(len, lane, tot);
+    const int64_t o = nb + ex;
+    if (len > 0 && o + len <= a.bcap) {
+      const uint8_t* src = a.tok_bytes + a.tok_off[id];
+      for (int q = 0; q < len; ++q) buf[o + q] = src[q];
     }
-    if (nb == 0) break;
-    const int b0 = buf[0];
-    int cp, used;
-    auto at = [&](int k) { return k < nb ? buf[k] : 0; };   // Rust's safe_get: 0 past the end
-    auto cont = [](int b) { return (b & 0xC0) == 0x80; };
-    if (b0 < 0x80) { cp = b0; used = 1; }
-    else if (b0 >= 0xC2 && b0 <= 0xDF) {
-      if (cont(at(1))) { cp = ((b0 & 0x1F) << 6) | (at(1) & 0x3F); used = 2; }
-      else { cp = 0xFFFD; used = 1; }
-    } else if (b0 >= 0xE0 && b0 <= 0xEF) {
-      const int b1 = at(1);
-      const bool ok1 = (b0 == 0xE0) ? (b1 >= 0xA0 && b1 <= 0xBF) : (b0 == 0xED) ? (b1 >= 0x80 && b1 <= 0x9F)
-                                                                                : (b1 >= 0x80 && b1 <= 0xBF);
-      if (!ok1) { cp = 0xFFFD; used = 1; }
-      else if (!cont(at(2))) { cp = 0xFFFD; used = 2; }
-      else { cp = ((b0 & 0x0F) << 12) | ((b1 & 0x3F) << 6) | (at(2) & 0x3F); used = 3; }
-    } else if (b0 >= 0xF0 && b0 <= 0xF4) {
-      const int b1 = at(1);
-      const bool ok1 = (b0 == 0xF0) ? (b1 >= 0x90 && b1 <= 0xBF) : (b0 == 0xF4) ? (b1 >= 0x80 && b1 <= 0x8F)
-                                                                                : (b1 >= 0x80 && b1 <= 0xBF);
-      if (!ok1) { cp = 0xFFFD; used = 1; }
-      else if (!cont(at(2))) { cp = 0xFFFD; used = 2; }
-      else if (!cont(at(3))) { cp = 0xFFFD; used = 3; }
-      else { cp = ((b0 & 0x07) << 18) | ((b1 & 0x3F) << 12) | ((at(2) & 0x3F) << 6) | (at(3) & 0x3F); used = 4; }
-    } else { cp = 0xFFFD; used = 1; }
-    if (cnt < a.L) out[cnt] = (long long)cp + a.min_tok;
-    ++cnt;
-    for (int k = used; k < nb; ++k) buf[k - used] = buf[k];
-    nb -= used;
+    nb += tot;
   }
-  a.out_count[r] = cnt;
+  const int flags = (__any(unk) ? 1 : 0) | (__any(ovf) ? 2 : 0);
+  wave_sync();
+  int cnt = -1;
+  if (nb <= a.bcap) {
+    // valid UTF-8 check and lane-parallel decode: every lead's sequence well-formed and
+    // the continuation bytes exactly those the leads claim
+    int bad = 0, claimed = 0, conts = 0;
+    for (int i = lane; i < nb; i += 64) {
+      const int b0 = buf[i];
+      if (cont(b0)) { ++conts; continue; }
+      const int b1 = i + 1 < nb ? buf[i + 1] : 0, b2 = i + 2 < nb ? buf[i + 2] : 0,
+                b3 = i + 3 < nb ? buf[i + 3] : 0;
+      int used;
+      const int cp = utf8_step(b0, b1, b2, b3, used);
+      bad |= (cp == 0xFFFD && !(b0 == 0xEF && b1 == 0xBF && b2 == 0xBD));   // a literal U+FFFD is valid
+      claimed += used - 1;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      claimed += __shfl_xor(claimed, o);
+      conts += __shfl_xor(conts, o);
+    }
+    if (!__any(bad) && claimed == conts) {
+      int carry = 0;
+      for (int base = 0; base < nb; base += 64) {
+        const int i = base + lane;
+        const bool lead = i < nb && !cont(buf[i]);
+        int tot;
+        const int ex = wave_excl_scan(lead ? 1 : 0, lane, tot);
+        if (lead) {
+          const int k = carry + ex;
+          if (k < a.L) {
+            const int b1 = i + 1 < nb ? buf[i + 1] : 0, b2 = i + 2 < nb ? buf[i + 2] : 0,
+                      b3 = i + 3 < nb ? buf[i + 3] : 0;
+            int used;
+            out[k] = (long long)utf8_step(buf[i], b1, b2, b3, used) + a.min_tok;
+          }
+        }
+        carry += tot;
+      }
+      cnt = carry;
+    } else if (lane == 0) {
+      cnt = decode_serial([&](int64_t i) { return (int)buf[i]; }, nb, out, a.L, a.min_tok);
+    }
+  } else if (lane == 0) {
+    // more bytes than the LDS buffer holds (the row cannot decode to L code points anyway):
+    // stream them from HBM to get HF's exact count for the error message
+    const int32_t* ids = a.ids + i0;
+    int64_t ti = 0;
+    int32_t bo = 0, be = 0;
+    auto next_byte = [&]() -> int {
+      while (bo >= be) {
+        if (ti >= n) return -1;
+        const int id = ids[ti++];
+        if (tok_len(a, id) == 0) continue;
+        bo = a.tok_off[id];
+        be = a.tok_off[id + 1];
+      }
+      return a.tok_bytes[bo++];
+    };
+    int bq[4], nq = 0, c = 0;
+    while (true) {
+      while (nq < 4) {
+        const int b = next_byte();
+        if (b < 0) break;
+        bq[nq++] = b;
+      }
+      if (nq == 0) break;
+      int used;
+      const int cp = utf8_step(bq[0], nq > 1 ? bq[1] : 0, nq > 2 ? bq[2] : 0, nq > 3 ? bq[3] : 0, used);
+      if (c < a.L) out[c] = (long long)cp + a.min_tok;
+      ++c;
+      for (int k = used; k < nq; ++k) bq[k - used] = bq[k];
+      nq -= used;
+    }
+    cnt = c;
+  }
+  if (lane == 0) { a.out_count[r] = cnt; a.status[r] = flags; }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_bpe_decode(DecArgs a) {
+  extern __shared__ __align__(16) char lds_raw[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* buf = (uint8_t*)lds_raw + (size_t)wave * al16(a.bcap);
+  for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
+    decode_row(a, buf, r, lane);
+    wave_sync();
+  }
 }
 
 inline int log2_ceil(int64_t x) {
@@ -500,7 +697,25 @@ inline int log2_ceil(int64_t x) {
   return l;
 }
 
+int grid_for(int64_t n_rows) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  const int64_t want = (n_rows + WAVES - 1) / WAVES;
+  const int64_t cap = (int64_t)cus * 4;
+  return (int)(want < cap ? want : cap);
+}
+
 }  // namespace
+
+#ifdef BPE_STAMPS
+extern "C" int beast_debug_bpe_stamps(unsigned long long* host16) {
+  return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_bpe_stamps), sizeof(g_bpe_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" int beast_bpe_mergemap_log2cap(int n_merges) {
   const int l = log2_ceil(2 * (int64_t)(n_merges > 0 ? n_merges : 1));
@@ -509,33 +724,43 @@ extern "C" int beast_bpe_mergemap_log2cap(int n_merges) {
 
 extern "C" size_t beast_bpe_mergemap_bytes(int n_merges) {
   const size_t cap = size_t(1) << beast_bpe_mergemap_log2cap(n_merges);
-  return cap * sizeof(unsigned long long) + cap * sizeof(uint32_t);
+  return al16(cap * 2 * sizeof(uint32_t)) + al16((size_t)(n_merges > 0 ? n_merges : 1) * sizeof(uint16_t));
+}
+
+static MergeMap map_view(const void* map, int n_merges) {
+  MergeMap m;
+  m.log2cap = beast_bpe_mergemap_log2cap(n_merges);
+  const size_t cap = size_t(1) << m.log2cap;
+  m.keys = reinterpret_cast<const uint32_t*>(map);
+  m.vals = m.keys + cap;
+  m.rank2new = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(map) + al16(cap * 2 * sizeof(uint32_t)));
+  return m;
 }
 
 extern "C" int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* merge_b, const int32_t* merge_new,
                                         int n_merges, void* map, size_t map_bytes, void* stream) {
-  BEAST_REQUIRE(n_merges >= 0 && n_merges < (1 << 30), "n_merges out of range: %d", n_merges);
+  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
   BEAST_REQUIRE(map != nullptr, "mergemap buffer is null");
   BEAST_REQUIRE_CODE(map_bytes >= beast_bpe_mergemap_bytes(n_merges), BEAST_E_WORKSPACE,
                      "mergemap buffer too small: %zu < %zu", map_bytes, beast_bpe_mergemap_bytes(n_merges));
   BEAST_REQUIRE(n_merges == 0 || (merge_a && merge_b && merge_new), "merge arrays are null");
-  const int lg = beast_bpe_mergemap_log2cap(n_merges);
-  const int cap = 1 << lg;
-  auto* vals = reinterpret_cast<unsigned long long*>(map);
-  auto* keys = reinterpret_cast<uint32_t*>(vals + cap);
+  const MergeMap m = map_view(map, n_merges);
+  const int cap = 1 << m.log2cap;
   hipStream_t s = beast::as_stream(stream);
-  hipLaunchKernelGGL(k_mergemap_clear, dim3((cap + 255) / 256), dim3(256), 0, s, keys, vals, cap);
+  hipLaunchKernelGGL(k_mergemap_clear, dim3((cap + 255) / 256), dim3(256), 0, s, const_cast<uint32_t*>(m.keys),
+                     const_cast<uint32_t*>(m.vals), cap);
   BEAST_LAUNCHED("k_mergemap_clear");
   if (n_merges > 0) {
     hipLaunchKernelGGL(k_mergemap_build, dim3((n_merges + 255) / 256), dim3(256), 0, s, merge_a, merge_b, merge_new,
-                       n_merges, keys, vals, lg);
+                       n_merges, const_cast<uint32_t*>(m.keys), const_cast<uint32_t*>(m.vals),
+                       const_cast<uint16_t*>(m.rank2new), m.log2cap);
     BEAST_LAUNCHED("k_mergemap_build");
   }
   return BEAST_OK;
 }
 
 extern "C" size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms) {
-  return enc_lds_bytes(max_row_cps, max_row_syms);
+  return (size_t)WAVES * enc_row_bytes(max_row_cps, max_row_syms);
 }
 
 extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
@@ -548,30 +773,39 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   if (n_rows == 0) return BEAST_OK;
   BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && map && out_ids && out_len && status, "null pointer argument");
   BEAST_REQUIRE(lut_n > 0 && lut_n <= 65536, "class LUT size %lld out of range", (long long)lut_n);
+  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
   BEAST_REQUIRE(max_row_cps >= 0 && max_row_cps < 32768, "max_row_cps %d out of range", max_row_cps);
   BEAST_REQUIRE_CODE(max_row_syms >= 0 && max_row_syms <= 16384, BEAST_E_UNSUPPORTED,
                      "rows of %d byte symbols exceed the encoder's per-row LDS budget (16384)", max_row_syms);
   BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
   BEAST_REQUIRE(n_spec >= 0 && n_spec <= MAX_SPECIAL, "at most %d special tokens are supported", MAX_SPECIAL);
   BEAST_REQUIRE(n_spec == 0 || (spec_cps && spec_len && spec_id), "special-token arrays are null");
-  const size_t lds = enc_lds_bytes(max_row_cps, max_row_syms);
-  BEAST_REQUIRE_CODE(lds <= 65536, BEAST_E_UNSUPPORTED,
-                     "rows of %d code points / %d byte symbols need %zu B of LDS (> 64 KiB)", max_row_cps,
-                     max_row_syms, lds);
-  const int lg = beast_bpe_mergemap_log2cap(n_merges);
-  const int cap = 1 << lg;
+  const size_t rows_lds = (size_t)WAVES * enc_row_bytes(max_row_cps, max_row_syms);
+  BEAST_REQUIRE_CODE(rows_lds <= LDS_BUDGET, BEAST_E_UNSUPPORTED,
+                     "rows of %d code points / %d byte symbols need %zu B of LDS (> 160 KiB)", max_row_cps,
+                     max_row_syms, rows_lds);
   EncArgs a;
   a.tok = reinterpret_cast<const long long*>(tok);
   a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
   a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
-  a.mm_vals = reinterpret_cast<const unsigned long long*>(map);
-  a.mm_keys = reinterpret_cast<const uint32_t*>(a.mm_vals + cap);
-  a.mm_log2cap = lg;
+  a.map = map_view(map, n_merges);
+  a.n_merges = n_merges;
+  const size_t map_lds = map_lds_bytes(a.map.log2cap, n_merges);
+  a.map_in_lds = (map_lds > 0 && rows_lds + map_lds <= LDS_BUDGET) ? 1 : 0;
   a.spec_cps = spec_cps; a.spec_len = spec_len; a.spec_id = spec_id; a.n_spec = n_spec;
   a.unk_id = unk_id; a.fuse_unk = fuse_unk;
   a.Lc = max_row_cps; a.S = max_row_syms;
   a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
-  hipLaunchKernelGGL(k_bpe_encode, dim3((unsigned)n_rows), dim3(ENC_T), lds, beast::as_stream(stream), a);
+  const size_t lds = rows_lds + (a.map_in_lds ? map_lds : 0);
+  const void* fn = a.map_in_lds ? reinterpret_cast<const void*>(&k_bpe_encode<true>)
+                                : reinterpret_cast<const void*>(&k_bpe_encode<false>);
+  if (lds > 65536)
+    BEAST_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+              "hipFuncSetAttribute(k_bpe_encode)");
+  if (a.map_in_lds)
+    hipLaunchKernelGGL(k_bpe_encode<true>, dim3(grid_for(n_rows)), dim3(BLOCK), lds, beast::as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(k_bpe_encode<false>, dim3(grid_for(n_rows)), dim3(BLOCK), lds, beast::as_stream(stream), a);
   BEAST_LAUNCHED("k_bpe_encode");
   return BEAST_OK;
 }
@@ -588,8 +822,13 @@ extern "C" int beast_bpe_decode_rows(const int32_t* ids, const int64_t* row_off,
   DecArgs a;
   a.ids = ids; a.row_off = row_off; a.n_rows = n_rows; a.tok_off = tok_off; a.tok_bytes = tok_bytes;
   a.tok_skip = tok_skip; a.n_vocab = n_vocab; a.unk_id = unk_id; a.min_tok = min_tok; a.L = L;
+  // a row that decodes to L code points holds at most 4 L bytes; more -> streamed from HBM
+  int64_t bcap = 4 * (int64_t)L + 16;
+  if (bcap > (int64_t)(LDS_BUDGET / WAVES)) bcap = LDS_BUDGET / WAVES;
+  a.bcap = (int)bcap;
   a.out = reinterpret_cast<long long*>(out); a.out_count = out_count; a.status = status;
-  hipLaunchKernelGGL(k_bpe_decode, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, beast::as_stream(stream), a);
+  hipLaunchKernelGGL(k_bpe_decode, dim3(grid_for(n_rows)), dim3(BLOCK), (size_t)WAVES * al16(a.bcap),
+                     beast::as_stream(stream), a);
   BEAST_LAUNCHED("k_bpe_decode");
   return BEAST_OK;
 }

@@ -251,7 +251,7 @@ int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* merge_b, con
  * unk_id (fused when fuse_unk) if the model has an unk token).  Special tokens:
  * spec_cps[n_spec][64] code points, spec_len, spec_id.  Output: out_ids[r][0 .. out_len[r])
  * (row stride out_stride >= max_row_syms).  LDS per row: beast_bpe_encode_lds_bytes
- * (must be <= 64 KiB, else BEAST_E_UNSUPPORTED). */
+ * (at most 160 KiB with the staged merge map, else BEAST_E_UNSUPPORTED). */
 size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms);
 int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
                           int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,

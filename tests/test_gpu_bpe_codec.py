@@ -73,7 +73,8 @@ def test_decode_matches_hf_golden(case, gpu_device):
 
 
 @pytest.mark.parametrize("span,rows,width,vocab", [(255, 3000, 140, 2048), (700, 1500, 60, 1500),
-                                                    (3000, 800, 50, 4000), (127, 2000, 140, 800)])
+                                                    (3000, 800, 50, 4000), (127, 2000, 140, 800),
+                                                    (255, 6000, 140, 6000)])
 def test_codec_matches_live_hf(span, rows, width, vocab, gpu_device):
     """Train with HF (the reference's trainer), then every row of a fresh corpus -- including
     bins never seen in training -- encodes and decodes exactly as HF does."""
@@ -102,6 +103,12 @@ def test_codec_matches_live_hf(span, rows, width, vocab, gpu_device):
     Lg = max(len(w) for w in want_g) + 1
     got_g, counts_g, _ = decode_rows(model, garbage, gpu_device, Lg)
     assert got_g == want_g
+    # narrow output rows: rows of more bytes than 4 L take the streamed path; counts stay HF's
+    got_n, counts_n, _ = decode_rows(model, garbage, gpu_device, width)
+    assert counts_n.tolist() == [len(w) for w in want_g]
+    assert got_n == [w[:width] for w in want_g]
+    if span == 255 and vocab == 6000:
+        assert model.n_merges > 2048     # merge map too large for LDS: probed in HBM
 
 
 def test_bpe_tokenizer_api_and_errors(gpu_device):
