@@ -110,7 +110,7 @@ class _Plan:
         self.enc, self.rec = lib.beast_encode_f32, lib.beast_reconstruct_f32
         fp = _fastpath()
         self.fast = None
-        if fp is not None:
+        if fp is not None and not tok._conditioned:
             import ctypes
             addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value   # noqa: E731
             self.fast = fp.make_plan(addr(lib.beast_encode_f32), addr(lib.beast_reconstruct_f32),
@@ -131,8 +131,6 @@ class BEASTBsplineTokenizer(TokenizerBase):
                  use_bpe=False, device="cuda", llm_vocab_size: Optional[int] = None,
                  tokenizer_type: Optional[str] = None):
         super().__init__()
-        if init_cond_order != 0 or end_cond_order != 0:
-            raise NotImplementedError("init/end condition order != 0 is not supported by the HIP path")
 
         self.dt = 0.01  # reference :53
 
@@ -174,7 +172,13 @@ class BEASTBsplineTokenizer(TokenizerBase):
         self.seq_length = seq_len
         self.use_bpe = use_bpe
 
-        self._basis = DeviceBasis(num_basis, degree_p, duration, self.gripper_mp is not None)
+        self._basis = DeviceBasis(num_basis, degree_p, duration, self.gripper_mp is not None,
+                                  init_cond_order=init_cond_order, end_cond_order=end_cond_order)
+        # boundary conditions of the joint MP: the reference's MP object keeps the last fit's
+        # init / end conditions and reuses them in get_traj_pos (uni_bspline.py:126-166)
+        self._conditioned = self._basis.conditioned and self.joint_dof > 0
+        self._cond_state = None
+        self._full_basis = {}
         self._times_version = 0
         # tensor_linspace(0, duration, seq_len) == torch.linspace in fp32 (util_matrix.py:114-116)
         self.times = torch.linspace(0, duration, seq_len).to(device)
@@ -305,7 +309,46 @@ class BEASTBsplineTokenizer(TokenizerBase):
                    p_tok, _lib.raw_stream(p.idx))
         if rc:
             _lib.check(rc, "beast_encode_f32")
+        if self._conditioned:
+            self._store_conditions(trajs)
         return params, tokens
+
+    def _store_conditions(self, trajs: torch.Tensor) -> None:
+        """init / end conditions of the joint MP from this batch (uni_bspline.py:499-550), kept
+        for the next reconstruct as the reference's MP object keeps them."""
+        yj = trajs[..., self.joint_indices]
+        t = self.times.to(trajs.device, torch.float32).reshape(-1)
+        ip, iv, ep, ev, p_init, p_end = self._basis.fixed_ctrl(yj, t[1] - t[0])
+        self._cond_state = {"B": trajs.shape[0], "init_pos": ip, "init_vel": iv, "end_pos": ep, "end_vel": ev,
+                            "params_init": p_init, "params_end": p_end}
+
+    def _cond_dict(self) -> dict:
+        st = self._cond_state if self._conditioned else None
+        if st is None:
+            return {"init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+        return {k: st[k] for k in ("init_pos", "init_vel", "end_pos", "end_vel")}
+
+    def _add_conditions(self, pos: torch.Tensor, times, B: int, dev: torch.device) -> torch.Tensor:
+        """pos[..., joints] += boundary control points' term + init_pos (get_traj_pos with the
+        last fit's conditions, uni_bspline.py:126-166)."""
+        st = self._cond_state
+        if st is None:
+            raise RuntimeError("reconstruct with init/end conditions needs the conditions of a previous "
+                               "encode / compute_weights (the reference keeps them in its MP object)")
+        if st["B"] != B:
+            raise RuntimeError(f"Sizes of tensors must match except in dimension 2. Expected size {st['B']} "
+                               f"but got size {B} (boundary conditions were fitted on a batch of {st['B']})")
+        if times is None:
+            key = (dev, self._times_version)
+            full = self._full_basis.get(key)
+            if full is None:
+                self._full_basis = {key: self._basis.full_basis_at(self.times.to(dev).reshape(-1))}
+                full = self._full_basis[key]
+        else:   # [T] or per-row [B, T] grids -> [T, C] / [B, T, C]
+            full = self._basis.full_basis_at(times.to(dev, dtype=torch.float32))
+        bias = self._basis.fixed_term(full, st["params_init"], st["params_end"], st["init_pos"], fit=False)
+        pos[..., self.joint_indices] += bias
+        return pos
 
     # ===============================================
     #           - tokenizer preparation -
@@ -501,7 +544,7 @@ class BEASTBsplineTokenizer(TokenizerBase):
                 tokens = self._quantize(params, offset, p.dev, mode=0)
         else:
             params, tokens = self._fit(trajs, offset, p)
-        return tokens, {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+        return tokens, {"params": params, **self._cond_dict()}
 
     def _quantize(self, params: torch.Tensor, offset: int, dev: torch.device, mode: int):
         B = params.shape[0]
@@ -526,7 +569,7 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if update_bounds:
             self.update_weights_bounds_per_batch(params)
         tokens = self._quantize(params, 0, p.dev, mode=1)
-        params_dict = {"params": params, "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+        params_dict = {"params": params, **self._cond_dict()}
         return tokens, params_dict
 
     # ===============================================
@@ -628,6 +671,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
                    None if ntokens is None else ntokens.data_ptr(), _lib.raw_stream(p.idx))
         if rc:
             _lib.check(rc, "beast_reconstruct_f32")
+        if self._conditioned:
+            pos = self._add_conditions(pos, times, B, p.dev)
         return pos
 
     def reconstruct_traj(self, tokens, times=None, **kwargs):

@@ -226,3 +226,88 @@ def lerp_np(a, b, g):
     a, b, g = F32(a), F32(b), F32(g)
     d = F32(b - a)
     return F32(b - F32(d * F32(F32(1) - g))) if g >= F32(0.5) else F32(a + F32(d * g))
+
+
+# ------------------------------------------------ §8f rank 4: conditions ----
+# init_cond_order ic / end_cond_order ec != 0 of the joint MP, restated in float64 from
+# MP_lite_PyTorch/mp_pytorch/basis_gn/uni_bspline_basis.py:38-55 (C = N + ic + |ec| control
+# points), :192-301 (compute_init_params / compute_end_params, goal_basis False), :326-343
+# (the N fitted columns) and mp/uni_bspline.py:471-602 (learn: conditions from y0, y1,
+# y_{T-2}, y_{T-1}; fit of y - pos_det), :114-177 (get_traj_pos: fixed control points +
+# init_pos).  The reference keeps the last learn's conditions in its MP object and uses them
+# in the next get_traj_pos; ``cond_state`` carries them explicitly here.
+def cond_full_basis(times, tau, degree, num_basis, ic, ec):
+    return basis(times, tau, degree, num_basis + ic + abs(ec))
+
+
+def cond_effective(full, ic, ec):
+    C = full.shape[-1]
+    if ec == -1:
+        return np.concatenate([full[..., ic:C - 2], (full[..., -1] + full[..., -2])[..., None]], axis=-1)
+    return full[..., ic:C - ec]
+
+
+def cond_state(yj, times, tau, degree, num_basis, ic, ec):
+    """Boundary control points of trajectories yj [B, T, Dj] (float64)."""
+    y = np.asarray(yj, dtype=np.float64)
+    C = num_basis + ic + abs(ec)
+    kv = knots(degree, C).astype(np.float64)
+    dt = np.float64(F32(times[1]) - F32(times[0]))
+    dk0, dke = kv[1 + degree] - kv[1], kv[C - 1 + degree] - kv[C - 1]
+    st = {"init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None, "p_init": None, "p_end": None}
+    if ic:
+        st["init_pos"] = y[:, 0]
+        st["init_vel"] = (y[:, 1] - y[:, 0]) / dt
+        cols = [np.zeros_like(y[:, 0])]
+        if ic == 2:
+            cols.append(st["init_vel"] * tau * dk0 / degree)
+        st["p_init"] = np.stack(cols, axis=-1)
+    if ec:
+        st["end_vel"] = (y[:, -1] - y[:, -2]) / dt
+        e = y[:, -1] - (st["init_pos"] if ic else 0.0)
+        if ec == -1:
+            st["p_end"] = (st["end_vel"] * tau * dke / degree)[..., None]
+        elif ec == 1:
+            st["p_end"] = e[..., None]
+        else:
+            st["p_end"] = np.stack([e - st["end_vel"] * tau * dke / degree, e], axis=-1)
+        st["end_pos"] = y[:, -1]
+    return st
+
+
+def cond_fixed_term(full, st, ic, ec, fit):
+    """Fixed control points' term (+ init_pos) [B, T, Dj]; fit=True: learn's pos_det, else
+    get_traj_pos's extension (end order -1 subtracts its term from column C-2)."""
+    full = np.asarray(full, dtype=np.float64)
+    C = full.shape[-1]
+    ref = st["p_init"] if st["p_init"] is not None else st["p_end"]
+    ext = np.zeros(ref.shape[:-1] + (C,))
+    if st["p_init"] is not None:
+        ext[..., :ic] = st["p_init"]
+    if st["p_end"] is not None:
+        if ec == -1 and not fit:
+            ext[..., C - 2] = -st["p_end"][..., 0]
+        else:
+            ext[..., C - abs(ec):] = st["p_end"]
+    out = np.einsum("...tk,bdk->btd", full, ext)
+    if st["init_pos"] is not None:
+        out = out + st["init_pos"][:, None, :]
+    return out
+
+
+def cond_fit(yj, times, tau, degree, num_basis, ic, ec, reg=1e-9):
+    """Joint params [B, Dj*N] (d n) of the conditioned ridge fit, float64 rounded to fp32."""
+    full = cond_full_basis(times, tau, degree, num_basis, ic, ec)
+    eff = cond_effective(full, ic, ec).astype(np.float64)
+    st = cond_state(yj, times, tau, degree, num_basis, ic, ec)
+    r = np.asarray(yj, dtype=np.float64) - cond_fixed_term(full, st, ic, ec, fit=True)
+    P = np.linalg.solve(eff.T @ eff + reg * np.eye(num_basis), eff.T)
+    w = np.einsum("nt,btd->bdn", P, r)
+    return w.reshape(len(w), -1).astype(F32), st
+
+
+def cond_reconstruct_joint(params_joint, full, st, ic, ec):
+    """Joint positions [B, T, Dj] from params [B, Dj, N] and the conditions of the fit."""
+    eff = cond_effective(np.asarray(full, dtype=np.float64), ic, ec)
+    pj = np.einsum("...tn,bdn->btd", eff, np.asarray(params_joint, dtype=np.float64))
+    return (pj + cond_fixed_term(full, st, ic, ec, fit=False)).astype(F32)

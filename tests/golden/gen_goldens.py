@@ -50,7 +50,7 @@ class RefGlue:
     """Restates BEASTBsplineTokenizer glue (beast/beast_bspline_tokenizer.py:47-138, 399-536)."""
 
     def __init__(self, num_dof, num_basis=10, duration=2 * torch.pi, seq_len=50, vocab_size=256, degree_p=4,
-                 gripper_zero_order=False, gripper_indices=None):
+                 gripper_zero_order=False, gripper_indices=None, init_cond_order=0, end_cond_order=0):
         if gripper_indices is None or not gripper_zero_order:                    # :56-57
             gripper_indices = []
         self.gripper_indices = sorted(gripper_indices)
@@ -58,8 +58,9 @@ class RefGlue:
         self.joint_dof = num_dof - self.gripper_dof
         self.joint_indices = sorted(set(range(num_dof)) - set(self.gripper_indices))  # :68-70
         self.mp = MPFactory.init_mp(mp_type="uni_bspline", device="cpu", num_dof=self.joint_dof, tau=duration,
-                                    mp_args=dict(num_basis=num_basis, degree_p=degree_p, init_condition_order=0,
-                                                 end_condition_order=0, dt=0.01))     # :71-84
+                                    mp_args=dict(num_basis=num_basis, degree_p=degree_p,
+                                                 init_condition_order=init_cond_order,
+                                                 end_condition_order=end_cond_order, dt=0.01))     # :71-84
         self.gripper_mp = None
         if gripper_zero_order and self.gripper_dof > 0:                            # :88-96
             self.gripper_mp = MPFactory.init_mp(mp_type="uni_bspline", device="cpu", num_dof=self.gripper_dof,
@@ -70,13 +71,14 @@ class RefGlue:
         self.w_max = 0.02 * torch.ones(num_dof * num_basis)
         self.llm_vocab_size = None
 
-    def compute_weights(self, demos):                                              # :344-360
+    def compute_weights(self, demos, full=False):                                  # :344-360
         times = einops.repeat(self.times, 't -> b t', b=demos.shape[0])
-        w = self.mp.learn_mp_params_from_trajs(times, demos[..., self.joint_indices])['params']
+        res = self.mp.learn_mp_params_from_trajs(times, demos[..., self.joint_indices])
+        w = res['params']
         if self.gripper_mp is not None:
             g = self.gripper_mp.learn_mp_params_from_trajs(times, demos[..., self.gripper_indices])['params']
             w = torch.cat([w, g], dim=-1)
-        return w
+        return (w, res) if full else w
 
     def encode(self, trajs):                                                       # :399-428
         params = self.compute_weights(trajs.to(torch.float32))
@@ -258,8 +260,44 @@ def gen_bpe(out):
     print("bpe done")
 
 
+def gen_conditions(out):
+    """init_cond_order / end_cond_order != 0: the joint MP with boundary
+    conditions (uni_bspline.py:471-602 learn, :114-177 get_traj_pos; uni_bspline_basis.py:192-359).
+    Reconstruct runs right after the encode, so the MP object holds that batch's conditions."""
+    res = {}
+    combos = {"k1": ((1, 0), (2, 0), (0, 1), (0, 2), (1, 1), (2, 2), (1, 2), (2, -1)),
+              "k3": ((2, 2), (1, 0), (0, 2))}
+    for name, nd, g in (("k1", 7, []), ("k3", 14, [6, 13])):
+        for ic, ec in combos[name]:
+            ref = RefGlue(nd, gripper_zero_order=bool(g), gripper_indices=g, init_cond_order=ic,
+                          end_cond_order=ec)
+            ref.fit_parameters([synth_trajectories(512, 50, nd, seed=1, gripper_indices=g, start=512 * i)
+                                for i in range(4)])
+            x = synth_trajectories(32, 50, nd, seed=5, gripper_indices=g)   # regenerated by the tests
+            xt = torch.from_numpy(x)
+            w, d = ref.compute_weights(xt, full=True)
+            tok, params = ref.encode(xt)
+            pos = ref.reconstruct_traj(tok)
+            t30 = mp_utils.tensor_linspace(0, 2 * torch.pi, 30)
+            pos_t30 = ref.reconstruct_traj(tok, times=einops.repeat(t30, 't -> b t', b=32))
+            k = f"{name}_{ic}_{ec}"
+            res[k + "_x_sha256"] = np.frombuffer(hashlib.sha256(x.tobytes()).digest(), dtype=np.uint8)
+            res[k + "_w_min"], res[k + "_w_max"] = ref.w_min.numpy(), ref.w_max.numpy()
+            res[k + "_params"], res[k + "_tokens"] = params.numpy(), tok.numpy()
+            res[k + "_pos"], res[k + "_pos_t30"] = pos.numpy(), pos_t30.numpy()
+            for c in ("init_pos", "init_vel", "end_pos", "end_vel"):
+                if d[c] is not None:
+                    res[f"{k}_{c}"] = d[c].numpy()
+    np.savez_compressed(os.path.join(out, "conditions.npz"), **res)
+    print("conditions done")
+
+
 if __name__ == "__main__":
     out = HERE
+    if sys.argv[1:] == ["conditions"]:
+        gen_conditions(out)
+        sys.exit(0)
+    gen_conditions(out)
     gen_quantile(out)
     gen_bspline(out)
     gen_bpe(out)

@@ -528,3 +528,47 @@ def test_bpe_tokenizer_end_to_end(gpu_device):
     model = json.loads(bpe._tokenizer.to_str())["model"]
     assert tok._last_bpe_result.vocab == model["vocab"]
     assert [list(m) for m in tok._last_bpe_result.merges] == model["merges"]
+
+
+# -------------------------------------------- init / end conditions (§8f rank 4) ----
+COND = load_npz("conditions.npz")
+COND_CASES = sorted({k.rsplit("_", 1)[0] for k in COND if k.endswith("_params")})
+
+
+@pytest.mark.parametrize("case", COND_CASES)
+def test_conditions_match_reference(case, gpu_device):
+    """init_cond_order / end_cond_order != 0: params within 1e-5 of the reference, its
+    conditions, tokens up to rounding ties, and reconstruct (which reuses the last fit's
+    conditions, as the reference's MP object does) within 1e-5 -- default and custom times."""
+    name, ic, ec = case.split("_")
+    ic, ec = int(ic), int(ec)
+    nd, g = (7, []) if name == "k1" else (14, [6, 13])
+    x = torch.from_numpy(synth_trajectories(32, 50, nd, seed=5, gripper_indices=g)).to(gpu_device)
+    tok = BEASTBsplineTokenizer(num_dof=nd, gripper_zero_order=bool(g), gripper_indices=g or None,
+                                init_cond_order=ic, end_cond_order=ec, device=str(gpu_device))
+    tok.w_min.copy_(torch.from_numpy(COND[case + "_w_min"]))
+    tok.w_max.copy_(torch.from_numpy(COND[case + "_w_max"]))
+    with pytest.raises(RuntimeError):
+        tok.reconstruct_traj(torch.from_numpy(COND[case + "_tokens"]))   # no fit yet: no conditions
+    tokens, pd = tok.encode(x)
+    ref = COND[case + "_params"]
+    got = pd["params"].cpu().numpy()
+    scale = np.maximum(1.0, np.abs(ref).max(axis=1, keepdims=True))
+    assert np.all(np.abs(got - ref) <= 1e-5 * scale)
+    for c in ("init_pos", "init_vel", "end_pos", "end_vel"):
+        if case + "_" + c in COND:
+            np.testing.assert_allclose(pd[c].cpu().numpy(), COND[case + "_" + c], rtol=1e-6, atol=1e-6)
+        else:
+            assert pd[c] is None
+    rt = COND[case + "_tokens"]
+    diff = tokens.cpu().numpy() - rt
+    assert np.abs(diff).max() <= 1 and (diff != 0).sum() <= 3          # rounding ties only
+    pos = tok.reconstruct_traj(torch.from_numpy(rt).to(gpu_device)).cpu().numpy()
+    rp = COND[case + "_pos"]
+    assert np.abs(pos - rp).max() <= 1e-5 * max(1.0, np.abs(rp).max())
+    t30 = torch.linspace(0, 2 * torch.pi, 30).to(gpu_device).repeat(32, 1)
+    pos30 = tok.reconstruct_traj(torch.from_numpy(rt).to(gpu_device), times=t30).cpu().numpy()
+    rp30 = COND[case + "_pos_t30"]
+    assert np.abs(pos30 - rp30).max() <= 1e-5 * max(1.0, np.abs(rp30).max())
+    with pytest.raises(RuntimeError):
+        tok.reconstruct_traj(torch.from_numpy(rt[:5]).to(gpu_device))    # conditions fitted on 32 rows

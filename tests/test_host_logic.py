@@ -146,11 +146,15 @@ def test_config_layout_matches_reference():
     assert torch.equal(t.times, torch.linspace(0, 2 * torch.pi, 50))
 
 
-def test_unsupported_condition_orders_raise():
-    with pytest.raises(NotImplementedError):
-        _tok(init_cond_order=1)
-    with pytest.raises(NotImplementedError):
-        _tok(end_cond_order=2)
+def test_condition_orders():
+    """init/end condition orders 0..2 (and end -1) build; others are rejected."""
+    t = _tok(init_cond_order=2, end_cond_order=2)
+    assert t._basis.n_ctrl == t.num_basis + 4 and t._conditioned
+    assert _tok(end_cond_order=-1)._basis.n_ctrl == 11
+    with pytest.raises(ValueError):
+        _tok(init_cond_order=3)
+    with pytest.raises(ValueError):
+        _tok(end_cond_order=-2)
 
 
 def test_llm_vocab_handling():

@@ -206,3 +206,47 @@ def test_bpe_codec_oracle_matches_hf_golden(case):
         assert om.encode("".join(map(chr, cps))) == ids
     for ids, cps in spec["decode"]:
         assert [ord(c) for c in om.decode(ids)] == cps
+
+
+# -------------------------------------------- init / end conditions (§8f rank 4) ----
+COND = load_npz("conditions.npz")
+COND_CASES = sorted({k.rsplit("_", 1)[0] for k in COND if k.endswith("_params")})
+
+
+def _cond_setup(case):
+    from beast_tokenizer_amd.synthetic import synth_trajectories
+    import hashlib
+    name, ic, ec = case.split("_")
+    ic, ec = int(ic), int(ec)
+    nd, g = (7, []) if name == "k1" else (14, [6, 13])
+    x = synth_trajectories(32, 50, nd, seed=5, gripper_indices=g)
+    assert hashlib.sha256(x.tobytes()).digest() == COND[case + "_x_sha256"].tobytes()
+    lay = O.Layout.make(nd, g, bool(g))
+    return x, lay, ic, ec
+
+
+@pytest.mark.parametrize("case", COND_CASES)
+def test_condition_oracle_matches_reference(case):
+    """oracle/beast_oracle.py cond_* == the reference MP with init/end conditions (params within
+    the fp32-LU bound, conditions, and get_traj_pos of the golden tokens)."""
+    x, lay, ic, ec = _cond_setup(case)
+    t = O.times_grid(2 * np.pi, 50)
+    tau = float(np.float32(2 * np.pi))
+    yj = x[..., lay.joint_indices]
+    pj, st = O.cond_fit(yj, t, tau, 4, 10, ic, ec)
+    ref = COND[case + "_params"][:, : len(lay.joint_indices) * 10]
+    scale = np.maximum(1.0, np.abs(ref).max(axis=1, keepdims=True))
+    assert np.all(np.abs(pj - ref) <= 1e-5 * scale)
+    for c in ("init_pos", "init_vel", "end_pos", "end_vel"):
+        if case + "_" + c in COND:
+            assert np.allclose(st[c], COND[case + "_" + c], rtol=1e-5, atol=1e-5), c
+        else:
+            assert st[c] is None, c
+    # reconstruct of the golden tokens (joint DoFs) with those conditions
+    wmin, wmax = COND[case + "_w_min"], COND[case + "_w_max"]
+    params = O.decode(COND[case + "_tokens"], lay, 10, wmin, wmax, 256)
+    nj = len(lay.joint_indices)
+    full = O.cond_full_basis(t, tau, 4, 10, ic, ec)
+    pos_j = O.cond_reconstruct_joint(params.reshape(32, -1, 10)[:, :nj], full, st, ic, ec)
+    ref_pos = COND[case + "_pos"][..., lay.joint_indices]
+    assert np.abs(pos_j - ref_pos).max() <= 1e-5 * max(1.0, np.abs(ref_pos).max())
