@@ -42,6 +42,7 @@ SIGNATURES = {
     "beast_colminmax_f32": (_i32, [_vp, _i64, _i32, _i64, _vp, _vp, _vp, _sz, _vp]),
     "beast_quantile_workspace_bytes": (_sz, [_i64, _i32, _i32]),
     "beast_quantile_prepare": (_i32, [_vp, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _sz, _vp]),
+    "beast_quantile_prepare_segments": (_i32, [_vp, _i32, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _sz, _vp]),
     "beast_quantile_hist_ptr": (_vp, [_vp, _i32, _i32]),
     "beast_quantile_hist_count": (_i64, [_i32, _i32]),
     "beast_quantile_hist": (_i32, [_i32, _i64, _i32, _i32, _vp, _vp]),

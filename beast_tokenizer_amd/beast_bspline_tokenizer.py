@@ -408,8 +408,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
                 break
         if not params and process_group is None:
             raise RuntimeError("No parameters were gathered from the dataloader.")
-        allp = torch.cat(params, dim=0) if params else torch.empty((0, self.num_dof * self.num_basis),
-                                                                   device=dev)
+        # per-batch params are read in place by the quantile kernels (no concatenation)
+        allp = params if params else torch.empty((0, self.num_dof * self.num_basis), device=dev)
         reduce = no_reduce if process_group is None else torch_dist_reducer(
             None if process_group is True else process_group)
         q = column_quantiles(allp, [0.01, 0.99], reduce)
@@ -493,7 +493,12 @@ class BEASTBsplineTokenizer(TokenizerBase):
     @torch.no_grad()
     def compute_weights(self, demos):
         """Fitted params [B, num_dof*num_basis] in (d n) order (reference :344-360)."""
-        params, _ = self._fit(demos, None, self._plan())
+        p = self._plan()
+        if p.fast is not None:
+            r = p.fast.fit(demos, torch._C._cuda_getCurrentRawStream(p.idx))
+            if r is not None:
+                return r
+        params, _ = self._fit(demos, None, p)
         return params
 
     @torch.no_grad()

@@ -53,6 +53,21 @@ struct Plan {
     return py::make_tuple(tokens, params);
   }
 
+  // params fp32 [B, D*N] only (compute_weights / fit_parameters) or None
+  py::object fit(const at::Tensor& x, int64_t stream) const {
+    if (!x.is_cuda() || x.get_device() != device || x.scalar_type() != at::kFloat || x.dim() != 3 ||
+        x.size(1) != T || x.size(2) < min_din || x.stride(2) != 1)
+      return py::none();
+    const int64_t B = x.size(0);
+    at::Tensor params = at::empty({B, D * N}, x.options());
+    const int rc = enc(x.data_ptr<float>(), B, (int)T, x.stride(0), x.stride(1), x.stride(2), (int)x.size(2), (int)D,
+                       (int)nj, reinterpret_cast<const int32_t*>(p_src), reinterpret_cast<const float*>(p_proj),
+                       (int)N, nullptr, nullptr, (int)V, 0, params.data_ptr<float>(), nullptr,
+                       reinterpret_cast<void*>(stream));
+    if (rc) fail(rc, "beast_encode_f32");
+    return py::cast(params);
+  }
+
   // positions fp32 [B, T, D] from int64 tokens [B, N*D] (or [B, N, D]) or None
   py::object reconstruct(const at::Tensor& tok, int64_t offset, int64_t stream) const {
     if (!tok.is_cuda() || tok.get_device() != device || tok.scalar_type() != at::kLong || !tok.is_contiguous())
@@ -93,6 +108,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "host fast path of the BEAST encode / reconstruct calls (see csrc/fastpath.cpp)";
   py::class_<Plan>(m, "Plan")
       .def("encode", &Plan::encode, py::arg("x"), py::arg("offset"), py::arg("stream"))
+      .def("fit", &Plan::fit, py::arg("x"), py::arg("stream"))
       .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"));
   m.def("make_plan", &make_plan);
 }

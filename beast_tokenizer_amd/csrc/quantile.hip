@@ -93,6 +93,40 @@ __global__ void k_keys(const float* __restrict__ x, int64_t rows, int cols, int6
   }
 }
 
+// The same transpose over a list of row-major segments (fit_parameters' per-batch params,
+// no torch.cat): seg[i] = {ptr, first row, row stride}, rows of segment i are
+// [seg[i].first, seg[i + 1].first) of the concatenated space.  Grid x = nseg * tiles_per_seg
+// 32-row tiles (tiles past a segment's end exit), so no tile never straddles two segments.
+struct QSeg {
+  const float* ptr;
+  int64_t first;
+  int64_t stride;
+};
+
+__global__ void k_keys_seg(const QSeg* __restrict__ seg, int nseg, int tiles_per_seg, int64_t rows, int cols,
+                           uint32_t* __restrict__ keys) {
+  __shared__ uint32_t tile[32][33];
+  const int si = blockIdx.x / tiles_per_seg;
+  const int64_t t0 = (int64_t)(blockIdx.x % tiles_per_seg) * 32;
+  const QSeg sg = seg[si];
+  const int64_t seg_rows = ((si + 1 < nseg) ? seg[si + 1].first : rows) - sg.first;
+  if (t0 >= seg_rows) return;
+  const int nr = (int)min<int64_t>(32, seg_rows - t0);
+  const int64_t r0 = sg.first + t0;
+  const int c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  const float* src = sg.ptr + t0 * sg.stride;
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + tx;
+    if (k < nr && c < cols) tile[k][tx] = f2key(src[(int64_t)k * sg.stride + c]);
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k;
+    if (tx < nr && c < cols) keys[(int64_t)c * rows + r0 + tx] = tile[tx][k];
+  }
+}
+
 __global__ void k_init(QState* __restrict__ st, uint32_t* __restrict__ nanf, QHeader* __restrict__ hdr, int cols,
                        QHeader h) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -105,11 +139,29 @@ __global__ void k_init(QState* __restrict__ st, uint32_t* __restrict__ nanf, QHe
   if (i < cols) nanf[i] = 0;
 }
 
-// grid (chunks, cols)
+// grid (chunks, cols).  Keys are read 16 B per lane; every thread keeps a run-length counter
+// (bin, count) per histogram and only flushes it to the LDS histogram when the bin changes:
+// parameter columns are narrow, so the top digits of most keys fall into a handful of bins,
+// and one LDS atomic per key would serialise on them.
+// LDS histograms hold 16-bit counts, two bins per word (a chunk has <= 32768 keys, so a bin
+// never carries into its neighbour): 4 KiB per histogram keeps 8 workgroups per CU resident.
+static_assert(HIST_CHUNK < 65536, "16-bit LDS bins");
+__device__ __forceinline__ void bin_add(uint32_t* h, uint32_t bin, uint32_t cnt) {
+  atomicAdd(&h[bin >> 1], cnt << ((bin & 1u) * 16));
+}
+
+__device__ __forceinline__ void run_add(uint32_t* h, uint32_t& bin, uint32_t& cnt, uint32_t b) {
+  if (b == bin) { ++cnt; return; }
+  if (cnt) bin_add(h, bin, cnt);
+  bin = b;
+  cnt = 1;
+}
+
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restrict__ keys, int64_t rows, int ntg,
                                                        int pass, const QState* __restrict__ st,
                                                        uint64_t* __restrict__ hist) {
-  __shared__ uint32_t h[MAXTG][NBIN];
+  extern __shared__ uint32_t h_raw[];   // [nh][NBIN / 2] packed 16-bit bins
+  uint32_t (*h)[NBIN / 2] = reinterpret_cast<uint32_t (*)[NBIN / 2]>(h_raw);
   const int c = blockIdx.y;
   int shift, bits;
   pass_geom(pass, shift, bits);
@@ -117,29 +169,57 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restric
   const int hi_shift = shift + bits;  // bits above the digit are known
   // targets that need their own histogram (pass 0: one shared histogram)
   const int nh = (pass == 0) ? 1 : ntg;
-  uint32_t pref[MAXTG];
-  for (int t = 0; t < nh; ++t) pref[t] = (hi_shift >= 32) ? 0u : (st[c * ntg + t].prefix >> hi_shift);
-  for (int i = threadIdx.x; i < nh * NBIN; i += HIST_THREADS) (&h[0][0])[i] = 0;
+  uint32_t pref[MAXTG], rbin[MAXTG], rcnt[MAXTG];
+  for (int t = 0; t < MAXTG; ++t) {
+    pref[t] = (t < nh && hi_shift < 32) ? (st[c * ntg + t].prefix >> hi_shift) : 0u;
+    rbin[t] = 0;
+    rcnt[t] = 0;
+  }
+  for (int i = threadIdx.x; i < nh * NBIN / 2; i += HIST_THREADS) (&h[0][0])[i] = 0;
   __syncthreads();
   const uint32_t* kc = keys + (int64_t)c * rows;
-  const int64_t i0 = (int64_t)blockIdx.x * HIST_CHUNK;
-  const int64_t i1 = min<int64_t>(rows, i0 + HIST_CHUNK);
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += HIST_THREADS) {
-    const uint32_t k = kc[i];
+  const int64_t chunk = HIST_CHUNK;
+  const int64_t i0 = (int64_t)blockIdx.x * chunk;
+  const int64_t i1 = min<int64_t>(rows, i0 + chunk);
+  auto add = [&](uint32_t k) {
     const uint32_t dg = (k >> shift) & mask;
     if (pass == 0) {
-      atomicAdd(&h[0][dg], 1u);
+      run_add(h[0], rbin[0], rcnt[0], dg);
     } else {
       const uint32_t hk = k >> hi_shift;
-      for (int t = 0; t < nh; ++t)
-        if (hk == pref[t]) atomicAdd(&h[t][dg], 1u);
+#pragma unroll
+      for (int t = 0; t < MAXTG; ++t)
+        if (t < nh && hk == pref[t]) run_add(h[t], rbin[t], rcnt[t], dg);
     }
+  };
+  // column c's keys start at c * rows: 16-B aligned only if rows % 4 == 0 -> scalar head
+  const int64_t a0 = min<int64_t>(i1, (i0 + (int64_t)((4 - ((c * rows + i0) & 3)) & 3)));
+  for (int64_t i = i0 + threadIdx.x; i < a0; i += HIST_THREADS) add(kc[i]);
+  const int64_t nv = (i1 - a0) / 4;
+  const uint4* kv = reinterpret_cast<const uint4*>(kc + a0);
+  constexpr int UNR = 4;   // 64 B per lane in flight
+  int64_t v = threadIdx.x;
+  for (; v + (UNR - 1) * HIST_THREADS < nv; v += UNR * HIST_THREADS) {
+    uint4 q[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) q[u] = kv[v + u * HIST_THREADS];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) { add(q[u].x); add(q[u].y); add(q[u].z); add(q[u].w); }
   }
+  for (; v < nv; v += HIST_THREADS) {
+    const uint4 q = kv[v];
+    add(q.x); add(q.y); add(q.z); add(q.w);
+  }
+  for (int64_t i = a0 + 4 * nv + threadIdx.x; i < i1; i += HIST_THREADS) add(kc[i]);
+#pragma unroll
+  for (int t = 0; t < MAXTG; ++t)
+    if (rcnt[t]) bin_add(h[t], rbin[t], rcnt[t]);
   __syncthreads();
   uint64_t* hc = hist + (int64_t)c * ntg * NBIN;
-  for (int i = threadIdx.x; i < nh * NBIN; i += HIST_THREADS) {
+  for (int i = threadIdx.x; i < nh * NBIN / 2; i += HIST_THREADS) {
     const uint32_t v = (&h[0][0])[i];
-    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(hc + i), (unsigned long long)v);
+    if (v & 0xFFFFu) atomicAdd(reinterpret_cast<unsigned long long*>(hc + 2 * i), (unsigned long long)(v & 0xFFFFu));
+    if (v >> 16) atomicAdd(reinterpret_cast<unsigned long long*>(hc + 2 * i + 1), (unsigned long long)(v >> 16));
   }
 }
 
@@ -274,6 +354,30 @@ extern "C" int beast_quantile_prepare(const float* x, int64_t rows, int cols, in
   return BEAST_OK;
 }
 
+extern "C" int beast_quantile_prepare_segments(const void* seg_table, int nseg, int64_t max_seg_rows, int64_t rows,
+                                               int cols, int64_t n_total, int n_q, const float* host_q,
+                                               void* workspace, size_t ws_bytes, void* stream) {
+  BEAST_REQUIRE(nseg >= 1 && seg_table, "beast_quantile_prepare_segments: need >= 1 segment");
+  const int64_t tps = (max_seg_rows + 31) / 32;
+  BEAST_REQUIRE(max_seg_rows >= 0 && tps * nseg < (int64_t(1) << 31), "beast_quantile_prepare_segments: "
+                "%d segments of up to %lld rows are too many tiles", nseg, (long long)max_seg_rows);
+  // header, state and ranks as for one matrix; x is only dereferenced by k_keys
+  int rc = beast_quantile_prepare(nullptr, 0, cols, cols, n_total, n_q, host_q, workspace, ws_bytes, stream);
+  if (rc) return rc;
+  BEAST_REQUIRE(rows >= 0 && rows <= n_total && rows < (int64_t(1) << 31), "bad segment rows %lld",
+                (long long)rows);
+  const WsLayout w = ws_layout(rows, cols, n_q);
+  BEAST_REQUIRE_CODE(ws_bytes >= w.total, BEAST_E_WORKSPACE, "quantile workspace %zu < %zu", ws_bytes, w.total);
+  if (rows > 0 && tps > 0) {
+    dim3 grid((unsigned)(tps * nseg), (unsigned)((cols + 31) / 32));
+    hipLaunchKernelGGL(k_keys_seg, grid, dim3(256), 0, beast::as_stream(stream), static_cast<const QSeg*>(seg_table),
+                       nseg, (int)tps, rows, cols,
+                       reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) + w.keys));
+    BEAST_LAUNCHED("k_keys_seg");
+  }
+  return BEAST_OK;
+}
+
 extern "C" int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream) {
   BEAST_REQUIRE(workspace && pass >= 0 && pass <= 2 && n_q >= 1 && n_q <= MAXQ, "beast_quantile_hist: bad args");
   const WsLayout w = ws_layout(rows, cols, n_q);
@@ -282,8 +386,10 @@ extern "C" int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, vo
   const int ntg = 2 * n_q;
   BEAST_HIP(hipMemsetAsync(ws + w.hist, 0, sizeof(uint64_t) * (size_t)cols * ntg * NBIN, s), "hist memset");
   if (rows > 0) {
-    dim3 grid((unsigned)((rows + HIST_CHUNK - 1) / HIST_CHUNK), (unsigned)cols);
-    hipLaunchKernelGGL(k_hist, grid, dim3(HIST_THREADS), 0, s, reinterpret_cast<const uint32_t*>(ws + w.keys), rows,
+    const int64_t chunk = HIST_CHUNK;
+    dim3 grid((unsigned)((rows + chunk - 1) / chunk), (unsigned)cols);
+    const size_t lds = sizeof(uint32_t) * (NBIN / 2) * (pass == 0 ? 1 : ntg);
+    hipLaunchKernelGGL(k_hist, grid, dim3(HIST_THREADS), lds, s, reinterpret_cast<const uint32_t*>(ws + w.keys), rows,
                        ntg, pass, reinterpret_cast<const QState*>(ws + w.state),
                        reinterpret_cast<uint64_t*>(ws + w.hist));
     BEAST_LAUNCHED("k_hist");

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 from typing import Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -25,13 +26,28 @@ class GpuQuantileOps:
         self.stream = _lib.stream_of(device)
         self.lib = _lib.load()
 
-    def prepare(self, x: torch.Tensor, n_total: int, qs: Sequence[float]) -> None:
-        rows, cols = x.shape
+    def prepare(self, x, n_total: int, qs: Sequence[float]) -> None:
+        """x: one [rows, cols] fp32 tensor, or a list of them (row segments, read in place)."""
+        segs = x if isinstance(x, (list, tuple)) else None
+        rows = sum(int(t.shape[0]) for t in segs) if segs is not None else x.shape[0]
+        cols = (segs[0] if segs else x).shape[1]
         self.rows, self.cols, self.nq = rows, cols, len(qs)
         qh = (ctypes.c_float * self.nq)(*[float(q) for q in qs])
         self.ws = torch.empty(self.lib.beast_quantile_workspace_bytes(rows, cols, self.nq), dtype=torch.uint8,
                               device=self.device)
-        _lib.run("beast_quantile_prepare", x.data_ptr() if rows else None, rows, cols, x.stride(0), n_total,
+        if segs is None:
+            _lib.run("beast_quantile_prepare", x.data_ptr() if rows else None, rows, cols, x.stride(0), n_total,
+                     self.nq, ctypes.cast(qh, ctypes.c_void_p), self.ws.data_ptr(), self.ws.numel(), self.stream)
+            return
+        # {ptr, first_row, row_stride} per segment (QSeg in csrc/quantile.hip)
+        table, first, longest = [], 0, 0
+        for t in segs:
+            table += [t.data_ptr(), first, t.stride(0)]
+            first += int(t.shape[0])
+            longest = max(longest, int(t.shape[0]))
+        self._segs = segs   # read asynchronously by k_keys_seg
+        self._table = torch.tensor(np.array(table, dtype=np.uint64).view(np.int64)).to(self.device)
+        _lib.run("beast_quantile_prepare_segments", self._table.data_ptr(), len(segs), longest, rows, cols, n_total,
                  self.nq, ctypes.cast(qh, ctypes.c_void_p), self.ws.data_ptr(), self.ws.numel(), self.stream)
 
     def hist_tensor(self) -> torch.Tensor:
@@ -52,19 +68,28 @@ class GpuQuantileOps:
         return out
 
 
-def column_quantiles(x: torch.Tensor, qs: Sequence[float], reduce: Reducer = no_reduce, ops=None) -> torch.Tensor:
-    """x [rows, cols] fp32 (this rank's rows) -> [len(qs), cols] fp32 quantiles of all ranks' rows."""
+def column_quantiles(x, qs: Sequence[float], reduce: Reducer = no_reduce, ops=None) -> torch.Tensor:
+    """x [rows, cols] fp32 (this rank's rows), or a list of such row blocks with equal cols
+    (read in place, no concatenation) -> [len(qs), cols] fp32 quantiles of all ranks' rows."""
+    blocks = list(x) if isinstance(x, (list, tuple)) else [x]
+    if not blocks:
+        raise RuntimeError("No parameters were gathered from the dataloader.")
+    dev = blocks[0].device
     if ops is None:
-        _lib.require_gpu(x, "params")
-        ops = GpuQuantileOps(x.device)
-    if x.dim() != 2:
-        raise ValueError("column_quantiles expects a 2-D [rows, cols] tensor")
-    x = x.to(torch.float32)
-    if x.stride(1) != 1:
-        x = x.contiguous()
-    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
-    reduce(n, "sum")
-    n_total = int(n.item())
+        _lib.require_gpu(blocks[0], "params")
+        ops = GpuQuantileOps(dev)
+    for b in blocks:
+        if b.dim() != 2 or b.shape[1] != blocks[0].shape[1]:
+            raise ValueError("column_quantiles expects 2-D [rows, cols] blocks with equal cols")
+    blocks = [b if (b.dtype is torch.float32 and b.stride(1) == 1 and b.device == dev) else
+              b.to(dev, torch.float32).contiguous() for b in blocks]
+    blocks = [b for b in blocks if b.shape[0]] or blocks[:1]
+    x = blocks if len(blocks) > 1 else blocks[0]
+    n_total = sum(int(b.shape[0]) for b in blocks)
+    if reduce is not no_reduce:   # ranks' row counts (one all-reduce); single process: no sync
+        n = torch.tensor([n_total], dtype=torch.int64, device=dev)
+        reduce(n, "sum")
+        n_total = int(n.item())
     if n_total == 0:
         raise RuntimeError("No parameters were gathered from the dataloader.")
     ops.prepare(x, n_total, qs)

@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-bpe", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true")
+    ap.add_argument("--no-large", action="store_true")
+    ap.add_argument("--large-batch", type=int, default=262144,
+                    help="batch of the supplementary HBM-bound roofline point")
     ap.add_argument("--fit-trajs", type=int, default=1000000, help="fit_parameters corpus (all ranks)")
     ap.add_argument("--bpe-seqs", type=int, default=500000, help="BPE corpus (trajectories, all ranks)")
     ap.add_argument("--bpe-vocab", type=int, default=2048)
@@ -81,6 +84,36 @@ def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 100, rounds: i
             stream.synchronize()
             per.append(s.elapsed_time(e) * 1e3 / reps)
     return float(np.median(per))
+
+
+def large_batch_roofline(tok, dev, stream, B: int):
+    """Supplementary point: the same two kernels at a batch large enough to be HBM-bound
+    (the B=4096 launches are latency-bound: one 8-trajectory tile per workgroup)."""
+    x = synth_trajectories_device(B, T, D, seed=3, device=dev)
+    phi, _, proj = tok._constants(dev)
+    src, dst = tok._dof_maps(dev)
+    wmn, wmx = tok._bounds(dev)
+    params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
+    tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
+    pos = torch.empty((B, T, D), dtype=torch.float32, device=dev)
+    sp = stream.cuda_stream
+
+    def enc():
+        _lib.run("beast_encode_f32", x.data_ptr(), B, T, x.stride(0), x.stride(1), x.stride(2), D, D, D,
+                 src.data_ptr(), proj.data_ptr(), N, wmn.data_ptr(), wmx.data_ptr(), V, 0, params.data_ptr(),
+                 tokens.data_ptr(), sp)
+
+    def rec():
+        _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, D, N, V, 0, wmn.data_ptr(), wmx.data_ptr(),
+                 phi.data_ptr(), 0, T, dst.data_ptr(), D, None, 0, None, None, pos.data_ptr(), None, sp)
+    te = kernel_time_us(enc, stream, reps=20, rounds=3)
+    tr = kernel_time_us(rec, stream, reps=20, rounds=3)
+    out = {"batch": B, "k_encode_us": te, "k_reconstruct_us": tr,
+           "k_encode_GBps": ENC_BYTES * B / (te * 1e-6) / 1e9, "k_reconstruct_GBps": REC_BYTES * B / (tr * 1e-6) / 1e9}
+    out["k_encode_frac"] = out["k_encode_GBps"] * 1e9 / HBM_PEAK
+    out["k_reconstruct_frac"] = out["k_reconstruct_GBps"] * 1e9 / HBM_PEAK
+    del x, params, tokens, pos
+    return out
 
 
 def cpu_baseline(tok_bounds, seconds: float):
@@ -370,6 +403,8 @@ def main():
             "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
             "algo_bytes_per_launch": kbytes,
             "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
+    if not args.no_large:
+        roof["large_batch"] = large_batch_roofline(tok, dev, stream, args.large_batch)
 
     fitb = None
     if not args.no_fit:

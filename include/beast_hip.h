@@ -137,6 +137,12 @@ int beast_quantile_prepare(const float* x, int64_t rows, int cols, int64_t row_s
                            int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream);
 uint64_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q);
 int64_t beast_quantile_hist_count(int cols, int n_q);
+/* prepare over a list of row-major segments instead of one matrix (fit_parameters' per-batch
+ * params without a concatenation): seg_table = device array of nseg {const float* ptr;
+ * int64_t first_row; int64_t row_stride} (24 B each, first_row ascending from 0), rows = the
+ * total, max_seg_rows = the largest segment. */
+int beast_quantile_prepare_segments(const void* seg_table, int nseg, int64_t max_seg_rows, int64_t rows, int cols,
+                                    int64_t n_total, int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream);
 int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream);
 int beast_quantile_select(int pass, int cols, int n_q, void* workspace, void* stream);
 int beast_quantile_finalize(int cols, int n_q, void* workspace, float* out, void* stream);

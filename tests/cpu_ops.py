@@ -126,7 +126,7 @@ class NumpyQuantileOps:
     GEOM = [(21, 11), (10, 11), (0, 10)]
 
     def prepare(self, x, n_total, qs):
-        self.x = x.numpy()
+        self.x = np.concatenate([b.numpy() for b in x]) if isinstance(x, (list, tuple)) else x.numpy()
         self.rows, self.cols = self.x.shape
         self.keys = _keys(self.x).T.copy()          # [cols][rows]
         self.ntg = 2 * len(qs)

@@ -330,6 +330,15 @@ def test_quantile_kat(gpu_device):
         q = column_quantiles(torch.from_numpy(x).to(gpu_device), [0.01, 0.99]).cpu().numpy()
         assert np.array_equal(q[0], z[k + "_lo"].astype(np.float32)), k
         assert np.array_equal(q[1], z[k + "_hi"].astype(np.float32)), k
+    # row blocks read in place (fit_parameters' per-batch params) == one matrix
+    for k, x in quantile_inputs().items():
+        if x.shape[0] < 10:
+            continue
+        cuts = [0, 3, x.shape[0] // 2, x.shape[0] // 2, x.shape[0]]
+        blocks = [torch.from_numpy(x[a:b]).to(gpu_device) for a, b in zip(cuts[:-1], cuts[1:])]
+        q = column_quantiles(blocks, [0.01, 0.99]).cpu().numpy()
+        assert np.array_equal(q[0], z[k + "_lo"].astype(np.float32)), k
+        assert np.array_equal(q[1], z[k + "_hi"].astype(np.float32)), k
     xn = quantile_inputs()["n101"].copy()
     xn[7, 3] = np.nan
     q = column_quantiles(torch.from_numpy(xn).to(gpu_device), [0.01, 0.99]).cpu().numpy()

@@ -120,6 +120,15 @@ def test_column_quantiles_driver(rows):
     assert np.array_equal(out, ref, equal_nan=True)
 
 
+def test_column_quantiles_blocks_driver():
+    """A list of row blocks (fit_parameters passes its per-batch params) == the matrix."""
+    rng = np.random.default_rng(5)
+    x = rng.normal(size=(301, 9)).astype(np.float32)
+    blocks = [torch.from_numpy(x[:100]), torch.from_numpy(x[100:100]), torch.from_numpy(x[100:])]
+    out = column_quantiles(blocks, [0.01, 0.99], ops=NumpyQuantileOps()).numpy()
+    assert np.array_equal(out, np.quantile(x, [0.01, 0.99], axis=0).astype(np.float32))
+
+
 def test_column_quantiles_arbitrary_q():
     rng = np.random.default_rng(3)
     x = rng.standard_normal((517, 3)).astype(np.float32)
