@@ -64,6 +64,11 @@ SIGNATURES = {
     "beast_bpe_build_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _sz, _vp]),
     "beast_bpe_word_signatures": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "beast_bpe_apply_argmax": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp]),
+    "beast_bpe_loop_workspace_bytes": (_sz, [_i32, _i32]),
+    "beast_bpe_loop_init": (_i32, [_vp, _sz, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    "beast_bpe_loop_steps": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp,
+                                    _i32, _vp]),
+    "beast_bpe_loop_state": (_i32, [_vp, _i32, _i32, _vp, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),

@@ -205,6 +205,55 @@ class GpuBpeOps:
                  self._argws.data_ptr(), k, self.stream)
         return self._read_i64(self._argws[2 + (k & 1):], 1)[0] & 0xFFFFFFFFFFFFFFFF
 
+    # -- device-driven merge loop (csrc/bpe.hip k_loop_step): no host round trip per merge
+    LOOP_P = 0x9E3779B97F4A7C15   # odd multiplier of the token-string hash
+
+    def loop_supported(self, Vt: int) -> bool:
+        return 4 * Vt * 4 <= 64 * 1024 and getattr(self, "_index", None) is None
+
+    def loop_run(self, words, table, Vt: int, id2str, vocab_size: int, min_frequency: int, max_len: int,
+                 chunk: int = 64):
+        """Run the merge loop on the device from the current argmax; returns the merge log
+        [(a, b, nid, reused)] for the host to replay and verify."""
+        lib = _lib.load()
+        n_tok = len(id2str)
+        max_merges = 4 * max(vocab_size - n_tok, 0) + 1024
+        P, M = self.LOOP_P, (1 << 64) - 1
+        h0, p0 = np.zeros(n_tok, dtype=np.uint64), np.zeros(n_tok, dtype=np.uint64)
+        for i, t in enumerate(id2str):
+            h, pw = 0, 1
+            for byte in t.encode("utf-8"):
+                h = (h * P + byte) & M
+                pw = (pw * P) & M
+            h0[i], p0[i] = h, pw
+        hp = torch.from_numpy(np.stack([h0, p0]).view(np.int64)).to(self.device)
+        nb = lib.beast_bpe_loop_workspace_bytes(Vt, max_merges)
+        ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        parity = (self._calls - 1) & 1          # slot of the argmax that produced `key`
+        _lib.run("beast_bpe_loop_init", ws.data_ptr(), nb, Vt, max_merges, n_tok, vocab_size, min_frequency, parity,
+                 hp[0].data_ptr(), hp[1].data_ptr(), self._tlen.data_ptr(), self.stream)
+        import ctypes
+        st_p, log_p = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.run("beast_bpe_loop_state", ws.data_ptr(), Vt, max_merges, ctypes.byref(st_p), ctypes.byref(log_p))
+        st_off, log_off = st_p.value - ws.data_ptr(), log_p.value - ws.data_ptr()
+        state = ws[st_off:st_off + 32].view(torch.int32)     # active, a, b, nid, reused, vcur, parity, n
+        host = torch.empty(8, dtype=torch.int32, pin_memory=True)
+        vcur = n_tok
+        while True:
+            steps = max(1, min(chunk, vocab_size - vcur))
+            _lib.run("beast_bpe_loop_steps", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
+                     words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
+                     words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
+                     _lib.ptr(words.get("sig")), table.data_ptr(), self._argws.data_ptr(), vocab_size, self.stream)
+            host.copy_(state, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            active, vcur, n = int(host[0]), int(host[5]), int(host[7])
+            if not active or vcur >= vocab_size:
+                break
+        full = n >= max_merges
+        log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
+        return [tuple(int(v) for v in r) for r in log], full
+
     def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int, count: int = 1 << 62) -> torch.Tensor:
         _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
                  _lib.ptr(words.get("wcount")), words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len,
@@ -239,8 +288,13 @@ def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special
 def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
-              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False) -> BPEResult:
-    """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard)."""
+              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False,
+              device_loop: bool = True) -> BPEResult:
+    """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard).
+
+    Single process on the GPU ops: the merge loop runs device-driven (``GpuBpeOps.loop_run``,
+    no host round trip per merge); multi-rank (per-merge delta all-reduce) and the CPU model
+    run the host-driven loop below."""
     import time
     t0 = time.perf_counter()
     if ops is None:
@@ -286,6 +340,31 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     merges: List[Tuple[str, str]] = []
     t1 = time.perf_counter()
     key = ops.argmax(table, Vt, len(id2str))
+    if (device_loop and reduce is no_reduce and not compact_every and hasattr(ops, "loop_supported")
+            and ops.loop_supported(Vt)):
+        # merges decided on the GPU; the host replays the log against the real strings
+        log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
+        for a, b, nid, reused in log:
+            new_tok = id2str[a] + id2str[b]
+            have = str2id.get(new_tok)
+            if (have is not None) != bool(reused) or (have is not None and have != nid) or \
+                    (have is None and nid != len(id2str)):
+                full = True     # a 64-bit string-hash collision: redo on the host-driven loop
+                break
+            if have is None:
+                str2id[new_tok] = nid
+                id2str.append(new_tok)
+            merges.append((id2str[a], id2str[b]))
+        if full:
+            return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
+                             max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=None,
+                             reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, use_index=use_index,
+                             device_loop=False)
+        t2 = time.perf_counter()
+        stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
+                 "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
+                 "Vt": Vt, "device_loop": True}
+        return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
     while len(id2str) < vocab_size:
         count = key >> 32
         if count < 1 or count < min_frequency:

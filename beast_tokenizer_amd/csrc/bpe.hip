@@ -274,6 +274,22 @@ __device__ __forceinline__ unsigned long long sig_bit(uint32_t x) { return 1ull 
 // longer holds the symbol) are harmless: the probe finds no pair there.
 constexpr uint32_t IDX_INEXACT = 0xFFFFFFFFu;
 constexpr int64_t MERGE_LDS_MIN_COUNT = 1 << 16;
+
+// Device-driven merge loop (beast_bpe_loop_*): the merge picked by the previous argmax is
+// decided ON the GPU by k_loop_step and handed to k_merge / k_apply_argmax through this record,
+// so the host enqueues merges without a round trip per merge.
+struct LoopState {
+  int32_t active;        // 0 once the loop has stopped (later launches are no-ops)
+  int32_t a, b, nid, reused;
+  int32_t vcur;          // vocabulary size after this step's merge
+  int32_t parity;        // argmax result slot the next k_apply_argmax writes
+  int32_t n_merges;      // merges logged
+  int32_t target;        // vocab_size
+  int32_t min_freq;
+  int32_t log2cap;       // token-string hash table
+  int32_t max_merges;    // log capacity
+  unsigned long long count;
+};
 constexpr int MERGE_UNROLL = 4;
 struct WordIndex {
   uint32_t* start;   // [Vt]
@@ -353,14 +369,23 @@ __global__ __launch_bounds__(1024) void k_index_scan(WordIndex ix, int Vt, uint3
 // (A last-workgroup-applies variant was measured slower: every workgroup's device-scope
 // fence writes back its XCD's L2.)  Candidate words: the shorter exact index list of a
 // and b, else every word (pre-filtered by the Bloom signature).
-template <bool LDS>
+// MODE 0: deltas by global atomics, 1: LDS-privatised, 2: (a, b, nid, count) from the device
+// loop record, LDS-privatised when the pair is frequent (dynamic LDS always allocated)
+template <int MODE>
 __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
                                                int64_t nw, int a, int b, int nid, uint32_t* __restrict__ tlen,
                                                int max_len, int32_t* __restrict__ deltas, int Vt,
-                                               unsigned long long* __restrict__ sig, WordIndex ix, bool use_ix) {
+                                               unsigned long long* __restrict__ sig, WordIndex ix, bool use_ix,
+                                               const LoopState* __restrict__ loop) {
   extern __shared__ __attribute__((aligned(16))) int32_t dl[];
   __shared__ int touched;
+  bool LDS = (MODE == 1);
+  if (MODE == 2) {
+    if (!loop->active) return;
+    a = loop->a; b = loop->b; nid = loop->nid;
+    LDS = loop->count >= (unsigned long long)MERGE_LDS_MIN_COUNT;
+  }
   const uint32_t* cand = nullptr;
   int64_t ncand = nw;
   if (use_ix) {
@@ -476,10 +501,15 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
 __global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ table, int32_t* __restrict__ deltas,
                                                       int Vt, int vcur, ArgWs aw, int parity, int apply, int a, int b,
                                                       int nid, uint32_t* __restrict__ tlen, WordIndex ix, bool use_ix,
-                                                      bool reused) {
+                                                      bool reused, const LoopState* __restrict__ loop) {
   __shared__ unsigned long long sh[4];
   __shared__ int changed;
   const int x = blockIdx.x;
+  if (loop != nullptr) {   // device-driven loop: this step's merge from the record
+    if (!loop->active) return;
+    vcur = loop->vcur; parity = loop->parity; a = loop->a; b = loop->b; nid = loop->nid;
+    reused = loop->reused != 0;
+  }
   uint32_t* row = table + (size_t)x * Vt;
   if (x == 0 && threadIdx.x == 0) aw.slot[parity ^ 1] = 0ull;
   if (threadIdx.x == 0) changed = 0;
@@ -554,6 +584,63 @@ __global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ tab
     unsigned long long* slot = aw.slot + parity;
     if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
   }
+}
+
+// ------------------------------------------------------- device merge loop --
+// Token strings are identified by (64-bit polynomial hash of their UTF-8 bytes, byte length):
+// h(xy) = h(x) * P^len(y) + h(y), so a merge's string is hashed from its parts.  The table maps
+// (h, len) -> id; equal strings always collide (HF reuses the id), different strings collide
+// with probability ~2^-64 -- the host re-checks every logged merge against the real strings
+// and reruns the loop on the host path if it ever finds one (beast_tokenizer_amd/bpe_train.py).
+constexpr uint32_t LOOP_EMPTY = 0xFFFFFFFFu;
+struct LoopHash {
+  unsigned long long* key;   // [cap] h
+  uint32_t* klen;            // [cap] byte length, LOOP_EMPTY = free slot
+  int32_t* kid;              // [cap]
+  unsigned long long* th;    // [Vt] token hash
+  unsigned long long* tp;    // [Vt] P^len
+  int32_t* log;              // [max_merges][4] a, b, nid, reused
+};
+
+__device__ __forceinline__ uint64_t loop_slot(unsigned long long h, uint32_t len, int log2cap) {
+  return ((h ^ ((unsigned long long)len * 0x9E3779B97F4A7C15ull)) * 0xbf58476d1ce4e5b9ull) >> (64 - log2cap);
+}
+
+__global__ void k_loop_step(LoopState* __restrict__ st, ArgWs aw, int Vt, LoopHash lh,
+                            const uint32_t* __restrict__ tlen) {
+  if (threadIdx.x != 0 || !st->active) return;
+  const unsigned long long key = aw.slot[st->parity];
+  const unsigned long long count = key >> 32;
+  if (st->vcur >= st->target || count < 1 || count < (unsigned long long)st->min_freq ||
+      st->n_merges >= st->max_merges) {
+    st->active = 0;
+    return;
+  }
+  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
+  const int a = (int)(idx / (uint32_t)Vt), b = (int)(idx % (uint32_t)Vt);
+  const unsigned long long h = lh.th[a] * lh.tp[b] + lh.th[b];
+  const uint32_t len = tlen[a] + tlen[b];
+  const uint64_t mask = (1ull << st->log2cap) - 1;
+  uint64_t sl = loop_slot(h, len, st->log2cap);
+  int nid = -1;
+  while (lh.klen[sl] != LOOP_EMPTY) {
+    if (lh.key[sl] == h && lh.klen[sl] == len) { nid = lh.kid[sl]; break; }
+    sl = (sl + 1) & mask;
+  }
+  const int reused = nid >= 0;
+  if (!reused) {
+    nid = st->vcur++;
+    lh.key[sl] = h;
+    lh.klen[sl] = len;
+    lh.kid[sl] = nid;
+    lh.th[nid] = h;
+    lh.tp[nid] = lh.tp[a] * lh.tp[b];
+  }
+  int32_t* lg = lh.log + 4 * (int64_t)st->n_merges;
+  lg[0] = a; lg[1] = b; lg[2] = nid; lg[3] = reused;
+  st->n_merges += 1;
+  st->a = a; st->b = b; st->nid = nid; st->reused = reused; st->count = count;
+  st->parity ^= 1;
 }
 
 // ------------------------------------------------------------ word dedup --
@@ -836,7 +923,7 @@ extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_
   BEAST_REQUIRE(table && ws && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
   BEAST_REQUIRE(call >= 0, "beast_bpe_argmax: call index must be >= 0");
   hipLaunchKernelGGL(k_apply_argmax, dim3(vcur), dim3(256), 0, beast::as_stream(stream), const_cast<uint32_t*>(table),
-                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false);
+                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false, nullptr);
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -852,7 +939,8 @@ extern "C" int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, 
   // every row that can change must run: rows < vcur, and a / b / new_id
   const int rows = std::max(vcur, std::max(a, std::max(b, new_id)) + 1);
   hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, vcur,
-                     argws_view(ws, Vt), call & 1, 1, a, b, new_id, tlen, ix, index != nullptr, new_id_reused != 0);
+                     argws_view(ws, Vt), call & 1, 1, a, b, new_id, tlen, ix, index != nullptr, new_id_reused != 0,
+                     nullptr);
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -919,15 +1007,146 @@ extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* 
   // LDS-privatised deltas only for frequent pairs: a rare pair touches few words, and the
   // per-workgroup LDS clear / flush would dominate (global atomics then)
   if (lds <= 64 * 1024 && pair_count >= MERGE_LDS_MIN_COUNT)
-    hipLaunchKernelGGL(k_merge<true>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr);
+    hipLaunchKernelGGL(k_merge<1>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr);
   else
-    hipLaunchKernelGGL(k_merge<false>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr);
+    hipLaunchKernelGGL(k_merge<0>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr);
   BEAST_LAUNCHED("k_merge");
   return BEAST_OK;
 }
 
+
+// ---- device-driven loop: workspace = LoopState | hash table | token hashes | merge log
+static int loop_log2cap(int Vt) {
+  int l = 6;
+  while ((1 << l) < 2 * Vt) ++l;
+  return l;
+}
+
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct LoopLayout {
+  size_t st, key, klen, kid, th, tp, log, total;
+};
+
+static LoopLayout loop_layout(int Vt, int max_merges) {
+  const size_t cap = size_t(1) << loop_log2cap(Vt);
+  LoopLayout L;
+  size_t o = 0;
+  L.st = o;   o += al256(sizeof(LoopState));
+  L.key = o;  o += al256(cap * 8);
+  L.klen = o; o += al256(cap * 4);
+  L.kid = o;  o += al256(cap * 4);
+  L.th = o;   o += al256((size_t)Vt * 8);
+  L.tp = o;   o += al256((size_t)Vt * 8);
+  L.log = o;  o += al256((size_t)max_merges * 16);
+  L.total = o;
+  return L;
+}
+
+static LoopHash loop_hash_view(void* ws, int Vt, int max_merges) {
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  unsigned char* w = static_cast<unsigned char*>(ws);
+  LoopHash lh;
+  lh.key = reinterpret_cast<unsigned long long*>(w + L.key);
+  lh.klen = reinterpret_cast<uint32_t*>(w + L.klen);
+  lh.kid = reinterpret_cast<int32_t*>(w + L.kid);
+  lh.th = reinterpret_cast<unsigned long long*>(w + L.th);
+  lh.tp = reinterpret_cast<unsigned long long*>(w + L.tp);
+  lh.log = reinterpret_cast<int32_t*>(w + L.log);
+  return lh;
+}
+
+static __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, int n_tok, int log2cap,
+                            const unsigned long long* __restrict__ h0, const unsigned long long* __restrict__ p0,
+                            const uint32_t* __restrict__ tlen) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *st = init;
+  if (i >= n_tok) return;
+  const unsigned long long h = h0[i];
+  lh.th[i] = h;
+  lh.tp[i] = p0[i];
+  const uint64_t mask = (1ull << log2cap) - 1;
+  uint64_t sl = loop_slot(h, tlen[i], log2cap);
+  while (true) {   // the initial tokens are distinct strings
+    const uint32_t prev = atomicCAS(&lh.klen[sl], LOOP_EMPTY, tlen[i]);
+    if (prev == LOOP_EMPTY) { lh.key[sl] = h; lh.kid[sl] = i; break; }
+    sl = (sl + 1) & mask;
+  }
+}
+
+extern "C" size_t beast_bpe_loop_workspace_bytes(int Vt, int max_merges) {
+  return loop_layout(Vt, max_merges).total;
+}
+
+extern "C" int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_merges, int n_tokens, int vocab_size,
+                                   int min_frequency, int argmax_parity, const uint64_t* tok_hash,
+                                   const uint64_t* tok_pow, const uint32_t* tlen, void* stream) {
+  BEAST_REQUIRE(ws && tok_hash && tok_pow && tlen, "beast_bpe_loop_init: null pointer");
+  BEAST_REQUIRE(Vt >= 1 && Vt <= 32768 && n_tokens >= 0 && n_tokens <= Vt && max_merges >= 1,
+                "beast_bpe_loop_init: bad sizes");
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  BEAST_REQUIRE_CODE(ws_bytes >= L.total, BEAST_E_WORKSPACE, "loop workspace %zu < %zu", ws_bytes, L.total);
+  hipStream_t s = beast::as_stream(stream);
+  unsigned char* w = static_cast<unsigned char*>(ws);
+  BEAST_HIP(hipMemsetAsync(w + L.klen, 0xFF, L.kid - L.klen, s), "loop hash memset");
+  LoopState init{};
+  init.active = 1;
+  init.vcur = n_tokens;
+  init.parity = argmax_parity & 1;
+  init.target = vocab_size;
+  init.min_freq = min_frequency;
+  init.log2cap = loop_log2cap(Vt);
+  init.max_merges = max_merges;
+  const int n = n_tokens > 0 ? n_tokens : 1;
+  hipLaunchKernelGGL(k_loop_init, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<LoopState*>(w + L.st), init,
+                     loop_hash_view(ws, Vt, max_merges), n_tokens, init.log2cap,
+                     reinterpret_cast<const unsigned long long*>(tok_hash),
+                     reinterpret_cast<const unsigned long long*>(tok_pow), tlen);
+  BEAST_LAUNCHED("k_loop_init");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym,
+                                    const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
+                                    uint32_t* tlen, int max_token_length, int32_t* deltas, uint64_t* sig,
+                                    uint32_t* table, uint64_t* argws, int vocab_size, void* stream) {
+  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws, "beast_bpe_loop_steps: null pointer");
+  BEAST_REQUIRE(Vt >= 1 && Vt <= 32768 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_steps: bad sizes");
+  hipStream_t s = beast::as_stream(stream);
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  LoopState* st = reinterpret_cast<LoopState*>(static_cast<unsigned char*>(ws) + L.st);
+  const LoopHash lh = loop_hash_view(ws, Vt, max_merges);
+  const ArgWs aw = argws_view(argws, Vt);
+  const int grid = n_words > 0 ? grid_for(n_words, 256, 2048) : 0;
+  const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  BEAST_REQUIRE_CODE(lds <= 64 * 1024, BEAST_E_UNSUPPORTED, "device loop needs 4*Vt int32 of LDS (Vt <= 4096)");
+  unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
+  // every row that can change: ids < vocab_size (and < Vt)
+  const int rows = std::min(Vt, std::max(vocab_size, 1));
+  for (int i = 0; i < n_steps; ++i) {
+    hipLaunchKernelGGL(k_loop_step, dim3(1), dim3(64), 0, s, st, aw, Vt, lh, tlen);
+    BEAST_LAUNCHED("k_loop_step");
+    if (grid > 0) {
+      hipLaunchKernelGGL(k_merge<2>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, 0, 0, 0, tlen,
+                         max_token_length, deltas, Vt, sg, WordIndex{}, false, st);
+      BEAST_LAUNCHED("k_merge");
+    }
+    hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, s, table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen,
+                       WordIndex{}, false, false, st);
+    BEAST_LAUNCHED("k_apply_argmax");
+  }
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log) {
+  BEAST_REQUIRE(ws && state && log, "beast_bpe_loop_state: null pointer");
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  *state = static_cast<const unsigned char*>(ws) + L.st;
+  *log = static_cast<const unsigned char*>(ws) + L.log;
+  return BEAST_OK;
+}
 
 extern "C" size_t beast_bpe_dedup_workspace_bytes(int64_t n_words) {
   const uint64_t cap = dedup_cap(n_words > 0 ? n_words : 1);

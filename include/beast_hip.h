@@ -211,6 +211,27 @@ int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const
  * x, y < vcur (vcur counting new_id). */
 int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, int a, int b, int new_id,
                            uint32_t* tlen, void* index, int new_id_reused, uint64_t* ws, int call, void* stream);
+
+/* Device-driven merge loop: the next merge is decided on the GPU from the previous argmax
+ * (stop when vocab_size is reached, the count drops below min_frequency, or the log is full),
+ * its id by a (64-bit string hash, byte length) table of the vocabulary (HF's id reuse), and
+ * merge + apply_argmax read it from the loop record -- no host round trip per merge.
+ * tok_hash / tok_pow: per initial token, h = sum bytes[i] * P^(n-1-i) and P^n (mod 2^64) of its
+ * UTF-8 string, tlen its byte length (the same tlen array merge / apply_argmax maintain);
+ * argmax_parity: the `call & 1` of the beast_bpe_argmax that produced the first pair.
+ * beast_bpe_loop_steps enqueues n_steps (step, merge, apply_argmax) triples; steps after
+ * the loop stopped are no-ops.  beast_bpe_loop_state returns device pointers to the record
+ * {int32 active, a, b, nid, reused, vcur, parity, n_merges, ...} and the log
+ * [max_merges][4] int32 {a, b, nid, reused} for the host to read and verify. */
+size_t beast_bpe_loop_workspace_bytes(int Vt, int max_merges);
+int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_merges, int n_tokens, int vocab_size,
+                        int min_frequency, int argmax_parity, const uint64_t* tok_hash, const uint64_t* tok_pow,
+                        const uint32_t* tlen, void* stream);
+int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
+                         uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen, int max_token_length,
+                         int32_t* deltas, uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
+                         void* stream);
+int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),
