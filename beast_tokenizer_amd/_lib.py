@@ -23,6 +23,7 @@ BEAST_E_WORKSPACE = -4
 ABI_VERSION = 1
 OPT_GENERIC_KERNELS = 1
 OPT_BLOCK_WAVES = 2
+OPT_MERGE_LDS_MIN = 3
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 
@@ -67,7 +68,7 @@ SIGNATURES = {
     "beast_bpe_loop_workspace_bytes": (_sz, [_i32, _i32]),
     "beast_bpe_loop_init": (_i32, [_vp, _sz, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "beast_bpe_loop_steps": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp,
-                                    _i32, _vp]),
+                                    _vp, _i32, _vp]),
     "beast_bpe_loop_state": (_i32, [_vp, _i32, _i32, _vp, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),

@@ -209,7 +209,7 @@ class GpuBpeOps:
     LOOP_P = 0x9E3779B97F4A7C15   # odd multiplier of the token-string hash
 
     def loop_supported(self, Vt: int) -> bool:
-        return 4 * Vt * 4 <= 64 * 1024 and getattr(self, "_index", None) is None
+        return 4 * Vt * 4 <= 64 * 1024
 
     def loop_run(self, words, table, Vt: int, id2str, vocab_size: int, min_frequency: int, max_len: int,
                  chunk: int = 64):
@@ -244,7 +244,8 @@ class GpuBpeOps:
             _lib.run("beast_bpe_loop_steps", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
                      words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
                      words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
-                     _lib.ptr(words.get("sig")), table.data_ptr(), self._argws.data_ptr(), vocab_size, self.stream)
+                     _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)), table.data_ptr(),
+                     self._argws.data_ptr(), vocab_size, self.stream)
             host.copy_(state, non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
             active, vcur, n = int(host[0]), int(host[5]), int(host[7])

@@ -263,8 +263,114 @@ __host__ __device__ inline ArgWs argws_view(void* ws, int Vt) {
   return v;
 }
 
+// Device-driven merge loop (beast_bpe_loop_*): each k_merge decides its merge ON the GPU from
+// the previous argmax (workgroup 0 records the decision), the following k_apply_argmax applies
+// it and commits it (vocabulary hash, log, vcur, parity), so the host enqueues merges without a
+// round trip per merge.
+struct LoopState {
+  // loop state: written by k_apply_argmax's workgroup 0 (and init), read by k_merge
+  int32_t active;        // 0 once the loop has stopped (later launches are no-ops)
+  int32_t a, b, nid, reused;   // last committed merge
+  int32_t vcur;          // vocabulary size
+  int32_t parity;        // argmax slot holding the pair for the next merge
+  int32_t n_merges;      // merges logged
+  int32_t target;        // vocab_size
+  int32_t min_freq;
+  int32_t log2cap;       // token-string hash table
+  int32_t max_merges;    // log capacity
+  unsigned long long count;
+  // the step k_merge decided for the following k_apply_argmax (written by its workgroup 0)
+  int32_t r_active, r_a, r_b, r_nid, r_reused, r_vcur, r_parity;
+  uint32_t r_len;
+  unsigned long long r_count, r_h;
+};
+
+// ------------------------------------------------------- device merge loop --
+// Token strings are identified by (64-bit polynomial hash of their UTF-8 bytes, byte length):
+// h(xy) = h(x) * P^len(y) + h(y), so a merge's string is hashed from its parts.  The table maps
+// (h, len) -> id; equal strings always collide (HF reuses the id), different strings collide
+// with probability ~2^-64 -- the host re-checks every logged merge against the real strings
+// and reruns the loop on the host path if it ever finds one (beast_tokenizer_amd/bpe_train.py).
+constexpr uint32_t LOOP_EMPTY = 0xFFFFFFFFu;
+struct LoopHash {
+  unsigned long long* key;   // [cap] h
+  uint32_t* klen;            // [cap] byte length, LOOP_EMPTY = free slot
+  int32_t* kid;              // [cap]
+  unsigned long long* th;    // [Vt] token hash
+  unsigned long long* tp;    // [Vt] P^len
+  int32_t* log;              // [max_merges][4] a, b, nid, reused
+};
+
+__device__ __forceinline__ uint64_t loop_slot(unsigned long long h, uint32_t len, int log2cap) {
+  return ((h ^ ((unsigned long long)len * 0x9E3779B97F4A7C15ull)) * 0xbf58476d1ce4e5b9ull) >> (64 - log2cap);
+}
+
+struct LoopStep {
+  int active, a, b, nid, reused, vcur;
+  uint32_t len;
+  unsigned long long count, h;
+};
+
+// The merge after the previous argmax (read-only on the loop state: every k_merge workgroup
+// computes the same answer).  HF's loop: stop at vocab_size, below min_frequency or an empty
+// queue; the merged string's id is an existing one (HF id reuse) or the next free one.
+__device__ LoopStep loop_decide(const LoopState* __restrict__ st, ArgWs aw, int Vt, const LoopHash& lh,
+                                const uint32_t* __restrict__ tlen) {
+  LoopStep r{};
+  if (!st->active) return r;
+  const unsigned long long key = aw.slot[st->parity];
+  const unsigned long long count = key >> 32;
+  if (st->vcur >= st->target || count < 1 || count < (unsigned long long)st->min_freq ||
+      st->n_merges >= st->max_merges)
+    return r;
+  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
+  r.a = (int)(idx / (uint32_t)Vt);
+  r.b = (int)(idx % (uint32_t)Vt);
+  r.h = lh.th[r.a] * lh.tp[r.b] + lh.th[r.b];
+  r.len = tlen[r.a] + tlen[r.b];
+  const uint64_t mask = (1ull << st->log2cap) - 1;
+  uint64_t sl = loop_slot(r.h, r.len, st->log2cap);
+  r.nid = -1;
+  while (lh.klen[sl] != LOOP_EMPTY) {
+    if (lh.key[sl] == r.h && lh.klen[sl] == r.len) { r.nid = lh.kid[sl]; break; }
+    sl = (sl + 1) & mask;
+  }
+  r.reused = r.nid >= 0;
+  if (!r.reused) r.nid = st->vcur;
+  r.vcur = st->vcur + (r.reused ? 0 : 1);
+  r.count = count;
+  r.active = 1;
+  return r;
+}
+
+// k_apply_argmax's workgroup 0, after the apply: the decided merge becomes part of the
+// vocabulary (string hash -> id), the log and the loop state.
+__device__ void loop_commit(LoopState* __restrict__ st, const LoopHash& lh) {
+  const int a = st->r_a, b = st->r_b, nid = st->r_nid;
+  if (!st->r_reused) {
+    const uint64_t mask = (1ull << st->log2cap) - 1;
+    uint64_t sl = loop_slot(st->r_h, st->r_len, st->log2cap);
+    while (lh.klen[sl] != LOOP_EMPTY) sl = (sl + 1) & mask;
+    lh.key[sl] = st->r_h;
+    lh.klen[sl] = st->r_len;
+    lh.kid[sl] = nid;
+    lh.th[nid] = st->r_h;
+    lh.tp[nid] = lh.tp[a] * lh.tp[b];
+  }
+  int32_t* lg = lh.log + 4 * (int64_t)st->n_merges;
+  lg[0] = a; lg[1] = b; lg[2] = nid; lg[3] = st->r_reused;
+  st->n_merges += 1;
+  st->a = a; st->b = b; st->nid = nid; st->reused = st->r_reused; st->count = st->r_count;
+  st->vcur = st->r_vcur;
+  st->parity = st->r_parity ^ 1;
+}
+
 // ------------------------------------------------------------------ merge --
-__device__ __forceinline__ unsigned long long sig_bit(uint32_t x) { return 1ull << (x & 63u); }
+// Bloom signature bits of symbol x: two of 64 (k = 2 keeps false positives of a 2-symbol query
+// ~(2n/64)^4 for a word of n distinct symbols, vs (n/64)^2 with one bit)
+__device__ __forceinline__ unsigned long long sig_bit(uint32_t x) {
+  return (1ull << (x & 63u)) | (1ull << (((x * 0x9E3779B1u) >> 26) & 63u));
+}
 
 // Inverted index symbol -> distinct words that may contain it (HF's where_to_update, on
 // the GPU).  Built once from the distinct words; the merge creating token `new` appends
@@ -275,22 +381,14 @@ __device__ __forceinline__ unsigned long long sig_bit(uint32_t x) { return 1ull 
 constexpr uint32_t IDX_INEXACT = 0xFFFFFFFFu;
 constexpr int64_t MERGE_LDS_MIN_COUNT = 1 << 16;
 
-// Device-driven merge loop (beast_bpe_loop_*): the merge picked by the previous argmax is
-// decided ON the GPU by k_loop_step and handed to k_merge / k_apply_argmax through this record,
-// so the host enqueues merges without a round trip per merge.
-struct LoopState {
-  int32_t active;        // 0 once the loop has stopped (later launches are no-ops)
-  int32_t a, b, nid, reused;
-  int32_t vcur;          // vocabulary size after this step's merge
-  int32_t parity;        // argmax result slot the next k_apply_argmax writes
-  int32_t n_merges;      // merges logged
-  int32_t target;        // vocab_size
-  int32_t min_freq;
-  int32_t log2cap;       // token-string hash table
-  int32_t max_merges;    // log capacity
-  unsigned long long count;
-};
+
+#ifdef BPE_MERGE_STATS
+// tools only: [0] Bloom candidates, [1] words holding the pair, [2] their symbols, [3] symbols probed
+__device__ unsigned long long g_merge_stats[4];
+#endif
 constexpr int MERGE_UNROLL = 4;
+constexpr int MERGE_SCAN = 8;       // signature loads in flight per thread (two-phase scan)
+constexpr int MERGE_CLIST = 2048;   // LDS candidate list per workgroup
 struct WordIndex {
   uint32_t* start;   // [Vt]
   uint32_t* len;     // [Vt]
@@ -377,14 +475,39 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
                                                int64_t nw, int a, int b, int nid, uint32_t* __restrict__ tlen,
                                                int max_len, int32_t* __restrict__ deltas, int Vt,
                                                unsigned long long* __restrict__ sig, WordIndex ix, bool use_ix,
-                                               const LoopState* __restrict__ loop) {
+                                               LoopState* __restrict__ loop, long long lds_min, ArgWs aw,
+                                               LoopHash lh) {
   extern __shared__ __attribute__((aligned(16))) int32_t dl[];
   __shared__ int touched;
+  __shared__ LoopStep dec;
   bool LDS = (MODE == 1);
+  // first signature batch of the two-phase scan: issued before the merge is known (MODE 2
+  // decides it below; the loads overlap the decision's dependent reads)
+  unsigned long long sgv[MERGE_SCAN];
+  const bool two_phase = !use_ix && sig != nullptr;
+  const int64_t nchunks = (nw + 255) / 256;
+  if (two_phase) {
+#pragma unroll
+    for (int u = 0; u < MERGE_SCAN; ++u) {
+      const int64_t w = (blockIdx.x + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+      sgv[u] = w < nw ? sig[w] : 0ull;
+    }
+  }
   if (MODE == 2) {
-    if (!loop->active) return;
-    a = loop->a; b = loop->b; nid = loop->nid;
-    LDS = loop->count >= (unsigned long long)MERGE_LDS_MIN_COUNT;
+    if (threadIdx.x == 0) {
+      dec = loop_decide(loop, aw, Vt, lh, tlen);
+      if (blockIdx.x == 0) {   // the record k_apply_argmax applies and commits
+        loop->r_active = dec.active;
+        loop->r_a = dec.a; loop->r_b = dec.b; loop->r_nid = dec.nid; loop->r_reused = dec.reused;
+        loop->r_vcur = dec.vcur; loop->r_parity = loop->parity; loop->r_len = dec.len;
+        loop->r_count = dec.count; loop->r_h = dec.h;
+        if (!dec.active) loop->active = 0;
+      }
+    }
+    __syncthreads();
+    if (!dec.active) return;
+    a = dec.a; b = dec.b; nid = dec.nid;
+    LDS = dec.count >= (unsigned long long)lds_min;
   }
   const uint32_t* cand = nullptr;
   int64_t ncand = nw;
@@ -413,6 +536,99 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   int32_t* rowN = dv + 3 * Vt;
   bool any = false;
   const unsigned long long need = sig_bit(a) | sig_bit(b);
+  auto merge_word = [&](int64_t w) {
+    const uint32_t L = wlen[w];
+    if (L < 2) return;
+#ifdef BPE_MERGE_STATS
+    atomicAdd(&g_merge_stats[3], (unsigned long long)L);
+#endif
+    uint16_t* s = sym + wstart[w];
+    bool hit = false;
+    uint32_t prev = s[0];
+#pragma unroll 8
+    for (uint32_t k = 1; k < L; ++k) {
+      const uint32_t cur = s[k];
+      hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
+      prev = cur;
+    }
+    if (!hit) return;
+    any = true;
+#ifdef BPE_MERGE_STATS
+    atomicAdd(&g_merge_stats[1], 1ull);
+    atomicAdd(&g_merge_stats[2], (unsigned long long)L);
+#endif
+    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+    uint32_t r = 0, o = 0;
+    while (r < L) {
+      const int x = s[r];
+      if (x == a && r + 1 < L && s[r + 1] == b) {
+        if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
+          const int p = s[o - 1];
+          atomicAdd(&colA[p], -cnt);
+          if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
+        }
+        if (r + 2 < L) {                       // HF: ((b, next), -1), ((new, next), +1)
+          const int nx = s[r + 2];
+          atomicAdd(&rowB[nx], -cnt);
+          if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
+        }
+        s[o++] = (uint16_t)nid;
+        r += 2;
+      } else {
+        s[o++] = (uint16_t)x;
+        r += 1;
+      }
+    }
+    wlen[w] = o;
+    if (sig != nullptr) {
+      unsigned long long g = 0;
+      for (uint32_t k = 0; k < o; ++k) g |= sig_bit(s[k]);
+      sig[w] = g;
+    }
+    if (use_ix) {   // w now holds `new`: it goes on new's list
+      const uint32_t pos = atomicAdd(&ix.ctl[0], 1u);
+      if (pos < ix.ctl[2]) ix.pool[pos] = (uint32_t)w;
+    }
+  };
+  if (cand == nullptr && two_phase) {
+    // Two phases per workgroup over its contiguous range of words: (1) every thread issues all
+    // its signature loads at once and pushes the words that pass the Bloom test onto an LDS
+    // list; (2) the workgroup's threads take the listed words in parallel, so the dependent
+    // wlen -> wstart -> symbols chains of the few candidates overlap instead of trailing the
+    // scan of one thread.
+    // Words are stored in length order, so the candidates (long words fail the Bloom test
+    // more often) concentrate at the end: workgroups take 256-word chunks round-robin.
+    __shared__ uint32_t clist[MERGE_CLIST];
+    __shared__ int cn;
+    if (threadIdx.x == 0) cn = 0;
+    __syncthreads();
+    // phase 1 over every chunk of this workgroup: only LDS appends between the load rounds
+    for (int64_t c0 = blockIdx.x; c0 < nchunks; c0 += (int64_t)MERGE_SCAN * gridDim.x) {
+      if (c0 != blockIdx.x) {
+#pragma unroll
+        for (int u = 0; u < MERGE_SCAN; ++u) {
+          const int64_t w = (c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+          sgv[u] = w < nw ? sig[w] : 0ull;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < MERGE_SCAN; ++u) {
+        if ((sgv[u] & need) == need) {
+          const int64_t w = (c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+          const int slot = atomicAdd(&cn, 1);
+          if (slot < MERGE_CLIST) clist[slot] = (uint32_t)w;
+          else merge_word(w);            // list full: this thread handles it itself
+        }
+      }
+    }
+    __syncthreads();
+    // phase 2: the listed candidates, one per thread
+    const int n = min(cn, MERGE_CLIST);
+#ifdef BPE_MERGE_STATS
+    if (threadIdx.x == 0) atomicAdd(&g_merge_stats[0], (unsigned long long)cn);
+#endif
+    for (int k = threadIdx.x; k < n; k += blockDim.x) merge_word(clist[k]);
+  } else {
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < ncand; i0 += MERGE_UNROLL * G) {
    // MERGE_UNROLL candidates per pass: their signature loads are all in flight together
@@ -481,6 +697,7 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
     }
    }
   }
+  }
   if (LDS) {
     if (any) touched = 1;
     __syncthreads();
@@ -501,14 +718,15 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
 __global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ table, int32_t* __restrict__ deltas,
                                                       int Vt, int vcur, ArgWs aw, int parity, int apply, int a, int b,
                                                       int nid, uint32_t* __restrict__ tlen, WordIndex ix, bool use_ix,
-                                                      bool reused, const LoopState* __restrict__ loop) {
+                                                      bool reused, LoopState* __restrict__ loop, LoopHash lh) {
   __shared__ unsigned long long sh[4];
   __shared__ int changed;
   const int x = blockIdx.x;
-  if (loop != nullptr) {   // device-driven loop: this step's merge from the record
-    if (!loop->active) return;
-    vcur = loop->vcur; parity = loop->parity; a = loop->a; b = loop->b; nid = loop->nid;
-    reused = loop->reused != 0;
+  if (loop != nullptr) {   // device-driven loop: the merge k_merge decided (record r_*)
+    if (!loop->r_active) return;
+    vcur = loop->r_vcur; parity = loop->r_parity ^ 1; a = loop->r_a; b = loop->r_b; nid = loop->r_nid;
+    reused = loop->r_reused != 0;
+    if (x == 0 && threadIdx.x == 0) loop_commit(loop, lh);   // no other workgroup reads what it writes
   }
   uint32_t* row = table + (size_t)x * Vt;
   if (x == 0 && threadIdx.x == 0) aw.slot[parity ^ 1] = 0ull;
@@ -584,63 +802,6 @@ __global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ tab
     unsigned long long* slot = aw.slot + parity;
     if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
   }
-}
-
-// ------------------------------------------------------- device merge loop --
-// Token strings are identified by (64-bit polynomial hash of their UTF-8 bytes, byte length):
-// h(xy) = h(x) * P^len(y) + h(y), so a merge's string is hashed from its parts.  The table maps
-// (h, len) -> id; equal strings always collide (HF reuses the id), different strings collide
-// with probability ~2^-64 -- the host re-checks every logged merge against the real strings
-// and reruns the loop on the host path if it ever finds one (beast_tokenizer_amd/bpe_train.py).
-constexpr uint32_t LOOP_EMPTY = 0xFFFFFFFFu;
-struct LoopHash {
-  unsigned long long* key;   // [cap] h
-  uint32_t* klen;            // [cap] byte length, LOOP_EMPTY = free slot
-  int32_t* kid;              // [cap]
-  unsigned long long* th;    // [Vt] token hash
-  unsigned long long* tp;    // [Vt] P^len
-  int32_t* log;              // [max_merges][4] a, b, nid, reused
-};
-
-__device__ __forceinline__ uint64_t loop_slot(unsigned long long h, uint32_t len, int log2cap) {
-  return ((h ^ ((unsigned long long)len * 0x9E3779B97F4A7C15ull)) * 0xbf58476d1ce4e5b9ull) >> (64 - log2cap);
-}
-
-__global__ void k_loop_step(LoopState* __restrict__ st, ArgWs aw, int Vt, LoopHash lh,
-                            const uint32_t* __restrict__ tlen) {
-  if (threadIdx.x != 0 || !st->active) return;
-  const unsigned long long key = aw.slot[st->parity];
-  const unsigned long long count = key >> 32;
-  if (st->vcur >= st->target || count < 1 || count < (unsigned long long)st->min_freq ||
-      st->n_merges >= st->max_merges) {
-    st->active = 0;
-    return;
-  }
-  const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull);
-  const int a = (int)(idx / (uint32_t)Vt), b = (int)(idx % (uint32_t)Vt);
-  const unsigned long long h = lh.th[a] * lh.tp[b] + lh.th[b];
-  const uint32_t len = tlen[a] + tlen[b];
-  const uint64_t mask = (1ull << st->log2cap) - 1;
-  uint64_t sl = loop_slot(h, len, st->log2cap);
-  int nid = -1;
-  while (lh.klen[sl] != LOOP_EMPTY) {
-    if (lh.key[sl] == h && lh.klen[sl] == len) { nid = lh.kid[sl]; break; }
-    sl = (sl + 1) & mask;
-  }
-  const int reused = nid >= 0;
-  if (!reused) {
-    nid = st->vcur++;
-    lh.key[sl] = h;
-    lh.klen[sl] = len;
-    lh.kid[sl] = nid;
-    lh.th[nid] = h;
-    lh.tp[nid] = lh.tp[a] * lh.tp[b];
-  }
-  int32_t* lg = lh.log + 4 * (int64_t)st->n_merges;
-  lg[0] = a; lg[1] = b; lg[2] = nid; lg[3] = reused;
-  st->n_merges += 1;
-  st->a = a; st->b = b; st->nid = nid; st->reused = reused; st->count = count;
-  st->parity ^= 1;
 }
 
 // ------------------------------------------------------------ word dedup --
@@ -842,6 +1003,24 @@ int grid_for(int64_t n, int per_block, int cap) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(g, cap));
 }
 
+// k_merge's grid: the workgroups the device holds at once (one pass over the words, each
+// workgroup its contiguous range, MERGE_SCAN signature loads in flight per thread), not more
+template <int MODE>
+int merge_grid(int64_t nw, size_t lds) {
+  static int resident[2] = {0, 0};   // [lds != 0]
+  int& r = resident[lds != 0];
+  if (r == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_merge<MODE>, 256, lds) != hipSuccess || per <= 0)
+      per = 4;
+    r = cus * per;
+  }
+  return grid_for(nw, MERGE_SCAN * 256, r);
+}
+
 }  // namespace
 
 // =================================================================== C-ABI ==
@@ -923,7 +1102,8 @@ extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_
   BEAST_REQUIRE(table && ws && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
   BEAST_REQUIRE(call >= 0, "beast_bpe_argmax: call index must be >= 0");
   hipLaunchKernelGGL(k_apply_argmax, dim3(vcur), dim3(256), 0, beast::as_stream(stream), const_cast<uint32_t*>(table),
-                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false, nullptr);
+                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false, nullptr,
+                     LoopHash{});
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -940,7 +1120,7 @@ extern "C" int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, 
   const int rows = std::max(vcur, std::max(a, std::max(b, new_id)) + 1);
   hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, vcur,
                      argws_view(ws, Vt), call & 1, 1, a, b, new_id, tlen, ix, index != nullptr, new_id_reused != 0,
-                     nullptr);
+                     nullptr, LoopHash{});
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -1000,18 +1180,21 @@ extern "C" int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* 
                 "beast_bpe_merge: ids out of range (a=%d b=%d new=%d Vt=%d)", a, b, new_id, Vt);
   if (n_words <= 0) return BEAST_OK;
   hipStream_t s = beast::as_stream(stream);
-  const int grid = grid_for(n_words, 256, 2048);
   const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  const bool use_lds = lds <= 64 * 1024 && pair_count >= beast::g_merge_lds_min;
+  const int grid = use_lds ? merge_grid<1>(n_words, lds) : merge_grid<0>(n_words, 0);
   unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
   const WordIndex ix = index ? index_view(index, Vt) : WordIndex{};
   // LDS-privatised deltas only for frequent pairs: a rare pair touches few words, and the
   // per-workgroup LDS clear / flush would dominate (global atomics then)
-  if (lds <= 64 * 1024 && pair_count >= MERGE_LDS_MIN_COUNT)
+  if (use_lds)
     hipLaunchKernelGGL(k_merge<1>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr, 0ll,
+                       ArgWs{}, LoopHash{});
   else
     hipLaunchKernelGGL(k_merge<0>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, a, b, new_id,
-                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr);
+                       const_cast<uint32_t*>(tlen), max_token_length, deltas, Vt, sg, ix, index != nullptr, nullptr, 0ll,
+                       ArgWs{}, LoopHash{});
   BEAST_LAUNCHED("k_merge");
   return BEAST_OK;
 }
@@ -1076,6 +1259,12 @@ static __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, i
   }
 }
 
+#ifdef BPE_MERGE_STATS
+extern "C" int beast_debug_merge_stats(unsigned long long* host4) {
+  return hipMemcpyFromSymbol(host4, HIP_SYMBOL(g_merge_stats), sizeof(g_merge_stats)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 extern "C" size_t beast_bpe_loop_workspace_bytes(int Vt, int max_merges) {
   return loop_layout(Vt, max_merges).total;
 }
@@ -1111,7 +1300,7 @@ extern "C" int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_me
 extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym,
                                     const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
                                     uint32_t* tlen, int max_token_length, int32_t* deltas, uint64_t* sig,
-                                    uint32_t* table, uint64_t* argws, int vocab_size, void* stream) {
+                                    void* index, uint32_t* table, uint64_t* argws, int vocab_size, void* stream) {
   BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws, "beast_bpe_loop_steps: null pointer");
   BEAST_REQUIRE(Vt >= 1 && Vt <= 32768 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_steps: bad sizes");
   hipStream_t s = beast::as_stream(stream);
@@ -1119,22 +1308,20 @@ extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_step
   LoopState* st = reinterpret_cast<LoopState*>(static_cast<unsigned char*>(ws) + L.st);
   const LoopHash lh = loop_hash_view(ws, Vt, max_merges);
   const ArgWs aw = argws_view(argws, Vt);
-  const int grid = n_words > 0 ? grid_for(n_words, 256, 2048) : 0;
   const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
   BEAST_REQUIRE_CODE(lds <= 64 * 1024, BEAST_E_UNSUPPORTED, "device loop needs 4*Vt int32 of LDS (Vt <= 4096)");
+  const int grid = merge_grid<2>(n_words > 0 ? n_words : 1, lds);
   unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
+  const WordIndex ix = index ? index_view(index, Vt) : WordIndex{};
   // every row that can change: ids < vocab_size (and < Vt)
   const int rows = std::min(Vt, std::max(vocab_size, 1));
-  for (int i = 0; i < n_steps; ++i) {
-    hipLaunchKernelGGL(k_loop_step, dim3(1), dim3(64), 0, s, st, aw, Vt, lh, tlen);
-    BEAST_LAUNCHED("k_loop_step");
-    if (grid > 0) {
-      hipLaunchKernelGGL(k_merge<2>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, 0, 0, 0, tlen,
-                         max_token_length, deltas, Vt, sg, WordIndex{}, false, st);
-      BEAST_LAUNCHED("k_merge");
-    }
+  for (int i = 0; i < n_steps; ++i) {   // k_merge decides the merge (even with no words left)
+    hipLaunchKernelGGL(k_merge<2>, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, 0, 0, 0, tlen,
+                       max_token_length, deltas, Vt, sg, ix, index != nullptr, st, (long long)beast::g_merge_lds_min,
+                       aw, lh);
+    BEAST_LAUNCHED("k_merge");
     hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, s, table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen,
-                       WordIndex{}, false, false, st);
+                       ix, index != nullptr, false, st, lh);
     BEAST_LAUNCHED("k_apply_argmax");
   }
   return BEAST_OK;

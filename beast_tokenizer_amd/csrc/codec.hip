@@ -1033,6 +1033,11 @@ extern "C" int beast_set_option(int option, int value) {
     g_block_waves = value;
     return BEAST_OK;
   }
+  if (option == BEAST_OPT_MERGE_LDS_MIN) {
+    BEAST_REQUIRE(value >= 0, "BEAST_OPT_MERGE_LDS_MIN: %d < 0", value);
+    beast::g_merge_lds_min = value;
+    return BEAST_OK;
+  }
   BEAST_REQUIRE(false, "unknown option %d", option);
   return BEAST_E_INVALID;
 }

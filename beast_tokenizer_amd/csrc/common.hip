@@ -6,6 +6,7 @@
 namespace beast {
 
 static thread_local char g_err[512] = "";
+int64_t g_merge_lds_min = int64_t(1) << 16;
 
 void set_error(const char* fmt, ...) {
   va_list ap;

@@ -330,11 +330,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    # BEAST_BENCH_ONE_DEVICE=1 + BEAST_BENCH_BACKEND=gloo: rehearse the multi-rank path with all
+    # ranks on one GPU (tests only; the driver's runs use one GPU per rank over RCCL)
+    dev = torch.device("cuda", 0 if os.environ.get("BEAST_BENCH_ONE_DEVICE") == "1" else local)
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("BEAST_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from beast_tokenizer_amd.bpe_train import no_reduce, torch_dist_reducer
     reduce = torch_dist_reducer() if world > 1 else no_reduce
 

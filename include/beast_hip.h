@@ -47,9 +47,12 @@ const char* beast_last_error(void);
  * exists (the BEAST defaults T = 50, N = 10, D = 7 / 14); results are identical.
  * BEAST_OPT_BLOCK_WAVES = 4 or 7 forces the workgroup width of the specialised 14-DoF
  * kernels (0 = chosen by batch size); results are identical.
+ * BEAST_OPT_MERGE_LDS_MIN = n: BPE merges of pairs counted >= n privatise their pair-count deltas
+ * in LDS (default 65536; below, global atomics); results are identical.
  * Not thread-safe with concurrent launches. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
+#define BEAST_OPT_MERGE_LDS_MIN 3
 int beast_set_option(int option, int value);
 
 /* ---------------------------------------------------------------- H1/H2 ---
@@ -219,7 +222,8 @@ int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, i
  * tok_hash / tok_pow: per initial token, h = sum bytes[i] * P^(n-1-i) and P^n (mod 2^64) of its
  * UTF-8 string, tlen its byte length (the same tlen array merge / apply_argmax maintain);
  * argmax_parity: the `call & 1` of the beast_bpe_argmax that produced the first pair.
- * beast_bpe_loop_steps enqueues n_steps (step, merge, apply_argmax) triples; steps after
+ * beast_bpe_loop_steps enqueues n_steps (step, merge, apply_argmax) triples (index: see
+ * beast_bpe_build_index, nullable); steps after
  * the loop stopped are no-ops.  beast_bpe_loop_state returns device pointers to the record
  * {int32 active, a, b, nid, reused, vcur, parity, n_merges, ...} and the log
  * [max_merges][4] int32 {a, b, nid, reused} for the host to read and verify. */
@@ -229,8 +233,8 @@ int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_merges, int n
                         const uint32_t* tlen, void* stream);
 int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
                          uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen, int max_token_length,
-                         int32_t* deltas, uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
-                         void* stream);
+                         int32_t* deltas, uint64_t* sig, void* index, uint32_t* table, uint64_t* argws,
+                         int vocab_size, void* stream);
 int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge

@@ -13,7 +13,11 @@ from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe  # noq
 from beast_tokenizer_amd.synthetic import synth_trajectories  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 500000
-ce = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+ce = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+ix = bool(int(sys.argv[3])) if len(sys.argv) > 3 else False
+if len(sys.argv) > 4:   # BEAST_OPT_MERGE_LDS_MIN
+    from beast_tokenizer_amd import _lib
+    _lib.load().beast_set_option(_lib.OPT_MERGE_LDS_MIN, int(sys.argv[4]))
 dev = torch.device("cuda", 0)
 tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
 fit = [{"actions": torch.from_numpy(synth_trajectories(4096, 50, 14, seed=1, start=4096 * i))} for i in range(2)]
@@ -27,7 +31,7 @@ torch.cuda.synchronize()
 for rep in range(2):
     t0 = time.perf_counter()
     flat, off = fixed_rows_to_device(allrows)
-    res = train_bpe(flat, off, 2048, compact_every=ce)
+    res = train_bpe(flat, off, 2048, compact_every=ce, use_index=ix)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(json.dumps({"rep": rep, "seconds": el, "merges_per_s": res.stats["n_merges"] / el, **res.stats}))
