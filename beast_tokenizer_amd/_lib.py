@@ -56,7 +56,7 @@ SIGNATURES = {
     "beast_scan_workspace_bytes": (_sz, [_i64]),
     "beast_exclusive_scan_i64": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "beast_bpe_pretok_emit": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "beast_bpe_count_pairs": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp]),
+    "beast_bpe_count_pairs": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp]),
     "beast_bpe_argmax_workspace_bytes": (_sz, [_i32]),
     "beast_bpe_argmax": (_i32, [_vp, _i32, _i32, _vp, _i32, _vp]),
     "beast_bpe_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i64,

@@ -167,11 +167,11 @@ class GpuBpeOps:
                      out["wlen"].data_ptr(), m, out["sig"].data_ptr(), self.stream)
         return out
 
-    def count_pairs(self, words, Vt: int) -> torch.Tensor:
+    def count_pairs(self, words, Vt: int, n_sym: int = 0) -> torch.Tensor:
         table = torch.zeros(Vt * Vt, dtype=torch.int32, device=self.device)
         _lib.run("beast_bpe_count_pairs", words["sym"].data_ptr(), words["wstart"].data_ptr(),
                  words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")), words["n_words"], table.data_ptr(), Vt,
-                 self.stream)
+                 n_sym or Vt, self.stream)
         return table
 
     def build_index(self, words, Vt: int):
@@ -329,7 +329,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     n_words, n_syms = words["n_words"], words["n_syms"]
     if hasattr(ops, "dedup"):
         words = ops.dedup(words)
-    table = ops.count_pairs(words, Vt)
+    table = ops.count_pairs(words, Vt, len(id2str))
     reduce(table, "sum")
     tlen = np.zeros(Vt, dtype=np.int64)
     for i, s in enumerate(id2str):

@@ -244,6 +244,45 @@ __global__ void k_count_pairs(const uint16_t* __restrict__ sym, const uint32_t* 
   }
 }
 
+// The same count with the table privatised in LDS: rows [r0, r0 + R) of the n_sym x n_sym
+// block of the symbols present at setup (R * n_sym u32 <= 160 KiB), one row group per grid y.
+// The workgroup takes 256-word chunks round-robin (words are stored in length order), counts
+// its pairs with LDS atomics and flushes row segments to the table with contiguous global
+// atomics: device-scope atomics execute at the memory side, so one per (pair, occurrence)
+// was the bottleneck of k_count_pairs.
+__global__ __launch_bounds__(256) void k_count_pairs_lds(const uint16_t* __restrict__ sym,
+                                                         const uint32_t* __restrict__ wstart,
+                                                         const uint32_t* __restrict__ wlen,
+                                                         const uint32_t* __restrict__ wcount, int64_t nw,
+                                                         uint32_t* __restrict__ table, int Vt, int n_sym, int R) {
+  extern __shared__ uint32_t hs[];   // [R][n_sym]
+  const int r0 = blockIdx.y * R;
+  const int rr = min(R, n_sym - r0);
+  for (int i = threadIdx.x; i < rr * n_sym; i += blockDim.x) hs[i] = 0;
+  __syncthreads();
+  const int64_t nchunks = (nw + 255) / 256;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t w = c * 256 + threadIdx.x;
+    if (w >= nw) continue;
+    const uint32_t L = wlen[w];
+    if (L < 2) continue;
+    const uint32_t cnt = wcount ? wcount[w] : 1u;
+    const uint16_t* s = sym + wstart[w];
+    uint32_t prev = s[0];
+    for (uint32_t i = 1; i < L; ++i) {
+      const uint32_t cur = s[i];
+      const int p = (int)prev - r0;
+      if (p >= 0 && p < rr && cur < (uint32_t)n_sym) atomicAdd(&hs[p * n_sym + cur], cnt);   // ids < n_sym
+      prev = cur;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < rr * n_sym; i += blockDim.x) {
+    const uint32_t v = hs[i];
+    if (v) atomicAdd(&table[(size_t)(r0 + i / n_sym) * Vt + (i % n_sym)], v);
+  }
+}
+
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 
 // Incremental argmax.  ws layout (u64): [2 + parity] result slots, [4, 4+Vt) the best key of
@@ -1087,10 +1126,33 @@ extern "C" int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off,
 }
 
 extern "C" int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
-                                     const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream) {
+                                     const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, int n_sym,
+                                     void* stream) {
   BEAST_REQUIRE(sym && wstart && wlen && table && Vt >= 1 && Vt <= 65535, "beast_bpe_count_pairs: bad args");
+  BEAST_REQUIRE(n_sym >= 0 && n_sym <= Vt, "beast_bpe_count_pairs: n_sym %d not in [0, Vt]", n_sym);
   if (n_words <= 0) return BEAST_OK;
-  hipLaunchKernelGGL(k_count_pairs, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, beast::as_stream(stream), sym,
+  hipStream_t s = beast::as_stream(stream);
+  const size_t budget = 160 * 1024;
+  const int R = n_sym > 0 ? (int)std::min<size_t>((size_t)n_sym, budget / (4 * (size_t)n_sym)) : 0;
+  const int groups = R > 0 ? (n_sym + R - 1) / R : 0;
+  if (R > 0 && groups <= 16) {   // LDS-privatised (the words are read once per row group)
+    const size_t lds = (size_t)R * n_sym * 4;
+    if (lds > 65536)
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_count_pairs_lds),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                "hipFuncSetAttribute(k_count_pairs_lds)");
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int per_cu = std::max(1, (int)(budget / std::max<size_t>(lds, 1)));
+    const int gx = std::max(1, std::min<int>(cus * per_cu / groups, (int)((n_words + 255) / 256)));
+    hipLaunchKernelGGL(k_count_pairs_lds, dim3(gx, groups), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words,
+                       table, Vt, n_sym, R);
+    BEAST_LAUNCHED("k_count_pairs_lds");
+    return BEAST_OK;
+  }
+  hipLaunchKernelGGL(k_count_pairs, dim3(grid_for(n_words, 256, 8192)), dim3(256), 0, s, sym,
                      wstart, wlen, wcount, n_words, table, Vt);
   BEAST_LAUNCHED("k_count_pairs");
   return BEAST_OK;

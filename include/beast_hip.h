@@ -174,9 +174,11 @@ int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off, int64_t n_
                           const uint8_t* cls_lut, int64_t lut_n, const int64_t* word_off,
                           const int64_t* sym_off, const uint16_t* byte2id, uint16_t* sym,
                           uint32_t* wstart, uint32_t* wlen, void* stream);
-/* pair table [Vt][Vt] uint32 += word count for each adjacent pair (BpeTrainer::count_pairs). */
+/* pair table [Vt][Vt] uint32 += word count for each adjacent pair (BpeTrainer::count_pairs).
+ * n_sym: every symbol id is < n_sym (the setup vocabulary); small n_sym count in LDS. */
 int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
-                          const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, void* stream);
+                          const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, int n_sym,
+                          void* stream);
 /* max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)) (0 if the table is empty)
  * into ws[2 + (call & 1)], where call = 0, 1, 2, ... numbers the calls on this workspace
  * (each call zeroes the other slot for the next one: no memset per call).  Incremental:

@@ -54,7 +54,7 @@ class NumpyBpeOps:
         return dict(words, words=[words["words"][i] for i in keep], counts=[words["counts"][i] for i in keep],
                     n_words=len(keep))
 
-    def count_pairs(self, words, Vt):
+    def count_pairs(self, words, Vt, n_sym=0):
         table = np.zeros(Vt * Vt, dtype=np.int64)
         for w, n in zip(words["words"], words["counts"]):
             for x, y in zip(w, w[1:]):
