@@ -754,44 +754,73 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
 // own adds (the only deltas that can reach (a, b) are row a's, when a == b), tlen[new] set.
 // A row rescans only if it changed (or was never scanned); then each workgroup folds its
 // row's best into the result slot.
-__global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ table, int32_t* __restrict__ deltas,
-                                                      int Vt, int vcur, ArgWs aw, int parity, int apply, int a, int b,
-                                                      int nid, uint32_t* __restrict__ tlen, WordIndex ix, bool use_ix,
-                                                      bool reused, LoopState* __restrict__ loop, LoopHash lh) {
-  __shared__ unsigned long long sh[4];
-  __shared__ int changed;
-  const int x = blockIdx.x;
+__device__ __forceinline__ void wave_fence_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per row x, four rows per workgroup (the apply touches only entries of rows it
+// owns: (x, a) and (x, new) for every x, rows b and new entirely).  When `apply`:
+// table += deltas for row x, deltas consumed are zeroed, row a's (a, b) is retired after its
+// own adds (the only deltas that can reach (a, b) are row a's, when a == b), tlen[new] set.
+// A row rescans only if it changed (or was never scanned); the workgroup folds its rows'
+// bests and makes one atomicMax into the result slot.
+constexpr int APPLY_ROWS = 4;   // rows (waves) per workgroup
+__global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_argmax(uint32_t* __restrict__ table,
+                                                                 int32_t* __restrict__ deltas, int Vt, int vcur,
+                                                                 ArgWs aw, int parity, int apply, int a, int b,
+                                                                 int nid, uint32_t* __restrict__ tlen, WordIndex ix,
+                                                                 bool use_ix, bool reused,
+                                                                 LoopState* __restrict__ loop, LoopHash lh, int nrows) {
+  __shared__ unsigned long long wbest[APPLY_ROWS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (loop != nullptr) {   // device-driven loop: the merge k_merge decided (record r_*)
     if (!loop->r_active) return;
     vcur = loop->r_vcur; parity = loop->r_parity ^ 1; a = loop->r_a; b = loop->r_b; nid = loop->r_nid;
     reused = loop->r_reused != 0;
-    if (x == 0 && threadIdx.x == 0) loop_commit(loop, lh);   // no other workgroup reads what it writes
+    if (blockIdx.x == 0 && threadIdx.x == 0) loop_commit(loop, lh);   // no other workgroup reads what it writes
   }
-  uint32_t* row = table + (size_t)x * Vt;
-  if (x == 0 && threadIdx.x == 0) aw.slot[parity ^ 1] = 0ull;
-  if (threadIdx.x == 0) changed = 0;
-  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) aw.slot[parity ^ 1] = 0ull;
+  const int x0 = blockIdx.x * APPLY_ROWS;
+  const int x = x0 + wave;
+  __shared__ int changed_w[APPLY_ROWS];
+  unsigned long long best = 0;
+  int changed = 0;
   if (apply) {
-    if (threadIdx.x == 0) {
+    // (1) each wave's single entries (x, a) and (x, new)
+    if (lane == 0 && x < nrows) {
+      uint32_t* row = table + (size_t)x * Vt;
       int32_t v;
       if ((v = deltas[x])) { row[a] += (uint32_t)v; deltas[x] = 0; changed = 1; }
       if ((v = deltas[Vt + x])) { row[nid] += (uint32_t)v; deltas[Vt + x] = 0; changed = 1; }
     }
-    __syncthreads();   // row[a] / row[nid] before the row-wide adds below (x == b or x == nid)
-    if (x == b || x == nid) {
-      int any = 0;
-      for (int y = threadIdx.x; y < Vt; y += 256) {
-        int32_t v;
-        if (x == b && (v = deltas[2 * Vt + y])) { row[y] += (uint32_t)v; deltas[2 * Vt + y] = 0; any = 1; }
-        if (x == nid && (v = deltas[3 * Vt + y])) { row[y] += (uint32_t)v; deltas[3 * Vt + y] = 0; any = 1; }
-      }
-      if (any) changed = 1;
-    }
+    if (lane == 0) changed_w[wave] = changed;
+    // (2) rows b and new entirely, by the whole workgroup that owns them (after (1): row[a] /
+    //     row[new] of those rows may be among the entries)
+    const bool own_b = b >= x0 && b < x0 + APPLY_ROWS && b < nrows;
+    const bool own_n = nid >= x0 && nid < x0 + APPLY_ROWS && nid < nrows;
     __syncthreads();
-    if (x == a && threadIdx.x == 0) {
-      row[b] = 0u;   // merged pair retired (never re-picked)
+    if (own_b || own_n) {
+      for (int r = 0; r < 2; ++r) {
+        const int xr = r == 0 ? b : nid;
+        if (!(r == 0 ? own_b : own_n) || (r == 1 && nid == b)) continue;
+        uint32_t* row = table + (size_t)xr * Vt;
+        int any = 0;
+        for (int y = threadIdx.x; y < Vt; y += 64 * APPLY_ROWS) {
+          int32_t v;
+          if (xr == b && (v = deltas[2 * Vt + y])) { row[y] += (uint32_t)v; deltas[2 * Vt + y] = 0; any = 1; }
+          if (xr == nid && (v = deltas[3 * Vt + y])) { row[y] += (uint32_t)v; deltas[3 * Vt + y] = 0; any = 1; }
+        }
+        if (any) changed_w[xr - x0] = 1;
+      }
+      __syncthreads();
+    }
+    // (3) row a: the merged pair retired after its own adds
+    if (x == a && lane == 0) {
+      uint32_t* row = table + (size_t)x * Vt;
+      row[b] = 0u;   // never re-picked
       tlen[nid] = tlen[a] + tlen[b];
-      changed = 1;
       if (use_ix) {   // the pool range appended by the merge becomes new's word list
         const uint32_t top = ix.ctl[0], mark = ix.ctl[1], cap = ix.ctl[2];
         if (reused || top > cap) {
@@ -804,42 +833,54 @@ __global__ __launch_bounds__(256) void k_apply_argmax(uint32_t* __restrict__ tab
         ix.ctl[0] = t;
         ix.ctl[1] = t;
       }
+      changed_w[wave] = 1;
     }
-    __syncthreads();
+    if (a >= x0 && a < x0 + APPLY_ROWS) __syncthreads();
+    changed = changed_w[wave];
   }
-  if (x >= vcur) return;
-  unsigned long long best = 0;
-  if (aw.clean[x] && !changed) {
-    best = aw.rowbest[x];
-  } else {
-    for (int y0 = threadIdx.x * 8; y0 < vcur; y0 += 256 * 8) {
-      uint32_t c[8];
-      if (((Vt & 3) == 0) && y0 + 8 <= vcur) {
-        const uint4 u0 = *reinterpret_cast<const uint4*>(row + y0);
-        const uint4 u1 = *reinterpret_cast<const uint4*>(row + y0 + 4);
-        c[0] = u0.x; c[1] = u0.y; c[2] = u0.z; c[3] = u0.w; c[4] = u1.x; c[5] = u1.y; c[6] = u1.z; c[7] = u1.w;
-      } else {
+  if (x < nrows && x < vcur) {
+    uint32_t* row = table + (size_t)x * Vt;
+    if (aw.clean[x] && !changed) {
+      best = aw.rowbest[x];
+    } else {
+      // all of a lane's loads of a 2,048-entry stretch in flight together
+      for (int base = 0; base < vcur; base += 64 * 32) {
+        uint32_t c[32];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) c[k] = y0 + k < vcur ? row[y0 + k] : 0u;
-      }
+        for (int k = 0; k < 8; ++k) {
+          const int y0 = base + (k * 64 + lane) * 4;
+          if (((Vt & 3) == 0) && y0 + 4 <= vcur) {
+            const uint4 u = *reinterpret_cast<const uint4*>(row + y0);
+            c[4 * k] = u.x; c[4 * k + 1] = u.y; c[4 * k + 2] = u.z; c[4 * k + 3] = u.w;
+          } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)(y0 + k);
-        if (c[k]) best = umax64(best, ((unsigned long long)c[k] << 32) | (unsigned long long)(~idx));
+            for (int q = 0; q < 4; ++q) c[4 * k + q] = y0 + q < vcur ? row[y0 + q] : 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int y = base + (k * 64 + lane) * 4 + q;
+            const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
+            const uint32_t cv = c[4 * k + q];
+            if (cv) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
+          }
       }
-    }
-    for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = best;
-    __syncthreads();
-    best = umax64(umax64(sh[0], sh[1]), umax64(sh[2], sh[3]));
-    if (threadIdx.x == 0) {
-      aw.rowbest[x] = best;
-      aw.clean[x] = 1u;
+      for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
+      if (lane == 0) {
+        aw.rowbest[x] = best;
+        aw.clean[x] = 1u;
+      }
     }
   }
-  if (threadIdx.x == 0 && best) {
+  if (lane == 0) wbest[wave] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0;
+    for (int w = 0; w < APPLY_ROWS; ++w) m = umax64(m, wbest[w]);
     unsigned long long* slot = aw.slot + parity;
-    if (best > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, best);
+    if (m && m > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, m);
   }
 }
 
@@ -871,43 +912,83 @@ __host__ __device__ inline uint64_t dedup_cap(int64_t n) {
   return c;
 }
 
+// One thread per word.  The table slot of the word's content is found as before; then the
+// two atomics that serialised at the memory side are aggregated: new distinct words take their
+// list positions with one atomic per wave (ballot), and occurrence counts are summed per slot
+// in an LDS hash (DEDUP_LDS entries, linear probing; a full probe falls back to the global
+// atomic) and flushed once per workgroup -- the common words occur millions of times.
+constexpr int DEDUP_LDS = 4096;
 __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                       const uint32_t* __restrict__ wlen, int64_t nw, DedupWs ws) {
+  __shared__ uint32_t lkey[DEDUP_LDS];   // slot + 1, 0 = empty
+  __shared__ uint32_t lcnt[DEDUP_LDS];
+  for (int i = threadIdx.x; i < DEDUP_LDS; i += blockDim.x) { lkey[i] = 0; lcnt[i] = 0; }
+  __syncthreads();
   const uint64_t mask = ws.cap - 1;
-  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t L = wlen[w];
-    if (L < 2) continue;
-    const uint16_t* s = sym + wstart[w];
-    const uint64_t h = word_hash(s, L);
-    const unsigned long long mine = ((h >> 32) << 32) | (unsigned long long)(uint32_t)(w + 1);
-    uint64_t k = h & mask;
-    while (true) {
-      unsigned long long v = ws.keys[k];
-      if (v == 0ull) {
-        v = atomicCAS(&ws.keys[k], 0ull, mine);
-        if (v == 0ull) {   // new distinct word
-          atomicAdd(&ws.cnt[k], 1u);
-          const unsigned long long u = atomicAdd(ws.nu, 1ull);
-          ws.rep[u] = (uint32_t)w;
-          ws.slot[u] = (uint32_t)k;
-          break;
+  const int lane = threadIdx.x & 63;
+  const int64_t G = (int64_t)gridDim.x * blockDim.x;
+  // wave-uniform trip count: every lane reaches the ballot below
+  for (int64_t w0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); w0 < nw; w0 += G) {
+    const int64_t w = w0 + lane;
+    bool is_new = false;
+    uint64_t k = 0;
+    bool have = false;
+    if (w < nw) {
+      const uint32_t L = wlen[w];
+      if (L >= 2) {
+        have = true;
+        const uint16_t* s = sym + wstart[w];
+        const uint64_t h = word_hash(s, L);
+        const unsigned long long mine = ((h >> 32) << 32) | (unsigned long long)(uint32_t)(w + 1);
+        k = h & mask;
+        while (true) {
+          unsigned long long v = ws.keys[k];
+          if (v == 0ull) {
+            v = atomicCAS(&ws.keys[k], 0ull, mine);
+            if (v == 0ull) { is_new = true; break; }
+          }
+          if ((v >> 32) == (h >> 32)) {
+            const uint32_t r = (uint32_t)(v & 0xFFFFFFFFull) - 1u;
+            bool eq = wlen[r] == L;
+            if (eq) {
+              const uint16_t* t = sym + wstart[r];
+              for (uint32_t i = 0; i < L && eq; ++i) eq = t[i] == s[i];
+            }
+            if (eq) break;
+          }
+          k = (k + 1) & mask;
         }
       }
-      if ((v >> 32) == (h >> 32)) {
-        const uint32_t r = (uint32_t)(v & 0xFFFFFFFFull) - 1u;
-        bool eq = wlen[r] == L;
-        if (eq) {
-          const uint16_t* t = sym + wstart[r];
-          for (uint32_t i = 0; i < L && eq; ++i) eq = t[i] == s[i];
-        }
-        if (eq) {
-          atomicAdd(&ws.cnt[k], 1u);
-          break;
-        }
+    }
+    // distinct-word list positions: one atomic per wave
+    const unsigned long long nb = __ballot(is_new);
+    if (nb) {
+      unsigned long long base = 0;
+      const int leader = __ffsll((long long)nb) - 1;
+      if (lane == leader) base = atomicAdd(ws.nu, (unsigned long long)__popcll(nb));
+      base = __shfl(base, leader);
+      if (is_new) {
+        const unsigned long long u = base + __popcll(nb & ((1ull << lane) - 1ull));
+        ws.rep[u] = (uint32_t)w;
+        ws.slot[u] = (uint32_t)k;
       }
-      k = (k + 1) & mask;
+    }
+    // occurrence count of slot k, aggregated in LDS
+    if (have) {
+      const uint32_t key = (uint32_t)k + 1u;
+      uint32_t j = (key * 0x9E3779B1u) >> (32 - 12);
+      bool done = false;
+      for (int probe = 0; probe < 8 && !done; ++probe) {
+        const uint32_t cur = atomicCAS(&lkey[j], 0u, key);
+        if (cur == 0u || cur == key) { atomicAdd(&lcnt[j], 1u); done = true; }
+        j = (j + 1) & (DEDUP_LDS - 1);
+      }
+      if (!done) atomicAdd(&ws.cnt[k], 1u);
     }
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DEDUP_LDS; i += blockDim.x)
+    if (lkey[i]) atomicAdd(&ws.cnt[lkey[i] - 1u], lcnt[i]);
 }
 
 __global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict__ wstart,
@@ -1163,9 +1244,9 @@ extern "C" size_t beast_bpe_argmax_workspace_bytes(int Vt) { return (size_t)(4 +
 extern "C" int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int call, void* stream) {
   BEAST_REQUIRE(table && ws && vcur >= 1 && vcur <= Vt, "beast_bpe_argmax: bad args");
   BEAST_REQUIRE(call >= 0, "beast_bpe_argmax: call index must be >= 0");
-  hipLaunchKernelGGL(k_apply_argmax, dim3(vcur), dim3(256), 0, beast::as_stream(stream), const_cast<uint32_t*>(table),
-                     nullptr, Vt, vcur, argws_view(ws, Vt), call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false, nullptr,
-                     LoopHash{});
+  hipLaunchKernelGGL(k_apply_argmax, dim3((vcur + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0,
+                     beast::as_stream(stream), const_cast<uint32_t*>(table), nullptr, Vt, vcur, argws_view(ws, Vt),
+                     call & 1, 0, 0, 0, 0, nullptr, WordIndex{}, false, false, nullptr, LoopHash{}, vcur);
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -1180,9 +1261,9 @@ extern "C" int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, 
   const WordIndex ix = index ? index_view(index, Vt) : WordIndex{};
   // every row that can change must run: rows < vcur, and a / b / new_id
   const int rows = std::max(vcur, std::max(a, std::max(b, new_id)) + 1);
-  hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, beast::as_stream(stream), table, deltas, Vt, vcur,
-                     argws_view(ws, Vt), call & 1, 1, a, b, new_id, tlen, ix, index != nullptr, new_id_reused != 0,
-                     nullptr, LoopHash{});
+  hipLaunchKernelGGL(k_apply_argmax, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0,
+                     beast::as_stream(stream), table, deltas, Vt, vcur, argws_view(ws, Vt), call & 1, 1, a, b, new_id,
+                     tlen, ix, index != nullptr, new_id_reused != 0, nullptr, LoopHash{}, rows);
   BEAST_LAUNCHED("k_apply_argmax");
   return BEAST_OK;
 }
@@ -1382,8 +1463,8 @@ extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_step
                        max_token_length, deltas, Vt, sg, ix, index != nullptr, st, (long long)beast::g_merge_lds_min,
                        aw, lh);
     BEAST_LAUNCHED("k_merge");
-    hipLaunchKernelGGL(k_apply_argmax, dim3(rows), dim3(256), 0, s, table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen,
-                       ix, index != nullptr, false, st, lh);
+    hipLaunchKernelGGL(k_apply_argmax, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s,
+                       table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen, ix, index != nullptr, false, st, lh, rows);
     BEAST_LAUNCHED("k_apply_argmax");
   }
   return BEAST_OK;
