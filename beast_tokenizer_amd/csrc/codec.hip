@@ -254,7 +254,7 @@ __host__ __device__ inline EncSmem enc_smem(int T, int Tp, int Dl, int D, int N,
   s.P = o;    o += round_up(nkinds * 16 * Tp * 4 + 64 * ECH, 1024);   // fp32 [16][Tp] projection per kind
   s.Y = o;    o += round_up(TBT * T * Dl * 4, 1024);
   s.pb = o;   o += round_up(TBT * D * N * 4, 16);        // params, (d n) per trajectory
-  s.kq = o;   o += round_up(D * N * 4, 16);              // quantiser scale per (d n) column
+  s.kq = o;   o += round_up(D * N * 16, 16);             // {lo, hi, scale, 0} per (d n) column
   s.wlo = o;  o += round_up(D * N * 4, 256);
   s.whi = o;  o += round_up(D * N * 4, 256);
   s.lcol = o; o += round_up(D * 4, 256);
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
   float* pb = reinterpret_cast<float*>(smem + L.pb);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
-  float* kq = reinterpret_cast<float*>(smem + L.kq);
+  float4* kq = reinterpret_cast<float4*>(smem + L.kq);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x;
   const bool quant = a.tokens_out != nullptr;
@@ -329,7 +329,8 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
     if (tile == blockIdx.x) STAMP(0, 2);
     if (tile == blockIdx.x + gridDim.x) STAMP(0, 12);
     if (quant && tile == blockIdx.x)   // bounds landed with the first tile; read after the next barrier
-      for (int i = tid; i < DN; i += NT) kq[i] = beast::quantize_scale(wlo[i], whi[i], vm1);
+      for (int i = tid; i < DN; i += NT)
+        kq[i] = make_float4(wlo[i], whi[i], beast::quantize_scale(wlo[i], whi[i], vm1), 0.0f);
 
     // ---- fit: params[j][d][n] = sum_t P_kind[n][t] y[j][t][d]  (f32 MFMA 16x16x4; A = P, B = y).
     //      A wave owns two column tiles per pass (two independent chains), operands
@@ -425,15 +426,19 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
         const int n4 = total >> 2;
         for (int i = tid; i < n4; i += NT) {
           int bin[4], c[4], pj[4];
+          float pv[4];
+          float4 qv[4];
           bool ex = false;
+          // every LDS operand of the 4 tokens is requested before any is used (one round trip)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            c[u] = col_of(4 * i + u, pj[u]);
-            bin[u] = beast::quantize_bin_k(pb[pj[u] + c[u]], wlo[c[u]], whi[c[u]], kq[c[u]], vm1, ex);
-          }
+          for (int u = 0; u < 4; ++u) c[u] = col_of(4 * i + u, pj[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) { pv[u] = pb[pj[u] + c[u]]; qv[u] = kq[c[u]]; }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin_k(pv[u], qv[u].x, qv[u].y, qv[u].z, vm1, ex);
           if (ex) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pb[pj[u] + c[u]], wlo[c[u]], whi[c[u]], vm1);
+            for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
           }
           longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
           o2[0] = make_longlong2(beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
@@ -455,6 +460,238 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
   STAMP(0, 7);
   BSTAMP(0, 1);
 #endif
+}
+
+// ------------------------------------------------------- encode, pipelined --
+// Latency regime (at most two 8-trajectory tiles per CU, e.g. B = 4096 on 256 CUs).  Every
+// workgroup issues its loads at once, so without a pipeline the whole chip loads, then
+// computes (memory idle), then stores: the MFMA phase adds to the HBM time instead of
+// hiding under it.  Here a workgroup (8 waves) splits its 8 trajectories into two
+// sub-tiles A, B of PIPE_SUB and overlaps:
+//
+//   waves 0-3 (DMA + MFMA):  DMA A, constants, DMA B | wait A | fit A | wait B | fit B  | store B
+//   waves 4-7 (store):                                | scale  |       | store A         | store B
+//
+// The waits are explicit vmcnt counts: the DMA waves issue exactly PIPE_Y_OPS wave-
+// instructions per sub-tile (sources clamped to the batch, destinations padded), and
+// nothing else after B's, so "vmcnt(PIPE_Y_OPS)" is "A and the constants have landed".
+// A and B sit in distinct static LDS arrays, which lets the compiler's own LDS-DMA
+// tracking tell them apart (a single array would make it wait for B before reading A).
+// Results are bit-identical to k_encode's: same MFMA chain (even / odd K-steps), same
+// epilogue arithmetic.
+constexpr int PIPE_SUB = 4;       // trajectories per sub-tile
+constexpr int PIPE_MW = 4;        // DMA + MFMA waves
+constexpr int PIPE_W = 8;         // waves per workgroup
+constexpr int PIPE_MT = PIPE_MW * 64;
+
+template <class S>
+struct PipeShape {
+  static_assert(S::fixed && S::T > 0 && S::DL > 0 && ((S::T * S::DL) % 4) == 0, "pipelined encode: fixed shape");
+  static constexpr int T = S::T, DL = S::DL, D = S::D, N = S::N, DN = S::D * S::N, Tp = round_up(S::T, 4);
+  static constexpr int NST = Tp / 4;                              // MFMA K-steps
+  static constexpr int Y16 = PIPE_SUB * T * DL / 4;               // float4 per sub-tile
+  static constexpr int Y_OPS = (Y16 + PIPE_MT - 1) / PIPE_MT;     // DMA wave-instructions per DMA wave
+  static constexpr int P_OPS = (2 * 4 * Tp + PIPE_MT - 1) / PIPE_MT;
+};
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8])
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | ((N >> 4) << 14));
+}
+// Workgroup barrier that does not wait for this wave's outstanding global memory (the
+// caller has waited for what must be visible); a compiler-level memory fence on each side.
+__device__ __forceinline__ void bar_only() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// OPS wave-instructions of 16-byte LDS-DMA from each of the PIPE_MW DMA waves: slot
+// i = op * PIPE_MT + tid of the destination <- source float4 min(first + i, last).
+template <int OPS>
+__device__ __forceinline__ void dma16_fixed(void* lds, const float4* src, int64_t first, int64_t last) {
+  const int tid = threadIdx.x, wb = tid & ~63;
+#pragma unroll
+  for (int op = 0; op < OPS; ++op)
+    __builtin_amdgcn_global_load_lds(src + min(first + op * PIPE_MT + tid, last),
+                                     (lds_void*)(static_cast<uint4*>(lds) + op * PIPE_MT + wb), 16, 0, 0);
+}
+
+// params[j][d][n] of one sub-tile = sum_t P_kind[n][t] y[j][t][d]: a DMA wave per MFMA
+// column tile; all operands of the tile's K-steps are read before the chain (one LDS round
+// trip), even / odd steps accumulate separately as in k_encode.
+template <class S>
+__device__ __forceinline__ void pipe_fit(const Geom& g, const Dims<S>& m, const float* P, const float* Y,
+                                         const int* lcol, float* pb, int nb, int wave, int lane) {
+  using PS = PipeShape<S>;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int nq = n_coltiles<PIPE_SUB>(m);
+  for (int q = wave; q < nq; q += PIPE_MW) {
+    int j, d, k;
+    bool ok;
+    tile_col<PIPE_SUB>(g, m, q, lr, j, d, k, ok);
+    ok = ok && j < nb;
+    const int c = min(max(lcol[d], 0), PS::DL - 1);
+    const float* pa = P + (k * 16 + lr) * PS::Tp + lk;
+    const float* yc = Y + j * PS::T * PS::DL + c;
+    float xa[PS::NST], ya[PS::NST];
+#pragma unroll
+    for (int st = 0; st < PS::NST; ++st) {
+      xa[st] = pa[4 * st];
+      ya[st] = yc[min(4 * st + lk, PS::T - 1) * PS::DL];
+    }
+    float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0;
+#pragma unroll
+    for (int st = 0; st < PS::NST; ++st) {
+      if (st & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc1, 0, 0, 0);
+      else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = lk * 4 + r;
+      if (ok && n < PS::N) pb[j * PS::DN + d * PS::N + n] = __fadd_rn(acc0[r], acc1[r]);
+    }
+  }
+}
+
+// params (d n) and tokens (n d) of one sub-tile from its LDS params image, by threads
+// t in [0, nthr): k_encode's epilogue.
+template <class S>
+__device__ __forceinline__ void pipe_store(const EncArgs& a, const float* pb, const float4* kq, const float* wlo,
+                                           const float* whi, int64_t b0, int nb, int t, int nthr, float vm1) {
+  using PS = PipeShape<S>;
+  constexpr int per = PS::DN, D = PS::D, N = PS::N;
+  if (nb <= 0) return;
+  if (a.params_out != nullptr) {
+    float* dst = a.params_out + b0 * per;
+    const int count = nb * per;
+    if ((((uintptr_t)dst) & 15) == 0 && (per % 4) == 0) {
+      for (int i = t; i < count / 4; i += nthr)
+        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(pb)[i];
+    } else {
+      for (int i = t; i < count; i += nthr) dst[i] = pb[i];
+    }
+  }
+  if (a.tokens_out == nullptr) return;
+  const int total = nb * per;
+  long long* tout = a.tokens_out + b0 * per;
+  const unsigned long long off = (unsigned long long)a.tok_offset;
+  auto col_of = [&](int e, int& pj) {   // token e of the sub-tile -> (d n) column, trajectory
+    const int j = e / per, r = e - j * per, n = r / D;
+    pj = j * per;
+    return (r - n * D) * N + n;
+  };
+  int done = 0;
+  if ((((uintptr_t)tout) & 15) == 0) {
+    const int n4 = total >> 2;
+    for (int i = t; i < n4; i += nthr) {
+      int bin[4], c[4], pj[4];
+      float pv[4];
+      float4 qv[4];
+      bool ex = false;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c[u] = col_of(4 * i + u, pj[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { pv[u] = pb[pj[u] + c[u]]; qv[u] = kq[c[u]]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin_k(pv[u], qv[u].x, qv[u].y, qv[u].z, vm1, ex);
+      if (ex) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
+      }
+      longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
+      o2[0] = make_longlong2(beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
+      o2[1] = make_longlong2(beast::widen_bin(bin[2], off), beast::widen_bin(bin[3], off));
+    }
+    done = n4 << 2;
+  }
+  for (int e = done + t; e < total; e += nthr) {
+    int pj;
+    const int c = col_of(e, pj);
+    tout[e] = beast::widen_bin(beast::quantize_bin(pb[pj + c], wlo[c], whi[c], vm1), off);
+  }
+}
+
+struct PipeSmem {
+  int P, pbA, pbB, kq, wlo, whi, lcol, total;
+};
+template <class S>
+__host__ __device__ constexpr PipeSmem pipe_smem() {
+  using PS = PipeShape<S>;
+  PipeSmem s{};
+  int o = 0;
+  s.P = o;    o += PS::P_OPS * PIPE_MT * 16;
+  s.pbA = o;  o += round_up(PIPE_SUB * PS::DN * 4, 16);
+  s.pbB = o;  o += round_up(PIPE_SUB * PS::DN * 4, 16);
+  s.kq = o;   o += PS::DN * 16;
+  s.wlo = o;  o += round_up(PS::DN * 4, 256);
+  s.whi = o;  o += round_up(PS::DN * 4, 256);
+  s.lcol = o; o += round_up(PS::D * 4, 256);
+  s.total = o;
+  return s;
+}
+
+template <class S>
+__global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
+  using PS = PipeShape<S>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ __attribute__((aligned(16))) float YA[PS::Y_OPS * PIPE_MT * 4];
+  __shared__ __attribute__((aligned(16))) float YB[PS::Y_OPS * PIPE_MT * 4];
+  const Geom& g = a.g;
+  const Dims<S> m(g);
+  constexpr PipeSmem L = pipe_smem<S>();
+  float* P = reinterpret_cast<float*>(smem + L.P);
+  float* pbA = reinterpret_cast<float*>(smem + L.pbA);
+  float* pbB = reinterpret_cast<float*>(smem + L.pbB);
+  float4* kq = reinterpret_cast<float4*>(smem + L.kq);
+  float* wlo = reinterpret_cast<float*>(smem + L.wlo);
+  float* whi = reinterpret_cast<float*>(smem + L.whi);
+  int* lcol = reinterpret_cast<int*>(smem + L.lcol);
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const bool mw = wave < PIPE_MW;   // wave-uniform role
+  const bool quant = a.tokens_out != nullptr;
+  const float vm1 = (float)(a.vocab - 1);
+  const int64_t b0 = (int64_t)blockIdx.x * (2 * PIPE_SUB);
+  const int nbA = (int)min<int64_t>(PIPE_SUB, a.B - b0);
+  const int nbB = (int)max<int64_t>(0, min<int64_t>(PIPE_SUB, a.B - b0 - PIPE_SUB));
+  constexpr int tile16 = PS::T * PS::DL / 4;   // float4 per trajectory
+
+  if (mw) {
+    const float4* src = reinterpret_cast<const float4*>(a.traj);
+    const int64_t last = a.B * tile16 - 1;
+    dma16_fixed<PS::Y_OPS>(YA, src, b0 * tile16, last);
+    const int nk16 = ((m.nj < m.D) ? 2 : 1) * 4 * PS::Tp;
+    dma16_fixed<PS::P_OPS>(P, reinterpret_cast<const float4*>(a.proj), 0, nk16 - 1);
+    if (quant) {
+      dma4<PIPE_MT>(wlo, a.w_min, PS::DN);
+      dma4<PIPE_MT>(whi, a.w_max, PS::DN);
+    }
+    dma4<PIPE_MT>(lcol, a.dof_src, PS::D);
+    dma16_fixed<PS::Y_OPS>(YB, src, (b0 + PIPE_SUB) * tile16, last);
+    wait_vm_lgkm<PS::Y_OPS>();   // A and the constants have landed (B's DMA is the newest)
+  }
+  bar_only();
+  if (mw) {
+    pipe_fit<S>(g, m, P, YA, lcol, pbA, nbA, wave, lane);
+    wait_vm_lgkm<0>();           // B has landed; pbA written
+  } else {
+    if (quant)
+      for (int i = tid - PIPE_MT; i < PS::DN; i += PIPE_MT)
+        kq[i] = make_float4(wlo[i], whi[i], beast::quantize_scale(wlo[i], whi[i], vm1), 0.0f);
+    wait_vm_lgkm<0>();
+  }
+  bar_only();
+  if (mw) {
+    pipe_fit<S>(g, m, P, YB, lcol, pbB, nbB, wave, lane);
+    wait_vm_lgkm<0>();
+  } else {
+    pipe_store<S>(a, pbA, kq, wlo, whi, b0, nbA, tid - PIPE_MT, PIPE_MT, vm1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the LDS reads of pbA are done
+  }
+  bar_only();
+  pipe_store<S>(a, pbB, kq, wlo, whi, b0 + PIPE_SUB, nbB, tid, PIPE_W * 64, vm1);
 }
 
 // ------------------------------------------------------------ reconstruct --
@@ -498,6 +735,50 @@ __device__ __forceinline__ float rec_weight(const RecArgs& a, const unsigned cha
   const long long t = reinterpret_cast<const long long*>(tokl)[e] - a.tok_offset;
   const float nrm = (t >= 0 && t < a.lut_n) ? lut[t] : __fdiv_rn((float)t, vm1);
   return beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi, lo)), lo), lo, hi);
+}
+
+// B operand of one MFMA lane for KS K-steps: W[j][d][n], n = lk * KS + ks (clamped to N - 1
+// for the read; the caller zeroes n >= N).  rec_weight's arithmetic, with every LDS read of
+// the KS steps issued before any is used: tokens and bounds in one round trip, the LUT in
+// a second; tokens outside the LUT (rare) take the IEEE division behind an exec branch.
+template <int KS>
+__device__ __forceinline__ void rec_weights(const RecArgs& a, const unsigned char* tokl, int j, int d, int lk,
+                                            int N, int D, int per, const float* wlo, const float* whi,
+                                            const float* lut, float vm1, float (&w)[KS]) {
+  float lo[KS], hi[KS];
+  int e[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int n = min(lk * KS + ks, N - 1), k = d * N + n;
+    e[ks] = j * per + n * D + d;
+    lo[ks] = wlo[k];
+    hi[ks] = whi[k];
+  }
+  if (a.ntokens) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      w[ks] = beast::denormalize_one(reinterpret_cast<const float*>(tokl)[e[ks]], lo[ks], hi[ks]);
+    return;
+  }
+  long long t[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) t[ks] = reinterpret_cast<const long long*>(tokl)[e[ks]] - a.tok_offset;
+  float nrm[KS];
+  bool far = false;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const bool in = (t[ks] >= 0) & (t[ks] < a.lut_n);
+    far = far | !in;
+    nrm[ks] = lut[in ? (int)t[ks] : 0];
+  }
+  if (far) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      if (!((t[ks] >= 0) & (t[ks] < a.lut_n))) nrm[ks] = __fdiv_rn((float)t[ks], vm1);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    w[ks] = beast::clamp_t(__fadd_rn(__fmul_rn(nrm[ks], __fsub_rn(hi[ks], lo[ks])), lo[ks]), lo[ks], hi[ks]);
 }
 
 struct RecSmem {
@@ -665,12 +946,9 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(RecArgs a) {
       tile_col<TBT>(g, m, q, lr, j, d, kind, ok);
       ok = ok && j < nb;
       float w[KS];   // B operand, K-step ks: W[j][d][n], n = lane/16 * KS + ks
+      rec_weights<KS>(a, tokl, j, d, lk, N, D, per, wlo, whi, lut, vm1, w);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int n = min(lk * KS + ks, N - 1);
-        const float v = rec_weight(a, tokl, j * per + n * D + d, d * N + n, wlo, whi, lut, vm1);
-        w[ks] = (ok && lk * KS + ks < N) ? v : 0.0f;
-      }
+      for (int ks = 0; ks < KS; ++ks) w[ks] = (ok && lk * KS + ks < N) ? w[ks] : 0.0f;
       if (a.init_p != nullptr && lk == 0 && ok && d < nj)   // coefficient n = 0 of the joint DoFs <- init_p
         w[0] = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];   // (reference :505-510)
       float* oc = ob + (j * RTR + lk * 4) * ndo + min(max(dst[d], 0), ndo - 1);
@@ -863,8 +1141,21 @@ bool g_generic_only = false;
 // 4 | 7) forces one (tests, measurements); 0 = by batch size.
 int g_block_waves = 0;
 bool wide_blocks(int64_t ntiles) {
-  if (g_block_waves == 4 || g_block_waves == 7) return g_block_waves == 7;
+  if (g_block_waves == 4 || g_block_waves == 7 || g_block_waves == 8) return g_block_waves != 4;
   return ntiles <= 2 * (int64_t)cu_count();
+}
+// Encode in the latency regime: the pipelined 8-wave kernel (default; BEAST_OPT_BLOCK_WAVES
+// 8 forces it at any batch), or k_encode's 7-wave one (BEAST_OPT_BLOCK_WAVES 7).
+bool pipe_encode(int64_t ntiles) { return g_block_waves == 8 || (g_block_waves == 0 && wide_blocks(ntiles)); }
+
+template <class S>
+int launch_encode_pipe(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
+  a.g = make_geom<PIPE_SUB>(D, nj, N, T);
+  a.ntiles = (a.B + 2 * PIPE_SUB - 1) / (2 * PIPE_SUB);
+  constexpr PipeSmem L = pipe_smem<S>();
+  hipLaunchKernelGGL((k_encode_pipe<S>), dim3(a.ntiles), dim3(PIPE_W * 64), L.total, s, a);
+  BEAST_LAUNCHED("k_encode_pipe");
+  return BEAST_OK;
 }
 
 template <int TBT, class S>
@@ -899,6 +1190,10 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   if (forced == 1 || forced == 2 || forced == 4 || (forced == 8 && fast)) tbt = std::min(tbt, forced);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
     const bool wide = wide_blocks((a.B + 7) / 8);
+    if (pipe_encode((a.B + 7) / 8)) {
+      if (D == 14 && nj == 14) return launch_encode_pipe<Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, s);
+      if (D == 14 && nj == 12) return launch_encode_pipe<Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, s);
+    }
     if (D == 14 && nj == 14)
       return wide ? launch_encode_t<8, Shape<14, 14, 10, 50, 14, 7>>(a, T, D, nj, N, true, s)
                   : launch_encode_t<8, Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, true, s);
@@ -1029,7 +1324,8 @@ extern "C" int beast_set_option(int option, int value) {
     return BEAST_OK;
   }
   if (option == BEAST_OPT_BLOCK_WAVES) {
-    BEAST_REQUIRE(value == 0 || value == 4 || value == 7, "BEAST_OPT_BLOCK_WAVES: %d is not 0, 4 or 7", value);
+    BEAST_REQUIRE(value == 0 || value == 4 || value == 7 || value == 8,
+                  "BEAST_OPT_BLOCK_WAVES: %d is not 0, 4, 7 or 8", value);
     g_block_waves = value;
     return BEAST_OK;
   }

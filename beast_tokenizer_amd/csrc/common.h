@@ -89,7 +89,7 @@ __device__ __forceinline__ int quantize_bin_k(float p, float lo, float hi, float
   const float x = __builtin_amdgcn_fmed3f(p, lo, hi);
   const float va = __fmul_rn(__fsub_rn(x, lo), k);
   const float f = __builtin_amdgcn_fractf(va);
-  exact = exact || !(fabsf(__fsub_rn(f, 0.5f)) > 9.5367431640625e-7f * vm1) || (p != p);
+  exact = exact | !(fabsf(__fsub_rn(f, 0.5f)) > 9.5367431640625e-7f * vm1) | (p != p);   // branch-free
   return (int)rintf(fminf(fmaxf(va, 0.0f), vm1));
 }
 
