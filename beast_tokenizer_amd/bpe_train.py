@@ -19,9 +19,19 @@ The driver below is written against a small ``ops`` interface so the same code
 runs the HIP kernels (:class:`GpuBpeOps`) and, in the CPU tests, a numpy stand-in;
 ``reduce`` is the cross-rank all-reduce (``torch.distributed`` = RCCL over xGMI
 on MI355X; a no-op on one GPU).  Pair counts are additive over shards of the
-corpus, so data-parallel training all-reduces the initial pair table once and
-the four per-merge delta vectors ``[4][Vt]`` every merge; every rank then holds
-the same table and takes the same decisions.
+corpus.  Data-parallel training therefore has two forms:
+
+* **replicated merge loop** (default when ``reduce`` carries a ``gather``, as
+  :func:`torch_dist_reducer` does): every rank pretokenises and deduplicates its
+  own shard, the distinct words x counts are all-gathered once (a word repeated
+  across shards simply appears once per shard with its shard count -- pair counts
+  and merges are unchanged), and every rank runs the single-GPU device-driven loop
+  on the union with no per-merge collective.  The loop is latency-bound (tens of
+  microseconds per merge), so one gather beats a collective per merge;
+* **per-merge all-reduce**: the initial pair table is all-reduced once and the
+  four per-merge delta vectors ``[4][Vt]`` every merge.
+
+Either way every rank holds the same table and takes the same decisions.
 """
 from __future__ import annotations
 
@@ -42,11 +52,28 @@ def no_reduce(t: torch.Tensor, op: str) -> None:  # single GPU
 
 
 def torch_dist_reducer(group=None) -> Reducer:
+    """All-reduce over ``group``; ``red.gather(t)`` all-gathers a 1-D tensor whose length
+    differs per rank and returns the per-rank pieces in rank order."""
     import torch.distributed as dist
     ops = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
 
     def red(t: torch.Tensor, op: str) -> None:
         dist.all_reduce(t, op=ops[op], group=group)
+
+    def gather(t: torch.Tensor) -> List[torch.Tensor]:
+        if t.is_cuda and dist.get_backend(group) == "gloo":   # CPU rehearsal of the RCCL path
+            return [o.to(t.device) for o in gather(t.cpu())]
+        world = dist.get_world_size(group)
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+        sizes = [torch.empty_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(v) for v in torch.cat(sizes).tolist()]
+        buf = torch.zeros(max(max(sizes), 1), dtype=t.dtype, device=t.device)
+        buf[:t.numel()] = t
+        outs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(outs, buf, group=group)
+        return [o[:k] for o, k in zip(outs, sizes)]
+    red.gather = gather
     return red
 
 
@@ -129,21 +156,48 @@ class GpuBpeOps:
                  n, ws.data_ptr(), ws.numel(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), on.data_ptr(), s)
         nu = self._read_i64(on, 1)[0]
         del ws
-        # contiguous, length-ordered copy of the distinct words (coalesced merge scans)
+        return self._repack(words, words["sym"], ow, ol, oc, nu, words["n_syms"])
+
+    def _repack(self, words, sym, ow, ol, oc, nu: int, cap: int):
+        """Contiguous, length-ordered copy of words (start ow, length ol, count oc in ``sym``)
+        plus their Bloom signatures: the layout the merge loop scans."""
+        dev, s = self.device, self.stream
+        on = torch.empty(1, dtype=torch.int64, device=dev)
         ws = torch.empty(_lib.load().beast_bpe_repack_workspace_bytes(nu), dtype=torch.uint8, device=dev)
         m = max(nu, 1)
-        sym2 = torch.empty(max(words["n_syms"], 1), dtype=torch.int16, device=dev)
+        sym2 = torch.empty(max(cap, 1), dtype=torch.int16, device=dev)
         w2, l2, c2 = (torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3))
-        _lib.run("beast_bpe_repack_words", words["sym"].data_ptr(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), nu,
+        _lib.run("beast_bpe_repack_words", sym.data_ptr(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), nu,
                  ws.data_ptr(), ws.numel(), sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), c2.data_ptr(),
                  on.data_ptr(), s)
         ns = self._read_i64(on, 1)[0]
-        del ws, ow, ol, oc
+        del ws
         sym2 = sym2[:max(ns, 1)].clone()
         sig = torch.empty(m, dtype=torch.int64, device=dev)
         _lib.run("beast_bpe_word_signatures", sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), nu, sig.data_ptr(), s)
         return dict(words, sym=sym2, wstart=w2, wlen=l2, wcount=c2, sig=sig, n_words=nu, n_distinct=nu,
                     n_syms_distinct=ns)
+
+    def gather_words(self, words, gather):
+        """Every rank's distinct words x counts on every rank (one all-gather per array),
+        repacked for the merge loop.  Ranks are concatenated in rank order, so all ranks
+        hold identical word arrays."""
+        n, ns = words["n_words"], words.get("n_syms_distinct", 0)
+        syms = gather(words["sym"][:ns].to(torch.int32))      # RCCL has no int16
+        starts = gather(words["wstart"][:n].contiguous())
+        lens = gather(words["wlen"][:n].contiguous())
+        counts = gather(words["wcount"][:n].contiguous())
+        off, st = 0, []
+        for sy, w in zip(syms, starts):
+            st.append(w + off)
+            off += sy.numel()
+        dev = self.device
+        one = lambda parts, dt: torch.cat(parts).to(dt) if parts else torch.empty(0, dtype=dt, device=dev)  # noqa
+        sym = one(syms, torch.int16)
+        ow, ol, oc = one(st, torch.int32), one(lens, torch.int32), one(counts, torch.int32)
+        if sym.numel() == 0:
+            sym = torch.zeros(1, dtype=torch.int16, device=dev)
+        return self._repack(dict(words, n_syms=off), sym, ow, ol, oc, int(ow.numel()), off)
 
     def compact(self, words):
         """Drop words with < 2 symbols left (they can no longer merge).  Word indices change,
@@ -290,12 +344,14 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
               mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False,
-              device_loop: bool = True) -> BPEResult:
+              device_loop: bool = True, replicate: bool = True) -> BPEResult:
     """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard).
 
     Single process on the GPU ops: the merge loop runs device-driven (``GpuBpeOps.loop_run``,
-    no host round trip per merge); multi-rank (per-merge delta all-reduce) and the CPU model
-    run the host-driven loop below."""
+    no host round trip per merge).  Multi-rank with ``replicate`` (and a ``reduce.gather``):
+    the shards' distinct words are all-gathered after dedup and every rank runs that same
+    loop on the union.  Otherwise multi-rank is the host-driven loop below with a per-merge
+    delta all-reduce (also the CPU model's loop)."""
     import time
     t0 = time.perf_counter()
     if ops is None:
@@ -329,8 +385,13 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     n_words, n_syms = words["n_words"], words["n_syms"]
     if hasattr(ops, "dedup"):
         words = ops.dedup(words)
+    gather = getattr(reduce, "gather", None)
+    loop_reduce = reduce
+    if replicate and gather is not None and hasattr(ops, "gather_words") and reduce is not no_reduce:
+        words = ops.gather_words(words, gather)   # every rank: the union of the shards' words
+        loop_reduce = no_reduce
     table = ops.count_pairs(words, Vt, len(id2str))
-    reduce(table, "sum")
+    loop_reduce(table, "sum")
     tlen = np.zeros(Vt, dtype=np.int64)
     for i, s in enumerate(id2str):
         tlen[i] = len(s.encode("utf-8"))
@@ -341,7 +402,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     merges: List[Tuple[str, str]] = []
     t1 = time.perf_counter()
     key = ops.argmax(table, Vt, len(id2str))
-    if (device_loop and reduce is no_reduce and not compact_every and hasattr(ops, "loop_supported")
+    if (device_loop and loop_reduce is no_reduce and not compact_every and hasattr(ops, "loop_supported")
             and ops.loop_supported(Vt)):
         # merges decided on the GPU; the host replays the log against the real strings
         log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
@@ -360,11 +421,11 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
             return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
                              max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=None,
                              reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, use_index=use_index,
-                             device_loop=False)
+                             device_loop=False, replicate=replicate)
         t2 = time.perf_counter()
         stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
                  "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
-                 "Vt": Vt, "device_loop": True}
+                 "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce}
         return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
     while len(id2str) < vocab_size:
         count = key >> 32
@@ -381,7 +442,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
             id2str.append(new_tok)
         merges.append((id2str[a], id2str[b]))
         deltas = ops.merge(words, a, b, nid, max_len, Vt, count)
-        reduce(deltas, "sum")
+        loop_reduce(deltas, "sum")
         if len(id2str) >= vocab_size:          # last merge: apply without searching again
             ops.apply_argmax(table, deltas, Vt, len(id2str), a, b, nid, reused)
             break
@@ -391,7 +452,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     t2 = time.perf_counter()
     stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
              "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
-             "Vt": Vt}
+             "Vt": Vt, "replicated": loop_reduce is not reduce}
     return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
 
 

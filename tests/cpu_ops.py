@@ -49,6 +49,17 @@ class NumpyBpeOps:
         ws = [list(k) for k in c]
         return dict(words, words=ws, counts=[c[tuple(w)] for w in ws], n_words=len(ws), n_distinct=len(ws))
 
+    def gather_words(self, words, gather):
+        lens = torch.tensor([len(w) for w in words["words"]], dtype=torch.int64)
+        flat = torch.tensor([x for w in words["words"] for x in w], dtype=torch.int64)
+        cnt = torch.tensor(words["counts"], dtype=torch.int64)
+        L, F, C = (torch.cat(gather(t)).tolist() for t in (lens, flat, cnt))
+        ws, o = [], 0
+        for n in L:
+            ws.append(F[o:o + n])
+            o += n
+        return dict(words, words=ws, counts=C, n_words=len(ws), n_distinct=len(ws))
+
     def compact(self, words):
         keep = [i for i, w in enumerate(words["words"]) if len(w) >= 2]
         return dict(words, words=[words["words"][i] for i in keep], counts=[words["counts"][i] for i in keep],
