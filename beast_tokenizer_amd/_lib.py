@@ -36,6 +36,7 @@ SIGNATURES = {
     "beast_bspline_projection_f64": (_i32, [_vp, _i32, _i32, _f64, _vp, _vp]),
     "beast_encode_f32": (_i32, [_vp, _i64, _i32, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp,
                                 _i32, _i64, _vp, _vp, _vp]),
+    "beast_encode_list_f32": (_i32, [_vp, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),
     "beast_quantize_f32": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
     "beast_reconstruct_f32": (_i32, [_vp, _i64, _i32, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _i32,
                                      _vp, _i64, _vp, _vp, _vp, _vp, _vp]),

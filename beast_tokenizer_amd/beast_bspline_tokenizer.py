@@ -396,16 +396,28 @@ class BEASTBsplineTokenizer(TokenizerBase):
         iterator = _tqdm(dataloader, total=max_samples, desc="precomputing weight normalizer of MP",
                          unit="batch") if verbose else dataloader
         sample_count = 0
+        group = []   # device-resident batches of one shape, fitted together in one launch
         for batch in iterator:
             if "actions" not in batch:
                 raise KeyError("Expected batch to contain an 'actions' entry.")
             act_chunks = batch["actions"][..., : self.num_dof]
-            params.append(self.compute_weights(act_chunks))
+            if self._listable(act_chunks, group):
+                group.append(act_chunks)
+                if len(group) * act_chunks.shape[0] >= self._FIT_GROUP_ROWS:
+                    params.append(self._fit_list(group))
+                    group = []
+            else:
+                if group:
+                    params.append(self._fit_list(group))
+                    group = []
+                params.append(self.compute_weights(act_chunks))
             sample_count += 1
             if sample_count >= sample_limit:
                 if verbose:
                     print("Precomputed enough samples for weight normalizer of MP")
                 break
+        if group:
+            params.append(self._fit_list(group))
         if not params and process_group is None:
             raise RuntimeError("No parameters were gathered from the dataloader.")
         # per-batch params are read in place by the quantile kernels (no concatenation)
@@ -489,6 +501,36 @@ class BEASTBsplineTokenizer(TokenizerBase):
     # ===============================================
     #              - tokenizer utils -
     # ===============================================
+
+    _FIT_GROUP_ROWS = 1 << 18   # rows per grouped fit launch (HBM-bound from ~64 k rows)
+
+    def _listable(self, x, group) -> bool:
+        """Can batch ``x`` join ``group`` for one beast_encode_list_f32 launch?  Device-resident
+        contiguous fp32 [B, T, D] with B % 8 == 0 and 16-byte aligned rows, all of one shape
+        (anything else takes the per-batch path)."""
+        if not isinstance(x, torch.Tensor) or self._conditioned or x.dim() != 3:
+            return False
+        p = self._plan()
+        if (x.device != p.dev or x.dtype is not torch.float32 or not x.is_contiguous() or x.shape[0] == 0
+                or x.shape[0] % 8 or x.shape[1] != p.T or x.shape[2] < p.min_din or x.data_ptr() % 16
+                or (x.shape[1] * x.shape[2]) % 4):
+            return False
+        return not group or group[0].shape == x.shape
+
+    def _fit_list(self, group) -> torch.Tensor:
+        """Params of a group of batches by one launch (bitwise the per-batch params)."""
+        p = self._plan()
+        if len(group) == 1:
+            return self.compute_weights(group[0])
+        B, T, Din = group[0].shape
+        ptrs = torch.tensor([g.data_ptr() for g in group], dtype=torch.int64).pin_memory()
+        ptrs = ptrs.to(p.dev, non_blocking=True)
+        out = torch.empty((len(group) * B, self.num_dof * self.num_basis), dtype=torch.float32, device=p.dev)
+        _lib.run("beast_encode_list_f32", ptrs.data_ptr(), len(group), B, T, Din, self.num_dof, self.joint_dof,
+                 p.p_src, p.p_proj, self.num_basis, out.data_ptr(), _lib.raw_stream(p.idx))
+        # the pointer table and the batches may be freed after this: the caching allocators
+        # reuse their memory only in the order of the current stream (pinned: after the copy)
+        return out
 
     @torch.no_grad()
     def compute_weights(self, demos):

@@ -238,7 +238,16 @@ struct EncArgs {
   float* params_out;
   long long* tokens_out;
   Geom g;
+  const float* const* traj_list;   // list mode: batch i at traj_list[i], list_rows rows each
+  int64_t list_rows;               //   (a multiple of the tile, so no tile straddles two batches)
 };
+
+// First trajectory of tile row b0 (FAST path: contiguous rows of stride sb)
+__device__ __forceinline__ const float* enc_tile_src(const EncArgs& a, int64_t b0) {
+  if (a.traj_list == nullptr) return a.traj + b0 * a.sb;
+  const uint64_t bi = (uint64_t)b0 / (uint64_t)a.list_rows;
+  return a.traj_list[bi] + (b0 - (int64_t)bi * a.list_rows) * a.sb;
+}
 
 struct EncSmem {
   int P, Y, pb, kq, wlo, whi, lcol, total;
@@ -290,7 +299,7 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
   if (FAST && (a.phases & 1) && blockIdx.x < a.ntiles) {
     const int64_t b0 = (int64_t)blockIdx.x * TBT;
     const int nb = (int)min<int64_t>(TBT, a.B - b0);
-    dma16<NT>(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
+    dma16<NT>(Y, enc_tile_src(a, b0), (nb * tile_elems) >> 2);
   }
   STAMP(0, 9);
   dma16<NT>(P, a.proj, nkinds * 4 * Tp);
@@ -313,7 +322,7 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
     // ---- the trajectory tile lands in LDS (the first one is already in flight)
     if (a.phases & 1) {
       if (FAST) {
-        if (tile != blockIdx.x) dma16<NT>(Y, a.traj + b0 * a.sb, (nb * tile_elems) >> 2);
+        if (tile != blockIdx.x) dma16<NT>(Y, enc_tile_src(a, b0), (nb * tile_elems) >> 2);
       } else {
         const int pt = T * D;
         for (int e = tid; e < nb * pt; e += NT) {
@@ -1188,9 +1197,12 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   const bool fast = contiguous && tbt * traj_bytes <= 32 * 1024;
   if (!fast) tbt = 8;
   if (forced == 1 || forced == 2 || forced == 4 || (forced == 8 && fast)) tbt = std::min(tbt, forced);
+  // list mode: the contiguous DMA path only, tiles of one batch each
+  BEAST_REQUIRE(!a.traj_list || (fast && a.list_rows % tbt == 0),
+                "encode list: rows must be contiguous and rows per batch a multiple of %d", tbt);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
     const bool wide = wide_blocks((a.B + 7) / 8);
-    if (pipe_encode((a.B + 7) / 8)) {
+    if (!a.traj_list && pipe_encode((a.B + 7) / 8)) {
       if (D == 14 && nj == 14) return launch_encode_pipe<Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, s);
       if (D == 14 && nj == 12) return launch_encode_pipe<Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, s);
     }
@@ -1279,6 +1291,26 @@ extern "C" int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb,
   a.traj = traj; a.B = B; a.sb = sb; a.st = st; a.sd = sd; a.row_elems = row_elems; a.vocab = vocab;
   a.phases = debug_phases(); a.dof_src = dof_src; a.proj = proj; a.w_min = w_min; a.w_max = w_max;
   a.tok_offset = tok_offset; a.params_out = params_out; a.tokens_out = reinterpret_cast<long long*>(tokens_out);
+  return launch_encode(a, T, D, n_joint, N, beast::as_stream(stream));
+}
+
+extern "C" int beast_encode_list_f32(const float* const* traj_list, int nbatch, int64_t rows_per_batch, int T,
+                                     int row_elems, int D, int n_joint, const int32_t* dof_src, const float* proj,
+                                     int N, float* params_out, void* stream) {
+  BEAST_REQUIRE(traj_list && dof_src && proj && params_out, "beast_encode_list_f32: null pointer");
+  BEAST_REQUIRE(nbatch >= 0 && rows_per_batch >= 0, "beast_encode_list_f32: negative sizes");
+  BEAST_REQUIRE(rows_per_batch % 8 == 0, "rows_per_batch=%lld is not a multiple of 8", (long long)rows_per_batch);
+  BEAST_REQUIRE(T >= 1 && T <= MAX_T, "seq_len T=%d outside [1, %d]", T, MAX_T);
+  BEAST_REQUIRE(N >= 1 && N <= MAX_N, "num_basis N=%d outside [1, %d]", N, MAX_N);
+  BEAST_REQUIRE(D >= 1 && D <= MAX_D && n_joint >= 0 && n_joint <= D, "bad DoF split D=%d n_joint=%d", D, n_joint);
+  BEAST_REQUIRE(row_elems >= 1 && ((int64_t)T * row_elems) % 4 == 0,
+                "beast_encode_list_f32: T*row_elems must be a multiple of 4");
+  if (nbatch == 0 || rows_per_batch == 0) return BEAST_OK;
+  EncArgs a{};
+  a.traj = nullptr; a.traj_list = traj_list; a.list_rows = rows_per_batch;
+  a.B = (int64_t)nbatch * rows_per_batch; a.sb = (int64_t)T * row_elems; a.st = row_elems; a.sd = 1;
+  a.row_elems = row_elems; a.vocab = 0; a.phases = debug_phases(); a.dof_src = dof_src; a.proj = proj;
+  a.params_out = params_out;
   return launch_encode(a, T, D, n_joint, N, beast::as_stream(stream));
 }
 

@@ -167,11 +167,13 @@ def fit_bench(dev, args, world, rank):
             el = float(tt.item())
         times.append(el)
     el = float(np.median(times))
-    # stage split on this rank: the batched fits alone
+    # stage split on this rank: the fits alone, grouped as fit_parameters groups them
+    per = max(ftok._FIT_GROUP_ROWS // 4096, 1)
+    groups = [[b["actions"] for b in loader[i:i + per]] for i in range(0, len(loader), per)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for b in loader:
-        ftok.compute_weights(b["actions"])
+    for grp in groups:
+        ftok._fit_list(grp)
     torch.cuda.synchronize()
     t_fit = time.perf_counter() - t0
     n = per_rank * world

@@ -93,6 +93,16 @@ int beast_encode_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st
                      const float* w_min, const float* w_max, int vocab, int64_t tok_offset,
                      float* params_out, int64_t* tokens_out, void* stream);
 
+/* Params-only fit of a LIST of batches in one launch (fit_parameters, reference :181-220,
+ * which fits every dataloader batch then takes quantiles): batch i's rows start at the
+ * device pointer traj_list[i] (traj_list itself is a device array of nbatch pointers, each
+ * 16-byte aligned), every batch has rows_per_batch (a multiple of 8) contiguous rows of
+ * [T][row_elems] fp32; params_out [nbatch * rows_per_batch][D*N] (d n).  Same kernel and
+ * arithmetic as beast_encode_f32, so params are bitwise those of per-batch calls. */
+int beast_encode_list_f32(const float* const* traj_list, int nbatch, int64_t rows_per_batch, int T, int row_elems,
+                          int D, int n_joint, const int32_t* dof_src, const float* proj, int N, float* params_out,
+                          void* stream);
+
 /* Quantise-only epilogue of the above for already-fitted params [B][D*N] (d n):
  * used by encode(update_bounds=True) after the bounds move (:415-420).
  * mode 0: tokens_out int64 [B][N*D] (continuous_to_discrete + offset);

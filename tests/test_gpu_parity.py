@@ -369,6 +369,38 @@ def test_fit_parameters(name, golden, gpu_device):
         tok.fit_parameters([], verbose=False)
 
 
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_fit_parameters_grouped_launch(name, golden, gpu_device):
+    """Device-resident batches are fitted in groups by beast_encode_list_f32: params bitwise
+    those of per-batch compute_weights, bounds those of the oracle's quantiles; batches that
+    cannot join a group (host tensors, B % 8 != 0, another shape) interleave correctly."""
+    g = golden[name]
+    tok = make_tok(name, g, gpu_device)
+    gi = CONFIGS[name]["gripper_indices"] or []
+    D = CONFIGS[name]["num_dof"]
+    xs = [torch.from_numpy(synth_trajectories(n, 50, D, seed=3, gripper_indices=gi, start=4096 * i))
+          for i, n in enumerate([1024, 1024, 1024, 512, 1020, 1024, 1024, 1024, 1024, 8])]
+    loader = [{"actions": x.to(gpu_device)} for x in xs]
+    loader[5]["actions"] = xs[5]                     # a host batch in the middle of a group
+    tok._FIT_GROUP_ROWS = 2048                        # several groups, and a group of one
+    ptrs = [x.data_ptr() for x in (b["actions"] for b in loader)]
+    listable = (50 * D) % 4 == 0                       # whole 16-byte rows (not D = 7)
+    assert tok._listable(loader[0]["actions"], []) == listable and not tok._listable(loader[4]["actions"], [])
+    if listable:
+        grouped = tok._fit_list([b["actions"] for b in loader[6:9]])
+        single = torch.cat([tok.compute_weights(b["actions"]) for b in loader[6:9]])
+        assert torch.equal(grouped, single)
+    tok.fit_parameters(loader, verbose=False)
+    assert ptrs == [b["actions"].data_ptr() for b in loader]
+    allp = torch.cat([tok.compute_weights(b["actions"]) for b in loader]).cpu().numpy()
+    lo, hi = O.quantile_bounds(allp)
+    assert np.array_equal(tok.w_min.cpu().numpy(), lo)
+    assert np.array_equal(tok.w_max.cpu().numpy(), hi)
+    tok.fit_parameters(loader, max_samples=3, verbose=False)   # stops mid-group
+    lo3, hi3 = O.quantile_bounds(allp[:3072])
+    assert np.array_equal(tok.w_min.cpu().numpy(), lo3) and np.array_equal(tok.w_max.cpu().numpy(), hi3)
+
+
 def test_encode_continuous_and_back(golden, gpu_device):
     g = golden["k3"]
     tok = make_tok("k3", g, gpu_device)

@@ -63,6 +63,7 @@ def test_abi_version():
                           None)),
     ("beast_reconstruct_f32", (None, 4, 14, 14, 10, 256, 0, None, None, None, 0, 50, None, 14, None, 0, None,
                                None, None, None, None)),
+    ("beast_encode_list_f32", (None, 3, 4096, 50, 14, 14, 14, None, None, 10, None, None)),
     ("beast_bpe_argmax", (None, 300, 300, None, 0, None)),
 ])
 def test_null_pointers_are_rejected_before_any_hip_call(name, args):
@@ -121,3 +122,15 @@ def test_options_validate_and_reset():
     assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, 5) == _lib.BEAST_E_INVALID
     assert lib.beast_set_option(99, 0) == _lib.BEAST_E_INVALID
     assert b"option" in lib.beast_last_error()
+
+
+def test_encode_list_validation():
+    lib = _lib.load()
+    fake = C.c_void_p(16)                   # never dereferenced: validation fails first
+    # rows per batch not a multiple of the 8-trajectory tile
+    assert lib.beast_encode_list_f32(fake, 3, 4092, 50, 14, 14, 14, fake, fake, 10, fake, None) == _lib.BEAST_E_INVALID
+    assert b"multiple of 8" in lib.beast_last_error()
+    # T * row_elems not a whole number of 16-byte vectors
+    assert lib.beast_encode_list_f32(fake, 3, 4096, 49, 7, 7, 7, fake, fake, 10, fake, None) == _lib.BEAST_E_INVALID
+    assert lib.beast_encode_list_f32(fake, -1, 4096, 50, 14, 14, 14, fake, fake, 10, fake, None) == _lib.BEAST_E_INVALID
+    assert lib.beast_encode_list_f32(fake, 0, 4096, 50, 14, 14, 14, fake, fake, 10, fake, None) == 0
