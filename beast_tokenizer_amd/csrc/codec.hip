@@ -669,8 +669,10 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
 
   if (mw) {
     const float4* src = reinterpret_cast<const float4*>(a.traj);
+    // sources clamped to the sub-tile's own last vector (the padding re-reads a line this
+    // workgroup already fetches, not the next workgroup's trajectories)
     const int64_t last = a.B * tile16 - 1;
-    dma16_fixed<PS::Y_OPS>(YA, src, b0 * tile16, last);
+    dma16_fixed<PS::Y_OPS>(YA, src, b0 * tile16, min(last, (b0 + PIPE_SUB) * tile16 - 1));
     const int nk16 = ((m.nj < m.D) ? 2 : 1) * 4 * PS::Tp;
     dma16_fixed<PS::P_OPS>(P, reinterpret_cast<const float4*>(a.proj), 0, nk16 - 1);
     if (quant) {
@@ -678,7 +680,7 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
       dma4<PIPE_MT>(whi, a.w_max, PS::DN);
     }
     dma4<PIPE_MT>(lcol, a.dof_src, PS::D);
-    dma16_fixed<PS::Y_OPS>(YB, src, (b0 + PIPE_SUB) * tile16, last);
+    dma16_fixed<PS::Y_OPS>(YB, src, min(last, (b0 + PIPE_SUB) * tile16), min(last, (b0 + 2 * PIPE_SUB) * tile16 - 1));
     wait_vm_lgkm<PS::Y_OPS>();   // A and the constants have landed (B's DMA is the newest)
   }
   bar_only();
