@@ -2,9 +2,9 @@
 // driven by beast/beast_bpe_trainer.py:61-98; semantics in SURVEY.md §8a H9-H11).
 //
 //   k_minmax / k_bitmap      global min/max bin, occupied code points (alphabet)
-//   k_pretok<EMIT>           GPT-2 regex pre-tokeniser as a per-sequence state machine
-//                            over a code-point class LUT; pass 1 counts words / byte
-//                            symbols, pass 2 writes byte symbols as vocab ids
+//   k_pretok_wave<EMIT>      GPT-2 regex pre-tokeniser, one wave per sequence over a
+//                            code-point class LUT; pass 1 counts words / byte symbols,
+//                            pass 2 writes byte symbols as vocab ids
 //   k_scan_*                 exclusive prefix sums (word / symbol offsets)
 //   k_count_pairs            dense [Vt][Vt] uint32 pair table += word count
 //   k_argmax                 (count, -pair) max over the live table -> one u64 key
@@ -87,17 +87,15 @@ __device__ __forceinline__ int contraction(const long long* __restrict__ s, int6
   return 0;
 }
 
-// One thread per sequence.  Regex alternatives, leftmost first:
+// One sequence, serially.  Regex alternatives, leftmost first:
 //   contraction | ' '?L+ | ' '?N+ | ' '?[^\s L N]+ | \s+(?!\S) | \s+
 template <bool EMIT>
-__global__ void k_pretok(const long long* __restrict__ tok, const int64_t* __restrict__ seq_off, int64_t n_seq,
-                         long long mn, const uint8_t* __restrict__ lut, int64_t lut_n,
-                         int64_t* __restrict__ words_per_seq, int64_t* __restrict__ syms_per_seq,
-                         const int64_t* __restrict__ word_off, const int64_t* __restrict__ sym_off,
-                         const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym,
-                         uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlen) {
-  const int64_t sidx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (sidx >= n_seq) return;
+__device__ void pretok_serial(const long long* __restrict__ tok, const int64_t* __restrict__ seq_off, int64_t sidx,
+                              long long mn, const uint8_t* __restrict__ lut, int64_t lut_n,
+                              int64_t* __restrict__ words_per_seq, int64_t* __restrict__ syms_per_seq,
+                              const int64_t* __restrict__ word_off, const int64_t* __restrict__ sym_off,
+                              const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym,
+                              uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlen) {
   const long long* s = tok + seq_off[sidx];
   const int64_t n = seq_off[sidx + 1] - seq_off[sidx];
   int64_t nw = 0, ns = 0;
@@ -147,6 +145,152 @@ __global__ void k_pretok(const long long* __restrict__ tok, const int64_t* __res
   if (!EMIT) {
     words_per_seq[sidx] = nw;
     syms_per_seq[sidx] = ns;
+  }
+}
+
+// One thread per sequence (tools A/B: -DBPE_SERIAL_PRETOK_TRAIN)
+template <bool EMIT>
+__global__ void k_pretok(const long long* __restrict__ tok, const int64_t* __restrict__ seq_off, int64_t n_seq,
+                         long long mn, const uint8_t* __restrict__ lut, int64_t lut_n,
+                         int64_t* __restrict__ words_per_seq, int64_t* __restrict__ syms_per_seq,
+                         const int64_t* __restrict__ word_off, const int64_t* __restrict__ sym_off,
+                         const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym,
+                         uint32_t* __restrict__ wstart, uint32_t* __restrict__ wlen) {
+  const int64_t sidx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (sidx >= n_seq) return;
+  pretok_serial<EMIT>(tok, seq_off, sidx, mn, lut, lut_n, words_per_seq, syms_per_seq, word_off, sym_off, byte2id, sym,
+                      wstart, wlen);
+}
+
+// One wave per sequence.  A thread per sequence reads its row 8 B at a time at a 1 KiB
+// stride (every load instruction touches 64 cache lines), branches on its own word
+// structure, and scatters 2-byte stores the same way.  Here the lanes load the row coalesced
+// into LDS, classify it, evaluate the regex from every position at once (end of the word
+// that would start there), scan the UTF-8 lengths, and lane 0 only follows the word chain
+// 0 -> end[0] -> ...; the emission is lane-parallel over words and code points, so the
+// stores of a wave land in one contiguous stretch.  Rows longer than PT_LC code points (or
+// with code points outside [0, 2^31)) take pretok_serial on lane 0.
+constexpr int PT_LC = 512;
+constexpr int PT_WAVES = 4;
+struct PtLds {
+  int32_t cp[PT_LC];
+  int16_t nxt[PT_LC];       // end of the word starting at i
+  int16_t so[PT_LC + 1];    // byte-symbol offset of code point i
+  int16_t wcp[PT_LC + 1];   // first code point of word w
+  uint8_t cls[PT_LC];
+  int32_t nw;
+};
+
+__device__ __forceinline__ void pt_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(64 * PT_WAVES) void k_pretok_wave(
+    const long long* __restrict__ tok, const int64_t* __restrict__ seq_off, int64_t n_seq, long long mn,
+    const uint8_t* __restrict__ lut, int64_t lut_n, int64_t* __restrict__ words_per_seq,
+    int64_t* __restrict__ syms_per_seq, const int64_t* __restrict__ word_off, const int64_t* __restrict__ sym_off,
+    const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym, uint32_t* __restrict__ wstart,
+    uint32_t* __restrict__ wlen) {
+  __shared__ PtLds lds[PT_WAVES];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  PtLds& L = lds[wv];
+  for (int64_t sidx = (int64_t)blockIdx.x * PT_WAVES + wv; sidx < n_seq; sidx += (int64_t)gridDim.x * PT_WAVES) {
+    const int64_t r0 = seq_off[sidx], n64 = seq_off[sidx + 1] - r0;
+    bool serial = n64 > PT_LC;
+    const int n = serial ? 0 : (int)n64;
+    // 1. code points and classes (coalesced), then the UTF-8 symbol offsets
+    int carry = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      int len = 0;
+      if (i < n) {
+        const long long c = tok[r0 + i] - mn;
+        serial |= (c < 0) | (c > 0x7FFFFFFFLL);
+        L.cp[i] = (int32_t)c;
+        L.cls[i] = (c >= 0 && c < lut_n) ? lut[c] : (uint8_t)CLS_OTHER;
+        len = utf8_len(c);
+      }
+      int x = len;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      if (i < n) L.so[i] = (int16_t)(carry + x - len);
+      carry += __shfl(x, 63);
+    }
+    if (__any(serial)) {   // wave-uniform
+      if (lane == 0)
+        pretok_serial<EMIT>(tok, seq_off, sidx, mn, lut, lut_n, words_per_seq, syms_per_seq, word_off, sym_off,
+                            byte2id, sym, wstart, wlen);
+      continue;
+    }
+    if (lane == 0) L.so[n] = (int16_t)carry;
+    pt_wave_sync();
+    // 2. the end of the word that starts at every position (pretok_serial's rules)
+    for (int i = lane; i < n; i += 64) {
+      const int c = L.cp[i];
+      int j = 0;
+      if (c == '\'' && i + 1 < n) {
+        const int c1 = L.cp[i + 1];
+        if (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd') j = i + 2;
+        else if (i + 2 < n) {
+          const int c2 = L.cp[i + 2];
+          if ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l')) j = i + 3;
+        }
+      }
+      if (j == 0) {
+        int k = L.cls[i], st = i;
+        if (c == ' ' && i + 1 < n && L.cls[i + 1] != CLS_WS) { k = L.cls[i + 1]; st = i + 1; }
+        if (k != CLS_WS) {
+          j = st + 1;
+          while (j < n && L.cls[j] == k) ++j;
+        } else {
+          j = i + 1;
+          while (j < n && L.cls[j] == CLS_WS) ++j;
+          if (j < n && j - i >= 2) --j;   // \s+(?!\S): leave the last blank for the next word
+        }
+      }
+      L.nxt[i] = (int16_t)j;
+    }
+    pt_wave_sync();
+    // 3. lane 0 follows the chain
+    if (lane == 0) {
+      int nw = 0, p = 0;
+      while (p < n) {
+        L.wcp[nw++] = (int16_t)p;
+        p = L.nxt[p];
+      }
+      L.wcp[nw] = (int16_t)n;
+      L.nw = nw;
+    }
+    pt_wave_sync();
+    const int nw = L.nw;
+    if (!EMIT) {
+      if (lane == 0) {
+        words_per_seq[sidx] = nw;
+        syms_per_seq[sidx] = carry;
+      }
+    } else {
+      // 4. words (start, length) and byte symbols, lane-parallel
+      const int64_t wo = word_off[sidx], so0 = sym_off[sidx];
+      for (int w = lane; w < nw; w += 64) {
+        const int s0 = L.so[L.wcp[w]], s1 = L.so[L.wcp[w + 1]];
+        wstart[wo + w] = (uint32_t)(so0 + s0);
+        wlen[wo + w] = (uint32_t)(s1 - s0);
+      }
+      for (int i = lane; i < n; i += 64) {
+        uint8_t b[4];
+        const long long cp = L.cp[i];
+        const int Lb = utf8_len(cp);
+        utf8_bytes(cp, b);
+        uint16_t* o = sym + so0 + L.so[i];
+        for (int q = 0; q < Lb; ++q) o[q] = byte2id[b[q]];
+      }
+    }
+    pt_wave_sync();   // LDS is reused by the next sequence
   }
 }
 
@@ -1171,7 +1315,12 @@ extern "C" int beast_bpe_pretok_count(const int64_t* tok, const int64_t* seq_off
                                       int64_t* syms_per_seq, void* stream) {
   BEAST_REQUIRE(tok && seq_off && cls_lut && words_per_seq && syms_per_seq, "beast_bpe_pretok_count: null pointer");
   if (n_seq <= 0) return BEAST_OK;
+#ifdef BPE_SERIAL_PRETOK_TRAIN
   hipLaunchKernelGGL(k_pretok<false>, dim3((n_seq + 127) / 128), dim3(128), 0, beast::as_stream(stream),
+#else
+  hipLaunchKernelGGL(k_pretok_wave<false>, dim3(grid_for(n_seq, PT_WAVES, 16384)), dim3(64 * PT_WAVES), 0,
+                     beast::as_stream(stream),
+#endif
                      reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n,
                      words_per_seq, syms_per_seq, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   BEAST_LAUNCHED("k_pretok<count>");
@@ -1199,7 +1348,12 @@ extern "C" int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off,
   BEAST_REQUIRE(tok && seq_off && cls_lut && word_off && sym_off && byte2id && sym && wstart && wlen,
                 "beast_bpe_pretok_emit: null pointer");
   if (n_seq <= 0) return BEAST_OK;
+#ifdef BPE_SERIAL_PRETOK_TRAIN
   hipLaunchKernelGGL(k_pretok<true>, dim3((n_seq + 127) / 128), dim3(128), 0, beast::as_stream(stream),
+#else
+  hipLaunchKernelGGL(k_pretok_wave<true>, dim3(grid_for(n_seq, PT_WAVES, 16384)), dim3(64 * PT_WAVES), 0,
+                     beast::as_stream(stream),
+#endif
                      reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n,
                      nullptr, nullptr, word_off, sym_off, byte2id, sym, wstart, wlen);
   BEAST_LAUNCHED("k_pretok<emit>");

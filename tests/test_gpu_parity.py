@@ -500,6 +500,35 @@ def test_bpe_pretok_words_match_hf(gpu_device):
     assert got == pieces
 
 
+def test_bpe_pretok_ragged_rows_match_oracle(gpu_device):
+    """Wave-per-sequence pre-tokeniser on ragged rows: empty, one code point, rows at and past
+    the LDS row bound (512: lane 0 falls back to the serial walk), contractions, blank runs,
+    2-byte code points -- words and byte symbols equal the regex oracle's (bpe_oracle.pretokenize)."""
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet
+    from beast_tokenizer_amd.pretok import class_lut
+    from cpu_ops import NumpyBpeOps
+    rng = np.random.default_rng(5)
+    # letters, digits, blanks, apostrophe + contraction letters, punctuation, Latin-1 letters
+    alphabet = np.array([ord(c) for c in "ab z09 '  \t\nstrevmld!?,."] + [0xA0, 0xC4, 0xE9, 0xB5, 0xD7, 0x85])
+    lens = [0, 1, 2, 3, 63, 64, 65, 140, 511, 512, 513, 777, 140, 0, 2000] + list(rng.integers(0, 300, 40))
+    seqs = [alphabet[rng.integers(0, alphabet.size, n)].astype(np.int64) + 7 for n in lens]
+    tokens = torch.from_numpy(np.concatenate(seqs)).to(gpu_device)
+    off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(gpu_device)
+    K = int(alphabet.max()) + 1
+    present = np.zeros(K, dtype=bool)
+    present[alphabet] = True
+    _, _, byte2id = build_alphabet(present, [chr(i) for i in range(K)], [])
+    w = GpuBpeOps(gpu_device).pretokenize(tokens, off, 7, class_lut(K), byte2id)
+    sym = w["sym"].cpu().numpy().view(np.uint16)
+    ws, wl = w["wstart"].cpu().numpy(), w["wlen"].cpu().numpy()
+    got = [sym[a:a + n].tolist() for a, n in zip(ws[: w["n_words"]], wl[: w["n_words"]])]
+    want = NumpyBpeOps().pretokenize(tokens.cpu(), off.cpu(), 7, class_lut(K), byte2id)
+    assert w["n_syms"] == want["n_syms"]
+    assert got == want["words"]
+    # the words tile the symbol array in order
+    assert ws[0] == 0 and np.all(ws[1: w["n_words"]] == (ws + wl)[: w["n_words"] - 1])
+
+
 def test_bpe_dedup_and_compact_match_counter(gpu_device):
     """Distinct words x counts equal a Counter over the pre-tokenised words (>= 2 symbols);
     compaction keeps exactly the words that can still merge."""
