@@ -194,7 +194,12 @@ class GpuBpeModel:
             exc, msg = _ENC_ERRORS[int(ls[1][bad[0]])]
             raise exc(msg)
         w = int(ls[0].max())
-        ids_np = ids[:, :w].cpu().numpy()
+        ids_h = ids[:, :w].contiguous().cpu()
+        from .beast_bspline_tokenizer import _fastpath
+        fp = _fastpath()
+        if fp is not None:   # host C++ list builder (csrc/fastpath.cpp)
+            return fp.rows_to_lists(ids_h, torch.from_numpy(np.ascontiguousarray(ls[0], dtype=np.int32)))
+        ids_np = ids_h.numpy()
         lens_np = ls[0]
         return [ids_np[i, :lens_np[i]].tolist() for i in range(R)]
 

@@ -1,4 +1,5 @@
-// Host fast path for BEASTBsplineTokenizer.encode / reconstruct_traj (default time grid).
+// Host fast path for BEASTBsplineTokenizer.encode / reconstruct_traj (default time grid), and
+// the List[List[int]] builder of the BPE tokenizer's encode (rows_to_lists).
 //
 // Host-side C++ only: the same C-ABI entry points the ctypes binding calls
 // (beast_encode_f32 / beast_reconstruct_f32 in libbeast_hip.so, passed in as function
@@ -9,9 +10,11 @@
 // takes the general Python path, which raises the reference's exception types.
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace {
 
@@ -102,6 +105,42 @@ Plan make_plan(int64_t enc, int64_t rec, int64_t err, int64_t device, int64_t D,
   return p;
 }
 
+// BPE encode's result as the reference returns it, List[List[int]] (beast_bspline_bpe_tokenizer.py
+// :175-199 builds one list per row from HF's ids): rows ids[r, :lens[r]] of a host int32 [R, W]
+// tensor.  The per-element cost of building Python ints dominates the list comprehension, so ids
+// below 65,536 share one cached int object each (ints are immutable; each slot holds a reference).
+py::list rows_to_lists(const at::Tensor& ids, const at::Tensor& lens) {
+  if (ids.is_cuda() || lens.is_cuda() || ids.scalar_type() != at::kInt || lens.scalar_type() != at::kInt ||
+      ids.dim() != 2 || lens.dim() != 1 || lens.size(0) != ids.size(0) || !ids.is_contiguous() ||
+      !lens.is_contiguous())
+    throw std::invalid_argument("rows_to_lists: host int32 ids [R, W] and lens [R] expected");
+  static std::vector<PyObject*> cache;
+  if (cache.empty()) {
+    cache.resize(65536);
+    for (int i = 0; i < 65536; ++i) cache[i] = PyLong_FromLong(i);   // held for the process lifetime
+  }
+  const int64_t R = ids.size(0), W = ids.size(1);
+  const int32_t* p = ids.data_ptr<int32_t>();
+  const int32_t* L = lens.data_ptr<int32_t>();
+  PyObject* out = PyList_New(R);
+  if (!out) throw py::error_already_set();
+  for (int64_t r = 0; r < R; ++r) {
+    const int64_t n = std::min<int64_t>(std::max<int32_t>(L[r], 0), W);
+    PyObject* row = PyList_New(n);
+    if (!row) { Py_DECREF(out); throw py::error_already_set(); }
+    const int32_t* q = p + r * W;
+    for (int64_t i = 0; i < n; ++i) {
+      const int32_t v = q[i];
+      PyObject* o;
+      if (v >= 0 && v < 65536) { o = cache[v]; Py_INCREF(o); }
+      else if (!(o = PyLong_FromLong(v))) { Py_DECREF(row); Py_DECREF(out); throw py::error_already_set(); }
+      PyList_SET_ITEM(row, i, o);
+    }
+    PyList_SET_ITEM(out, r, row);
+  }
+  return py::reinterpret_steal<py::list>(out);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -111,4 +150,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("fit", &Plan::fit, py::arg("x"), py::arg("stream"))
       .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"));
   m.def("make_plan", &make_plan);
+  m.def("rows_to_lists", &rows_to_lists, py::arg("ids"), py::arg("lens"));
 }

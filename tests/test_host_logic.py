@@ -224,3 +224,22 @@ def test_times_version_bumps():
     v = t._times_version
     t.update_times(torch.linspace(0, 1, 80))
     assert t._times_version == v + 1 and t.times.numel() == 80
+
+
+def test_rows_to_lists_matches_numpy():
+    """The host C++ List[List[int]] builder of the BPE encode (csrc/fastpath.cpp) equals the
+    per-row numpy slicing it replaces: cached ids, ids outside the cache, empty and clipped rows."""
+    from beast_tokenizer_amd.beast_bspline_tokenizer import _fastpath
+    fp = _fastpath()
+    if fp is None:
+        pytest.skip("host fast path not built (python -m beast_tokenizer_amd._build)")
+    rng = np.random.default_rng(3)
+    ids = rng.integers(0, 2048, (64, 40)).astype(np.int32)
+    ids[1, :3] = [70000, -5, 65535]
+    lens = rng.integers(0, 41, 64).astype(np.int32)
+    lens[:3] = [40, 0, 41]   # a length past the width is clipped to it
+    got = fp.rows_to_lists(torch.from_numpy(ids), torch.from_numpy(lens))
+    assert got == [ids[i, :min(lens[i], 40)].tolist() for i in range(64)]
+    assert all(type(v) is int for row in got for v in row)
+    with pytest.raises(ValueError):
+        fp.rows_to_lists(torch.from_numpy(ids.astype(np.int64)), torch.from_numpy(lens))

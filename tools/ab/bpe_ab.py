@@ -1,6 +1,6 @@
 """A/B of the BPE training loop between two builds of libbeast_hip.so (tools only).
 
-    python tools/ab/bpe_ab.py build "-DX" "-DY"   # libA.so / libB.so from the tree with those defines
+    python tools/ab/bpe_ab.py build "-DX" "-DY" ...  # libA.so, libB.so, ... from the tree with those defines
     python tools/ab/bpe_ab.py run [n_traj]        # on the GPU box: interleaved, merges must agree
 """
 import json
@@ -15,9 +15,9 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
 
-def build(defs_a, defs_b):
+def build(*variants):
     from beast_tokenizer_amd import _build
-    for tag, defs in (("A", defs_a), ("B", defs_b)):
+    for tag, defs in zip("ABCDEFGH", variants):
         objs = []
         for f in sorted(os.listdir(_build.CSRC)):
             if f.endswith(".hip"):
@@ -43,10 +43,11 @@ def run(n):
             for s in range(0, n, 8192)]
     allrows = torch.cat(rows)
     torch.cuda.synchronize()
-    res = {"A": [], "B": []}
+    tags = [t for t in "ABCDEFGH" if os.path.exists(os.path.join(HERE, f"lib{t}.so"))]
+    res = {t: [] for t in tags}
     merges = {}
     for rep in range(3):
-        for tag in ("A", "B"):
+        for tag in tags:
             _lib._lib = None
             _lib.load(os.path.join(HERE, f"lib{tag}.so"))
             t0 = time.perf_counter()
@@ -57,13 +58,13 @@ def run(n):
             merges[tag] = r.merges
     out = {t: {"total_ms": round(1e3 * sorted(v)[1][0], 2), "setup_ms": round(1e3 * sorted(v)[1][1], 2),
                "loop_ms": round(1e3 * sorted(v)[1][2], 2)} for t, v in res.items()}
-    out["merges_equal"] = merges["A"] == merges["B"]
+    out["merges_equal"] = all(merges[t] == merges["A"] for t in tags)
     out["n_merges"] = len(merges["A"])
     print(json.dumps(out))
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
-        build(sys.argv[2], sys.argv[3])
+        build(*sys.argv[2:])
     else:
         run(int(sys.argv[2]) if len(sys.argv) > 2 else 500000)
