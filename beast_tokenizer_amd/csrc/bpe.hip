@@ -910,7 +910,10 @@ __device__ __forceinline__ void wave_fence_sync() {
 // own adds (the only deltas that can reach (a, b) are row a's, when a == b), tlen[new] set.
 // A row rescans only if it changed (or was never scanned); the workgroup folds its rows'
 // bests and makes one atomicMax into the result slot.
-constexpr int APPLY_ROWS = 4;   // rows (waves) per workgroup
+#ifndef APPLY_ROWS_N
+#define APPLY_ROWS_N 4
+#endif
+constexpr int APPLY_ROWS = APPLY_ROWS_N;   // rows (waves) per workgroup
 __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_argmax(uint32_t* __restrict__ table,
                                                                  int32_t* __restrict__ deltas, int Vt, int vcur,
                                                                  ArgWs aw, int parity, int apply, int a, int b,
@@ -1057,23 +1060,48 @@ __host__ __device__ inline uint64_t dedup_cap(int64_t n) {
 }
 
 // One thread per word.  The table slot of the word's content is found as before; then the
-// two atomics that serialised at the memory side are aggregated: new distinct words take their
-// list positions with one atomic per wave (ballot), and occurrence counts are summed per slot
-// in an LDS hash (DEDUP_LDS entries, linear probing; a full probe falls back to the global
-// atomic) and flushed once per workgroup -- the common words occur millions of times.
+// atomics that serialised at the memory side are aggregated.  New distinct words go to an LDS
+// list (one LDS atomic per wave) that the workgroup appends to the global list with ONE device
+// atomic when it is nearly full and at the end: the global list counter is a single address,
+// and one atomic per wave on it (576 k at K5, each waiting on the previous at the memory side)
+// took 7.2 ms of the 11.7 ms BPE setup.  Occurrence counts are summed per slot in an LDS hash
+// (DEDUP_LDS entries, linear probing; a full probe falls back to the global atomic) and flushed
+// once per workgroup -- the common words occur millions of times.
 constexpr int DEDUP_LDS = 4096;
+constexpr int DEDUP_NEW = 1024;   // LDS new-word list; flushed when a pass could overflow it
 __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                       const uint32_t* __restrict__ wlen, int64_t nw, DedupWs ws) {
   __shared__ uint32_t lkey[DEDUP_LDS];   // slot + 1, 0 = empty
   __shared__ uint32_t lcnt[DEDUP_LDS];
+  __shared__ uint32_t nrep[DEDUP_NEW], nslot[DEDUP_NEW];
+  __shared__ uint32_t ncnt;
+  __shared__ unsigned long long nbase;
   for (int i = threadIdx.x; i < DEDUP_LDS; i += blockDim.x) { lkey[i] = 0; lcnt[i] = 0; }
+  if (threadIdx.x == 0) ncnt = 0;
   __syncthreads();
   const uint64_t mask = ws.cap - 1;
   const int lane = threadIdx.x & 63;
   const int64_t G = (int64_t)gridDim.x * blockDim.x;
-  // wave-uniform trip count: every lane reaches the ballot below
-  for (int64_t w0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); w0 < nw; w0 += G) {
-    const int64_t w = w0 + lane;
+  // the workgroup's new words -> the global distinct list, one device atomic
+  auto flush_new = [&]() {
+    __syncthreads();
+    const uint32_t n = ncnt;
+    if (n) {
+      if (threadIdx.x == 0) nbase = atomicAdd(ws.nu, (unsigned long long)n);
+      __syncthreads();
+      const unsigned long long b = nbase;
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        ws.rep[b + i] = nrep[i];
+        ws.slot[b + i] = nslot[i];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) ncnt = 0;
+      __syncthreads();
+    }
+  };
+  // workgroup-uniform trip count: every thread reaches the barriers of flush_new
+  for (int64_t b0 = blockIdx.x * (int64_t)blockDim.x; b0 < nw; b0 += G) {
+    const int64_t w = b0 + threadIdx.x;
     bool is_new = false;
     uint64_t k = 0;
     bool have = false;
@@ -1104,17 +1132,17 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict
         }
       }
     }
-    // distinct-word list positions: one atomic per wave
+    // new distinct words -> the LDS list: one LDS atomic per wave
     const unsigned long long nb = __ballot(is_new);
     if (nb) {
-      unsigned long long base = 0;
+      uint32_t base = 0;
       const int leader = __ffsll((long long)nb) - 1;
-      if (lane == leader) base = atomicAdd(ws.nu, (unsigned long long)__popcll(nb));
+      if (lane == leader) base = atomicAdd(&ncnt, (uint32_t)__popcll(nb));
       base = __shfl(base, leader);
       if (is_new) {
-        const unsigned long long u = base + __popcll(nb & ((1ull << lane) - 1ull));
-        ws.rep[u] = (uint32_t)w;
-        ws.slot[u] = (uint32_t)k;
+        const uint32_t u = base + (uint32_t)__popcll(nb & ((1ull << lane) - 1ull));
+        nrep[u] = (uint32_t)w;
+        nslot[u] = (uint32_t)k;
       }
     }
     // occurrence count of slot k, aggregated in LDS
@@ -1129,7 +1157,10 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict
       }
       if (!done) atomicAdd(&ws.cnt[k], 1u);
     }
+    __syncthreads();
+    if (ncnt > (uint32_t)(DEDUP_NEW - 256)) flush_new();   // the next pass adds <= 256
   }
+  flush_new();
   __syncthreads();
   for (int i = threadIdx.x; i < DEDUP_LDS; i += blockDim.x)
     if (lkey[i]) atomicAdd(&ws.cnt[lkey[i] - 1u], lcnt[i]);
