@@ -562,7 +562,6 @@ __device__ __forceinline__ unsigned long long sig_bit(uint32_t x) {
 // merges involving it fall back to scanning every word.  Stale entries (a word that no
 // longer holds the symbol) are harmless: the probe finds no pair there.
 constexpr uint32_t IDX_INEXACT = 0xFFFFFFFFu;
-constexpr int64_t MERGE_LDS_MIN_COUNT = 1 << 16;
 
 
 #ifdef BPE_MERGE_STATS

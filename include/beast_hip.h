@@ -49,7 +49,7 @@ const char* beast_last_error(void);
  * kernels, 8 forces the pipelined 8-wave encode (0 = chosen by batch size); results are
  * identical.
  * BEAST_OPT_MERGE_LDS_MIN = n: BPE merges of pairs counted >= n privatise their pair-count deltas
- * in LDS (default 65536; below, global atomics); results are identical.
+ * in LDS (default 4096; below, global atomics); results are identical.
  * Not thread-safe with concurrent launches. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2

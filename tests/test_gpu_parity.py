@@ -481,6 +481,26 @@ def test_bpe_merge_paths_match_hf(case, index_mode, bpe_golden, gpu_device):
     assert [list(m) for m in res.merges] == ref[case]["merges"]
 
 
+@pytest.mark.parametrize("lds_min", [0, 1 << 30])
+@pytest.mark.parametrize("case", ["skew/2048", "traj_k3/2048"])
+def test_bpe_delta_paths_match_hf(case, lds_min, bpe_golden, gpu_device):
+    """k_merge's pair-count deltas privatised in LDS for every merge (threshold 0) and by global
+    atomics for every merge (threshold 2^30) both give HF's merges (default: LDS from 4,096)."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
+    ref, corpora = bpe_golden
+    cname, vs = case.split("/")
+    flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
+    lib = _lib.load()
+    assert lib.beast_set_option(_lib.OPT_MERGE_LDS_MIN, lds_min) == 0
+    try:
+        res = train_bpe(flat, off, int(vs))
+    finally:
+        lib.beast_set_option(_lib.OPT_MERGE_LDS_MIN, 4096)
+    assert res.vocab == ref[case]["vocab"]
+    assert [list(m) for m in res.merges] == ref[case]["merges"]
+
+
 def test_bpe_pretok_words_match_hf(gpu_device):
     from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, sequences_to_device
     from beast_tokenizer_amd.pretok import bytes_to_unicode, class_lut
