@@ -2,7 +2,7 @@
 // beast/beast_bspline_tokenizer.py:211-214) by radix select on gfx950.
 //
 // 1. k_keys      transpose x[rows][cols] (row-major params) into order-preserving
-//                uint32 keys [cols][rows] through a 32x33 LDS tile (coalesced both ways)
+//                uint32 keys [cols][rows] through a [KT_R][33] LDS tile (coalesced both ways)
 // 2. k_hist      per pass (digits of 11, 11, 10 bits from the top) and per target
 //                rank: LDS-privatised 2048-bin histograms of the keys whose
 //                higher bits equal the target's prefix, flushed with u64 atomics.
@@ -75,56 +75,61 @@ __device__ __forceinline__ void pass_geom(int pass, int& shift, int& bits) {
   bits = (pass == 2) ? 10 : 11;
 }
 
-__global__ void k_keys(const float* __restrict__ x, int64_t rows, int cols, int64_t rs, uint32_t* __restrict__ keys) {
-  __shared__ uint32_t tile[32][33];
-  const int64_t r0 = (int64_t)blockIdx.x * 32;
-  const int c0 = blockIdx.y * 32;
+// A workgroup moves a KT_R x 32 tile (16 KiB in, 16 KiB out; 16 loads in flight per thread):
+// a 32 x 32 tile kept too few bytes in flight per CU to cover HBM latency (3.2 TB/s at K4).
+constexpr int KT_R = 128;
+__device__ __forceinline__ void keys_tile(const float* __restrict__ src, int64_t stride, int nr, int c0, int cols,
+                                          uint32_t* __restrict__ dst, int64_t rows) {
+  __shared__ uint32_t tile[KT_R][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
-  for (int k = ty; k < 32; k += 8) {
-    const int64_t r = r0 + k;
-    const int c = c0 + tx;
-    if (r < rows && c < cols) tile[k][tx] = f2key(x[r * rs + c]);
+  const int c = c0 + tx;
+  float v[KT_R / 8];
+#pragma unroll
+  for (int i = 0; i < KT_R / 8; ++i) {
+    const int k = ty + 8 * i;
+    v[i] = (k < nr && c < cols) ? src[(int64_t)k * stride + c] : 0.0f;
   }
+#pragma unroll
+  for (int i = 0; i < KT_R / 8; ++i) tile[ty + 8 * i][tx] = f2key(v[i]);
   __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int c = c0 + k;
-    const int64_t r = r0 + tx;
-    if (r < rows && c < cols) keys[(int64_t)c * rows + r] = tile[tx][k];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cc = c0 + ty + 8 * j;
+    if (cc >= cols) continue;
+#pragma unroll
+    for (int i = 0; i < KT_R / 32; ++i) {
+      const int r = tx + 32 * i;
+      if (r < nr) dst[(int64_t)cc * rows + r] = tile[r][ty + 8 * j];
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void k_keys(const float* __restrict__ x, int64_t rows, int cols, int64_t rs,
+                                              uint32_t* __restrict__ keys) {
+  const int64_t r0 = (int64_t)blockIdx.x * KT_R;
+  const int nr = (int)min<int64_t>(KT_R, rows - r0);
+  keys_tile(x + r0 * rs, rs, nr, blockIdx.y * 32, cols, keys + r0, rows);
 }
 
 // The same transpose over a list of row-major segments (fit_parameters' per-batch params,
 // no torch.cat): seg[i] = {ptr, first row, row stride}, rows of segment i are
 // [seg[i].first, seg[i + 1].first) of the concatenated space.  Grid x = nseg * tiles_per_seg
-// 32-row tiles (tiles past a segment's end exit), so no tile never straddles two segments.
+// KT_R-row tiles (tiles past a segment's end exit), so no tile straddles two segments.
 struct QSeg {
   const float* ptr;
   int64_t first;
   int64_t stride;
 };
 
-__global__ void k_keys_seg(const QSeg* __restrict__ seg, int nseg, int tiles_per_seg, int64_t rows, int cols,
-                           uint32_t* __restrict__ keys) {
-  __shared__ uint32_t tile[32][33];
+__global__ __launch_bounds__(256) void k_keys_seg(const QSeg* __restrict__ seg, int nseg, int tiles_per_seg,
+                                                  int64_t rows, int cols, uint32_t* __restrict__ keys) {
   const int si = blockIdx.x / tiles_per_seg;
-  const int64_t t0 = (int64_t)(blockIdx.x % tiles_per_seg) * 32;
+  const int64_t t0 = (int64_t)(blockIdx.x % tiles_per_seg) * KT_R;
   const QSeg sg = seg[si];
   const int64_t seg_rows = ((si + 1 < nseg) ? seg[si + 1].first : rows) - sg.first;
-  if (t0 >= seg_rows) return;
-  const int nr = (int)min<int64_t>(32, seg_rows - t0);
-  const int64_t r0 = sg.first + t0;
-  const int c0 = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
-  const float* src = sg.ptr + t0 * sg.stride;
-  for (int k = ty; k < 32; k += 8) {
-    const int c = c0 + tx;
-    if (k < nr && c < cols) tile[k][tx] = f2key(src[(int64_t)k * sg.stride + c]);
-  }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int c = c0 + k;
-    if (tx < nr && c < cols) keys[(int64_t)c * rows + r0 + tx] = tile[tx][k];
-  }
+  if (t0 >= seg_rows) return;   // workgroup-uniform: before the tile's barrier
+  const int nr = (int)min<int64_t>(KT_R, seg_rows - t0);
+  keys_tile(sg.ptr + t0 * sg.stride, sg.stride, nr, blockIdx.y * 32, cols, keys + sg.first + t0, rows);
 }
 
 __global__ void k_init(QState* __restrict__ st, uint32_t* __restrict__ nanf, QHeader* __restrict__ hdr, int cols,
@@ -346,7 +351,7 @@ extern "C" int beast_quantile_prepare(const float* x, int64_t rows, int cols, in
                      reinterpret_cast<QHeader*>(ws + w.hdr), cols, h);
   BEAST_LAUNCHED("k_init");
   if (rows > 0) {
-    dim3 grid((unsigned)((rows + 31) / 32), (unsigned)((cols + 31) / 32));
+    dim3 grid((unsigned)((rows + KT_R - 1) / KT_R), (unsigned)((cols + 31) / 32));
     hipLaunchKernelGGL(k_keys, grid, dim3(256), 0, s, x, rows, cols, row_stride,
                        reinterpret_cast<uint32_t*>(ws + w.keys));
     BEAST_LAUNCHED("k_keys");
@@ -358,7 +363,7 @@ extern "C" int beast_quantile_prepare_segments(const void* seg_table, int nseg, 
                                                int cols, int64_t n_total, int n_q, const float* host_q,
                                                void* workspace, size_t ws_bytes, void* stream) {
   BEAST_REQUIRE(nseg >= 1 && seg_table, "beast_quantile_prepare_segments: need >= 1 segment");
-  const int64_t tps = (max_seg_rows + 31) / 32;
+  const int64_t tps = (max_seg_rows + KT_R - 1) / KT_R;
   BEAST_REQUIRE(max_seg_rows >= 0 && tps * nseg < (int64_t(1) << 31), "beast_quantile_prepare_segments: "
                 "%d segments of up to %lld rows are too many tiles", nseg, (long long)max_seg_rows);
   // header, state and ranks as for one matrix; x is only dereferenced by k_keys
