@@ -39,7 +39,17 @@ __global__ void k_minmax(const long long* __restrict__ x, int64_t n, long long* 
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
   }
-  if ((threadIdx.x & 63) == 0) {
+  // one pair of device atomics per workgroup: the two result words are single addresses,
+  // and atomics on one address serialise at the memory side
+  __shared__ long long smn[16], smx[16];
+  const int wv = threadIdx.x >> 6, nwv = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nwv; ++w) {
+      mn = smn[w] < mn ? smn[w] : mn;
+      mx = smx[w] > mx ? smx[w] : mx;
+    }
     atomicMin(&out[0], mn);
     atomicMax(&out[1], mx);
   }
@@ -54,7 +64,9 @@ __global__ void k_presence(const long long* __restrict__ x, int64_t n, long long
                            int64_t ncp) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const long long c = x[i] - mn;
-    if (c >= 0 && c < ncp) pr[c] = 1;  // every writer stores the same byte
+    // every writer stores the same byte; the few distinct bytes are written once each instead
+    // of once per token (the read hits the cache)
+    if (c >= 0 && c < ncp && !pr[c]) pr[c] = 1;
   }
 }
 
