@@ -24,6 +24,7 @@ ABI_VERSION = 1
 OPT_GENERIC_KERNELS = 1
 OPT_BLOCK_WAVES = 2
 OPT_MERGE_LDS_MIN = 3
+OPT_MERGE_LIST_RATIO = 4
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 
@@ -71,6 +72,11 @@ SIGNATURES = {
     "beast_bpe_loop_steps": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp,
                                     _vp, _i32, _vp]),
     "beast_bpe_loop_state": (_i32, [_vp, _i32, _i32, _vp, _vp]),
+    "beast_bpe_pair_index_bytes": (_sz, [_i32, _i64]),
+    "beast_bpe_build_pair_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _i64, _vp, _sz, _vp]),
+    "beast_bpe_token_index_init": (_i32, [_vp, _sz, _i32, _vp]),
+    "beast_bpe_loop_steps_ix": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
+                                       _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),

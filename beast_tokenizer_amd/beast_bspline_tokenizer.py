@@ -532,6 +532,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if len(group) == 1:
             return self.compute_weights(group[0])
         B, T, Din = group[0].shape
+        if any(g.shape != group[0].shape for g in group):   # the launch reads B rows from every pointer
+            raise ValueError("_fit_list: every batch of a group must have the same shape")
         ptrs = torch.tensor([g.data_ptr() for g in group], dtype=torch.int64).pin_memory()
         ptrs = ptrs.to(p.dev, non_blocking=True)
         out = torch.empty((len(group) * B, self.num_dof * self.num_basis), dtype=torch.float32, device=p.dev)

@@ -35,6 +35,7 @@ Either way every rank holds the same table and takes the same decisions.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -236,6 +237,24 @@ class GpuBpeOps:
         _lib.run("beast_bpe_build_index", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
                  words["n_words"], Vt, self._index.data_ptr(), nb, self.stream)
 
+    def build_pair_index(self, words, n_sym: int, Vt: int):
+        """Candidate lists for the device loop (csrc/bpe.hip PairIndex): the CSR of distinct words
+        per setup-symbol pair and an empty token index for the merged tokens' word lists."""
+        lib = _lib.load()
+        n, ns = int(words["n_words"]), int(words.get("n_syms_distinct", words["n_syms"]))
+        if n_sym < 1 or n_sym > 4096 or 4 * Vt * 4 > 64 * 1024:
+            self._pair = None
+            return
+        nb = lib.beast_bpe_pair_index_bytes(n_sym, ns)
+        self._pair = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        _lib.run("beast_bpe_build_pair_index", words["sym"].data_ptr(), words["wstart"].data_ptr(),
+                 words["wlen"].data_ptr(), n, n_sym, ns, self._pair.data_ptr(), nb, self.stream)
+        self._pair_nsym = n_sym
+        cap = max(8 * n, 1 << 20)
+        tb = lib.beast_bpe_index_workspace_bytes(Vt, cap)
+        self._tokix = torch.empty((tb + 3) // 4, dtype=torch.int32, device=self.device)
+        _lib.run("beast_bpe_token_index_init", self._tokix.data_ptr(), tb, Vt, self.stream)
+
     def new_state(self, Vt: int, tlen: np.ndarray):
         nb = _lib.load().beast_bpe_argmax_workspace_bytes(Vt)
         self._argws = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=self.device)
@@ -293,19 +312,34 @@ class GpuBpeOps:
         state = ws[st_off:st_off + 32].view(torch.int32)     # active, a, b, nid, reused, vcur, parity, n
         host = torch.empty(8, dtype=torch.int32, pin_memory=True)
         vcur = n_tok
+        pair = getattr(self, "_pair", None)
+        apps = torch.zeros(2 * max_merges, dtype=torch.int32, device=self.device) if pair is not None else None
         while True:
             steps = max(1, min(chunk, vocab_size - vcur))
-            _lib.run("beast_bpe_loop_steps", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
-                     words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
-                     words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
-                     _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)), table.data_ptr(),
-                     self._argws.data_ptr(), vocab_size, self.stream)
+            if pair is not None:
+                _lib.run("beast_bpe_loop_steps_ix", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
+                         words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
+                         words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
+                         pair.data_ptr(), self._pair_nsym, self._tokix.data_ptr(), _lib.ptr(words.get("sig")),
+                         table.data_ptr(),
+                         self._argws.data_ptr(), vocab_size, apps.data_ptr(), self.stream)
+            else:
+                _lib.run("beast_bpe_loop_steps", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
+                         words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
+                         words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
+                         _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)), table.data_ptr(),
+                         self._argws.data_ptr(), vocab_size, self.stream)
             host.copy_(state, non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
             active, vcur, n = int(host[0]), int(host[5]), int(host[7])
             if not active or vcur >= vocab_size:
                 break
         full = n >= max_merges
+        self.last_apps = None
+        if apps is not None:
+            a = apps.cpu().numpy().astype(np.int64)
+            self.last_apps = a[:n]
+            self.last_visits = a[max_merges:max_merges + n]
         log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
         return [tuple(int(v) for v in r) for r in log], full
 
@@ -344,7 +378,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
               mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False,
-              device_loop: bool = True, replicate: bool = True) -> BPEResult:
+              device_loop: bool = True, replicate: bool = True, merge_mode: Optional[str] = None) -> BPEResult:
     """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard).
 
     Single process on the GPU ops: the merge loop runs device-driven (``GpuBpeOps.loop_run``,
@@ -396,8 +430,13 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     for i, s in enumerate(id2str):
         tlen[i] = len(s.encode("utf-8"))
     ops.new_state(Vt, tlen)
+    if merge_mode is None:
+        merge_mode = os.environ.get("BEAST_BPE_MERGE", "signature_scan")
     if use_index and hasattr(ops, "build_index"):
         ops.build_index(words, Vt)
+    elif (merge_mode == "pair_index" and device_loop and loop_reduce is no_reduce and not compact_every
+          and hasattr(ops, "build_pair_index")):
+        ops.build_pair_index(words, len(id2str), Vt)   # candidate lists instead of signature scans
     max_len = int(max_token_length) if max_token_length is not None else 2 ** 31 - 1
     merges: List[Tuple[str, str]] = []
     t1 = time.perf_counter()
@@ -425,7 +464,13 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         t2 = time.perf_counter()
         stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
                  "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
-                 "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce}
+                 "n_syms_distinct": words.get("n_syms_distinct"),
+                 "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce,
+                 "merge_mode": "pair_index" if getattr(ops, "_pair", None) is not None else "signature_scan"}
+        apps = getattr(ops, "last_apps", None)
+        if apps is not None:
+            stats["applications"] = apps.tolist()
+            stats["words_visited"] = ops.last_visits.tolist()
         return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
     while len(id2str) < vocab_size:
         count = key >> 32
@@ -452,6 +497,7 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     t2 = time.perf_counter()
     stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
              "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
+                 "n_syms_distinct": words.get("n_syms_distinct"),
              "Vt": Vt, "replicated": loop_reduce is not reduce}
     return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
 

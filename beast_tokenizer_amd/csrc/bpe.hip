@@ -903,6 +903,364 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   }
 }
 
+// ------------------------------------------------------------ pair index --
+// Exact candidate words per merge, without scanning every word's signature.  An adjacency
+// (x, y) in a word is created either at setup (both ids < nb, the setup symbols) or by the
+// merge that created the LATER of x and y (merged ids grow with creation: the larger id), at
+// which moment the other was its left (y later) or right (x later) neighbour -- a merge only
+// creates adjacencies with its own new token, and a token id made by one merge is never made
+// again (an id re-used by a second merge marks its list INEXACT).  So:
+//  * (setup, setup): the distinct words that held the pair at setup (CSR over nb x nb pairs);
+//  * otherwise, t = max(x, y): the entries the merge creating t recorded -- per rewritten word,
+//    the distinct LEFT neighbours of t and the distinct RIGHT neighbours of t -- filtered to
+//    kind L and symbol x (t == y, x != y) or kind R and symbol y (t == x).
+// Both are supersets (later merges may have consumed an adjacency: the probe then finds
+// nothing) and list every word at most once.  Entries are 8 bytes {word, kind << 16 | sym} in
+// the token index's pool, [start[t], start[t] + len[t]) per token (k_apply_argmax commits them).
+constexpr uint32_t ENT_L = 0u, ENT_R = 1u;
+struct PairIndex {
+  const uint32_t* off;    // [nb * nb + 1]
+  const uint32_t* list;   // [off[nb * nb]] word ids
+  int nb;
+};
+
+// (p, q) = (s[i-1], s[i]) occurred earlier in the word (one list entry per distinct word)
+__device__ __forceinline__ bool pair_seen_before(const uint16_t* s, uint32_t i, uint32_t p, uint32_t q) {
+  for (uint32_t j = 1; j < i; ++j)
+    if (s[j - 1] == p && s[j] == q) return true;
+  return false;
+}
+
+// Count (FILL = false: LDS histogram of rows [r0, r0 + R) flushed into gcount) or fill (FILL:
+// the workgroup reserves each pair's slots with one atomic on the pair's cursor, then writes
+// its word ids at LDS cursors).  Workgroups take 256-word chunks round-robin (length-sorted
+// words); a workgroup visits the same chunks in both walks.
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_pair_lists(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                    const uint32_t* __restrict__ wlen, int64_t nw, int nb, int R,
+                                                    uint32_t* __restrict__ gcount, uint32_t* __restrict__ list) {
+  extern __shared__ uint32_t hs[];   // [R][nb]
+  const int r0 = blockIdx.y * R;
+  const int rr = min(R, nb - r0);
+  for (int i = threadIdx.x; i < rr * nb; i += blockDim.x) hs[i] = 0;
+  __syncthreads();
+  const int64_t nchunks = (nw + 255) / 256;
+  auto walk = [&](bool emit) {
+    for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+      const int64_t w = c * 256 + threadIdx.x;
+      if (w >= nw) continue;
+      const uint32_t L = wlen[w];
+      const uint16_t* s = sym + wstart[w];
+      for (uint32_t i = 1; i < L; ++i) {
+        const uint32_t p = s[i - 1], q = s[i];
+        const int pr = (int)p - r0;
+        if (pr < 0 || pr >= rr || q >= (uint32_t)nb || pair_seen_before(s, i, p, q)) continue;
+        const uint32_t slot = atomicAdd(&hs[pr * nb + q], 1u);
+        if (emit) list[slot] = (uint32_t)w;
+      }
+    }
+  };
+  walk(false);
+  __syncthreads();
+  for (int i = threadIdx.x; i < rr * nb; i += blockDim.x) {
+    const uint32_t v = hs[i];
+    if (!v) continue;
+    const uint32_t g = (uint32_t)(r0 + i / nb) * (uint32_t)nb + (uint32_t)(i % nb);
+    const uint32_t base = atomicAdd(&gcount[g], v);   // FILL: gcount holds the cursors
+    if (FILL) hs[i] = base;
+  }
+  if (!FILL) return;
+  __syncthreads();
+  walk(true);
+}
+
+// off = exclusive scan of the per-pair counts, cursors = off (one workgroup; nb^2 is small)
+__global__ __launch_bounds__(1024) void k_pair_scan(uint32_t* __restrict__ off, uint32_t* __restrict__ cursor, int64_t P) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (P + 1023) / 1024;
+  uint32_t acc = 0;
+  for (int64_t k = 0; k < per; ++k) {
+    const int64_t i = t * per + k;
+    if (i < P) acc += cursor[i];
+  }
+  part[t] = acc;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = t ? part[t - 1] : 0u;
+  for (int64_t k = 0; k < per; ++k) {
+    const int64_t i = t * per + k;
+    if (i < P) {
+      const uint32_t c = cursor[i];
+      off[i] = run;
+      cursor[i] = run;
+      run += c;
+    }
+  }
+  if (t == 1023) off[P] = part[1023];
+}
+
+// The device-driven merge over the pair index: k_merge<2>'s decision, then the candidate words.
+// A setup pair walks its CSR word list when it is shorter than nw / list_ratio (each entry a
+// dependent random visit); a pair with a merged token streams its creator's entry list (8 B
+// per entry, coalesced) and visits only the entries that match.  Otherwise -- a long setup
+// list, an INEXACT token -- the merge runs k_merge's two-phase Bloom-signature scan.  Rounds:
+// 256 * MIX_U candidates per workgroup (MIX_U in flight per thread); the rewritten words'
+// entries are counted, reserved with one atomic per workgroup and round, then written.
+// apps[m] = pair occurrences merge m rewrote (unweighted), apps[max_merges + m] = the list
+// elements it read (word list, entry list, or every word for a scan) -- bench.py's accounting.
+constexpr int MIX_U = 4;
+constexpr int MIX_NEW = 256 * MIX_U;
+__device__ __forceinline__ bool seen_neighbour(const uint16_t* s, uint32_t i, int nid, int side, uint32_t v) {
+  for (uint32_t j = side == 0 ? 1u : 0u; j < i; ++j)   // an earlier occurrence of nid, same neighbour
+    if (s[j] == (uint16_t)nid && (side == 0 ? s[j - 1] : s[j + 1]) == v) return true;
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                  uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
+                                                  int64_t nw, uint32_t* __restrict__ tlen, int max_len,
+                                                  int32_t* __restrict__ deltas, int Vt, WordIndex ix, PairIndex px,
+                                                  unsigned long long* __restrict__ sig, int list_ratio,
+                                                  LoopState* __restrict__ loop, long long lds_min, ArgWs aw,
+                                                  LoopHash lh, uint32_t* __restrict__ apps, int max_merges) {
+  extern __shared__ __attribute__((aligned(16))) int32_t dl[];
+  __shared__ LoopStep dec;
+  __shared__ const uint32_t* s_cand;
+  __shared__ long long s_n;
+  __shared__ int s_mi, touched, s_mode;   // mode 0: signature scan, 1: word list, 2: entry list
+  __shared__ uint32_t s_want;             // mode 2: kind << 16 | symbol of the entries to visit
+  __shared__ uint32_t clist[MERGE_CLIST];
+  __shared__ uint32_t ecnt, ebase, napps;
+  __shared__ int cn;
+  if (threadIdx.x == 0) {
+    dec = loop_decide(loop, aw, Vt, lh, tlen);
+    s_mi = loop->n_merges;
+    // an id made a second time (HF id re-use) breaks "the later token's merge made the
+    // adjacency": ctl[3] = 1 sends every merge after it to the signature scan
+    const bool lists_valid = ix.ctl[3] == 0u;
+    if (blockIdx.x == 0) {   // the record k_apply_argmax applies and commits
+      loop->r_active = dec.active;
+      loop->r_a = dec.a; loop->r_b = dec.b; loop->r_nid = dec.nid; loop->r_reused = dec.reused;
+      loop->r_vcur = dec.vcur; loop->r_parity = loop->parity; loop->r_len = dec.len;
+      loop->r_count = dec.count; loop->r_h = dec.h;
+      if (!dec.active) loop->active = 0;
+      if (dec.active && dec.reused) ix.ctl[3] = 1u;
+    }
+    int mode = 0;
+    const uint32_t* cand = nullptr;
+    long long n = nw;
+    uint32_t want = 0;
+    if (dec.active && px.off != nullptr && lists_valid) {
+      const int a = dec.a, b = dec.b;
+      if (a < px.nb && b < px.nb) {
+        const uint32_t p = (uint32_t)a * (uint32_t)px.nb + (uint32_t)b;
+        const uint32_t o0 = px.off[p], o1 = px.off[p + 1];
+        if (sig == nullptr || (long long)(o1 - o0) * list_ratio < nw) {
+          mode = 1;
+          cand = px.list + o0;
+          n = o1 - o0;
+        }
+      } else {
+        const int t = a > b ? a : b;
+        const uint32_t lt = ix.len[t];
+        if (lt != IDX_INEXACT && (sig == nullptr || list_ratio == 0 || (long long)lt < nw)) {
+          mode = 2;
+          cand = ix.pool + 2 * (size_t)ix.start[t];
+          n = lt;
+          want = (t == b && a != b) ? (ENT_L << 16) | (uint32_t)a : (ENT_R << 16) | (uint32_t)b;
+        }
+      }
+    }
+    s_mode = mode;
+    s_cand = cand;
+    s_n = n;
+    s_want = want;
+    if (blockIdx.x == 0 && dec.active && apps != nullptr && s_mi < max_merges)
+      apps[max_merges + s_mi] = (uint32_t)n;
+    ecnt = 0;
+    napps = 0;
+    touched = 0;
+    cn = 0;
+  }
+  __syncthreads();
+  if (!dec.active) return;
+  const int mode = s_mode;
+  const long long ncand = s_n;
+  const uint32_t* cand = s_cand;
+  const uint32_t want = s_want;
+  const int64_t per_round = (int64_t)MIX_U * 256;
+  const int64_t nchunks = (nw + 255) / 256;
+  if (mode ? (int64_t)blockIdx.x * per_round >= ncand : (int64_t)blockIdx.x >= nchunks) return;   // uniform
+  const int a = dec.a, b = dec.b, nid = dec.nid;
+  const bool LDS = dec.count >= (unsigned long long)lds_min;
+  int32_t* dv = LDS ? dl : deltas;
+  if (LDS) {
+    for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) dl[i] = 0;
+    __syncthreads();
+  }
+  const uint32_t newlen = tlen[a] + tlen[b];
+  int32_t* colA = dv;
+  int32_t* colN = dv + Vt;
+  int32_t* rowB = dv + 2 * Vt;
+  int32_t* rowN = dv + 3 * Vt;
+  uint32_t my_apps = 0;
+  const uint32_t cap = ix.ctl[2];
+  // one round: every thread's (up to MIX_U) candidate words, then the block's entry appends
+  auto round = [&](const int64_t (&wv)[MIX_U]) {
+    uint32_t Lv[MIX_U], Sv[MIX_U], Ov[MIX_U];
+#pragma unroll
+    for (int u = 0; u < MIX_U; ++u) {
+      Lv[u] = wv[u] >= 0 ? wlen[wv[u]] : 0u;
+      Sv[u] = wv[u] >= 0 ? wstart[wv[u]] : 0u;
+    }
+    uint32_t my_ent = 0;
+    for (int u = 0; u < MIX_U; ++u) {
+      Ov[u] = 0;
+      const uint32_t L = Lv[u];
+      if (L < 2) continue;
+      uint16_t* s = sym + Sv[u];
+      bool hit = false;
+      uint32_t prev = s[0];
+#pragma unroll 8
+      for (uint32_t k = 1; k < L; ++k) {
+        const uint32_t cur = s[k];
+        hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
+        prev = cur;
+      }
+      if (!hit) continue;
+      const int32_t cnt = wcount ? (int32_t)wcount[wv[u]] : 1;
+      uint32_t rr = 0, o = 0;
+      unsigned long long g = 0;
+      while (rr < L) {
+        const int x = s[rr];
+        int y = x;
+        if (x == a && rr + 1 < L && s[rr + 1] == b) {
+          if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
+            const int p = s[o - 1];
+            atomicAdd(&colA[p], -cnt);
+            if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
+          }
+          if (rr + 2 < L) {                      // HF: ((b, next), -1), ((new, next), +1)
+            const int nx = s[rr + 2];
+            atomicAdd(&rowB[nx], -cnt);
+            if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
+          }
+          y = nid;
+          rr += 2;
+          ++my_apps;
+        } else {
+          rr += 1;
+        }
+        s[o++] = (uint16_t)y;
+        g |= sig_bit((uint32_t)y);
+      }
+      wlen[wv[u]] = o;
+      if (sig != nullptr) sig[wv[u]] = g;
+      Ov[u] = o;
+      for (uint32_t i = 0; i < o; ++i)   // distinct left / right neighbours of new in the word
+        if (s[i] == (uint16_t)nid) {
+          my_ent += (i > 0 && !seen_neighbour(s, i, nid, 0, s[i - 1])) ? 1u : 0u;
+          my_ent += (i + 1 < o && !seen_neighbour(s, i, nid, 1, s[i + 1])) ? 1u : 0u;
+        }
+    }
+    const uint32_t my_off = my_ent ? atomicAdd(&ecnt, my_ent) : 0u;
+    __syncthreads();
+    const uint32_t c = ecnt;
+    if (c) {
+      if (threadIdx.x == 0) {
+        ebase = atomicAdd(&ix.ctl[0], c);
+        touched = 1;
+      }
+      __syncthreads();
+      uint32_t k = ebase + my_off;
+      for (int u = 0; u < MIX_U && my_ent; ++u) {
+        const uint32_t o = Ov[u];
+        if (!o) continue;
+        const uint16_t* s = sym + Sv[u];
+        for (uint32_t i = 0; i < o; ++i)
+          if (s[i] == (uint16_t)nid) {
+            if (i > 0 && !seen_neighbour(s, i, nid, 0, s[i - 1])) {
+              if (k < cap) { ix.pool[2 * (size_t)k] = (uint32_t)wv[u]; ix.pool[2 * (size_t)k + 1] = (ENT_L << 16) | s[i - 1]; }
+              ++k;
+            }
+            if (i + 1 < o && !seen_neighbour(s, i, nid, 1, s[i + 1])) {
+              if (k < cap) { ix.pool[2 * (size_t)k] = (uint32_t)wv[u]; ix.pool[2 * (size_t)k + 1] = (ENT_R << 16) | s[i + 1]; }
+              ++k;
+            }
+          }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) ecnt = 0;
+    }
+    __syncthreads();
+  };
+  if (mode != 0) {
+    for (int64_t r0 = (int64_t)blockIdx.x * per_round; r0 < ncand; r0 += (int64_t)gridDim.x * per_round) {
+      int64_t wv[MIX_U];
+      if (mode == 1) {
+#pragma unroll
+        for (int u = 0; u < MIX_U; ++u) {
+          const int64_t i = r0 + u * 256 + threadIdx.x;
+          wv[u] = i < ncand ? (int64_t)cand[i] : -1;
+        }
+      } else {
+        uint2 e[MIX_U];
+#pragma unroll
+        for (int u = 0; u < MIX_U; ++u) {
+          const int64_t i = r0 + u * 256 + threadIdx.x;
+          e[u] = i < ncand ? reinterpret_cast<const uint2*>(cand)[i] : make_uint2(0u, 0xFFFFFFFFu);
+        }
+#pragma unroll
+        for (int u = 0; u < MIX_U; ++u) wv[u] = e[u].y == want ? (int64_t)e[u].x : -1;
+      }
+      round(wv);
+    }
+  } else {
+    // k_merge's two-phase scan: MERGE_SCAN signature loads per thread over 256-word chunks taken
+    // round-robin (length-sorted words), candidates listed in LDS (<= 8 per thread: they fit),
+    // then visited in rounds of MIX_U per thread
+    const unsigned long long need = sig_bit(a) | sig_bit(b);
+    for (int64_t c0 = blockIdx.x; c0 < nchunks; c0 += (int64_t)MERGE_SCAN * gridDim.x) {
+      unsigned long long sgv[MERGE_SCAN];
+#pragma unroll
+      for (int u = 0; u < MERGE_SCAN; ++u) {
+        const int64_t w = (c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+        sgv[u] = (sig != nullptr && w < nw) ? sig[w] : (w < nw ? need : 0ull);
+      }
+#pragma unroll
+      for (int u = 0; u < MERGE_SCAN; ++u)
+        if ((sgv[u] & need) == need) clist[atomicAdd(&cn, 1)] = (uint32_t)((c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x);
+      __syncthreads();
+      const int n = cn;
+      for (int k0 = 0; k0 < n; k0 += MIX_NEW) {
+        int64_t wv[MIX_U];
+#pragma unroll
+        for (int u = 0; u < MIX_U; ++u) {
+          const int k = k0 + u * 256 + threadIdx.x;
+          wv[u] = k < n ? (int64_t)clist[k] : -1;
+        }
+        round(wv);
+      }
+      if (threadIdx.x == 0) cn = 0;
+      __syncthreads();
+    }
+  }
+  if (my_apps) atomicAdd(&napps, my_apps);
+  __syncthreads();
+  if (threadIdx.x == 0 && napps && apps != nullptr && s_mi < max_merges) atomicAdd(&apps[s_mi], napps);
+  if (LDS && touched)   // contiguous atomics (one cache line per 32 entries)
+    for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) {
+      const int32_t v = dl[i];
+      if (v) atomicAdd(&deltas[i], v);
+    }
+}
+
 // Fused apply + argmax, one workgroup per row x (the apply touches only entries of rows it
 // owns: (x, a) and (x, new) for every x, rows b and new entirely).  When `apply`:
 // table += deltas for row x, deltas consumed are zeroed, row a's (a, b) is retired after its
@@ -1664,6 +2022,126 @@ extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_step
     BEAST_LAUNCHED("k_merge");
     hipLaunchKernelGGL(k_apply_argmax, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s,
                        table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen, ix, index != nullptr, false, st, lh, rows);
+    BEAST_LAUNCHED("k_apply_argmax");
+  }
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_pair_index_bytes(int n_sym, int64_t n_symbols) {
+  const size_t P = (size_t)(n_sym > 0 ? n_sym : 1) * (size_t)(n_sym > 0 ? n_sym : 1);
+  return al256((P + 1) * 4) + al256(P * 4) + al256((size_t)(n_symbols > 0 ? n_symbols : 1) * 4);
+}
+
+extern "C" int beast_bpe_build_pair_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
+                                          int64_t n_words, int n_sym, int64_t n_symbols, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  BEAST_REQUIRE(sym && wstart && wlen && ws && n_words >= 0 && n_symbols >= 0, "beast_bpe_build_pair_index: bad args");
+  BEAST_REQUIRE(n_sym >= 1 && n_sym <= 4096, "beast_bpe_build_pair_index: n_sym %d not in [1, 4096]", n_sym);
+  BEAST_REQUIRE(n_symbols < (int64_t)0xFFFFFFFF, "beast_bpe_build_pair_index: too many symbols");
+  BEAST_REQUIRE_CODE(ws_bytes >= beast_bpe_pair_index_bytes(n_sym, n_symbols), BEAST_E_WORKSPACE,
+                     "pair index workspace %zu < %zu", ws_bytes, beast_bpe_pair_index_bytes(n_sym, n_symbols));
+  hipStream_t s = beast::as_stream(stream);
+  const int64_t P = (int64_t)n_sym * n_sym;
+  unsigned char* w = static_cast<unsigned char*>(ws);
+  uint32_t* off = reinterpret_cast<uint32_t*>(w);
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(w + al256((P + 1) * 4));
+  uint32_t* list = reinterpret_cast<uint32_t*>(w + al256((P + 1) * 4) + al256(P * 4));
+  BEAST_HIP(hipMemsetAsync(cursor, 0, P * 4, s), "pair index memset");
+  if (n_words > 0) {
+    const size_t budget = 160 * 1024;
+    const int R = (int)std::max<size_t>(1, std::min<size_t>((size_t)n_sym, budget / (4 * (size_t)n_sym)));
+    const int groups = (n_sym + R - 1) / R;
+    const size_t lds = (size_t)R * n_sym * 4;
+    BEAST_REQUIRE_CODE(lds <= budget, BEAST_E_UNSUPPORTED, "pair index: one row needs %zu B of LDS", lds);
+    if (lds > 65536) {
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pair_lists<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute");
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_pair_lists<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute");
+    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int per_cu = std::max(1, (int)(budget / lds));
+    const int gx = std::max(1, std::min<int>(std::max(1, cus * per_cu / groups), (int)((n_words + 255) / 256)));
+    hipLaunchKernelGGL(k_pair_lists<false>, dim3(gx, groups), dim3(256), lds, s, sym, wstart, wlen, n_words, n_sym, R,
+                       cursor, list);
+    BEAST_LAUNCHED("k_pair_lists<count>");
+    hipLaunchKernelGGL(k_pair_scan, dim3(1), dim3(1024), 0, s, off, cursor, P);
+    BEAST_LAUNCHED("k_pair_scan");
+    hipLaunchKernelGGL(k_pair_lists<true>, dim3(gx, groups), dim3(256), lds, s, sym, wstart, wlen, n_words, n_sym, R,
+                       cursor, list);
+    BEAST_LAUNCHED("k_pair_lists<fill>");
+  } else {
+    BEAST_HIP(hipMemsetAsync(off, 0, (P + 1) * 4, s), "pair index memset");
+  }
+  return BEAST_OK;
+}
+
+// Token index for the pair-index loop: no setup lists (the pair CSR serves setup symbols), every
+// id INEXACT until a merge creates it; the pool (8-byte entries) receives k_merge_ix's appends.
+extern "C" int beast_bpe_token_index_init(void* index, size_t index_bytes, int Vt, void* stream) {
+  BEAST_REQUIRE(index && Vt >= 1 && Vt <= 65535, "beast_bpe_token_index_init: bad args");
+  const size_t head = (size_t)(2 * (int64_t)Vt + 4) * 4;
+  BEAST_REQUIRE_CODE(index_bytes >= head + 4, BEAST_E_WORKSPACE, "token index workspace too small");
+  const int64_t cap = (int64_t)(index_bytes - head) / 8;   // 8-byte {word, kind << 16 | symbol} entries
+  BEAST_REQUIRE(cap < (int64_t)IDX_INEXACT, "token index pool too large");
+  hipStream_t s = beast::as_stream(stream);
+  WordIndex ix = index_view(index, Vt);
+  BEAST_HIP(hipMemsetAsync(ix.start, 0, (size_t)Vt * 4, s), "token index memset");
+  BEAST_HIP(hipMemsetAsync(ix.len, 0xFF, (size_t)Vt * 4, s), "token index memset");
+  const uint32_t ctl[4] = {0u, 0u, (uint32_t)cap, 0u};
+  BEAST_HIP(hipMemcpyAsync(ix.ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, s), "token index ctl");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym,
+                                       const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
+                                       int64_t n_words, uint32_t* tlen, int max_token_length, int32_t* deltas,
+                                       const void* pair_index, int n_sym, void* token_index, uint64_t* sig,
+                                       uint32_t* table, uint64_t* argws, int vocab_size, uint32_t* apps,
+                                       void* stream) {
+  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws && token_index,
+                "beast_bpe_loop_steps_ix: null pointer");
+  BEAST_REQUIRE(Vt >= 1 && Vt <= 32768 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_steps_ix: bad sizes");
+  BEAST_REQUIRE(pair_index == nullptr || (n_sym >= 1 && n_sym <= Vt), "beast_bpe_loop_steps_ix: bad n_sym");
+  hipStream_t s = beast::as_stream(stream);
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  LoopState* st = reinterpret_cast<LoopState*>(static_cast<unsigned char*>(ws) + L.st);
+  const LoopHash lh = loop_hash_view(ws, Vt, max_merges);
+  const ArgWs aw = argws_view(argws, Vt);
+  const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  BEAST_REQUIRE_CODE(lds <= 64 * 1024, BEAST_E_UNSUPPORTED, "device loop needs 4*Vt int32 of LDS (Vt <= 4096)");
+  PairIndex px{};
+  if (pair_index != nullptr) {
+    const int64_t P = (int64_t)n_sym * n_sym;
+    const unsigned char* w = static_cast<const unsigned char*>(pair_index);
+    px.off = reinterpret_cast<const uint32_t*>(w);
+    px.list = reinterpret_cast<const uint32_t*>(w + al256((P + 1) * 4) + al256(P * 4));
+    px.nb = n_sym;
+  }
+  const WordIndex ix = index_view(token_index, Vt);
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_merge_ix, 256, lds) != hipSuccess || per <= 0) per = 4;
+    resident = cus * per;
+  }
+  // as many workgroups as are resident: a list round or a signature sweep per workgroup
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(resident, (n_words + 255) / 256));
+  unsigned long long* sg = reinterpret_cast<unsigned long long*>(sig);
+  const int rows = std::min(Vt, std::max(vocab_size, 1));
+  for (int i = 0; i < n_steps; ++i) {
+    hipLaunchKernelGGL(k_merge_ix, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, tlen,
+                       max_token_length, deltas, Vt, ix, px, sg, beast::g_merge_list_ratio, st,
+                       (long long)beast::g_merge_lds_min, aw, lh, apps, max_merges);
+    BEAST_LAUNCHED("k_merge_ix");
+    hipLaunchKernelGGL(k_apply_argmax, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s,
+                       table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen, ix, true, false, st, lh, rows);
     BEAST_LAUNCHED("k_apply_argmax");
   }
   return BEAST_OK;

@@ -1368,6 +1368,11 @@ extern "C" int beast_set_option(int option, int value) {
     beast::g_merge_lds_min = value;
     return BEAST_OK;
   }
+  if (option == BEAST_OPT_MERGE_LIST_RATIO) {
+    BEAST_REQUIRE(value >= 0, "BEAST_OPT_MERGE_LIST_RATIO: %d < 0", value);
+    beast::g_merge_list_ratio = value;
+    return BEAST_OK;
+  }
   BEAST_REQUIRE(false, "unknown option %d", option);
   return BEAST_E_INVALID;
 }

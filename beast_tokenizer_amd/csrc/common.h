@@ -15,6 +15,9 @@ namespace beast {
 void set_error(const char* fmt, ...);
 // BEAST_OPT_MERGE_LDS_MIN: pair count from which k_merge privatises its deltas in LDS
 extern int64_t g_merge_lds_min;
+// BEAST_OPT_MERGE_LIST_RATIO: a merge walks its candidate list when list * ratio < words,
+// else it scans the Bloom signatures of every word
+extern int g_merge_list_ratio;
 int hip_fail(hipError_t e, const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -9,29 +9,52 @@ rank per GPU (torch.distributed.run); every rank processes its own B
 trajectories (data-parallel, no collective on this path: weak scaling); the time
 is the max over ranks.  rank 0 prints ONE JSON line.
 
+Timing: W untimed warm-up steps, then ``--windows`` windows of exactly K steps, each
+bracketed by barrier + device synchronize (wall clock, max over ranks) and by HIP events
+on the stream the kernels run on; ``value`` / ``ms_per_step`` come from the median window
+(one 20-step window is ~0.3 ms of wall clock: start-up jitter would dominate a single one).
+
 Extra objects in that line:
   roofline      dominant kernel: algorithmic bytes / its average launch duration
                 (HIP events on the kernel's stream around back-to-back launches)
+  mfma          the fit kernel's MFMA utilisation: issued MFMA flops per launch from the
+                rocprofv3 SQ_INSTS_MFMA pass (profiles/pmc_mfma.json) over the live launch
+                duration, against the f32 MFMA peak
   cpu_baseline  the oracle's restatement of the reference op sequence (oracle/
                 beast_oracle.py, bitwise equal to the reference in the build
-                container) timed on this host's cores on a bounded sample
+                container) timed on this host's cores on the SAME B=4096 batch the GPU
+                steps on; ``token_parity`` = the GPU's tokens against those reference
+                tokens (every flip must sit on a .5 rounding tie of the exact fit)
   fit           fit_parameters (config K4: 1e6 trajectories, sharded over ranks with the
-                quantile histograms all-reduced) in trajectories/s, with the reference
-                op sequence + np.quantile timed on a bounded host sample
-  bpe           BEASTBsplineBPETokenizer-style BPE training (vocab 2048) on GPU,
-                merges/s, with HF tokenizers (the reference's BPE) timed on a
-                bounded sample of the same corpus on the host
+                quantile histograms all-reduced) in trajectories/s; the bounds are checked
+                bitwise against np.quantile of the same GPU params
+  bpe           BPE training (config K5: 5e5 trajectories, vocab 2048) on GPU, merges/s and
+                GB/s against SURVEY.md §8d's byte count; merges checked against the golden
+                HF BpeTrainer merges of the same corpus (tests/golden/k5_bpe.json); HF timed
+                beside the GPU on one identical 20k-sequence sample
+Every CPU leg runs under one threading policy (``host`` object: threads, affinity, model).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
 import time
 
-import numpy as np
-import torch
+
+def _host_threads() -> int:
+    """One threading policy for every CPU leg: OMP_NUM_THREADS if set (16 on the GPU
+    box: its share of the host), else this process's CPU affinity."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(env)) if env and env.isdigit() else len(os.sched_getaffinity(0))
+
+
+os.environ.setdefault("RAYON_NUM_THREADS", str(_host_threads()))   # HF tokenizers' pool, before import
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -40,10 +63,14 @@ from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib  # noqa: E402
 from beast_tokenizer_amd.synthetic import synth_trajectories, synth_trajectories_device  # noqa: E402
 
 HBM_PEAK = 8.0e12          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK = 157.3e12   # dense f32 MFMA peak (MI355X_MICROARCH.md, = vector f32 peak)
 T, D, N, V = 50, 14, 10, 256
 ENC_BYTES = T * D * 4 + N * D * 8 + D * N * 4    # read traj, write int64 tokens + fp32 params
 REC_BYTES = N * D * 8 + T * D * 4                # read tokens, write positions
 FIT_BYTES = T * D * 4 + D * N * 4 * (1 + 4)      # read traj; params written once, read/written per radix pass
+FIT_FLOPS = 2 * T * N * D                        # per trajectory per direction
+K5_GOLDEN = os.path.join(REPO, "tests", "golden", "k5_bpe.json")
+K5_CHUNK = 8192
 
 
 def parse():
@@ -51,6 +78,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--windows", type=int, default=5, help="timed windows of --steps steps (median reported)")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-bpe", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -61,10 +89,30 @@ def parse():
     ap.add_argument("--fit-trajs", type=int, default=1000000, help="fit_parameters corpus (all ranks)")
     ap.add_argument("--bpe-seqs", type=int, default=500000, help="BPE corpus (trajectories, all ranks)")
     ap.add_argument("--bpe-vocab", type=int, default=2048)
+    ap.add_argument("--bpe-sample", type=int, default=20000, help="sequences of the same-sample GPU/HF comparison")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--dump-k5", default=None, help="write the K5 corpus (uint8 bins, npz) and exit")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM bytes from rocprofv3 --pmc (see profiles/README.md)")
+                    help="per-launch HBM bytes from rocprofv3 --pmc (tools/gpu_pmc.sh)")
+    ap.add_argument("--pmc-mfma", default=os.path.join(REPO, "profiles", "pmc_mfma.json"),
+                    help="per-launch MFMA instruction counts from rocprofv3 --pmc SQ_INSTS_MFMA")
     return ap.parse_args()
+
+
+def host_info() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"threads": torch.get_num_threads(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "os_cpu_count": os.cpu_count(), "cpu_model": model,
+            "policy": "OMP_NUM_THREADS if set, else the process's CPU affinity; torch and RAYON (HF) alike",
+            "rayon_threads": int(os.environ.get("RAYON_NUM_THREADS", "0"))}
 
 
 def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 100, rounds: int = 5) -> float:
@@ -86,10 +134,23 @@ def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 100, rounds: i
     return float(np.median(per))
 
 
-def large_batch_roofline(tok, dev, stream, B: int):
-    """Supplementary point: the same two kernels at a batch large enough to be HBM-bound
-    (the B=4096 launches are latency-bound: one 8-trajectory tile per workgroup)."""
-    x = synth_trajectories_device(B, T, D, seed=3, device=dev)
+def max_over_ranks(v: float, world: int, dev) -> float:
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sync(world: int) -> None:
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+
+
+def launchers(tok, dev, stream, x, B):
+    """Raw C-ABI launches of the two kernels on ``stream`` (roofline / MFMA timing)."""
     phi, _, proj = tok._constants(dev)
     src, dst = tok._dof_maps(dev)
     wmn, wmx = tok._bounds(dev)
@@ -106,39 +167,89 @@ def large_batch_roofline(tok, dev, stream, B: int):
     def rec():
         _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, D, N, V, 0, wmn.data_ptr(), wmx.data_ptr(),
                  phi.data_ptr(), 0, T, dst.data_ptr(), D, None, 0, None, None, pos.data_ptr(), None, sp)
+    enc()
+    return enc, rec
+
+
+def large_batch_roofline(tok, dev, stream, B: int):
+    """Supplementary point: the same two kernels at a batch large enough to be HBM-bound
+    (the B=4096 launches are latency-bound: one 8-trajectory tile per workgroup)."""
+    x = synth_trajectories_device(B, T, D, seed=3, device=dev)
+    enc, rec = launchers(tok, dev, stream, x, B)
     te = kernel_time_us(enc, stream, reps=20, rounds=3)
     tr = kernel_time_us(rec, stream, reps=20, rounds=3)
     out = {"batch": B, "k_encode_us": te, "k_reconstruct_us": tr,
            "k_encode_GBps": ENC_BYTES * B / (te * 1e-6) / 1e9, "k_reconstruct_GBps": REC_BYTES * B / (tr * 1e-6) / 1e9}
     out["k_encode_frac"] = out["k_encode_GBps"] * 1e9 / HBM_PEAK
     out["k_reconstruct_frac"] = out["k_reconstruct_GBps"] * 1e9 / HBM_PEAK
-    del x, params, tokens, pos
+    del x
     return out
 
 
-def cpu_baseline(tok_bounds, seconds: float):
-    """Oracle port of the reference op sequence (fit via block-diag bmm + linalg.solve,
-    quantise, dequantise, einsum reconstruct) timed on a bounded sample."""
+def mfma_utilisation(path: str, times_us: dict) -> dict:
+    """MFMA utilisation of the fit GEMM (north_star; reference GEMM mp/uni_bspline.py:564-586):
+    issued MFMA flops per launch (rocprofv3 --pmc SQ_INSTS_MFMA, each v_mfma_f32_16x16x4_f32 =
+    16*16*4*2 flops) and the algorithmic 2*T*N*D flops per trajectory, both over the live
+    launch duration, against the dense f32 MFMA peak."""
+    if not os.path.exists(path):
+        return {"error": f"{os.path.relpath(path, REPO)} missing"}
+    with open(path) as f:
+        pmc = json.load(f)
+    out = {"peak_tflops": F32_MFMA_PEAK / 1e12, "source": os.path.relpath(path, REPO),
+           "flops_per_mfma": pmc.get("flops_per_mfma", 2048)}
+    for key, rec in pmc.get("launches", {}).items():
+        us = times_us.get(key)
+        if us is None:
+            continue
+        B = rec["batch"]
+        issued = rec["mfma_insts_per_launch"] * out["flops_per_mfma"]
+        algo = FIT_FLOPS * B
+        out[key] = {"kernel": rec["kernel"], "batch": B, "avg_launch_us": us,
+                    "issued_flops_per_launch": issued, "algorithmic_flops_per_launch": algo,
+                    "issued_tflops": issued / (us * 1e-6) / 1e12, "util_issued": issued / (us * 1e-6) / F32_MFMA_PEAK,
+                    "util_algorithmic": algo / (us * 1e-6) / F32_MFMA_PEAK,
+                    "mfma_busy_cycles_per_launch": rec.get("mfma_busy_cycles_per_launch")}
+    return out
+
+
+def cpu_baseline(x_np: np.ndarray, gpu_tokens: np.ndarray, tok_bounds, seconds: float):
+    """Oracle port of the reference op sequence (fit via block-diagonal bmm + linalg.solve,
+    quantise, dequantise, einsum reconstruct; beast_bspline_tokenizer.py:399-428, 498-536) on
+    the same B=4096 batch the GPU steps on, median of the timed repetitions; and the token
+    census of the GPU against those reference tokens."""
     from oracle import beast_oracle as O
     wmin, wmax = tok_bounds
     lay = O.Layout.make(D, None, False)
     t = O.times_grid(2 * np.pi, T)
     pj = O.basis(t, np.float32(2 * np.pi), 4, N)
-    Bc = 512
-    x = synth_trajectories(Bc, T, D, seed=0)
-    O.reconstruct(O.encode(x, pj, pj, lay, wmin, wmax, V)[0], pj, pj, lay, wmin, wmax, V)  # warm-up
-    n, t0 = 0, time.perf_counter()
+    B = x_np.shape[0]
+    ref_tok, _ = O.encode(x_np, pj, pj, lay, wmin, wmax, V)      # warm-up, and the census tokens
+    O.reconstruct(ref_tok, pj, pj, lay, wmin, wmax, V)
+    reps, t0 = [], time.perf_counter()
     while True:
-        tokens, _ = O.encode(x, pj, pj, lay, wmin, wmax, V)
-        O.reconstruct(tokens, pj, pj, lay, wmin, wmax, V)
-        n += Bc
-        el = time.perf_counter() - t0
-        if el >= seconds:
+        s = time.perf_counter()
+        tk, _ = O.encode(x_np, pj, pj, lay, wmin, wmax, V)
+        O.reconstruct(tk, pj, pj, lay, wmin, wmax, V)
+        reps.append(time.perf_counter() - s)
+        if time.perf_counter() - t0 >= seconds and len(reps) >= 3:
             break
-    return {"value": n / el, "unit": "trajectories/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} trajectories in batches of {Bc} (D=14,T=50,N=10,V=256), encode+reconstruct via "
+    med = float(np.median(reps))
+    # token parity: flips against the reference op sequence must be .5 ties of the exact fit
+    units = O.normalized_units(O.fit_exact(x_np, pj), wmin, wmax, V)
+    units = units.reshape(B, D, N).transpose(0, 2, 1).reshape(B, N * D)
+    diff = gpu_tokens != ref_tok
+    dist = np.abs(units[diff] - np.floor(units[diff]) - 0.5)
+    parity = {"tokens": int(gpu_tokens.size), "flips": int(diff.sum()),
+              "max_flip_tie_distance": float(dist.max()) if diff.any() else None,
+              "max_flip_size": int(np.abs(gpu_tokens[diff] - ref_tok[diff]).max()) if diff.any() else 0,
+              "contract": "every flip within 1e-3 of a .5 rounding tie of the exact fit, by one bin "
+                          "(tests/test_gpu_parity.py TIE_TOL)"}
+    parity["ok"] = bool(not diff.any() or (dist.max() < 1e-3 and parity["max_flip_size"] == 1))
+    return {"value": B / med, "unit": "trajectories/s", "cores": torch.get_num_threads(), "kind": "port",
+            "seconds_per_batch_median": med, "repetitions": len(reps),
+            "sample": f"{len(reps)} x the bench's own B={B} batch (D=14,T=50,N=10,V=256), encode+reconstruct via "
                       f"oracle/beast_oracle.py (reference ATen op sequence: block-diagonal bmm + "
-                      f"torch.linalg.solve), {el:.1f}s"}
+                      f"torch.linalg.solve), median of the repetitions"}, parity
 
 
 def fit_bench(dev, args, world, rank):
@@ -151,29 +262,22 @@ def fit_bench(dev, args, world, rank):
     ftok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, device=str(dev))
     pg = True if world > 1 else None
     ftok.fit_parameters(loader[:4], verbose=False, process_group=pg)          # warm-up
-    torch.cuda.synchronize()
     times = []
     for _ in range(3):
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
+        sync(world)
         t0 = time.perf_counter()
         ftok.fit_parameters(loader, verbose=False, process_group=pg)
         torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([el], device=dev)
-            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-            el = float(tt.item())
-        times.append(el)
+        times.append(max_over_ranks(time.perf_counter() - t0, world, dev))
     el = float(np.median(times))
     # stage split on this rank: the fits alone, grouped as fit_parameters groups them
     per = max(ftok._FIT_GROUP_ROWS // 4096, 1)
-    groups = [[b["actions"] for b in loader[i:i + per]] for i in range(0, len(loader), per)]
+    full = [b["actions"] for b in loader if b["actions"].shape[0] == 4096]
+    groups = [full[i:i + per] for i in range(0, len(full), per)]
+    groups += [[b["actions"]] for b in loader if b["actions"].shape[0] != 4096]   # the ragged tail alone
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for grp in groups:
-        ftok._fit_list(grp)
+    params = [ftok._fit_list(grp) for grp in groups]
     torch.cuda.synchronize()
     t_fit = time.perf_counter() - t0
     n = per_rank * world
@@ -183,23 +287,36 @@ def fit_bench(dev, args, world, rank):
            "algo_bytes_per_traj": FIT_BYTES, "achieved_GBps": FIT_BYTES * n / el / 1e9 / world,
            "hbm_frac": FIT_BYTES * n / el / world / HBM_PEAK,
            "w_min_checksum": float(ftok.w_min.double().sum()), "w_max_checksum": float(ftok.w_max.double().sum())}
+    if world == 1:
+        # full-size parity: the bounds are np.quantile (numpy 2.x linear method, the reference's
+        # beast_bspline_tokenizer.py:211-214) of the very params the GPU fitted
+        allp = torch.cat([p.reshape(-1, D * N) for p in params]).cpu().numpy()
+        t0 = time.perf_counter()
+        lo, hi = np.quantile(allp, 0.01, axis=0), np.quantile(allp, 0.99, axis=0)
+        t_np = time.perf_counter() - t0
+        eq_lo = np.array_equal(ftok.w_min.cpu().numpy(), lo.astype(np.float32))
+        eq_hi = np.array_equal(ftok.w_max.cpu().numpy(), hi.astype(np.float32))
+        out["parity"] = {"bounds_equal_np_quantile": bool(eq_lo and eq_hi), "rows": int(allp.shape[0]),
+                         "np_quantile_seconds": t_np}
+        assert eq_lo and eq_hi, "K4 bounds differ from np.quantile of the same GPU params"
+        del allp
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_fit_baseline(args.cpu_seconds / 2)
-    del x, loader
+    del x, loader, params
     return out
 
 
 def cpu_fit_baseline(seconds: float):
-    """Reference fit_parameters on the host: per-batch fit through the reference op sequence
-    (oracle/beast_oracle.py:fit_reference_ops) then np.quantile(q=0.01/0.99, axis=0)."""
+    """Reference fit_parameters on the host (:181-220): per-batch fit of B=4096 through the
+    reference op sequence (oracle/beast_oracle.py:fit_reference_ops), then np.quantile."""
     from oracle import beast_oracle as O
     t = O.times_grid(2 * np.pi, T)
     pj = O.basis(t, np.float32(2 * np.pi), 4, N)
-    Bc = 512
+    Bc = 4096
     xs = synth_trajectories(Bc, T, D, seed=11)
-    O.fit_reference_ops(xs, pj)
+    O.fit_reference_ops(xs[:64], pj)
     params, n, t0 = [], 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < seconds or n == 0:
         params.append(O.fit_reference_ops(xs, pj).reshape(Bc, -1))
         n += Bc
     allp = np.concatenate(params)
@@ -210,37 +327,130 @@ def cpu_fit_baseline(seconds: float):
                       f"(block-diagonal bmm + torch.linalg.solve) + np.quantile, {el:.1f}s"}
 
 
-def bpe_bench(tok, dev, args, world, rank, reduce):
-    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
-    per_rank = args.bpe_seqs // world
+def k5_golden():
+    if not os.path.exists(K5_GOLDEN):
+        return None
+    with open(K5_GOLDEN) as f:
+        return json.load(f)
+
+
+def k5_corpus(dev, n_total: int, rank: int, world: int, golden) -> torch.Tensor:
+    """Config K5's corpus: BEAST bins of ``n_total`` synthetic trajectories (seed 7) encoded on
+    the GPU with the reference's own fit_parameters bounds (tests/golden/k5_bpe.json, 2 x 4096
+    trajectories of seed 1 through beast_bspline_tokenizer.py:181-220); this rank's shard."""
+    tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, device=str(dev))
+    if golden is not None:
+        tok.w_min.copy_(torch.tensor(golden["w_min"], dtype=torch.float32))
+        tok.w_max.copy_(torch.tensor(golden["w_max"], dtype=torch.float32))
+    else:
+        tok.fit_parameters([{"actions": torch.from_numpy(synth_trajectories(4096, T, D, seed=1, start=4096 * i))}
+                            for i in range(2)], verbose=False)
+    per_rank = n_total // world
     rows = []
-    for s in range(0, per_rank, 8192):
-        b = min(8192, per_rank - s)
+    for s in range(0, per_rank, K5_CHUNK):
+        b = min(K5_CHUNK, per_rank - s)
         x = torch.from_numpy(synth_trajectories(b, T, D, seed=7, start=rank * per_rank + s)).to(dev)
         rows.append(tok.encode(x)[0])
-    allrows = torch.cat(rows)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    flat, off = fixed_rows_to_device(allrows)
-    res = train_bpe(flat, off, args.bpe_vocab, reduce=reduce)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        el = float(tt.item())
+    return torch.cat(rows)
+
+
+def bpe_bytes(stats: dict) -> dict:
+    """Σ over merges of (4 B x live symbols + 4 B x live words) + the initial
+    count pass (4 B x distinct-word symbols + 8 B x distinct words)."""
+    S0, W = stats.get("n_syms_distinct"), stats.get("n_distinct")
+    apps = stats.get("applications")
+    if S0 is None or W is None or apps is None:
+        return {"error": "per-merge application counts not available"}
+    live = S0 - np.concatenate([[0], np.cumsum(apps)[:-1]]) if len(apps) else np.zeros(0)
+    merge_bytes = float(np.sum(4.0 * live + 4.0 * W))
+    setup_bytes = 4.0 * S0 + 8.0 * W
+    return {"algo_bytes": merge_bytes + setup_bytes, "merge_bytes": merge_bytes, "setup_bytes": setup_bytes,
+            "symbols_start": int(S0), "symbols_end": int(S0 - int(np.sum(apps))), "distinct_words": int(W)}
+
+
+def bpe_bench(dev, args, world, rank, reduce):
+    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
+    golden = k5_golden()
+    allrows = k5_corpus(dev, args.bpe_seqs, rank, world, golden)
+    sha = hashlib.sha256(allrows.to(torch.uint8).cpu().numpy().tobytes()).hexdigest() \
+        if world == 1 and int(allrows.max()) < 256 else None
+    times, res = [], None
+    for _ in range(2):            # first run pays one-time allocator growth; report the second
+        sync(world)
+        t0 = time.perf_counter()
+        flat, off = fixed_rows_to_device(allrows)
+        res = train_bpe(flat, off, args.bpe_vocab, reduce=reduce)
+        torch.cuda.synchronize()
+        times.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+        del flat, off
+    el = times[-1]
+    st = res.stats
     out = {"metric": "BPE merges/sec (fit_from_trajectories core: pretokenise + count + merge loop)",
-           "value": res.stats["n_merges"] / el, "unit": "merges/s", "merges": res.stats["n_merges"],
-           "seconds": el, "trajectories": per_rank * world, "vocab_size": args.bpe_vocab,
-           "setup_s": res.stats["setup_s"], "merge_loop_s": res.stats["merge_loop_s"],
-           "words": res.stats["n_words"], "symbols": res.stats["n_syms"],
-           "distinct_words": res.stats.get("n_distinct"), "live_words_at_end": res.stats.get("n_live_end")}
+           "value": st["n_merges"] / el, "unit": "merges/s", "merges": st["n_merges"],
+           "seconds": el, "seconds_runs": times, "trajectories": args.bpe_seqs - args.bpe_seqs % world,
+           "vocab_size": args.bpe_vocab, "setup_s": st["setup_s"], "merge_loop_s": st["merge_loop_s"],
+           "us_per_merge": st["merge_loop_s"] / max(st["n_merges"], 1) * 1e6,
+           "words": st["n_words"], "symbols": st["n_syms"], "distinct_words": st.get("n_distinct"),
+           "corpus_sha256": sha}
+    rb = bpe_bytes(st)
+    if "algo_bytes" in rb:
+        rb.update({"achieved_GBps": rb["algo_bytes"] / el / 1e9, "peak_GBps": HBM_PEAK / 1e9,
+                   "frac": rb["algo_bytes"] / el / HBM_PEAK, "bound": "hbm",
+                   "note": "§8d counts a full scan of the live symbols per merge; the kernels visit only "
+                           "candidate words, so this is an effective rate, not bytes moved"})
+    out["roofline"] = rb
+    if golden is not None and golden.get("merges") is not None and args.bpe_seqs == golden["trajectories"] \
+            and args.bpe_vocab == golden["vocab_size"]:
+        got = [list(m) for m in res.merges]
+        same = got == golden["merges"] and res.vocab == golden["vocab"]
+        out["parity"] = {"golden": os.path.relpath(K5_GOLDEN, REPO), "merges_equal_hf": bool(same),
+                         "corpus_sha256_equal": (sha == golden["corpus_sha256"]) if sha else None,
+                         "hf": golden.get("hf_version")}
+        assert same, "K5 merges differ from the golden HF BpeTrainer merges of the same corpus"
+    else:
+        out["parity"] = {"golden": None, "note": "no K5 golden for this corpus size / vocab (parity unpinned)"}
     if rank == 0 and not args.no_cpu:
-        out["cpu_baseline"] = hf_bpe_baseline(allrows[:20000].cpu().numpy(), args.bpe_vocab, res)
+        out["cpu_baseline"] = hf_bpe_same_sample(allrows[:args.bpe_sample], args.bpe_vocab)
     out["codec"] = bpe_codec_bench(res, allrows[:args.batch], dev, args)
+    del allrows
     return out
+
+
+def hf_bpe_same_sample(rows: torch.Tensor, vocab: int):
+    """HF tokenizers BpeTrainer (the reference's BPE, beast_bpe_trainer.py:61-98) and the GPU
+    trainer on ONE identical sample, merges/s both, merges compared."""
+    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
+    try:
+        from tokenizers import ByteLevelBPETokenizer
+        from tokenizers.trainers import BpeTrainer
+    except Exception as e:  # pragma: no cover
+        return {"value": None, "error": str(e)}
+    host = rows.cpu().numpy()
+    lo, hi = int(host.min()), int(host.max())
+    strings = ["".join(map(chr, r - lo)) for r in host]
+    t0 = time.perf_counter()
+    bpe = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=vocab, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=10000)
+    bpe._tokenizer.train_from_iterator(strings, trainer=tr)
+    el = time.perf_counter() - t0
+    model = json.loads(bpe._tokenizer.to_str())["model"]
+    nm = len(model["merges"])
+    flat, off = fixed_rows_to_device(rows)
+    train_bpe(flat, off, vocab)                       # warm-up at this size
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = train_bpe(flat, off, vocab)
+    torch.cuda.synchronize()
+    el_gpu = time.perf_counter() - t0
+    same = [list(m) for m in g.merges] == model["merges"] and g.vocab == model["vocab"]
+    return {"value": nm / el, "unit": "merges/s", "kind": "reference",
+            "cores": int(os.environ.get("RAYON_NUM_THREADS", "1")),
+            "gpu_same_sample_merges_per_s": len(g.merges) / el_gpu, "gpu_same_sample_s": el_gpu,
+            "hf_seconds": el, "merges_equal": bool(same),
+            "sample": f"HF tokenizers {__import__('tokenizers').__version__} BpeTrainer on the first {len(host)} "
+                      f"sequences x 140 bins of the K5 corpus ({nm} merges, {el:.2f}s) and the GPU trainer "
+                      f"on the same sequences"}
 
 
 def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
@@ -265,7 +475,6 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     ids, lens, _ = enc["r"]
     lens_np = lens.cpu().numpy()
     n_ids = int(lens_np.sum())
-    # flat ids for decode
     mask = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]
     dflat = ids[mask].contiguous()
     doff = torch.zeros(R + 1, dtype=torch.int64, device=dev)
@@ -287,7 +496,6 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
                 "encode_kernel_GBps": (R * width * 8 + n_ids * 4) / (t_enc * 1e-6) / 1e9,
                 "decode_kernel_GBps": (n_ids * 4 + R * width * 8) / (t_dec * 1e-6) / 1e9})
     if not args.no_cpu:
-        # the reference's per-row HF loop on a bounded sample
         host = rows.cpu().numpy() - lo
         n = min(R, 2048)
         t0 = time.perf_counter()
@@ -305,30 +513,18 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     return out
 
 
-def hf_bpe_baseline(rows: np.ndarray, vocab: int, gpu_res):
-    """HF tokenizers BpeTrainer (the reference's BPE, beast_bpe_trainer.py:61-74) on a bounded sample."""
-    try:
-        from tokenizers import ByteLevelBPETokenizer
-        from tokenizers.trainers import BpeTrainer
-    except Exception as e:  # pragma: no cover
-        return {"value": None, "error": str(e)}
-    lo, hi = int(rows.min()), int(rows.max())
-    strings = ["".join(map(chr, r - lo)) for r in rows]
-    t0 = time.perf_counter()
-    bpe = ByteLevelBPETokenizer()
-    tr = BpeTrainer(vocab_size=vocab, min_frequency=2, show_progress=False, special_tokens=[],
-                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=10000)
-    bpe._tokenizer.train_from_iterator(strings, trainer=tr)
-    el = time.perf_counter() - t0
-    nm = len(json.loads(bpe._tokenizer.to_str())["model"]["merges"])
-    return {"value": nm / el, "unit": "merges/s", "kind": "reference",
-            "cores": int(os.environ.get("RAYON_NUM_THREADS", os.cpu_count() or 1)),
-            "sample": f"HF tokenizers {__import__('tokenizers').__version__} BpeTrainer on {len(rows)} sequences "
-                      f"x 140 bins (first rows of the GPU corpus), {nm} merges, {el:.2f}s"}
+def dump_k5(dev, args):
+    tokens = k5_corpus(dev, args.bpe_seqs, 0, 1, k5_golden()).cpu().numpy()
+    assert tokens.min() >= 0 and tokens.max() < 256
+    u8 = tokens.astype(np.uint8)
+    np.savez_compressed(args.dump_k5, tokens=u8)
+    print(json.dumps({"dumped": args.dump_k5, "rows": int(u8.shape[0]),
+                      "sha256": hashlib.sha256(u8.tobytes()).hexdigest()}))
 
 
 def main():
     args = parse()
+    torch.set_num_threads(_host_threads())
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -336,6 +532,8 @@ def main():
     # ranks on one GPU (tests only; the driver's runs use one GPU per rank over RCCL)
     dev = torch.device("cuda", 0 if os.environ.get("BEAST_BENCH_ONE_DEVICE") == "1" else local)
     torch.cuda.set_device(dev)
+    if args.dump_k5:
+        return dump_k5(dev, args)
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("BEAST_BENCH_BACKEND", "nccl")
@@ -350,7 +548,9 @@ def main():
     tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, device=str(dev))
     fit = [{"actions": torch.from_numpy(synth_trajectories(4096, T, D, seed=1, start=4096 * i))} for i in range(2)]
     tok.fit_parameters(fit, verbose=False)
-    x = torch.from_numpy(synth_trajectories(B, T, D, seed=100 + rank)).to(dev)
+    x_np = synth_trajectories(B, T, D, seed=100 + rank)
+    x = torch.from_numpy(x_np).to(dev)
+    stream = torch.cuda.current_stream(dev)
 
     def step():
         tokens, _ = tok.encode(x)
@@ -358,43 +558,24 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        el = float(tt.item())
+    walls, gpu_ms = [], []
+    for _ in range(max(args.windows, 1)):
+        sync(world)
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        s_ev.record(stream)
+        for _ in range(args.steps):
+            step()
+        e_ev.record(stream)
+        sync(world)
+        walls.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+        gpu_ms.append(max_over_ranks(s_ev.elapsed_time(e_ev), world, dev))
+    el = float(np.median(walls))
     value = B * world * args.steps / el
+    gpu_tokens = tok.encode(x)[0].cpu().numpy()
 
     # ---- dominant-kernel roofline, measured live on the kernel's stream
-    stream = torch.cuda.current_stream(dev)
-    phi, _, proj = tok._constants(dev)
-    src, dst = tok._dof_maps(dev)
-    wmn, wmx = tok._bounds(dev)
-    params = torch.empty((B, D * N), dtype=torch.float32, device=dev)
-    tokens = torch.empty((B, N * D), dtype=torch.int64, device=dev)
-    pos = torch.empty((B, T, D), dtype=torch.float32, device=dev)
-    sp = stream.cuda_stream
-
-    def launch_enc():
-        _lib.run("beast_encode_f32", x.data_ptr(), B, T, x.stride(0), x.stride(1), x.stride(2), D, D, D,
-                 src.data_ptr(), proj.data_ptr(), N, wmn.data_ptr(), wmx.data_ptr(), V, 0, params.data_ptr(),
-                 tokens.data_ptr(), sp)
-
-    def launch_rec():
-        _lib.run("beast_reconstruct_f32", tokens.data_ptr(), B, D, D, N, V, 0, wmn.data_ptr(), wmx.data_ptr(),
-                 phi.data_ptr(), 0, T, dst.data_ptr(), D, None, 0, None, None, pos.data_ptr(), None, sp)
-
+    launch_enc, launch_rec = launchers(tok, dev, stream, x, B)
     t_enc = kernel_time_us(launch_enc, stream)
     t_rec = kernel_time_us(launch_rec, stream)
     if t_enc >= t_rec:
@@ -411,8 +592,11 @@ def main():
             "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
             "algo_bytes_per_launch": kbytes,
             "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
+    times_us = {"encode_4096": t_enc}
     if not args.no_large:
-        roof["large_batch"] = large_batch_roofline(tok, dev, stream, args.large_batch)
+        roof["large_batch"] = lb = large_batch_roofline(tok, dev, stream, args.large_batch)
+        times_us[f"encode_{args.large_batch}"] = lb["k_encode_us"]
+    mfma = mfma_utilisation(args.pmc_mfma, times_us)
 
     fitb = None
     if not args.no_fit:
@@ -420,11 +604,12 @@ def main():
 
     bpe = None
     if not args.no_bpe:
-        bpe = bpe_bench(tok, dev, args, world, rank, reduce)
+        bpe = bpe_bench(dev, args, world, rank, reduce)
 
-    cpu = None
+    cpu, parity = None, None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline((tok.w_min.cpu().numpy(), tok.w_max.cpu().numpy()), args.cpu_seconds)
+        cpu, parity = cpu_baseline(x_np, gpu_tokens, (tok.w_min.cpu().numpy(), tok.w_max.cpu().numpy()),
+                                   args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -436,7 +621,10 @@ def main():
             "config": {"workload": "BEASTBsplineTokenizer encode->reconstruct_traj, num_dof=14 num_basis=10 "
                                    "seq_len=50 vocab=256 degree_p=4", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "fit": fitb, "bpe": bpe,
+            "timing": {"windows": len(walls), "window_wall_s": walls, "window_gpu_event_ms": gpu_ms,
+                       "median_gpu_event_us_per_step": float(np.median(gpu_ms)) / args.steps * 1e3},
+            "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "token_parity": parity,
+            "host": host_info(), "fit": fitb, "bpe": bpe,
         }
         if cpu and cpu.get("value"):
             line["gpu_over_cpu"] = value / cpu["value"]

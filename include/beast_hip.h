@@ -50,10 +50,14 @@ const char* beast_last_error(void);
  * identical.
  * BEAST_OPT_MERGE_LDS_MIN = n: BPE merges of pairs counted >= n privatise their pair-count deltas
  * in LDS (default 4096; below, global atomics); results are identical.
+ * BEAST_OPT_MERGE_LIST_RATIO = r: a pair-index merge walks its candidate list when the list is
+ * shorter than (words / r), else it scans every word's Bloom signature (default 16; 0 = always
+ * the list); results are identical.
  * Not thread-safe with concurrent launches. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
 #define BEAST_OPT_MERGE_LDS_MIN 3
+#define BEAST_OPT_MERGE_LIST_RATIO 4
 int beast_set_option(int option, int value);
 
 /* ---------------------------------------------------------------- H1/H2 ---
@@ -249,6 +253,26 @@ int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t
                          int32_t* deltas, uint64_t* sig, void* index, uint32_t* table, uint64_t* argws,
                          int vocab_size, void* stream);
 int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
+/* Pair index for the device-driven loop (replaces the per-merge signature scan): a CSR of
+ * the distinct words holding each pair of two setup symbols (ids < n_sym), built once from the
+ * distinct words (n_symbols = their total symbol count bounds the entries), plus a token index
+ * (beast_bpe_index_workspace_bytes(Vt, capacity), initialised by beast_bpe_token_index_init)
+ * that receives the words each merge rewrote -- the candidates of any later pair with that
+ * merged token.  beast_bpe_loop_steps_ix is beast_bpe_loop_steps over these candidate lists
+ * (pair_index nullable: every merge then visits every word); a merge whose list is long scans
+ * the words' Bloom signatures instead (sig: beast_bpe_word_signatures, nullable = lists only;
+ * BEAST_OPT_MERGE_LIST_RATIO).  apps[2][max_merges] (nullable, zeroed by the caller) receives
+ * per merge the pair occurrences it rewrote in distinct words, then the words it visited.
+ * Replaces the loop of HF BpeTrainer::do_train as called from beast/beast_bpe_trainer.py:61-74. */
+size_t beast_bpe_pair_index_bytes(int n_sym, int64_t n_symbols);
+int beast_bpe_build_pair_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                               int n_sym, int64_t n_symbols, void* ws, size_t ws_bytes, void* stream);
+int beast_bpe_token_index_init(void* index, size_t index_bytes, int Vt, void* stream);
+int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
+                            uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
+                            int max_token_length, int32_t* deltas, const void* pair_index, int n_sym,
+                            void* token_index, uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
+                            uint32_t* apps, void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

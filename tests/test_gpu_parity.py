@@ -481,6 +481,56 @@ def test_bpe_merge_paths_match_hf(case, index_mode, bpe_golden, gpu_device):
     assert [list(m) for m in res.merges] == ref[case]["merges"]
 
 
+@pytest.mark.parametrize("mode", ["pair_index", "lists_always", "pair_index_tiny_pool", "no_pair_lists",
+                                  "reuse_flag", "signature_scan"])
+@pytest.mark.parametrize("case", ["skew/2048", "rand256/700", "traj_k2/2048", "repeat700/300", "wide3000/2048"])
+def test_bpe_merge_modes_match_hf(case, mode, bpe_golden, gpu_device):
+    """The device loop's candidate sources all give HF's merges: the pair index (setup-pair CSR +
+    merged-token word lists), a token pool too small for the lists (lists INEXACT -> those merges
+    visit every word), a loop without the setup-pair CSR (every merge visits every word), and the
+    Bloom-signature scan of round 1.  The per-merge rewrite counts are consistent."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+    ref, corpora = bpe_golden
+    cname, vs = case.split("/")
+
+    class Ops(GpuBpeOps):
+        def build_pair_index(self, words, n_sym, Vt):
+            GpuBpeOps.build_pair_index(self, words, n_sym, Vt)
+            if mode == "pair_index_tiny_pool":
+                tb = _lib.load().beast_bpe_index_workspace_bytes(Vt, 16)
+                self._tokix = torch.empty((tb + 3) // 4, dtype=torch.int32, device=self.device)
+                _lib.run("beast_bpe_token_index_init", self._tokix.data_ptr(), tb, Vt, self.stream)
+            if mode == "reuse_flag":     # as after an id re-use: every merge scans
+                self._tokix[2 * Vt + 3] = 1
+    flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
+    ops = Ops(gpu_device)
+    if mode == "no_pair_lists":
+        ops._pair_nsym = 0
+        orig = ops.build_pair_index
+
+        def no_csr(words, n_sym, Vt):
+            orig(words, n_sym, Vt)
+            ops._pair = torch.empty(0, dtype=torch.uint8, device=gpu_device)   # non-None, null CSR below
+        ops.build_pair_index = no_csr
+    lib = _lib.load()
+    assert lib.beast_set_option(_lib.OPT_MERGE_LIST_RATIO, 0 if mode == "lists_always" else 16) == 0
+    try:
+        res = train_bpe(flat, off, int(vs), ops=ops,
+                        merge_mode="signature_scan" if mode == "signature_scan" else "pair_index")
+    finally:
+        lib.beast_set_option(_lib.OPT_MERGE_LIST_RATIO, 16)
+    assert res.vocab == ref[case]["vocab"]
+    assert [list(m) for m in res.merges] == ref[case]["merges"]
+    if mode != "signature_scan":
+        apps = np.asarray(res.stats["applications"])
+        visits = np.asarray(res.stats["words_visited"])
+        assert len(apps) == len(res.merges) and (apps >= 1).all()
+        assert apps.sum() <= res.stats["n_syms_distinct"] and (visits >= 1).all()
+        if mode in ("reuse_flag", "no_pair_lists"):
+            assert (visits == res.stats["n_distinct"]).all()
+
+
 @pytest.mark.parametrize("lds_min", [0, 1 << 30])
 @pytest.mark.parametrize("case", ["skew/2048", "traj_k3/2048"])
 def test_bpe_delta_paths_match_hf(case, lds_min, bpe_golden, gpu_device):
