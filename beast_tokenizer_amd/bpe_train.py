@@ -87,6 +87,10 @@ class BPEResult:
     stats: Dict[str, float] = field(default_factory=dict)
 
 
+class _PersistentAbort(RuntimeError):
+    """The persistent merge loop's grid barrier timed out (workgroups not co-resident)."""
+
+
 class GpuBpeOps:
     """The HIP kernels of csrc/bpe.hip behind the driver's ops interface."""
 
@@ -250,10 +254,11 @@ class GpuBpeOps:
         _lib.run("beast_bpe_build_pair_index", words["sym"].data_ptr(), words["wstart"].data_ptr(),
                  words["wlen"].data_ptr(), n, n_sym, ns, self._pair.data_ptr(), nb, self.stream)
         self._pair_nsym = n_sym
-        cap = max(8 * n, 1 << 20)
+        cap = max(24 * n, 1 << 21)      # in u32: 8-byte entries, ~2 per rewritten word
         tb = lib.beast_bpe_index_workspace_bytes(Vt, cap)
         self._tokix = torch.empty((tb + 3) // 4, dtype=torch.int32, device=self.device)
         _lib.run("beast_bpe_token_index_init", self._tokix.data_ptr(), tb, Vt, self.stream)
+        self._claim = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
 
     def new_state(self, Vt: int, tlen: np.ndarray):
         nb = _lib.load().beast_bpe_argmax_workspace_bytes(Vt)
@@ -280,6 +285,12 @@ class GpuBpeOps:
 
     # -- device-driven merge loop (csrc/bpe.hip k_loop_step): no host round trip per merge
     LOOP_P = 0x9E3779B97F4A7C15   # odd multiplier of the token-string hash
+
+    def loop_kind(self) -> str:
+        """'steps' (two launches per merge, the default: faster at K5) or
+        'persistent' (one launch for the whole loop, csrc/bpe.hip k_bpe_loop); BEAST_BPE_LOOP
+        overrides."""
+        return os.environ.get("BEAST_BPE_LOOP", getattr(self, "_loop_kind", "steps"))
 
     def loop_supported(self, Vt: int) -> bool:
         return 4 * Vt * 4 <= 64 * 1024
@@ -312,6 +323,29 @@ class GpuBpeOps:
         state = ws[st_off:st_off + 32].view(torch.int32)     # active, a, b, nid, reused, vcur, parity, n
         host = torch.empty(8, dtype=torch.int32, pin_memory=True)
         vcur = n_tok
+        launched = False
+        if self.loop_kind() == "persistent" and getattr(self, "_pair", None) is None:
+            bb = lib.beast_bpe_loop_persistent_bytes()
+            bar = torch.empty(bb, dtype=torch.uint8, device=self.device)
+            try:
+                _lib.run("beast_bpe_loop_persistent", ws.data_ptr(), Vt, max_merges, max(vocab_size - n_tok, 0),
+                         words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                         _lib.ptr(words.get("wcount")), words["n_words"], self._tlen.data_ptr(), max_len,
+                         self._deltas.data_ptr(), _lib.ptr(words.get("sig")), table.data_ptr(),
+                         self._argws.data_ptr(), vocab_size, bar.data_ptr(), bb, self.stream)
+                launched = True
+            except NotImplementedError:     # too few CUs for the table rows: two launches per merge
+                pass
+        if launched:
+            host.copy_(state, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            flag = bar[36:40].view(torch.int32).cpu()
+            if int(flag[0]):
+                raise _PersistentAbort("a grid barrier of the persistent merge loop timed out")
+            n = int(host[7])
+            log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
+            self.last_apps = None
+            return [tuple(int(v) for v in r) for r in log], n >= max_merges
         pair = getattr(self, "_pair", None)
         apps = torch.zeros(2 * max_merges, dtype=torch.int32, device=self.device) if pair is not None else None
         while True:
@@ -320,7 +354,8 @@ class GpuBpeOps:
                 _lib.run("beast_bpe_loop_steps_ix", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
                          words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
                          words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
-                         pair.data_ptr(), self._pair_nsym, self._tokix.data_ptr(), _lib.ptr(words.get("sig")),
+                         pair.data_ptr(), self._pair_nsym, self._tokix.data_ptr(), self._claim.data_ptr(),
+                         _lib.ptr(words.get("sig")),
                          table.data_ptr(),
                          self._argws.data_ptr(), vocab_size, apps.data_ptr(), self.stream)
             else:
@@ -444,7 +479,16 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     if (device_loop and loop_reduce is no_reduce and not compact_every and hasattr(ops, "loop_supported")
             and ops.loop_supported(Vt)):
         # merges decided on the GPU; the host replays the log against the real strings
-        log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
+        try:
+            log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
+        except _PersistentAbort:
+            # workgroups were not all resident (another process on the GPU?): the launch-per-merge loop
+            ops2 = type(ops)(ops.device)
+            ops2._loop_kind = "steps"
+            return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
+                             max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=ops2,
+                             reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, use_index=use_index,
+                             device_loop=device_loop, replicate=replicate, merge_mode=merge_mode)
         for a, b, nid, reused in log:
             new_tok = id2str[a] + id2str[b]
             have = str2id.get(new_tok)
@@ -466,7 +510,8 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
                  "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
                  "n_syms_distinct": words.get("n_syms_distinct"),
                  "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce,
-                 "merge_mode": "pair_index" if getattr(ops, "_pair", None) is not None else "signature_scan"}
+                 "merge_mode": "pair_index" if getattr(ops, "_pair", None) is not None else "signature_scan",
+                 "loop": ops.loop_kind() if hasattr(ops, "loop_kind") else "steps"}
         apps = getattr(ops, "last_apps", None)
         if apps is not None:
             stats["applications"] = apps.tolist()

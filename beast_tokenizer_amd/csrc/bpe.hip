@@ -567,6 +567,100 @@ __device__ __forceinline__ unsigned long long sig_bit(uint32_t x) {
   return (1ull << (x & 63u)) | (1ull << (((x * 0x9E3779B1u) >> 26) & 63u));
 }
 
+// HF's merge of (a, b) -> new in one word (Word::merge: left to right, non-overlapping) with the
+// pair-count changes ((prev, a) -1, (prev, new) +1, (b, next) -1, (new, next) +1, weighted by the
+// word's count; the +1s only while the new string stays shorter than max_token_length).  Returns
+// the new length (0: the word holds no (a, b)), the new Bloom signature in g and the occurrences
+// merged in napp.  Words of <= MERGE_REG symbols are read once into registers (all loads in
+// flight together) and rewritten there: the in-place loop over global memory made every symbol a
+// dependent round trip, and a merge waits for its slowest word.
+constexpr int MERGE_REG = 32;
+struct MergeOp {
+  int a, b, nid, max_len;
+  uint32_t newlen;
+  const uint32_t* __restrict__ tlen;
+  int32_t* colA;
+  int32_t* colN;
+  int32_t* rowB;
+  int32_t* rowN;
+  __device__ __forceinline__ void left(uint32_t p, int32_t cnt) const {     // HF: ((prev, a), -1), ((prev, new), +1)
+    atomicAdd(&colA[p], -cnt);
+    if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
+  }
+  __device__ __forceinline__ void right(uint32_t nx, int32_t cnt) const {   // HF: ((b, next), -1), ((new, next), +1)
+    atomicAdd(&rowB[nx], -cnt);
+    if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
+  }
+};
+
+__device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint32_t L, const uint32_t* __restrict__ wcount,
+                                                  int64_t w, const MergeOp& m, unsigned long long& g, uint32_t& napp) {
+  const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
+  if (L <= (uint32_t)MERGE_REG) {
+    uint32_t v[MERGE_REG + 2];
+#pragma unroll
+    for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? (uint32_t)s[i] : 0xFFFFFFFFu;   // sentinel
+    v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < MERGE_REG - 1; ++i) hit |= (v[i] == a) & (v[i + 1] == b);
+    if (!hit) return 0;
+    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+    uint32_t o = 0, last = 0, skip = 0;
+    unsigned long long sg = 0;
+#pragma unroll
+    for (int i = 0; i < MERGE_REG; ++i) {
+      if ((uint32_t)i < L) {
+        uint32_t y = v[i];
+        if (skip) {
+          skip = 0;
+          continue;
+        }
+        if (v[i] == a && v[i + 1] == b) {   // v[i + 1] is the sentinel past the end
+          if (o > 0) m.left(last, cnt);
+          if (v[i + 2] != 0xFFFFFFFFu) m.right(v[i + 2], cnt);
+          y = nid;
+          skip = 1;
+          ++napp;
+        }
+        s[o++] = (uint16_t)y;
+        last = y;
+        sg |= sig_bit(y);
+      }
+    }
+    g = sg;
+    return o;
+  }
+  bool hit = false;
+  uint32_t prev = s[0];
+#pragma unroll 8
+  for (uint32_t k = 1; k < L; ++k) {
+    const uint32_t cur = s[k];
+    hit |= (prev == a) & (cur == b);
+    prev = cur;
+  }
+  if (!hit) return 0;
+  const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+  uint32_t r = 0, o = 0;
+  unsigned long long sg = 0;
+  while (r < L) {
+    uint32_t y = s[r];
+    if (y == a && r + 1 < L && s[r + 1] == b) {
+      if (o > 0) m.left(s[o - 1], cnt);
+      if (r + 2 < L) m.right(s[r + 2], cnt);
+      y = nid;
+      r += 2;
+      ++napp;
+    } else {
+      r += 1;
+    }
+    s[o++] = (uint16_t)y;
+    sg |= sig_bit(y);
+  }
+  g = sg;
+  return o;
+}
+
 // Inverted index symbol -> distinct words that may contain it (HF's where_to_update, on
 // the GPU).  Built once from the distinct words; the merge creating token `new` appends
 // the words it rewrote to a pool and k_apply_argmax turns that range into new's list.
@@ -583,6 +677,23 @@ __device__ unsigned long long g_merge_stats[4];
 constexpr int MERGE_UNROLL = 4;
 constexpr int MERGE_SCAN = 8;       // signature loads in flight per thread (two-phase scan)
 constexpr int MERGE_CLIST = 2048;   // LDS candidate list per workgroup
+// Per-workgroup phase stamps of the merge kernels (tools/ab builds with -DBPE_MERGE_STAMPS=<first
+// merge>; the product library compiles them out): s_memrealtime (100 MHz) of thread 0 at
+// entry, after the decision, after the candidate pass, before the delta flush and at exit,
+// for 64 merges x the first 1024 workgroups.
+#ifdef BPE_MERGE_STAMPS
+__device__ unsigned long long g_bpe_stamps[64][1024][6];
+#define MSTAMP(mi, k)                                                                            \
+  do {                                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && (mi) >= BPE_MERGE_STAMPS && (mi) < BPE_MERGE_STAMPS + 64)  \
+      g_bpe_stamps[(mi) - BPE_MERGE_STAMPS][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+#else
+#define MSTAMP(mi, k) do { } while (0)
+#endif
+#ifndef BPE_MERGE_STAMPS
+#define KM_MI 0
+#endif
 struct WordIndex {
   uint32_t* start;   // [Vt]
   uint32_t* len;     // [Vt]
@@ -687,8 +798,17 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
       sgv[u] = w < nw ? sig[w] : 0ull;
     }
   }
+#ifdef BPE_MERGE_STAMPS
+  __shared__ int st_mi;
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+  if (MODE != 2 && threadIdx.x == 0) st_mi = -1;
+#define KM_MI st_mi
+#endif
   if (MODE == 2) {
     if (threadIdx.x == 0) {
+#ifdef BPE_MERGE_STAMPS
+      st_mi = loop->n_merges;
+#endif
       dec = loop_decide(loop, aw, Vt, lh, tlen);
       if (blockIdx.x == 0) {   // the record k_apply_argmax applies and commits
         loop->r_active = dec.active;
@@ -702,6 +822,11 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
     if (!dec.active) return;
     a = dec.a; b = dec.b; nid = dec.nid;
     LDS = dec.count >= (unsigned long long)lds_min;
+#ifdef BPE_MERGE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && st_mi >= BPE_MERGE_STAMPS && st_mi < BPE_MERGE_STAMPS + 64)
+      g_bpe_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][0] = t_entry;
+#endif
+    MSTAMP(KM_MI, 1);
   }
   const uint32_t* cand = nullptr;
   int64_t ncand = nw;
@@ -730,55 +855,24 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   int32_t* rowN = dv + 3 * Vt;
   bool any = false;
   const unsigned long long need = sig_bit(a) | sig_bit(b);
+  const MergeOp mop{a, b, nid, max_len, newlen, tlen, colA, colN, rowB, rowN};
   auto merge_word = [&](int64_t w) {
     const uint32_t L = wlen[w];
     if (L < 2) return;
 #ifdef BPE_MERGE_STATS
     atomicAdd(&g_merge_stats[3], (unsigned long long)L);
 #endif
-    uint16_t* s = sym + wstart[w];
-    bool hit = false;
-    uint32_t prev = s[0];
-#pragma unroll 8
-    for (uint32_t k = 1; k < L; ++k) {
-      const uint32_t cur = s[k];
-      hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
-      prev = cur;
-    }
-    if (!hit) return;
+    unsigned long long g = 0;
+    uint32_t napp = 0;
+    const uint32_t o = merge_symbols(sym + wstart[w], L, wcount, w, mop, g, napp);
+    if (!o) return;
     any = true;
 #ifdef BPE_MERGE_STATS
     atomicAdd(&g_merge_stats[1], 1ull);
     atomicAdd(&g_merge_stats[2], (unsigned long long)L);
 #endif
-    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
-    uint32_t r = 0, o = 0;
-    while (r < L) {
-      const int x = s[r];
-      if (x == a && r + 1 < L && s[r + 1] == b) {
-        if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
-          const int p = s[o - 1];
-          atomicAdd(&colA[p], -cnt);
-          if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
-        }
-        if (r + 2 < L) {                       // HF: ((b, next), -1), ((new, next), +1)
-          const int nx = s[r + 2];
-          atomicAdd(&rowB[nx], -cnt);
-          if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
-        }
-        s[o++] = (uint16_t)nid;
-        r += 2;
-      } else {
-        s[o++] = (uint16_t)x;
-        r += 1;
-      }
-    }
     wlen[w] = o;
-    if (sig != nullptr) {
-      unsigned long long g = 0;
-      for (uint32_t k = 0; k < o; ++k) g |= sig_bit(s[k]);
-      sig[w] = g;
-    }
+    if (sig != nullptr) sig[w] = g;
     if (use_ix) {   // w now holds `new`: it goes on new's list
       const uint32_t pos = atomicAdd(&ix.ctl[0], 1u);
       if (pos < ix.ctl[2]) ix.pool[pos] = (uint32_t)w;
@@ -816,6 +910,7 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
       }
     }
     __syncthreads();
+    MSTAMP(KM_MI, 2);
     // phase 2: the listed candidates, one per thread
     const int n = min(cn, MERGE_CLIST);
 #ifdef BPE_MERGE_STATS
@@ -841,66 +936,22 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
     // the word's symbol signature (64-bit Bloom mask) rules out most words without
     // touching their symbols
     if ((sg[u] & need) != need) continue;
-    const uint32_t L = wlen[w];
-    if (L < 2) continue;
-    uint16_t* s = sym + wstart[w];
-    // read-only probe first: most words do not contain the pair.  No early exit: the
-    // loads do not wait on the compares, so they stream (long words are frequent
-    // signature false positives)
-    bool hit = false;
-    uint32_t prev = s[0];
-#pragma unroll 8
-    for (uint32_t k = 1; k < L; ++k) {
-      const uint32_t cur = s[k];
-      hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
-      prev = cur;
-    }
-    if (!hit) continue;
-    any = true;
-    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
-    uint32_t r = 0, o = 0;
-    while (r < L) {
-      const int x = s[r];
-      if (x == a && r + 1 < L && s[r + 1] == b) {
-        if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
-          const int p = s[o - 1];
-          atomicAdd(&colA[p], -cnt);
-          if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
-        }
-        if (r + 2 < L) {                       // HF: ((b, next), -1), ((new, next), +1)
-          const int nx = s[r + 2];
-          atomicAdd(&rowB[nx], -cnt);
-          if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
-        }
-        s[o++] = (uint16_t)nid;
-        r += 2;
-      } else {
-        s[o++] = (uint16_t)x;
-        r += 1;
-      }
-    }
-    wlen[w] = o;
-    if (sig != nullptr) {
-      unsigned long long g = 0;
-      for (uint32_t k = 0; k < o; ++k) g |= sig_bit(s[k]);
-      sig[w] = g;
-    }
-    if (use_ix) {   // w now holds `new`: it goes on new's list
-      const uint32_t pos = atomicAdd(&ix.ctl[0], 1u);
-      if (pos < ix.ctl[2]) ix.pool[pos] = (uint32_t)w;
-    }
+    merge_word(w);
    }
   }
   }
+  MSTAMP(KM_MI, 3);
   if (LDS) {
     if (any) touched = 1;
     __syncthreads();
     if (touched)   // contiguous atomics (one cache line per 32 entries)
+#pragma unroll 8
       for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) {
         const int32_t v = dl[i];
         if (v) atomicAdd(&deltas[i], v);
       }
   }
+  MSTAMP(KM_MI, 4);
 }
 
 // ------------------------------------------------------------ pair index --
@@ -1016,19 +1067,54 @@ __global__ __launch_bounds__(1024) void k_pair_scan(uint32_t* __restrict__ off, 
 // elements it read (word list, entry list, or every word for a scan) -- bench.py's accounting.
 constexpr int MIX_U = 4;
 constexpr int MIX_NEW = 256 * MIX_U;
-__device__ __forceinline__ bool seen_neighbour(const uint16_t* s, uint32_t i, int nid, int side, uint32_t v) {
-  for (uint32_t j = side == 0 ? 1u : 0u; j < i; ++j)   // an earlier occurrence of nid, same neighbour
-    if (s[j] == (uint16_t)nid && (side == 0 ? s[j - 1] : s[j + 1]) == v) return true;
-  return false;
+// The neighbours of new in a rewritten word, as entries: an L entry per occurrence unless the
+// previous occurrence had the same left neighbour, likewise R (O(L); a word may still be listed
+// twice under one (kind, symbol) -- k_merge_ix claims every entry-list word once per merge).
+template <bool WRITE>
+__device__ __forceinline__ uint32_t word_entries(const uint16_t* __restrict__ s, uint32_t o, uint32_t nid, uint32_t w,
+                                                 uint32_t* __restrict__ pool, uint32_t k, uint32_t cap) {
+  uint32_t n = 0, pl = 0xFFFFFFFFu, pr = 0xFFFFFFFFu;
+  auto emit = [&](uint32_t kind, uint32_t x) {
+    if (WRITE) {
+      if (k < cap) *reinterpret_cast<uint2*>(pool + 2 * (size_t)k) = make_uint2(w, (kind << 16) | x);
+      ++k;
+    } else {
+      ++n;
+    }
+  };
+  if (o <= (uint32_t)MERGE_REG) {   // the rewritten word in registers: one round trip, no chain
+    uint32_t v[MERGE_REG + 1];
+#pragma unroll
+    for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < o ? (uint32_t)s[i] : 0xFFFFFFFFu;
+    v[MERGE_REG] = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < MERGE_REG; ++i)
+      if (v[i] == nid) {
+        if (i > 0 && v[i - 1] != pl) { emit(ENT_L, v[i - 1]); pl = v[i - 1]; }
+        if (v[i + 1] != 0xFFFFFFFFu && v[i + 1] != pr) { emit(ENT_R, v[i + 1]); pr = v[i + 1]; }
+      }
+  } else {
+    uint32_t prev = 0xFFFFFFFFu, cur = s[0];
+    for (uint32_t i = 0; i < o; ++i) {
+      const uint32_t next = i + 1 < o ? s[i + 1] : 0xFFFFFFFFu;
+      if (cur == nid) {
+        if (i > 0 && prev != pl) { emit(ENT_L, prev); pl = prev; }
+        if (i + 1 < o && next != pr) { emit(ENT_R, next); pr = next; }
+      }
+      prev = cur;
+      cur = next;
+    }
+  }
+  return WRITE ? k : n;
 }
 
 __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                   uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
                                                   int64_t nw, uint32_t* __restrict__ tlen, int max_len,
                                                   int32_t* __restrict__ deltas, int Vt, WordIndex ix, PairIndex px,
-                                                  unsigned long long* __restrict__ sig, int list_ratio,
-                                                  LoopState* __restrict__ loop, long long lds_min, ArgWs aw,
-                                                  LoopHash lh, uint32_t* __restrict__ apps, int max_merges) {
+                                                  uint32_t* __restrict__ claim, unsigned long long* __restrict__ sig,
+                                                  int list_ratio, LoopState* __restrict__ loop, long long lds_min,
+                                                  ArgWs aw, LoopHash lh, uint32_t* __restrict__ apps, int max_merges) {
   extern __shared__ __attribute__((aligned(16))) int32_t dl[];
   __shared__ LoopStep dec;
   __shared__ const uint32_t* s_cand;
@@ -1038,6 +1124,9 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
   __shared__ uint32_t clist[MERGE_CLIST];
   __shared__ uint32_t ecnt, ebase, napps;
   __shared__ int cn;
+#ifdef BPE_MERGE_STAMPS
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   if (threadIdx.x == 0) {
     dec = loop_decide(loop, aw, Vt, lh, tlen);
     s_mi = loop->n_merges;
@@ -1090,11 +1179,20 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
   }
   __syncthreads();
   if (!dec.active) return;
+#ifdef BPE_MERGE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 1024 && s_mi >= BPE_MERGE_STAMPS && s_mi < BPE_MERGE_STAMPS + 64)
+    g_bpe_stamps[s_mi - BPE_MERGE_STAMPS][blockIdx.x][0] = t_entry;
+#endif
+  MSTAMP(s_mi, 1);
   const int mode = s_mode;
   const long long ncand = s_n;
   const uint32_t* cand = s_cand;
   const uint32_t want = s_want;
-  const int64_t per_round = (int64_t)MIX_U * 256;
+  // candidates per thread and round: as few as fill the grid (a thread's words are merged one
+  // after another, so a short list spreads over more workgroups)
+  const int U = (int)max((int64_t)1, min((int64_t)MIX_U, (int64_t)((ncand + (int64_t)gridDim.x * 256 - 1) /
+                                                                  ((int64_t)gridDim.x * 256))));
+  const int64_t per_round = (int64_t)U * 256;
   const int64_t nchunks = (nw + 255) / 256;
   if (mode ? (int64_t)blockIdx.x * per_round >= ncand : (int64_t)blockIdx.x >= nchunks) return;   // uniform
   const int a = dec.a, b = dec.b, nid = dec.nid;
@@ -1111,6 +1209,7 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
   int32_t* rowN = dv + 3 * Vt;
   uint32_t my_apps = 0;
   const uint32_t cap = ix.ctl[2];
+  const MergeOp mop{a, b, nid, max_len, newlen, tlen, colA, colN, rowB, rowN};
   // one round: every thread's (up to MIX_U) candidate words, then the block's entry appends
   auto round = [&](const int64_t (&wv)[MIX_U]) {
     uint32_t Lv[MIX_U], Sv[MIX_U], Ov[MIX_U];
@@ -1122,52 +1221,14 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
     uint32_t my_ent = 0;
     for (int u = 0; u < MIX_U; ++u) {
       Ov[u] = 0;
-      const uint32_t L = Lv[u];
-      if (L < 2) continue;
-      uint16_t* s = sym + Sv[u];
-      bool hit = false;
-      uint32_t prev = s[0];
-#pragma unroll 8
-      for (uint32_t k = 1; k < L; ++k) {
-        const uint32_t cur = s[k];
-        hit |= (prev == (uint32_t)a) & (cur == (uint32_t)b);
-        prev = cur;
-      }
-      if (!hit) continue;
-      const int32_t cnt = wcount ? (int32_t)wcount[wv[u]] : 1;
-      uint32_t rr = 0, o = 0;
+      if (Lv[u] < 2) continue;
       unsigned long long g = 0;
-      while (rr < L) {
-        const int x = s[rr];
-        int y = x;
-        if (x == a && rr + 1 < L && s[rr + 1] == b) {
-          if (o > 0) {                           // HF: ((prev, a), -1), ((prev, new), +1)
-            const int p = s[o - 1];
-            atomicAdd(&colA[p], -cnt);
-            if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
-          }
-          if (rr + 2 < L) {                      // HF: ((b, next), -1), ((new, next), +1)
-            const int nx = s[rr + 2];
-            atomicAdd(&rowB[nx], -cnt);
-            if ((int)(tlen[nx] + newlen) < max_len) atomicAdd(&rowN[nx], cnt);
-          }
-          y = nid;
-          rr += 2;
-          ++my_apps;
-        } else {
-          rr += 1;
-        }
-        s[o++] = (uint16_t)y;
-        g |= sig_bit((uint32_t)y);
-      }
+      const uint32_t o = merge_symbols(sym + Sv[u], Lv[u], wcount, wv[u], mop, g, my_apps);
+      if (!o) continue;
       wlen[wv[u]] = o;
       if (sig != nullptr) sig[wv[u]] = g;
       Ov[u] = o;
-      for (uint32_t i = 0; i < o; ++i)   // distinct left / right neighbours of new in the word
-        if (s[i] == (uint16_t)nid) {
-          my_ent += (i > 0 && !seen_neighbour(s, i, nid, 0, s[i - 1])) ? 1u : 0u;
-          my_ent += (i + 1 < o && !seen_neighbour(s, i, nid, 1, s[i + 1])) ? 1u : 0u;
-        }
+      my_ent += word_entries<false>(sym + Sv[u], o, (uint32_t)nid, 0u, nullptr, 0u, 0u);
     }
     const uint32_t my_off = my_ent ? atomicAdd(&ecnt, my_ent) : 0u;
     __syncthreads();
@@ -1179,22 +1240,8 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
       }
       __syncthreads();
       uint32_t k = ebase + my_off;
-      for (int u = 0; u < MIX_U && my_ent; ++u) {
-        const uint32_t o = Ov[u];
-        if (!o) continue;
-        const uint16_t* s = sym + Sv[u];
-        for (uint32_t i = 0; i < o; ++i)
-          if (s[i] == (uint16_t)nid) {
-            if (i > 0 && !seen_neighbour(s, i, nid, 0, s[i - 1])) {
-              if (k < cap) { ix.pool[2 * (size_t)k] = (uint32_t)wv[u]; ix.pool[2 * (size_t)k + 1] = (ENT_L << 16) | s[i - 1]; }
-              ++k;
-            }
-            if (i + 1 < o && !seen_neighbour(s, i, nid, 1, s[i + 1])) {
-              if (k < cap) { ix.pool[2 * (size_t)k] = (uint32_t)wv[u]; ix.pool[2 * (size_t)k + 1] = (ENT_R << 16) | s[i + 1]; }
-              ++k;
-            }
-          }
-      }
+      for (int u = 0; u < MIX_U && my_ent; ++u)
+        if (Ov[u]) k = word_entries<true>(sym + Sv[u], Ov[u], (uint32_t)nid, (uint32_t)wv[u], ix.pool, k, cap);
       __syncthreads();
       if (threadIdx.x == 0) ecnt = 0;
     }
@@ -1207,17 +1254,19 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
 #pragma unroll
         for (int u = 0; u < MIX_U; ++u) {
           const int64_t i = r0 + u * 256 + threadIdx.x;
-          wv[u] = i < ncand ? (int64_t)cand[i] : -1;
+          wv[u] = (u < U && i < ncand) ? (int64_t)cand[i] : -1;
         }
       } else {
         uint2 e[MIX_U];
 #pragma unroll
         for (int u = 0; u < MIX_U; ++u) {
           const int64_t i = r0 + u * 256 + threadIdx.x;
-          e[u] = i < ncand ? reinterpret_cast<const uint2*>(cand)[i] : make_uint2(0u, 0xFFFFFFFFu);
+          e[u] = (u < U && i < ncand) ? reinterpret_cast<const uint2*>(cand)[i] : make_uint2(0u, 0xFFFFFFFFu);
         }
+        const uint32_t stamp = (uint32_t)s_mi + 1u;   // a word listed twice is visited once
 #pragma unroll
-        for (int u = 0; u < MIX_U; ++u) wv[u] = e[u].y == want ? (int64_t)e[u].x : -1;
+        for (int u = 0; u < MIX_U; ++u)
+          wv[u] = (e[u].y == want && atomicMax(&claim[e[u].x], stamp) < stamp) ? (int64_t)e[u].x : -1;
       }
       round(wv);
     }
@@ -1251,14 +1300,18 @@ __global__ __launch_bounds__(256) void k_merge_ix(uint16_t* __restrict__ sym, co
       __syncthreads();
     }
   }
+  MSTAMP(s_mi, 2);
   if (my_apps) atomicAdd(&napps, my_apps);
   __syncthreads();
+  MSTAMP(s_mi, 3);
   if (threadIdx.x == 0 && napps && apps != nullptr && s_mi < max_merges) atomicAdd(&apps[s_mi], napps);
   if (LDS && touched)   // contiguous atomics (one cache line per 32 entries)
+#pragma unroll 8
     for (int i = threadIdx.x; i < 4 * Vt; i += blockDim.x) {
       const int32_t v = dl[i];
       if (v) atomicAdd(&deltas[i], v);
     }
+  MSTAMP(s_mi, 4);
 }
 
 // Fused apply + argmax, one workgroup per row x (the apply touches only entries of rows it
@@ -1400,6 +1453,267 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_argmax(uint32_t* __re
     for (int w = 0; w < APPLY_ROWS; ++w) m = umax64(m, wbest[w]);
     unsigned long long* slot = aw.slot + parity;
     if (m && m > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, m);
+  }
+}
+
+// -------------------------------------------------- persistent merge loop --
+// The whole device-driven loop in ONE launch (no kernel boundary per merge).  One workgroup of
+// 1024 threads per CU, all resident; per merge:
+//   D  every workgroup reduces the per-workgroup argmax keys of the previous phase A and makes
+//      the same decision (HF's stop rules, id by the string hash table; loop_decide's logic);
+//   M  the merge over the words: k_merge's two-phase Bloom-signature scan, LDS-privatised deltas
+//      flushed to `deltas`;
+//   -- grid barrier --
+//   A  apply + argmax (k_apply_argmax): one wave per table row, rows split over the workgroups;
+//      workgroup 0 also commits the merge (log, hash table, vcur) -- after every workgroup's
+//      decision, so no workgroup's hash probe can see this merge's string;
+//   -- grid barrier --
+// The barrier is arrival counters per group of workgroups (blockIdx & 7) plus one top counter
+// (a few dozen same-address atomics each, not one per workgroup), polled with an agent-scope
+// acquire; every spin is bounded: a timeout raises `abort`, every workgroup leaves the loop and
+// the host reruns the training on the launch-per-merge loop.
+constexpr int PL_T = 1024;           // threads per workgroup
+constexpr int PL_SCAN = 4;           // signature loads per thread and scan sub-batch
+constexpr int PL_CLIST = PL_T * PL_SCAN;
+constexpr int PL_GROUPS = 8;
+constexpr unsigned PL_SPIN_LIMIT = 1u << 26;
+
+struct PlBar {
+  unsigned int* sub;                 // [PL_GROUPS]
+  unsigned int* top;
+  unsigned int* abort_flag;
+  unsigned long long* bests;         // [grid] per-workgroup argmax key of the last phase A
+};
+
+__device__ __forceinline__ bool pl_barrier(const PlBar& pb, unsigned& epoch, int G) {
+  __shared__ int s_ok;
+  // every storing wave drains its stores (vmcnt(0); expcnt / lgkmcnt not waited), the
+  // workgroup meets, then one agent-scope release before the arrival (MI355X_MICROARCH.md,
+  // inter-workgroup visibility)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    ++epoch;
+    const int ng = G < PL_GROUPS ? G : PL_GROUPS;
+    const int grp = blockIdx.x % ng;
+    const unsigned gsize = (unsigned)((G - grp + ng - 1) / ng);
+    const unsigned old = __hip_atomic_fetch_add(&pb.sub[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == epoch * gsize) __hip_atomic_fetch_add(pb.top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = epoch * (unsigned)ng;
+    unsigned spins = 0;
+    int ok = 1;
+    while (__hip_atomic_load(pb.top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(pb.abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || ++spins > PL_SPIN_LIMIT) {
+        __hip_atomic_store(pb.abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // other workgroups' writes, after it
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__global__ __launch_bounds__(PL_T) void k_bpe_loop(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                  uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
+                                                  int64_t nw, uint32_t* __restrict__ tlen, int max_len,
+                                                  int32_t* __restrict__ deltas, int Vt, int nrows,
+                                                  unsigned long long* __restrict__ sig, uint32_t* __restrict__ table,
+                                                  LoopState* __restrict__ loop, LoopHash lh, ArgWs aw, PlBar pb,
+                                                  int n_steps, long long lds_min) {
+  extern __shared__ __attribute__((aligned(16))) int32_t dl[];
+  __shared__ uint32_t clist[PL_CLIST];
+  __shared__ int cn, any_s, changed_w[PL_T / 64];
+  __shared__ LoopStep dec;
+  __shared__ unsigned long long wbest[PL_T / 64];
+  const int G = gridDim.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rows_per = (nrows + G - 1) / G;   // <= 16 = waves per workgroup (host-checked)
+  const int x0 = blockIdx.x * rows_per;
+  unsigned epoch = 0;
+  // argmax of the row x this wave owns (rescan unless its cached best is still valid)
+  auto row_best = [&](int x, int vcur, bool changed) -> unsigned long long {
+    unsigned long long best = 0;
+    if (x >= nrows || x >= vcur) return 0;
+    if (aw.clean[x] && !changed) return aw.rowbest[x];
+    const uint32_t* row = table + (size_t)x * Vt;
+    for (int base = 0; base < vcur; base += 64 * 32) {
+      uint32_t c[32];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int y0 = base + (k * 64 + lane) * 4;
+        if (((Vt & 3) == 0) && y0 + 4 <= vcur) {
+          const uint4 u = *reinterpret_cast<const uint4*>(row + y0);
+          c[4 * k] = u.x; c[4 * k + 1] = u.y; c[4 * k + 2] = u.z; c[4 * k + 3] = u.w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) c[4 * k + q] = y0 + q < vcur ? row[y0 + q] : 0u;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int y = base + (k * 64 + lane) * 4 + q;
+          const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
+          const uint32_t cv = c[4 * k + q];
+          if (cv) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
+    if (lane == 0) {
+      aw.rowbest[x] = best;
+      aw.clean[x] = 1u;
+    }
+    return best;
+  };
+  auto publish_best = [&](unsigned long long best) {
+    if (lane == 0) wbest[wave] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long m = 0;
+      for (int w = 0; w < PL_T / 64; ++w) m = umax64(m, wbest[w]);
+      pb.bests[blockIdx.x] = m;
+    }
+  };
+  // initial argmax (phase A without an apply)
+  {
+    const int x = x0 + wave;
+    publish_best(wave < rows_per ? row_best(x, loop->vcur, false) : 0ull);
+  }
+  if (!pl_barrier(pb, epoch, G)) return;
+  for (int step = 0; step < n_steps; ++step) {
+#ifdef BPE_MERGE_STAMPS
+    const int smi = loop->n_merges;
+#else
+    const int smi = 0;
+#endif
+    MSTAMP(smi, 0);
+    // ---- D: the merge, decided identically by every workgroup
+    if (threadIdx.x < 64) {
+      unsigned long long m = 0;
+      for (int g = threadIdx.x; g < G; g += 64) m = umax64(m, pb.bests[g]);
+      for (int o = 32; o > 0; o >>= 1) m = umax64(m, __shfl_xor(m, o));
+      if (threadIdx.x == 0) {
+        aw.slot[loop->parity] = m;     // every workgroup writes the same value; loop_decide reads it
+        dec = loop_decide(loop, aw, Vt, lh, tlen);
+      }
+    }
+    __syncthreads();
+    if (!dec.active) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) loop->active = 0;
+      break;
+    }
+    MSTAMP(smi, 1);
+    const int a = dec.a, b = dec.b, nid = dec.nid;
+    const bool LDS = dec.count >= (unsigned long long)lds_min;
+    // ---- M: merge (a, b) -> nid in every word holding the pair
+    int32_t* dv = LDS ? dl : deltas;
+    if (LDS)
+      for (int i = threadIdx.x; i < 4 * Vt; i += PL_T) dl[i] = 0;
+    if (threadIdx.x == 0) { cn = 0; any_s = 0; }
+    __syncthreads();
+    const uint32_t newlen = tlen[a] + tlen[b];
+    const MergeOp mop{a, b, nid, max_len, newlen, tlen, dv, dv + Vt, dv + 2 * Vt, dv + 3 * Vt};
+    const unsigned long long need = sig_bit(a) | sig_bit(b);
+    const int64_t nchunks = (nw + 255) / 256;
+    bool any = false;
+    // chunks of 256 words taken round-robin: workgroup g, sub-batch r reads chunks
+    // g + (r * PL_SCAN*4 + u*4 + t/256) * G (4 chunks per 1024 threads)
+    for (int64_t c0 = blockIdx.x; c0 < nchunks; c0 += (int64_t)PL_SCAN * 4 * G) {
+      unsigned long long sgv[PL_SCAN];
+#pragma unroll
+      for (int u = 0; u < PL_SCAN; ++u) {
+        const int64_t c = c0 + ((int64_t)u * 4 + (threadIdx.x >> 8)) * G;
+        const int64_t w = c * 256 + (threadIdx.x & 255);
+        sgv[u] = (c < nchunks && w < nw) ? (sig != nullptr ? sig[w] : need) : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < PL_SCAN; ++u)
+        if ((sgv[u] & need) == need) {
+          const int64_t c = c0 + ((int64_t)u * 4 + (threadIdx.x >> 8)) * G;
+          clist[atomicAdd(&cn, 1)] = (uint32_t)(c * 256 + (threadIdx.x & 255));
+        }
+      __syncthreads();
+      const int n = cn;
+      for (int k = threadIdx.x; k < n; k += PL_T) {
+        const int64_t w = clist[k];
+        const uint32_t L = wlen[w];
+        if (L < 2) continue;
+        unsigned long long g = 0;
+        uint32_t napp = 0;
+        const uint32_t o = merge_symbols(sym + wstart[w], L, wcount, w, mop, g, napp);
+        if (!o) continue;
+        any = true;
+        wlen[w] = o;
+        if (sig != nullptr) sig[w] = g;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) cn = 0;
+      __syncthreads();
+    }
+    if (LDS) {
+      if (any) any_s = 1;
+      __syncthreads();
+      if (any_s)
+        for (int i = threadIdx.x; i < 4 * Vt; i += PL_T) {
+          const int32_t v = dl[i];
+          if (v) atomicAdd(&deltas[i], v);
+        }
+    }
+    MSTAMP(smi, 2);
+    if (!pl_barrier(pb, epoch, G)) return;
+    MSTAMP(smi, 3);
+    // ---- A: apply the deltas, retire (a, b), commit, argmax
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // every workgroup has decided: commit
+      loop->r_active = 1;
+      loop->r_a = a; loop->r_b = b; loop->r_nid = nid; loop->r_reused = dec.reused;
+      loop->r_vcur = dec.vcur; loop->r_parity = loop->parity; loop->r_len = dec.len;
+      loop->r_count = dec.count; loop->r_h = dec.h;
+      loop_commit(loop, lh);
+    }
+    const int x = x0 + wave;
+    const bool mine = wave < rows_per && x < nrows;
+    int changed = 0;
+    if (mine && lane == 0) {
+      uint32_t* row = table + (size_t)x * Vt;
+      int32_t v;
+      if ((v = deltas[x])) { row[a] += (uint32_t)v; deltas[x] = 0; changed = 1; }
+      if ((v = deltas[Vt + x])) { row[nid] += (uint32_t)v; deltas[Vt + x] = 0; changed = 1; }
+    }
+    if (lane == 0) changed_w[wave] = changed;
+    __syncthreads();
+    const bool own_b = b >= x0 && b < x0 + rows_per && b < nrows;
+    const bool own_n = nid >= x0 && nid < x0 + rows_per && nid < nrows;
+    if (own_b || own_n) {
+      for (int r = 0; r < 2; ++r) {
+        const int xr = r == 0 ? b : nid;
+        if (!(r == 0 ? own_b : own_n) || (r == 1 && nid == b)) continue;
+        uint32_t* row = table + (size_t)xr * Vt;
+        int anyr = 0;
+        for (int y = threadIdx.x; y < Vt; y += PL_T) {
+          int32_t v;
+          if (xr == b && (v = deltas[2 * Vt + y])) { row[y] += (uint32_t)v; deltas[2 * Vt + y] = 0; anyr = 1; }
+          if (xr == nid && (v = deltas[3 * Vt + y])) { row[y] += (uint32_t)v; deltas[3 * Vt + y] = 0; anyr = 1; }
+        }
+        if (anyr) changed_w[xr - x0] = 1;
+      }
+    }
+    __syncthreads();
+    if (x == a && mine && lane == 0) {
+      table[(size_t)a * Vt + b] = 0u;   // never re-picked
+      tlen[nid] = tlen[a] + tlen[b];
+      changed_w[wave] = 1;
+    }
+    __syncthreads();
+    publish_best(mine ? row_best(x, dec.vcur, changed_w[wave] != 0) : 0ull);
+    MSTAMP(smi, 4);
+    if (!pl_barrier(pb, epoch, G)) return;
+    MSTAMP(smi, 5);
   }
 }
 
@@ -1959,6 +2273,11 @@ static __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, i
   }
 }
 
+#ifdef BPE_MERGE_STAMPS
+extern "C" int beast_debug_merge_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_stamps), sizeof(g_bpe_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef BPE_MERGE_STATS
 extern "C" int beast_debug_merge_stats(unsigned long long* host4) {
   return hipMemcpyFromSymbol(host4, HIP_SYMBOL(g_merge_stats), sizeof(g_merge_stats)) == hipSuccess ? 0 : -2;
@@ -2099,10 +2418,10 @@ extern "C" int beast_bpe_token_index_init(void* index, size_t index_bytes, int V
 extern "C" int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym,
                                        const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                                        int64_t n_words, uint32_t* tlen, int max_token_length, int32_t* deltas,
-                                       const void* pair_index, int n_sym, void* token_index, uint64_t* sig,
-                                       uint32_t* table, uint64_t* argws, int vocab_size, uint32_t* apps,
-                                       void* stream) {
-  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws && token_index,
+                                       const void* pair_index, int n_sym, void* token_index, uint32_t* claim,
+                                       uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
+                                       uint32_t* apps, void* stream) {
+  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws && token_index && claim,
                 "beast_bpe_loop_steps_ix: null pointer");
   BEAST_REQUIRE(Vt >= 1 && Vt <= 32768 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_steps_ix: bad sizes");
   BEAST_REQUIRE(pair_index == nullptr || (n_sym >= 1 && n_sym <= Vt), "beast_bpe_loop_steps_ix: bad n_sym");
@@ -2137,13 +2456,57 @@ extern "C" int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_s
   const int rows = std::min(Vt, std::max(vocab_size, 1));
   for (int i = 0; i < n_steps; ++i) {
     hipLaunchKernelGGL(k_merge_ix, dim3(grid), dim3(256), lds, s, sym, wstart, wlen, wcount, n_words, tlen,
-                       max_token_length, deltas, Vt, ix, px, sg, beast::g_merge_list_ratio, st,
+                       max_token_length, deltas, Vt, ix, px, claim, sg, beast::g_merge_list_ratio, st,
                        (long long)beast::g_merge_lds_min, aw, lh, apps, max_merges);
     BEAST_LAUNCHED("k_merge_ix");
     hipLaunchKernelGGL(k_apply_argmax, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s,
                        table, deltas, Vt, 0, aw, 0, 1, 0, 0, 0, tlen, ix, true, false, st, lh, rows);
     BEAST_LAUNCHED("k_apply_argmax");
   }
+  return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_loop_persistent_bytes(void) { return 4096 + 8 * 4096; }
+
+extern "C" int beast_bpe_loop_persistent(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym,
+                                         const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
+                                         int64_t n_words, uint32_t* tlen, int max_token_length, int32_t* deltas,
+                                         uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
+                                         void* bar_ws, size_t bar_bytes, void* stream) {
+  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && deltas && table && argws && bar_ws,
+                "beast_bpe_loop_persistent: null pointer");
+  BEAST_REQUIRE(Vt >= 1 && Vt <= 4096 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_persistent: bad sizes");
+  BEAST_REQUIRE_CODE(bar_bytes >= beast_bpe_loop_persistent_bytes(), BEAST_E_WORKSPACE,
+                     "persistent loop workspace %zu < %zu", bar_bytes, beast_bpe_loop_persistent_bytes());
+  hipStream_t s = beast::as_stream(stream);
+  int dev = 0, cus = 0, per = 0;
+  BEAST_HIP(hipGetDevice(&dev), "hipGetDevice");
+  BEAST_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+  const size_t lds = (size_t)4 * Vt * sizeof(int32_t);
+  BEAST_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_bpe_loop, PL_T, lds), "occupancy");
+  // one workgroup per CU, and only if the device holds at least that many at once: the barrier
+  // needs every workgroup resident
+  BEAST_REQUIRE_CODE(per >= 1 && cus >= 1 && cus <= 4096, BEAST_E_UNSUPPORTED,
+                     "persistent loop: %d workgroups of %d threads per CU", per, PL_T);
+  const int G = cus;
+  const int rows = std::min(Vt, std::max(vocab_size, 1));
+  BEAST_REQUIRE_CODE((rows + G - 1) / G <= PL_T / 64, BEAST_E_UNSUPPORTED,
+                     "persistent loop: %d table rows over %d workgroups", rows, G);
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  LoopState* st = reinterpret_cast<LoopState*>(static_cast<unsigned char*>(ws) + L.st);
+  const LoopHash lh = loop_hash_view(ws, Vt, max_merges);
+  const ArgWs aw = argws_view(argws, Vt);
+  unsigned char* b = static_cast<unsigned char*>(bar_ws);
+  PlBar pb;
+  pb.sub = reinterpret_cast<unsigned int*>(b);
+  pb.top = pb.sub + PL_GROUPS;
+  pb.abort_flag = pb.top + 1;
+  pb.bests = reinterpret_cast<unsigned long long*>(b + 4096);
+  BEAST_HIP(hipMemsetAsync(bar_ws, 0, 4096, s), "persistent loop memset");
+  hipLaunchKernelGGL(k_bpe_loop, dim3(G), dim3(PL_T), lds, s, sym, wstart, wlen, wcount, n_words, tlen,
+                     max_token_length, deltas, Vt, rows, reinterpret_cast<unsigned long long*>(sig), table, st, lh,
+                     aw, pb, n_steps, (long long)beast::g_merge_lds_min);
+  BEAST_LAUNCHED("k_bpe_loop");
   return BEAST_OK;
 }
 

@@ -385,6 +385,14 @@ def bpe_bench(dev, args, world, rank, reduce):
         del flat, off
     el = times[-1]
     st = res.stats
+    if world == 1:
+        # §8d's byte count needs the pair occurrences every merge rewrote: an untimed rerun on the
+        # pair-index loop (same corpus -> same merges) records them
+        flat, off = fixed_rows_to_device(allrows)
+        rec = train_bpe(flat, off, args.bpe_vocab, reduce=reduce, merge_mode="pair_index")
+        assert rec.merges == res.merges, "pair-index loop and signature-scan loop disagree"
+        st = dict(st, applications=rec.stats.get("applications"))
+        del flat, off
     out = {"metric": "BPE merges/sec (fit_from_trajectories core: pretokenise + count + merge loop)",
            "value": st["n_merges"] / el, "unit": "merges/s", "merges": st["n_merges"],
            "seconds": el, "seconds_runs": times, "trajectories": args.bpe_seqs - args.bpe_seqs % world,

@@ -252,6 +252,16 @@ int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t
                          uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen, int max_token_length,
                          int32_t* deltas, uint64_t* sig, void* index, uint32_t* table, uint64_t* argws,
                          int vocab_size, void* stream);
+/* The same loop as ONE launch (one resident workgroup per CU; merge, grid barrier, apply +
+ * argmax, grid barrier per merge; no kernel boundary per merge).  bar_ws: at least
+ * beast_bpe_loop_persistent_bytes(); its first word group holds the barrier counters and the
+ * abort flag (uint32 at byte offset 36: nonzero = a barrier timed out, the loop state is then
+ * undefined and the caller reruns on beast_bpe_loop_steps).  Vt <= 4096. */
+size_t beast_bpe_loop_persistent_bytes(void);
+int beast_bpe_loop_persistent(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
+                              uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
+                              int max_token_length, int32_t* deltas, uint64_t* sig, uint32_t* table,
+                              uint64_t* argws, int vocab_size, void* bar_ws, size_t bar_bytes, void* stream);
 int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
 /* Pair index for the device-driven loop (replaces the per-merge signature scan): a CSR of
  * the distinct words holding each pair of two setup symbols (ids < n_sym), built once from the
@@ -261,7 +271,8 @@ int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** st
  * merged token.  beast_bpe_loop_steps_ix is beast_bpe_loop_steps over these candidate lists
  * (pair_index nullable: every merge then visits every word); a merge whose list is long scans
  * the words' Bloom signatures instead (sig: beast_bpe_word_signatures, nullable = lists only;
- * BEAST_OPT_MERGE_LIST_RATIO).  apps[2][max_merges] (nullable, zeroed by the caller) receives
+ * BEAST_OPT_MERGE_LIST_RATIO).  word_claim[n_words] (zeroed by the caller before the first step)
+ * marks the words a merge visited.  apps[2][max_merges] (nullable, zeroed by the caller) receives
  * per merge the pair occurrences it rewrote in distinct words, then the words it visited.
  * Replaces the loop of HF BpeTrainer::do_train as called from beast/beast_bpe_trainer.py:61-74. */
 size_t beast_bpe_pair_index_bytes(int n_sym, int64_t n_symbols);
@@ -271,8 +282,8 @@ int beast_bpe_token_index_init(void* index, size_t index_bytes, int Vt, void* st
 int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
                             uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
                             int max_token_length, int32_t* deltas, const void* pair_index, int n_sym,
-                            void* token_index, uint64_t* sig, uint32_t* table, uint64_t* argws, int vocab_size,
-                            uint32_t* apps, void* stream);
+                            void* token_index, uint32_t* word_claim, uint64_t* sig, uint32_t* table,
+                            uint64_t* argws, int vocab_size, uint32_t* apps, void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

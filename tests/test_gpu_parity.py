@@ -714,8 +714,9 @@ def test_conditions_match_reference(case, gpu_device):
         tok.reconstruct_traj(torch.from_numpy(rt[:5]).to(gpu_device))    # conditions fitted on 32 rows
 
 
+@pytest.mark.parametrize("loop", ["steps", "persistent"])
 @pytest.mark.parametrize("case", ["traj_k2/2048", "skew/700", "wide3000/2048", "repeat700/300"])
-def test_bpe_device_loop_matches_hf(case, bpe_golden, gpu_device):
+def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     """The device-driven merge loop (merges decided on the GPU, ids by string hash, replayed and
     verified on the host) gives HF's vocab and merges; so does its collision fallback (forced
     here with a degenerate hash multiplier, so that different strings collide)."""
@@ -723,13 +724,17 @@ def test_bpe_device_loop_matches_hf(case, bpe_golden, gpu_device):
     ref, corpora = bpe_golden
     cname, vs = case.split("/")
     flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
-    res = train_bpe(flat, off, int(vs))
-    assert res.stats.get("device_loop") is True
+    ops = GpuBpeOps(gpu_device)
+    ops._loop_kind = loop            # one launch for the whole loop, or two per merge
+    res = train_bpe(flat, off, int(vs), ops=ops)
+    assert res.stats.get("device_loop") is True and res.stats.get("loop") == loop
     assert res.vocab == ref[case]["vocab"]
     assert [list(m) for m in res.merges] == ref[case]["merges"]
 
     class Degenerate(GpuBpeOps):
         LOOP_P = 0          # h(string) = its last byte: distinct strings collide -> host fallback
-    res2 = train_bpe(flat, off, int(vs), ops=Degenerate(gpu_device))
+    dg = Degenerate(gpu_device)
+    dg._loop_kind = loop
+    res2 = train_bpe(flat, off, int(vs), ops=dg)
     assert res2.vocab == ref[case]["vocab"]
     assert [list(m) for m in res2.merges] == ref[case]["merges"]

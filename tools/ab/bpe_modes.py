@@ -15,14 +15,18 @@ from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe  # noq
 from beast_tokenizer_amd import _lib  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-CONFIGS = [("pair_index", 16), ("pair_index", 4), ("pair_index", 64), ("pair_index", 0), ("signature_scan", 16)]
+CONFIGS = [("signature_scan", 16, 4096, "persistent"), ("signature_scan", 16, 4096, "steps")]
+if os.environ.get("BPE_MODES"):
+    CONFIGS = [tuple(int(v) if v.isdigit() else v for v in c.split(":")) for c in os.environ["BPE_MODES"].split(",")]
 dev = torch.device("cuda", 0)
 rows = bench.k5_corpus(dev, 500000, 0, 1, bench.k5_golden())
 flat, off = fixed_rows_to_device(rows)
 out, ref = {}, None
 for r in range(reps):
-    for mode, ratio in CONFIGS:
+    for mode, ratio, ldsmin, loop in CONFIGS:
+        os.environ["BEAST_BPE_LOOP"] = loop
         _lib.load().beast_set_option(_lib.OPT_MERGE_LIST_RATIO, ratio)
+        _lib.load().beast_set_option(_lib.OPT_MERGE_LDS_MIN, ldsmin)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         res = train_bpe(flat, off, 2048, merge_mode=mode)
@@ -36,10 +40,10 @@ for r in range(reps):
             v = np.asarray(res.stats["words_visited"])
             print(f"  ratio {ratio}: words visited per merge: mean {v.mean():.0f}, median {np.median(v):.0f}, "
                   f"list merges {(v < res.stats['n_distinct']).sum()}, total {v.sum():.3g}")
-        mode = f"{mode}/{ratio}"
+        mode = f"{mode}/{ratio}/{ldsmin}/{loop}/{res.stats.get('loop')}"
         out.setdefault(mode, []).append({"s": el, "setup_s": res.stats["setup_s"], "loop_s": res.stats["merge_loop_s"],
                                          "merges": len(res.merges)})
-        print(mode, f"{el * 1e3:.1f} ms  setup {res.stats['setup_s'] * 1e3:.1f}  loop {res.stats['merge_loop_s'] * 1e3:.1f}",
+        print(mode, ratio, ldsmin, loop, res.stats.get("loop"), f"{el * 1e3:.1f} ms  setup {res.stats['setup_s'] * 1e3:.1f}  loop {res.stats['merge_loop_s'] * 1e3:.1f}",
               flush=True)
 g = bench.k5_golden()
 if g and g.get("merges"):
