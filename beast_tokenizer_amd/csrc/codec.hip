@@ -660,6 +660,8 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const bool mw = wave < PIPE_MW;   // wave-uniform role
+  BSTAMP(0, 0);
+  STAMP(0, 0);
   const bool quant = a.tokens_out != nullptr;
   const float vm1 = (float)(a.vocab - 1);
   const int64_t b0 = (int64_t)blockIdx.x * (2 * PIPE_SUB);
@@ -681,12 +683,16 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
     }
     dma4<PIPE_MT>(lcol, a.dof_src, PS::D);
     dma16_fixed<PS::Y_OPS>(YB, src, min(last, (b0 + PIPE_SUB) * tile16), min(last, (b0 + 2 * PIPE_SUB) * tile16 - 1));
+    STAMP(0, 1);
     wait_vm_lgkm<PS::Y_OPS>();   // A and the constants have landed (B's DMA is the newest)
+    STAMP(0, 2);
   }
   bar_only();
   if (mw) {
     pipe_fit<S>(g, m, P, YA, lcol, pbA, nbA, wave, lane);
+    STAMP(0, 3);
     wait_vm_lgkm<0>();           // B has landed; pbA written
+    STAMP(0, 4);
   } else {
     if (quant)
       for (int i = tid - PIPE_MT; i < PS::DN; i += PIPE_MT)
@@ -697,12 +703,22 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
   if (mw) {
     pipe_fit<S>(g, m, P, YB, lcol, pbB, nbB, wave, lane);
     wait_vm_lgkm<0>();
+    STAMP(0, 5);
   } else {
     pipe_store<S>(a, pbA, kq, wlo, whi, b0, nbA, tid - PIPE_MT, PIPE_MT, vm1);
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the LDS reads of pbA are done
+    STAMP(0, 5);
   }
   bar_only();
+  STAMP(0, 6);
   pipe_store<S>(a, pbB, kq, wlo, whi, b0 + PIPE_SUB, nbB, tid, PIPE_W * 64, vm1);
+  STAMP(0, 7);
+#ifdef BEAST_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(0, 8);
+  __syncthreads();
+#endif
+  BSTAMP(0, 1);
 }
 
 // ------------------------------------------------------------ reconstruct --

@@ -78,6 +78,8 @@ def main():
     stamps = (C.c_ulonglong * (2 * NW * 16))()
     lib.beast_stamps_read(stamps)
     sizes = [int(v) for v in sys.argv[1:]] or [4096, 1048576]
+    if os.environ.get("STAMPS_BLOCKS_ONLY"):
+        sizes = sizes
     s = torch._C._cuda_getCurrentRawStream(0)
     out = {}
     for B in sizes:
@@ -100,17 +102,22 @@ def main():
             return lib.beast_reconstruct_f32(tokens.data_ptr(), B, 14, 14, 10, 256, 0, p.p_wmn, p.p_wmx, p.p_phi, 0,
                                              50, p.p_dst, 14, None, 0, None, None, pos.data_ptr(), None, s)
         res = {}
-        for kname, fn, names, k in (("encode", enc, ENC, 0), ("encode_params_only", enc_params_only, ENC, 0),
+        pipe = ["start", "dma_issued", "A_landed", "fitA_done(mw)", "B_landed(mw)", "fitB_done|storeA_done", "bar3",
+                "storeB_issued", "drained"]
+        for kname, fn, names, k in (("encode", enc, pipe if B <= 8192 else ENC, 0),
+                                    ("encode_params_only", enc_params_only, pipe if B <= 8192 else ENC, 0),
                                     ("reconstruct", rec, REC, 1)):
             for _ in range(20):           # warm: code, constants and the tile in L2 as in back-to-back use
                 assert fn() == 0
             torch.cuda.synchronize()
             assert lib.beast_stamps_read(stamps) == 0
             v = [stamps[(k * NW + w) * 16: (k * NW + w) * 16 + 16] for w in range(NW)]
-            ws = [w for w in range(NW) if v[w][0]]   # waves that exist in this kernel
-            t0 = min(v[w][0] for w in ws)
-            res[kname] = {names[i]: [int(v[w][i] - t0) if v[w][i] >= t0 else None for w in ws]
-                          for i in range(len(names)) if names[i] != "-"}
+            ws = [w for w in range(NW) if v[w][0]]   # waves that stamped (none: kernel without STAMP)
+            res[kname] = {}
+            if ws:
+                t0 = min(v[w][0] for w in ws)
+                res[kname] = {names[i]: [int(v[w][i] - t0) if v[w][i] >= t0 else None for w in ws]
+                              for i in range(len(names)) if names[i] != "-"}
             assert lib.beast_bstamps_read(bst) == 0
             res[kname]["blocks"] = block_summary(bst, k, min(4096, grid_of(B)))
         out[B] = res
