@@ -54,11 +54,17 @@ def build_fastpath(force: bool = False, verbose: bool = False) -> str:
     """The host-side C++ fast path (csrc/fastpath.cpp, ATen only, no device code), built
     in-tree with torch.utils.cpp_extension so it travels with the repo."""
     so = fastpath_so()
-    if not force and os.path.exists(so) and os.path.getmtime(so) >= os.path.getmtime(FAST_SRC):
+    import hashlib
+    with open(FAST_SRC, "rb") as f:
+        digest = hashlib.sha256(f.read()).hexdigest()
+    stamp = so + ".sha256"
+    if not force and os.path.exists(so) and os.path.exists(stamp) and open(stamp).read().strip() == digest:
         return so
     from torch.utils.cpp_extension import load
     os.makedirs(FAST_DIR, exist_ok=True)
     load(name=FAST_NAME, sources=[FAST_SRC], build_directory=FAST_DIR, extra_cflags=["-O3"], verbose=verbose)
+    with open(stamp, "w") as f:
+        f.write(digest + "\n")
     return so
 
 
@@ -68,11 +74,28 @@ def _deps():
     return hdrs
 
 
+def _fingerprint() -> str:
+    """SHA-256 of every source, header and flag the library is built from.  Staleness is decided
+    by content, not mtime: the in-tree .so travels to the GPU box with the snapshot (its mtime
+    says nothing there), and a library built from other sources must never be reused."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(" ".join(CXXFLAGS).encode())
+    for p in _sources() + sorted(_deps()) + [__file__]:
+        h.update(os.path.relpath(p, REPO).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+STAMP = LIB + ".sha256"
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(STAMP):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in _sources() + _deps() + [__file__])
+    with open(STAMP) as f:
+        return f.read().strip() != _fingerprint()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -99,6 +122,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(STAMP, "w") as f:
+        f.write(_fingerprint() + "\n")
     return LIB
 
 
