@@ -75,6 +75,9 @@ SIGNATURES = {
     "beast_bpe_loop_persistent": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
                                          _vp, _i32, _vp, _sz, _vp]),
     "beast_bpe_loop_state": (_i32, [_vp, _i32, _i32, _vp, _vp]),
+    "beast_bpe_batch_workspace_bytes": (_sz, [_i32]),
+    "beast_bpe_loop_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
+                                    _vp, _sz, _i32, _i32, _vp]),
     "beast_bpe_pair_index_bytes": (_sz, [_i32, _i64]),
     "beast_bpe_build_pair_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _i64, _vp, _sz, _vp]),
     "beast_bpe_token_index_init": (_i32, [_vp, _sz, _i32, _vp]),

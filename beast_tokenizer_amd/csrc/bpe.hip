@@ -440,6 +440,7 @@ __global__ __launch_bounds__(256) void k_count_pairs_lds(const uint16_t* __restr
 }
 
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 
 // Incremental argmax.  ws layout (u64): [2 + parity] result slots, [4, 4+Vt) the best key of
 // each row, then u32 clean[Vt] (0 = never scanned: the zero-filled workspace starts
@@ -478,6 +479,11 @@ struct LoopState {
   int32_t r_active, r_a, r_b, r_nid, r_reused, r_vcur, r_parity;
   uint32_t r_len;
   unsigned long long r_count, r_h;
+  // the batch k_merge_batch decided for the following k_apply_batch (written by its workgroup 0)
+  int32_t bn, bvcur;
+  int32_t ba[8], bb[8], bnid[8], breused[8];
+  uint32_t blen[8];
+  unsigned long long bh[8];
 };
 
 // ------------------------------------------------------- device merge loop --
@@ -593,8 +599,9 @@ struct MergeOp {
   }
 };
 
+template <class Op>
 __device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint32_t L, const uint32_t* __restrict__ wcount,
-                                                  int64_t w, const MergeOp& m, unsigned long long& g, uint32_t& napp) {
+                                                  int64_t w, const Op& m, unsigned long long& g, uint32_t& napp) {
   const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
   if (L <= (uint32_t)MERGE_REG) {
     uint32_t v[MERGE_REG + 2];
@@ -677,12 +684,19 @@ __device__ unsigned long long g_merge_stats[4];
 constexpr int MERGE_UNROLL = 4;
 constexpr int MERGE_SCAN = 8;       // signature loads in flight per thread (two-phase scan)
 constexpr int MERGE_CLIST = 2048;   // LDS candidate list per workgroup
+constexpr int BATCH_CLIST = 2 * 256 * MERGE_SCAN;   // k_merge_batch's list: two scan rounds
 // Per-workgroup phase stamps of the merge kernels (tools/ab builds with -DBPE_MERGE_STAMPS=<first
 // merge>; the product library compiles them out): s_memrealtime (100 MHz) of thread 0 at
 // entry, after the decision, after the candidate pass, before the delta flush and at exit,
 // for 64 merges x the first 1024 workgroups.
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][6];
+__device__ unsigned long long g_bpe_dstamps[64][8];   // k_merge_batch's decision phases (workgroup 0)
+#define DSTAMP(mi, k)                                                                            \
+  do {                                                                                           \
+    if (blockIdx.x == 0 && lane == 0 && (mi) >= BPE_MERGE_STAMPS && (mi) < BPE_MERGE_STAMPS + 64)      \
+      g_bpe_dstamps[(mi) - BPE_MERGE_STAMPS][k] = __builtin_amdgcn_s_memrealtime();                      \
+  } while (0)
 #define MSTAMP(mi, k)                                                                            \
   do {                                                                                           \
     if (threadIdx.x == 0 && blockIdx.x < 1024 && (mi) >= BPE_MERGE_STAMPS && (mi) < BPE_MERGE_STAMPS + 64)  \
@@ -690,6 +704,7 @@ __device__ unsigned long long g_bpe_stamps[64][1024][6];
   } while (0)
 #else
 #define MSTAMP(mi, k) do { } while (0)
+#define DSTAMP(mi, k) do { } while (0)
 #endif
 #ifndef BPE_MERGE_STAMPS
 #define KM_MI 0
@@ -1453,6 +1468,514 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_argmax(uint32_t* __re
     for (int w = 0; w < APPLY_ROWS; ++w) m = umax64(m, wbest[w]);
     unsigned long long* slot = aw.slot + parity;
     if (m && m > __atomic_load_n(slot, __ATOMIC_RELAXED)) atomicMax(slot, m);
+  }
+}
+
+// --------------------------------------------------------- batched merges --
+// Several merges per (merge, apply) pass, exactly HF's sequence.  Let p1, p2, ... be the table's
+// pairs in HF order (count, then smallest (a, b)).  After merging p1 -> n1 every old pair keeps
+// or loses count; the only new pairs contain n1 and each is bounded by the old pair it grew
+// from: count(x, n1) <= count(x, a1), count(n1, y) <= count(b1, y), count(n1, n1) <=
+// count(b1, a1).  If p2 shares no symbol with p1 and p1 is not a self-pair (a1 == b1, where
+// "a a a a" -> "n n" breaks the bound), those old pairs are neither p1 nor p2, so they rank
+// below p2; a new pair at an equal count also ranks below (its new id exceeds every old one).
+// So p2 is the argmax after p1 -- and by the same argument p3 after p1, p2 (its bounding pairs
+// share a symbol with p1 or p2, so they are not batch members), and so on.  A batch therefore
+// takes the top pairs in order while each is symbol-disjoint from the batch, the previous one
+// was not a self-pair, its string is new (no HF id re-use; distinct within the batch), the
+// count clears min_frequency and the vocabulary and log have room; the first pair that fails
+// ends the batch (it is decided next pass, with the full rules, on the updated table).
+//
+// The order needs more than each row's best: the true next pair may be the second-best of a
+// row already taken.  k_apply_batch keeps every row's best and second-best key and hands each
+// workgroup's BK best rows (best, second) to the next k_merge_batch, whose wave 0 reduces them
+// to the global BK best rows and stops the batch where an accepted row's second-best would
+// come first.  Measured at K5: 1,724 merges in 627 passes (BK = 4) instead of 1,724.
+constexpr int BK = 8;                 // merges per batch at most (LoopState holds 8)
+constexpr int BATCH_LDS = 32768;      // bytes of LDS delta vectors per workgroup (k_merge's 4 * Vt int32 at Vt 2048)
+constexpr int BATCH_WG_LANE = 4;      // apply-workgroup lists per lane of the deciding wave (Vt <= 4096)
+
+struct BatchWs {
+  unsigned long long* rowsecond;      // [Vt]
+  unsigned long long* wgkey;          // [BK][nwg] each apply workgroup's BK best rows, best first (k-major:
+  unsigned long long* wgsec;          // [BK][nwg]  the deciding wave reads them coalesced) and their second-best
+  int32_t* deltas;                    // [BK][4][Vt]
+};
+__host__ __device__ inline int batch_nwg(int Vt) { return (Vt + APPLY_ROWS_N - 1) / APPLY_ROWS_N; }
+__host__ __device__ inline size_t batch_ws_bytes(int Vt) {
+  return ((size_t)Vt * 8 + (size_t)batch_nwg(Vt) * BK * 2 * 8 + (size_t)BK * 4 * Vt * 4 + 255) & ~size_t(255);
+}
+__host__ __device__ inline BatchWs batch_view(void* ws, int Vt) {
+  BatchWs v;
+  char* p = static_cast<char*>(ws);
+  const size_t nt = (size_t)batch_nwg(Vt) * BK;
+  v.rowsecond = reinterpret_cast<unsigned long long*>(p);
+  v.wgkey = v.rowsecond + Vt;
+  v.wgsec = v.wgkey + nt;
+  v.deltas = reinterpret_cast<int32_t*>(v.wgsec + nt);
+  return v;
+}
+
+// Pair-count changes of batch merge j: kind 0 (x, a_j) -1, 1 (x, new_j) +1, 2 (b_j, y) -1, 3
+// (new_j, y) +1 -- k_merge's four vectors per merge.  The first merges of the batch whose
+// vectors fit BATCH_LDS (symbols < stride = vcur + n, so several while the vocabulary is small)
+// sum them in LDS when their count is large (k_merge's rule), the rest add to the global
+// vectors.  A neighbour may be a token this batch creates: its length is in nlen (tlen is
+// written by the apply).
+struct BatchOp {
+  int a, b, nid, max_len, j, Vt, vbase, nnew, stride;
+  uint32_t newlen;
+  const uint32_t* __restrict__ tlen;
+  const uint32_t* nlen;
+  int32_t* dl;          // LDS vectors of this merge, or null
+  int32_t* gdel;
+  __device__ __forceinline__ uint32_t len_of(uint32_t x) const {
+    return (int)x >= vbase && (int)x < vbase + nnew ? nlen[x - vbase] : tlen[x];
+  }
+  __device__ __forceinline__ void add(int kind, uint32_t x, int32_t v) const {
+    if (dl != nullptr) atomicAdd(&dl[kind * stride + x], v);
+    else atomicAdd(&gdel[((size_t)j * 4 + kind) * Vt + x], v);
+  }
+  __device__ __forceinline__ void left(uint32_t p, int32_t cnt) const {
+    add(0, p, -cnt);
+    if ((int)(len_of(p) + newlen) < max_len) add(1, p, cnt);
+  }
+  __device__ __forceinline__ void right(uint32_t nx, int32_t cnt) const {
+    add(2, nx, -cnt);
+    if ((int)(len_of(nx) + newlen) < max_len) add(3, nx, cnt);
+  }
+};
+
+// 64-bit wave helpers: DPP row shifts and row broadcasts (gfx9) leave the wave max in lane 63
+template <int CTRL, int ROW_MASK, bool BC>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, 0xF, BC);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xF, BC);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+  v = umax64(v, dpp_u64<0x111, 0xF, true>(v));    // row_shr:1
+  v = umax64(v, dpp_u64<0x112, 0xF, true>(v));    // row_shr:2
+  v = umax64(v, dpp_u64<0x114, 0xF, true>(v));    // row_shr:4
+  v = umax64(v, dpp_u64<0x118, 0xF, true>(v));    // row_shr:8: lane 15 of a row holds its max
+  v = umax64(v, dpp_u64<0x142, 0xA, false>(v));   // row_bcast:15 into rows 1, 3
+  v = umax64(v, dpp_u64<0x143, 0xC, false>(v));   // row_bcast:31 into rows 2, 3
+  return readlane_u64(v, 63);
+}
+
+// Two descending (key, second) lists of KM -> the top KM of both, descending: the elementwise
+// max of one list against the other reversed is bitonic, and KM/2, KM/4, ... half-cleaners sort it.
+template <int KM>
+__device__ __forceinline__ void top_merge(unsigned long long (&K)[KM], unsigned long long (&S)[KM],
+                                          const unsigned long long (&OK)[KM], const unsigned long long (&OS)[KM]) {
+#pragma unroll
+  for (int i = 0; i < KM; ++i) {
+    const bool t = OK[KM - 1 - i] > K[i];
+    K[i] = t ? OK[KM - 1 - i] : K[i];
+    S[i] = t ? OS[KM - 1 - i] : S[i];
+  }
+#pragma unroll
+  for (int d = KM / 2; d > 0; d >>= 1)
+#pragma unroll
+    for (int i = 0; i < KM; ++i)
+      if ((i & d) == 0) {
+        const bool t = K[i + d] > K[i];
+        const unsigned long long k0 = K[i], s0 = S[i];
+        K[i] = t ? K[i + d] : k0;
+        S[i] = t ? S[i + d] : s0;
+        K[i + d] = t ? k0 : K[i + d];
+        S[i + d] = t ? s0 : S[i + d];
+      }
+}
+
+template <int KM>
+__global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+                                                     uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
+                                                     int64_t nw, const uint32_t* __restrict__ tlen, int max_len,
+                                                     int Vt, unsigned long long* __restrict__ sig,
+                                                     LoopState* __restrict__ loop, LoopHash lh, BatchWs bw,
+                                                     long long lds_min) {
+  __shared__ __attribute__((aligned(16))) int32_t dl[BATCH_LDS / 4];
+  __shared__ uint32_t clist[BATCH_CLIST];
+  __shared__ int cn, touched, s_n, s_kd;
+  __shared__ int s_a[BK], s_b[BK], s_nid[BK];
+  __shared__ uint32_t s_len[BK];
+  __shared__ unsigned long long s_need[BK];
+  const int lane = threadIdx.x & 63;
+  // first signature batch of the two-phase scan, issued before the batch is known
+  unsigned long long sgv[MERGE_SCAN];
+  const int64_t nchunks = (nw + 255) / 256;
+#pragma unroll
+  for (int u = 0; u < MERGE_SCAN; ++u) {
+    const int64_t w = (blockIdx.x + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+    sgv[u] = w < nw ? sig[w] : 0ull;
+  }
+  const int vcur = loop->vcur;
+#ifdef BPE_MERGE_STAMPS
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+  const int st_mi = loop->n_merges;
+#define KB_MI st_mi
+#else
+#define KB_MI 0
+#endif
+  if (threadIdx.x < 64) {
+    // ---- the batch.  Lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
+    // rows each), then KM wave-max rounds hand the global order out.
+    const int nwg = batch_nwg(Vt);
+    unsigned long long K[KM], S[KM];
+#pragma unroll
+    for (int i = 0; i < KM; ++i) K[i] = S[i] = 0ull;
+    unsigned long long LK[BATCH_WG_LANE][KM], LS[BATCH_WG_LANE][KM];
+#pragma unroll
+    for (int t = 0; t < BATCH_WG_LANE; ++t) {
+      const int g = t * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < KM; ++i) {
+        LK[t][i] = g < nwg ? bw.wgkey[(size_t)i * nwg + g] : 0ull;
+        LS[t][i] = g < nwg ? bw.wgsec[(size_t)i * nwg + g] : 0ull;
+      }
+    }
+    DSTAMP(KB_MI, 0);
+#pragma unroll
+    for (int t = 0; t < BATCH_WG_LANE; ++t)
+      if (t * 64 < nwg) top_merge<KM>(K, S, LK[t], LS[t]);
+    DSTAMP(KB_MI, 1);
+    // KM rounds: the wave max of the lanes' list heads (DPP, no LDS), its owner pops it; lane r
+    // keeps the r-th (best, second)
+    unsigned long long ckey = 0, csec = 0;
+#pragma unroll
+    for (int r = 0; r < KM; ++r) {
+      const unsigned long long m = wave_max_u64(K[0]);
+      const bool mine = m != 0ull && K[0] == m;   // keys are distinct: one owner
+      const unsigned long long ball = __ballot(mine);
+      const int src = ball ? (int)__builtin_ctzll(ball) : 0;
+      const unsigned long long sec = readlane_u64(S[0], src);
+      if (lane == r) { ckey = m; csec = ball ? sec : 0ull; }
+      if (mine) {
+#pragma unroll
+        for (int i = 0; i < KM - 1; ++i) { K[i] = K[i + 1]; S[i] = S[i + 1]; }
+        K[KM - 1] = S[KM - 1] = 0ull;
+      }
+    }
+    DSTAMP(KB_MI, 2);
+    // lanes j < KM: candidate j's string and its id if it exists (the probes run in parallel)
+    int cand_a = 0, cand_b = 0, exist = -1;
+    uint32_t clen = 0;
+    unsigned long long ch = 0;
+    if (lane < KM && ckey) {
+      const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(ckey & 0xFFFFFFFFull);
+      cand_a = (int)(idx / (uint32_t)Vt);
+      cand_b = (int)(idx % (uint32_t)Vt);
+      ch = lh.th[cand_a] * lh.tp[cand_b] + lh.th[cand_b];
+      clen = tlen[cand_a] + tlen[cand_b];
+      const uint64_t mask = (1ull << loop->log2cap) - 1;
+      uint64_t sl = loop_slot(ch, clen, loop->log2cap);
+      while (lh.klen[sl] != LOOP_EMPTY) {
+        if (lh.key[sl] == ch && lh.klen[sl] == clen) { exist = lh.kid[sl]; break; }
+        sl = (sl + 1) & mask;
+      }
+    }
+    DSTAMP(KB_MI, 3);
+    int A[KM], B[KM], E[KM];
+    uint32_t Ln[KM];
+    unsigned long long H[KM], Kc[KM], Sc[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      A[j] = __builtin_amdgcn_readlane(cand_a, j); B[j] = __builtin_amdgcn_readlane(cand_b, j);
+      E[j] = __builtin_amdgcn_readlane(exist, j); Ln[j] = (uint32_t)__builtin_amdgcn_readlane((int)clen, j);
+      H[j] = readlane_u64(ch, j); Kc[j] = readlane_u64(ckey, j); Sc[j] = readlane_u64(csec, j);
+    }
+    // HF's stopping rules per merge and the batch rules (see above); lane 0 decides
+    if (lane == 0) {
+      int n = 0;
+      unsigned long long sec = 0;
+      const bool live = loop->active != 0;
+      const int target = loop->target, nm = loop->n_merges, maxm = loop->max_merges;
+      const unsigned long long minf = (unsigned long long)loop->min_freq;
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        if (!live || n < j) break;
+        const unsigned long long count = Kc[j] >> 32;
+        if (count < 1 || count < minf || vcur + n >= target || nm + n >= maxm) break;
+        if (j > 0) {
+          bool stop = sec >= Kc[j] || E[j] >= 0;   // a taken row's second-best comes first / id re-use
+#pragma unroll
+          for (int i = 0; i < j; ++i)
+            stop |= A[j] == A[i] || A[j] == B[i] || B[j] == A[i] || B[j] == B[i] || (H[j] == H[i] && Ln[j] == Ln[i]);
+          if (stop) break;
+        }
+        const bool reused = j == 0 && E[0] >= 0;
+        s_a[n] = A[j];
+        s_b[n] = B[j];
+        s_nid[n] = reused ? E[0] : vcur + n;
+        s_len[n] = Ln[j];
+        s_need[n] = sig_bit((uint32_t)A[j]) | sig_bit((uint32_t)B[j]);
+        if (blockIdx.x == 0) {   // the record k_apply_batch applies and commits
+          loop->ba[n] = A[j]; loop->bb[n] = B[j]; loop->bnid[n] = s_nid[n];
+          loop->breused[n] = reused ? 1 : 0; loop->blen[n] = Ln[j]; loop->bh[n] = H[j];
+        }
+        sec = umax64(sec, Sc[j]);
+        ++n;
+        if (A[j] == B[j] || reused) break;   // a self-pair or a re-used id ends the batch
+      }
+      s_n = n;
+      DSTAMP(KB_MI, 4);
+      // merges 0 .. kd-1 sum their changes in LDS: the frequent ones whose vectors fit
+      const int stride = vcur + n;
+      int kd = 0;
+      while (kd < n && (kd + 1) * 16 * stride <= BATCH_LDS && (long long)(Kc[kd] >> 32) >= lds_min) ++kd;
+      s_kd = kd;
+      if (blockIdx.x == 0) {
+        loop->bn = n;
+        loop->bvcur = vcur + n - ((n > 0 && E[0] >= 0) ? 1 : 0);
+        if (n == 0) loop->active = 0;
+      }
+    }
+  }
+  if (threadIdx.x == 0) { cn = 0; touched = 0; }
+  __syncthreads();
+  const int n = s_n;
+  if (n == 0) return;
+#ifdef BPE_MERGE_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 1024 && st_mi >= BPE_MERGE_STAMPS && st_mi < BPE_MERGE_STAMPS + 64) {
+    g_bpe_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][0] = t_entry;
+    g_bpe_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][5] = (unsigned long long)n;
+  }
+#endif
+  MSTAMP(KB_MI, 1);
+  const int kd = s_kd;
+  const int stride = vcur + n;
+  const int nl = kd * 4 * stride;   // LDS entries in use
+  if (kd > 0) {
+    for (int i = threadIdx.x; i < nl; i += 256) dl[i] = 0;
+    __syncthreads();
+  }
+  const int vbase = s_nid[0] == vcur ? vcur : vcur + 1;   // first new id (merge 0 may re-use one)
+  const int nnew = n - (vbase == vcur ? 0 : 1);
+  const uint32_t* nlen = vbase == vcur ? s_len : s_len + 1;
+  unsigned long long need[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) need[j] = j < n ? s_need[j] : ~0ull;
+  bool any = false;
+  // the batch's merges in order on one word (one inlined merge_symbols: the op comes from LDS)
+  auto visit = [&](int64_t w, unsigned long long sgw) {
+    uint32_t L = wlen[w];
+    uint16_t* s = sym + wstart[w];
+    unsigned long long g = 0;
+    uint32_t napp = 0;
+    bool changed = false;
+#pragma unroll 1
+    for (int j = 0; j < n; ++j) {
+      const unsigned long long nd = s_need[j];
+      if (L < 2 || (sgw & nd) != nd) continue;
+      const BatchOp op{s_a[j], s_b[j], s_nid[j], max_len, j, Vt, vbase, nnew, stride, s_len[j], tlen, nlen,
+                       j < kd ? dl + j * 4 * stride : nullptr, bw.deltas};
+      unsigned long long gj = 0;
+      const uint32_t o = merge_symbols(s, L, wcount, w, op, gj, napp);
+      if (o) { L = o; g = gj; changed = true; }
+    }
+    if (!changed) return;
+    any = true;
+    wlen[w] = L;
+    sig[w] = g;
+  };
+  // two-phase scan (k_merge's): a word is a candidate if its signature holds some merge's pair.
+  // Rounds of MERGE_SCAN signatures per thread append to the LDS list; it is processed once at
+  // the end, or earlier when another round could overflow it (merge_symbols is inlined once).
+  for (int64_t c0 = blockIdx.x;; c0 += (int64_t)MERGE_SCAN * gridDim.x) {
+    const bool more = c0 < nchunks;   // uniform
+    if (more) {
+      if (c0 != blockIdx.x) {
+#pragma unroll
+        for (int u = 0; u < MERGE_SCAN; ++u) {
+          const int64_t w = (c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+          sgv[u] = w < nw ? sig[w] : 0ull;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < MERGE_SCAN; ++u) {
+        bool hit = false;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) hit |= (sgv[u] & need[j]) == need[j];
+        if (hit) clist[atomicAdd(&cn, 1)] = (uint32_t)((c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x);
+      }
+    }
+    __syncthreads();
+    const int nc = cn;
+    if (!more || nc > BATCH_CLIST - 256 * MERGE_SCAN) {
+      MSTAMP(KB_MI, 2);
+      for (int k = threadIdx.x; k < nc; k += 256) {
+        const int64_t w = clist[k];
+        visit(w, sig[w]);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) cn = 0;
+      __syncthreads();
+    }
+    if (!more) break;
+  }
+  MSTAMP(KB_MI, 3);
+  if (kd == 0) { MSTAMP(KB_MI, 4); return; }
+  if (any) touched = 1;
+  __syncthreads();
+  if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> global (j * 4 + kind) * Vt + x
+    for (int i = threadIdx.x; i < nl; i += 256) {
+      const int32_t v = dl[i];
+      if (v) {
+        const int jk = i / stride;
+        atomicAdd(&bw.deltas[(size_t)jk * Vt + (i - jk * stride)], v);
+      }
+    }
+  MSTAMP(KB_MI, 4);
+#undef KB_MI
+}
+
+// Apply a batch (k_apply_argmax's steps for each merge: rows own their entries), retire the
+// merged pairs after all adds, commit the batch (hash table, log, vcur) from workgroup 0, then
+// every changed row's best and second-best and this workgroup's BK best rows for the next
+// decision.  init: no batch, every row < vcur rescanned.
+__global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __restrict__ table, int Vt, ArgWs aw,
+                                                                 BatchWs bw, uint32_t* __restrict__ tlen,
+                                                                 LoopState* __restrict__ loop, LoopHash lh, int nrows,
+                                                                 int init) {
+  __shared__ unsigned long long wbest[APPLY_ROWS], wsec[APPLY_ROWS];
+  __shared__ int changed_w[APPLY_ROWS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = init ? 0 : loop->bn;
+  if (!init && (n == 0 || !loop->active)) return;
+  int A[BK], B[BK], N[BK];
+#pragma unroll
+  for (int j = 0; j < BK; ++j) {
+    A[j] = j < n ? loop->ba[j] : -1;
+    B[j] = j < n ? loop->bb[j] : -1;
+    N[j] = j < n ? loop->bnid[j] : -1;
+  }
+  const int vcur = init ? loop->vcur : loop->bvcur;
+  const int x0 = blockIdx.x * APPLY_ROWS;
+  const int x = x0 + wave;
+  int changed = 0;
+  if (lane == 0 && x < nrows) {   // (1) each wave's single entries (x, a_j) and (x, new_j)
+    uint32_t* row = table + (size_t)x * Vt;
+    for (int j = 0; j < n; ++j) {
+      int32_t* d = bw.deltas + (size_t)j * 4 * Vt;
+      int32_t v;
+      if ((v = d[x])) { row[A[j]] += (uint32_t)v; d[x] = 0; changed = 1; }
+      if ((v = d[Vt + x])) { row[N[j]] += (uint32_t)v; d[Vt + x] = 0; changed = 1; }
+    }
+  }
+  if (lane == 0) changed_w[wave] = changed;
+  __syncthreads();
+  for (int j = 0; j < n; ++j)     // (2) rows b_j and new_j entirely, by the workgroup owning them
+    for (int r = 0; r < 2; ++r) {
+      const int xr = r == 0 ? B[j] : N[j];
+      if (xr < x0 || xr >= x0 + APPLY_ROWS || xr >= nrows) continue;
+      int32_t* d = bw.deltas + ((size_t)j * 4 + 2 + r) * Vt;
+      uint32_t* row = table + (size_t)xr * Vt;
+      int anyr = 0;
+      for (int y = threadIdx.x; y < Vt; y += 64 * APPLY_ROWS) {
+        const int32_t v = d[y];
+        if (v) { row[y] += (uint32_t)v; d[y] = 0; anyr = 1; }
+      }
+      if (anyr) changed_w[xr - x0] = 1;
+    }
+  __syncthreads();
+  if (lane == 0 && x < nrows)     // (3) the merged pairs, after every add
+    for (int j = 0; j < n; ++j)
+      if (x == A[j]) {
+        table[(size_t)x * Vt + B[j]] = 0u;   // never re-picked
+        tlen[N[j]] = tlen[A[j]] + tlen[B[j]];
+        changed_w[wave] = 1;
+      }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0) {   // commit the batch (no other workgroup reads it)
+    const uint64_t mask = (1ull << loop->log2cap) - 1;
+    int nm = loop->n_merges;
+    for (int j = 0; j < n; ++j) {
+      const int reused = loop->breused[j];
+      if (!reused) {
+        const unsigned long long h = loop->bh[j];
+        const uint32_t len = loop->blen[j];
+        uint64_t sl = loop_slot(h, len, loop->log2cap);
+        while (lh.klen[sl] != LOOP_EMPTY) sl = (sl + 1) & mask;
+        lh.key[sl] = h;
+        lh.klen[sl] = len;
+        lh.kid[sl] = N[j];
+        lh.th[N[j]] = h;
+        lh.tp[N[j]] = lh.tp[A[j]] * lh.tp[B[j]];
+      }
+      int32_t* lg = lh.log + 4 * (int64_t)nm;
+      lg[0] = A[j]; lg[1] = B[j]; lg[2] = N[j]; lg[3] = reused;
+      ++nm;
+      loop->a = A[j]; loop->b = B[j]; loop->nid = N[j]; loop->reused = reused;
+    }
+    loop->n_merges = nm;
+    loop->vcur = vcur;
+  }
+  __syncthreads();
+  changed = init ? 1 : changed_w[wave];
+  unsigned long long best = 0, second = 0;
+  if (x < nrows && x < vcur) {
+    if (aw.clean[x] && !changed) {
+      best = aw.rowbest[x];
+      second = bw.rowsecond[x];
+    } else {
+      const uint32_t* row = table + (size_t)x * Vt;
+      for (int base = 0; base < vcur; base += 64 * 32) {
+        uint32_t c[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int y0 = base + (k * 64 + lane) * 4;
+          if (((Vt & 3) == 0) && y0 + 4 <= vcur) {
+            const uint4 u = *reinterpret_cast<const uint4*>(row + y0);
+            c[4 * k] = u.x; c[4 * k + 1] = u.y; c[4 * k + 2] = u.z; c[4 * k + 3] = u.w;
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[4 * k + q] = y0 + q < vcur ? row[y0 + q] : 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t cv = c[4 * k + q];
+            const int y = base + (k * 64 + lane) * 4 + q;
+            const unsigned long long key =
+                cv ? ((unsigned long long)cv << 32) | (unsigned long long)(~((uint32_t)x * (uint32_t)Vt + (uint32_t)y))
+                   : 0ull;
+            const unsigned long long lo = umin64(key, best);
+            best = umax64(key, best);
+            second = umax64(second, lo);
+          }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {   // the wave's top two
+        const unsigned long long b2 = __shfl_xor(best, o), s2 = __shfl_xor(second, o);
+        second = umax64(umax64(second, s2), umin64(best, b2));
+        best = umax64(best, b2);
+      }
+      if (lane == 0) {
+        aw.rowbest[x] = best;
+        bw.rowsecond[x] = second;
+        aw.clean[x] = 1u;
+      }
+    }
+  }
+  if (lane == 0) { wbest[wave] = best; wsec[wave] = second; }
+  __syncthreads();
+  if (threadIdx.x < BK) {   // this workgroup's BK best rows: thread k takes the k-th
+    const int k = threadIdx.x;
+    unsigned long long kb = 0, ks = 0;
+    for (int w = 0; w < APPLY_ROWS; ++w) {
+      int rank = 0;   // rows above w (keys are distinct unless 0)
+      for (int v = 0; v < APPLY_ROWS; ++v) rank += wbest[v] > wbest[w];
+      if (rank == k && wbest[w]) { kb = wbest[w]; ks = wsec[w]; }
+    }
+    bw.wgkey[(size_t)k * batch_nwg(Vt) + blockIdx.x] = kb;   // the grid may cover fewer rows than Vt
+    bw.wgsec[(size_t)k * batch_nwg(Vt) + blockIdx.x] = ks;
   }
 }
 
@@ -2277,6 +2800,9 @@ static __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, i
 extern "C" int beast_debug_merge_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_stamps), sizeof(g_bpe_stamps)) == hipSuccess ? 0 : -2;
 }
+extern "C" int beast_debug_decide_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_dstamps), sizeof(g_bpe_dstamps)) == hipSuccess ? 0 : -2;
+}
 #endif
 #ifdef BPE_MERGE_STATS
 extern "C" int beast_debug_merge_stats(unsigned long long* host4) {
@@ -2344,6 +2870,75 @@ extern "C" int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_step
     BEAST_LAUNCHED("k_apply_argmax");
   }
   return BEAST_OK;
+}
+
+extern "C" size_t beast_bpe_batch_workspace_bytes(int Vt) { return batch_ws_bytes(Vt > 0 ? Vt : 1); }
+
+template <int KM>
+static int batch_grid(int64_t nw) {
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_merge_batch<KM>, 256, 0) != hipSuccess || per <= 0)
+      per = 2;
+    resident = cus * per;
+  }
+  return grid_for(nw, MERGE_SCAN * 256, resident);
+}
+
+template <int KM>
+static int loop_batch(LoopState* st, const LoopHash& lh, BatchWs bw, ArgWs aw, int Vt, int n_steps, uint16_t* sym,
+                      const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
+                      int max_token_length, uint64_t* sig, uint32_t* table, int rows, hipStream_t s) {
+  const int grid = batch_grid<KM>(n_words > 0 ? n_words : 1);
+  const int agrid = (rows + APPLY_ROWS - 1) / APPLY_ROWS;
+  for (int i = 0; i < n_steps; ++i) {
+    hipLaunchKernelGGL(k_merge_batch<KM>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, tlen,
+                       max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, bw,
+                       (long long)beast::g_merge_lds_min);
+    BEAST_LAUNCHED("k_merge_batch");
+    hipLaunchKernelGGL(k_apply_batch, dim3(agrid), dim3(64 * APPLY_ROWS), 0, s, table, Vt, aw, bw, tlen, st, lh, rows, 0);
+    BEAST_LAUNCHED("k_apply_batch");
+  }
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_batch, uint16_t* sym,
+                                    const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
+                                    uint32_t* tlen, int max_token_length, uint64_t* sig, uint32_t* table,
+                                    uint64_t* argws, void* batch_ws, size_t batch_ws_bytes_, int vocab_size, int init,
+                                    void* stream) {
+  BEAST_REQUIRE(ws && sym && wstart && wlen && tlen && sig && table && argws && batch_ws,
+                "beast_bpe_loop_batch: null pointer");
+  BEAST_REQUIRE(Vt >= 1 && n_steps >= 0 && vocab_size >= 1, "beast_bpe_loop_batch: bad sizes");
+  BEAST_REQUIRE_CODE(Vt <= 4096, BEAST_E_UNSUPPORTED, "batched merge loop: Vt %d > 4096", Vt);
+  BEAST_REQUIRE(max_batch == 2 || max_batch == 4 || max_batch == 8, "beast_bpe_loop_batch: max_batch must be 2, 4 or 8");
+  BEAST_REQUIRE_CODE(batch_ws_bytes_ >= batch_ws_bytes(Vt), BEAST_E_WORKSPACE, "batch workspace %zu < %zu",
+                     batch_ws_bytes_, batch_ws_bytes(Vt));
+  hipStream_t s = beast::as_stream(stream);
+  const LoopLayout L = loop_layout(Vt, max_merges);
+  LoopState* st = reinterpret_cast<LoopState*>(static_cast<unsigned char*>(ws) + L.st);
+  const LoopHash lh = loop_hash_view(ws, Vt, max_merges);
+  const ArgWs aw = argws_view(argws, Vt);
+  const BatchWs bw = batch_view(batch_ws, Vt);
+  const int rows = std::min(Vt, std::max(vocab_size, 1));
+  if (init) {   // zero deltas, every row's best and second-best, the workgroups' best rows
+    BEAST_HIP(hipMemsetAsync(batch_ws, 0, batch_ws_bytes(Vt), s), "batch workspace memset");
+    hipLaunchKernelGGL(k_apply_batch, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s, table,
+                       Vt, aw, bw, tlen, st, lh, rows, 1);
+    BEAST_LAUNCHED("k_apply_batch(init)");
+  }
+  switch (max_batch) {
+    case 2: return loop_batch<2>(st, lh, bw, aw, Vt, n_steps, sym, wstart, wlen, wcount, n_words, tlen,
+                                 max_token_length, sig, table, rows, s);
+    case 4: return loop_batch<4>(st, lh, bw, aw, Vt, n_steps, sym, wstart, wlen, wcount, n_words, tlen,
+                                 max_token_length, sig, table, rows, s);
+    default: return loop_batch<8>(st, lh, bw, aw, Vt, n_steps, sym, wstart, wlen, wcount, n_words, tlen,
+                                  max_token_length, sig, table, rows, s);
+  }
 }
 
 extern "C" size_t beast_bpe_pair_index_bytes(int n_sym, int64_t n_symbols) {

@@ -263,6 +263,17 @@ int beast_bpe_loop_persistent(void* ws, int Vt, int max_merges, int n_steps, uin
                               int max_token_length, int32_t* deltas, uint64_t* sig, uint32_t* table,
                               uint64_t* argws, int vocab_size, void* bar_ws, size_t bar_bytes, void* stream);
 int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
+/* The same loop with several merges per (merge, apply) pair of launches, exactly HF's sequence:
+ * each pass takes the table's top pairs in HF order while they are symbol-disjoint, the last
+ * taken is not a self-pair, no string re-uses an id (only the first may) and no taken row's
+ * second-best pair ranks above the next (csrc/bpe.hip, "batched merges", has the proof);
+ * max_batch (2, 4 or 8) caps a pass; sig (beast_bpe_word_signatures) is required.  batch_ws: beast_bpe_batch_workspace_bytes(Vt); init = 1 on
+ * the first call after beast_bpe_loop_init (zeroes batch_ws and ranks every row).  Vt <= 4096. */
+size_t beast_bpe_batch_workspace_bytes(int Vt);
+int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_batch, uint16_t* sym,
+                         const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
+                         uint32_t* tlen, int max_token_length, uint64_t* sig, uint32_t* table, uint64_t* argws,
+                         void* batch_ws, size_t batch_ws_bytes, int vocab_size, int init, void* stream);
 /* Pair index for the device-driven loop (replaces the per-merge signature scan): a CSR of
  * the distinct words holding each pair of two setup symbols (ids < n_sym), built once from the
  * distinct words (n_symbols = their total symbol count bounds the entries), plus a token index

@@ -714,8 +714,8 @@ def test_conditions_match_reference(case, gpu_device):
         tok.reconstruct_traj(torch.from_numpy(rt[:5]).to(gpu_device))    # conditions fitted on 32 rows
 
 
-@pytest.mark.parametrize("loop", ["steps", "persistent"])
-@pytest.mark.parametrize("case", ["traj_k2/2048", "skew/700", "wide3000/2048", "repeat700/300"])
+@pytest.mark.parametrize("loop", ["steps", "persistent", "batch"])
+@pytest.mark.parametrize("case", ["traj_k2/2048", "skew/700", "wide3000/2048", "repeat700/300", "runs/2048"])
 def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     """The device-driven merge loop (merges decided on the GPU, ids by string hash, replayed and
     verified on the host) gives HF's vocab and merges; so does its collision fallback (forced
@@ -738,3 +738,23 @@ def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     res2 = train_bpe(flat, off, int(vs), ops=dg)
     assert res2.vocab == ref[case]["vocab"]
     assert [list(m) for m in res2.merges] == ref[case]["merges"]
+
+
+@pytest.mark.parametrize("loop", ["batch2", "batch4", "batch"])
+@pytest.mark.parametrize("case", ["skew/300", "skew/2048", "traj_k2/700", "traj_k3/2048", "rand256/2048",
+                                  "repeat700/700", "repeat700/2048", "runs/300", "runs/700"])
+def test_bpe_batched_loop_matches_hf(case, loop, bpe_golden, gpu_device):
+    """Several merges per pass (csrc/bpe.hip k_merge_batch: the top pairs in HF order while they
+    are symbol-disjoint, no id re-use after the first, no taken row's second-best above the next)
+    give exactly HF's sequential merges -- with batches of 2, 4 and 8, on corpora with id re-use
+    (repeat700), self-pair runs (runs), the min_frequency stop (repeat700/2048) and wide alphabets."""
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+    ref, corpora = bpe_golden
+    cname, vs = case.split("/")
+    flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
+    ops = GpuBpeOps(gpu_device)
+    ops._loop_kind = loop
+    res = train_bpe(flat, off, int(vs), ops=ops)
+    assert res.stats.get("device_loop") is True and res.stats.get("loop") == loop
+    assert [list(m) for m in res.merges] == ref[case]["merges"]
+    assert res.vocab == ref[case]["vocab"]

@@ -43,6 +43,9 @@ def run(mode):
     dev = torch.device("cuda", 0)
     rows = bench.k5_corpus(dev, 500000, 0, 1, bench.k5_golden())
     flat, off = fixed_rows_to_device(rows)
+    if mode.startswith("batch"):     # k_merge_batch: one record per pass, [5] = merges in it
+        os.environ["BEAST_BPE_LOOP"] = mode
+        mode = "signature_scan"
     res = train_bpe(flat, off, 2048, merge_mode=mode)
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * (64 * 1024 * 6))()
@@ -51,6 +54,12 @@ def run(mode):
     assert fn(buf) == 0
     st = np.frombuffer(buf, dtype=np.uint64).reshape(64, 1024, 6).astype(np.int64)
     out = []
+    dst = None
+    if os.environ.get("BEAST_BPE_LOOP", "").startswith("batch"):
+        dbuf = (C.c_ulonglong * (64 * 8))()
+        lib.beast_debug_decide_stamps.argtypes = [C.c_void_p]
+        assert lib.beast_debug_decide_stamps(dbuf) == 0
+        dst = np.frombuffer(dbuf, dtype=np.uint64).reshape(64, 8).astype(np.int64)
     for m in range(64):
         s = st[m]
         ran = s[:, 0] > 0
@@ -63,6 +72,11 @@ def run(mode):
         rec = {"wg": int(ran.sum()), "span_us": float((s[:, 4].max() - t0) / 100.0),
                "dispatch_spread_us": float((s[:, 0].max() - t0) / 100.0),
                "decide_us": [float(np.median(ph(0, 1))), float(ph(0, 1).max())]}
+        if os.environ.get("BEAST_BPE_LOOP", "").startswith("batch"):
+            rec["first_merge"] = m
+            rec["batch"] = int(s[0, 5])
+            e = st[m][0, 0]   # workgroup 0: entry, loads, list merges, shuffle merges, probes, rules
+            rec["decide_phases_us"] = [round(float(v), 2) for v in np.diff(np.r_[e, dst[m][:5]]) / 100.0]
         if done.any():
             d = s[done]
             rec.update({"wg_full": int(done.sum()),
@@ -71,7 +85,7 @@ def run(mode):
                         "flush_us": [float(np.median((d[:, 4] - d[:, 3]) / 100.0)), float(((d[:, 4] - d[:, 3]) / 100.0).max())],
                         "last_exit_us": float((d[:, 4].max() - t0) / 100.0)})
         out.append(rec)
-    print(json.dumps({"mode": mode, "merges": len(res.merges), "loop_s": res.stats["merge_loop_s"], "stamps": out}))
+    print(json.dumps({"mode": os.environ.get("BEAST_BPE_LOOP", mode), "merges": len(res.merges), "loop_s": res.stats["merge_loop_s"], "stamps": out}))
 
 
 def run_persistent():
