@@ -481,6 +481,7 @@ struct LoopState {
   unsigned long long r_count, r_h;
   // the batch k_merge_batch decided for the following k_apply_batch (written by its workgroup 0)
   int32_t bn, bvcur;
+  int32_t maxtlen;       // longest token (bytes): k_apply_batch keeps it
   int32_t ba[8], bb[8], bnid[8], breused[8];
   uint32_t blen[8];
   unsigned long long bh[8];
@@ -600,44 +601,9 @@ struct MergeOp {
 };
 
 template <class Op>
-__device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint32_t L, const uint32_t* __restrict__ wcount,
-                                                  int64_t w, const Op& m, unsigned long long& g, uint32_t& napp) {
+__device__ __forceinline__ uint32_t merge_global(uint16_t* __restrict__ s, uint32_t L, const uint32_t* __restrict__ wcount,
+                                                 int64_t w, const Op& m, unsigned long long& g, uint32_t& napp) {
   const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
-  if (L <= (uint32_t)MERGE_REG) {
-    uint32_t v[MERGE_REG + 2];
-#pragma unroll
-    for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? (uint32_t)s[i] : 0xFFFFFFFFu;   // sentinel
-    v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
-    bool hit = false;
-#pragma unroll
-    for (int i = 0; i < MERGE_REG - 1; ++i) hit |= (v[i] == a) & (v[i + 1] == b);
-    if (!hit) return 0;
-    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
-    uint32_t o = 0, last = 0, skip = 0;
-    unsigned long long sg = 0;
-#pragma unroll
-    for (int i = 0; i < MERGE_REG; ++i) {
-      if ((uint32_t)i < L) {
-        uint32_t y = v[i];
-        if (skip) {
-          skip = 0;
-          continue;
-        }
-        if (v[i] == a && v[i + 1] == b) {   // v[i + 1] is the sentinel past the end
-          if (o > 0) m.left(last, cnt);
-          if (v[i + 2] != 0xFFFFFFFFu) m.right(v[i + 2], cnt);
-          y = nid;
-          skip = 1;
-          ++napp;
-        }
-        s[o++] = (uint16_t)y;
-        last = y;
-        sg |= sig_bit(y);
-      }
-    }
-    g = sg;
-    return o;
-  }
   bool hit = false;
   uint32_t prev = s[0];
 #pragma unroll 8
@@ -668,6 +634,62 @@ __device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint
   return o;
 }
 
+// a word of L <= MERGE_REG symbols in registers (sentinels past the end)
+__device__ __forceinline__ void load_word(const uint16_t* __restrict__ s, uint32_t L, uint32_t (&v)[MERGE_REG + 2]) {
+#pragma unroll
+  for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? (uint32_t)s[i] : 0xFFFFFFFFu;
+  v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
+}
+__device__ __forceinline__ bool word_has_pair(const uint32_t (&v)[MERGE_REG + 2], uint32_t a, uint32_t b) {
+  bool hit = false;
+#pragma unroll
+  for (int i = 0; i < MERGE_REG - 1; ++i) hit |= (v[i] == a) & (v[i + 1] == b);
+  return hit;
+}
+// the merge of a word held in v (which holds the pair) written back to s
+template <class Op>
+__device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2], uint32_t L, uint16_t* __restrict__ s,
+                                               int32_t cnt, const Op& m, unsigned long long& g, uint32_t& napp) {
+  const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
+  uint32_t o = 0, last = 0, skip = 0;
+  unsigned long long sg = 0;
+#pragma unroll
+  for (int i = 0; i < MERGE_REG; ++i) {
+    if ((uint32_t)i < L) {
+      uint32_t y = v[i];
+      if (skip) {
+        skip = 0;
+        continue;
+      }
+      if (v[i] == a && v[i + 1] == b) {   // v[i + 1] is the sentinel past the end
+        if (o > 0) m.left(last, cnt);
+        if (v[i + 2] != 0xFFFFFFFFu) m.right(v[i + 2], cnt);
+        y = nid;
+        skip = 1;
+        ++napp;
+      }
+      s[o++] = (uint16_t)y;
+      last = y;
+      sg |= sig_bit(y);
+    }
+  }
+  g = sg;
+  return o;
+}
+
+template <class Op>
+__device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint32_t L, const uint32_t* __restrict__ wcount,
+                                                  int64_t w, const Op& m, unsigned long long& g, uint32_t& napp) {
+  const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
+  if (L <= (uint32_t)MERGE_REG) {
+    uint32_t v[MERGE_REG + 2];
+    load_word(s, L, v);
+    if (!word_has_pair(v, a, b)) return 0;
+    return merge_regs(v, L, s, wcount ? (int32_t)wcount[w] : 1, m, g, napp);
+  }
+  return merge_global(s, L, wcount, w, m, g, napp);
+}
+
 // Inverted index symbol -> distinct words that may contain it (HF's where_to_update, on
 // the GPU).  Built once from the distinct words; the merge creating token `new` appends
 // the words it rewrote to a pool and k_apply_argmax turns that range into new's list.
@@ -691,7 +713,8 @@ constexpr int BATCH_CLIST = 2 * 256 * MERGE_SCAN;   // k_merge_batch's list: two
 // for 64 merges x the first 1024 workgroups.
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][6];
-__device__ unsigned long long g_bpe_dstamps[64][8];   // k_merge_batch's decision phases (workgroup 0)
+__device__ unsigned long long g_bpe_dstamps[64][8];
+__device__ unsigned long long g_apply_stamps[64][256][6];   // k_apply_batch phases (first 256 workgroups)   // k_merge_batch's decision phases (workgroup 0)
 #define DSTAMP(mi, k)                                                                            \
   do {                                                                                           \
     if (blockIdx.x == 0 && lane == 0 && (mi) >= BPE_MERGE_STAMPS && (mi) < BPE_MERGE_STAMPS + 64)      \
@@ -1499,11 +1522,10 @@ struct BatchWs {
   unsigned long long* rowsecond;      // [Vt]
   unsigned long long* wgkey;          // [BK][nwg] each apply workgroup's BK best rows, best first (k-major:
   unsigned long long* wgsec;          // [BK][nwg]  the deciding wave reads them coalesced) and their second-best
-  int32_t* deltas;                    // [BK][4][Vt]
 };
 __host__ __device__ inline int batch_nwg(int Vt) { return (Vt + APPLY_ROWS_N - 1) / APPLY_ROWS_N; }
 __host__ __device__ inline size_t batch_ws_bytes(int Vt) {
-  return ((size_t)Vt * 8 + (size_t)batch_nwg(Vt) * BK * 2 * 8 + (size_t)BK * 4 * Vt * 4 + 255) & ~size_t(255);
+  return ((size_t)Vt * 8 + (size_t)batch_nwg(Vt) * BK * 2 * 8 + 255) & ~size_t(255);
 }
 __host__ __device__ inline BatchWs batch_view(void* ws, int Vt) {
   BatchWs v;
@@ -1512,37 +1534,47 @@ __host__ __device__ inline BatchWs batch_view(void* ws, int Vt) {
   v.rowsecond = reinterpret_cast<unsigned long long*>(p);
   v.wgkey = v.rowsecond + Vt;
   v.wgsec = v.wgkey + nt;
-  v.deltas = reinterpret_cast<int32_t*>(v.wgsec + nt);
   return v;
 }
 
-// Pair-count changes of batch merge j: kind 0 (x, a_j) -1, 1 (x, new_j) +1, 2 (b_j, y) -1, 3
-// (new_j, y) +1 -- k_merge's four vectors per merge.  The first merges of the batch whose
-// vectors fit BATCH_LDS (symbols < stride = vcur + n, so several while the vocabulary is small)
-// sum them in LDS when their count is large (k_merge's rule), the rest add to the global
-// vectors.  A neighbour may be a token this batch creates: its length is in nlen (tlen is
-// written by the apply).
+// Pair-count changes of batch merge j go straight into the pair table (no delta vectors, so the
+// apply has nothing to add): kind 0 (x, a_j) -1, 1 (x, new_j) +1, 2 (b_j, y) -1, 3 (new_j, y) +1.
+// A row x touched through kinds 0 / 1 is marked for re-ranking (clean[x] = 0); rows b_j, new_j
+// and a_j always are.  The first merges of the batch whose four vectors fit BATCH_LDS (symbols <
+// stride = vcur + n, so several while the vocabulary is small) sum them in LDS first when their
+// count is large (k_merge's rule).  A neighbour may be a token this batch creates: its length
+// is in nlen (tlen is written by the apply).
 struct BatchOp {
-  int a, b, nid, max_len, j, Vt, vbase, nnew, stride;
+  int a, b, nid, max_len, Vt, vbase, nnew, stride;
+  bool short_all;       // every token + the new one < max_len: no length lookups
   uint32_t newlen;
   const uint32_t* __restrict__ tlen;
   const uint32_t* nlen;
   int32_t* dl;          // LDS vectors of this merge, or null
-  int32_t* gdel;
+  uint32_t* table;
+  uint32_t* clean;
   __device__ __forceinline__ uint32_t len_of(uint32_t x) const {
     return (int)x >= vbase && (int)x < vbase + nnew ? nlen[x - vbase] : tlen[x];
   }
+  __device__ __forceinline__ void table_add(int kind, uint32_t x, int32_t v) const {
+    if (kind < 2) {
+      atomicAdd(&table[(size_t)x * Vt + (kind == 0 ? a : nid)], (uint32_t)v);
+      clean[x] = 0u;
+    } else {
+      atomicAdd(&table[(size_t)(kind == 2 ? b : nid) * Vt + x], (uint32_t)v);
+    }
+  }
   __device__ __forceinline__ void add(int kind, uint32_t x, int32_t v) const {
     if (dl != nullptr) atomicAdd(&dl[kind * stride + x], v);
-    else atomicAdd(&gdel[((size_t)j * 4 + kind) * Vt + x], v);
+    else table_add(kind, x, v);
   }
   __device__ __forceinline__ void left(uint32_t p, int32_t cnt) const {
     add(0, p, -cnt);
-    if ((int)(len_of(p) + newlen) < max_len) add(1, p, cnt);
+    if (short_all || (int)(len_of(p) + newlen) < max_len) add(1, p, cnt);
   }
   __device__ __forceinline__ void right(uint32_t nx, int32_t cnt) const {
     add(2, nx, -cnt);
-    if ((int)(len_of(nx) + newlen) < max_len) add(3, nx, cnt);
+    if (short_all || (int)(len_of(nx) + newlen) < max_len) add(3, nx, cnt);
   }
 };
 
@@ -1599,7 +1631,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
                                                      int64_t nw, const uint32_t* __restrict__ tlen, int max_len,
                                                      int Vt, unsigned long long* __restrict__ sig,
                                                      LoopState* __restrict__ loop, LoopHash lh, BatchWs bw,
-                                                     long long lds_min) {
+                                                     uint32_t* __restrict__ table, ArgWs aw, long long lds_min) {
   __shared__ __attribute__((aligned(16))) int32_t dl[BATCH_LDS / 4];
   __shared__ uint32_t clist[BATCH_CLIST];
   __shared__ int cn, touched, s_n, s_kd;
@@ -1616,6 +1648,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     sgv[u] = w < nw ? sig[w] : 0ull;
   }
   const int vcur = loop->vcur;
+  const int maxtlen = loop->maxtlen;
 #ifdef BPE_MERGE_STAMPS
   const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
   const int st_mi = loop->n_merges;
@@ -1755,6 +1788,8 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     for (int i = threadIdx.x; i < nl; i += 256) dl[i] = 0;
     __syncthreads();
   }
+  int mt = maxtlen;   // longest token a word can hold now (this batch's new ones included)
+  for (int j = 0; j < n; ++j) mt = max(mt, (int)s_len[j]);
   const int vbase = s_nid[0] == vcur ? vcur : vcur + 1;   // first new id (merge 0 may re-use one)
   const int nnew = n - (vbase == vcur ? 0 : 1);
   const uint32_t* nlen = vbase == vcur ? s_len : s_len + 1;
@@ -1763,23 +1798,63 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   for (int j = 0; j < KM; ++j) need[j] = j < n ? s_need[j] : ~0ull;
   bool any = false;
   // the batch's merges in order on one word (one inlined merge_symbols: the op comes from LDS)
+  // The batch's merges in order on one word.  Its symbols are read once: the merges it holds
+  // are known up front (batch pairs are symbol-disjoint, so one merge neither makes nor breaks
+  // another's pair), the first merges from the registers, a rare second re-reads the word.
   auto visit = [&](int64_t w, unsigned long long sgw) {
     uint32_t L = wlen[w];
     uint16_t* s = sym + wstart[w];
+    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
     unsigned long long g = 0;
     uint32_t napp = 0;
     bool changed = false;
+#ifdef BPE_MERGE_STATS
+    atomicAdd(&g_merge_stats[0], 1ull);
+    atomicAdd(&g_merge_stats[3], (unsigned long long)L);
+#endif
+    if (L < 2) return;
+    if (L <= (uint32_t)MERGE_REG) {
+      uint32_t v[MERGE_REG + 2];
+      load_word(s, L, v);
+      uint32_t hits = 0;
 #pragma unroll 1
-    for (int j = 0; j < n; ++j) {
-      const unsigned long long nd = s_need[j];
-      if (L < 2 || (sgw & nd) != nd) continue;
-      const BatchOp op{s_a[j], s_b[j], s_nid[j], max_len, j, Vt, vbase, nnew, stride, s_len[j], tlen, nlen,
-                       j < kd ? dl + j * 4 * stride : nullptr, bw.deltas};
-      unsigned long long gj = 0;
-      const uint32_t o = merge_symbols(s, L, wcount, w, op, gj, napp);
-      if (o) { L = o; g = gj; changed = true; }
+      for (int j = 0; j < n; ++j) {
+        const unsigned long long nd = s_need[j];
+        if ((sgw & nd) == nd && word_has_pair(v, (uint32_t)s_a[j], (uint32_t)s_b[j])) hits |= 1u << j;
+      }
+      if (!hits) return;
+      // one merge_regs pass per set bit: lanes of a wave holding different merges share it
+      // (the op is per lane), so a wave runs as many passes as its lanes' most merges (~1)
+      bool fresh = true;
+      while (hits) {
+        const int j = __builtin_ctz(hits);
+        hits &= hits - 1;
+        if (!fresh) load_word(s, L, v);
+        const BatchOp op{s_a[j], s_b[j], s_nid[j], max_len, Vt, vbase, nnew, stride,
+                         mt + (int)s_len[j] < max_len, s_len[j], tlen, nlen,
+                         j < kd ? dl + j * 4 * stride : nullptr, table, aw.clean};
+        L = merge_regs(v, L, s, cnt, op, g, napp);
+        fresh = false;
+      }
+      changed = true;
+    } else {
+#pragma unroll 1
+      for (int j = 0; j < n; ++j) {
+        const unsigned long long nd = s_need[j];
+        if (L < 2 || (sgw & nd) != nd) continue;
+        const BatchOp op{s_a[j], s_b[j], s_nid[j], max_len, Vt, vbase, nnew, stride,
+                         mt + (int)s_len[j] < max_len, s_len[j], tlen, nlen,
+                         j < kd ? dl + j * 4 * stride : nullptr, table, aw.clean};
+        unsigned long long gj = 0;
+        const uint32_t o = merge_global(s, L, wcount, w, op, gj, napp);
+        if (o) { L = o; g = gj; changed = true; }
+      }
     }
     if (!changed) return;
+#ifdef BPE_MERGE_STATS
+    atomicAdd(&g_merge_stats[1], 1ull);
+    atomicAdd(&g_merge_stats[2], (unsigned long long)napp);
+#endif
     any = true;
     wlen[w] = L;
     sig[w] = g;
@@ -1809,6 +1884,10 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     const int nc = cn;
     if (!more || nc > BATCH_CLIST - 256 * MERGE_SCAN) {
       MSTAMP(KB_MI, 2);
+#ifdef BPE_MERGE_STAMPS
+      if (threadIdx.x == 0 && blockIdx.x < 1024 && st_mi >= BPE_MERGE_STAMPS && st_mi < BPE_MERGE_STAMPS + 64)
+        g_bpe_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][5] += (unsigned long long)nc << 8;   // candidates
+#endif
       for (int k = threadIdx.x; k < nc; k += 256) {
         const int64_t w = clist[k];
         visit(w, sig[w]);
@@ -1823,31 +1902,45 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   if (kd == 0) { MSTAMP(KB_MI, 4); return; }
   if (any) touched = 1;
   __syncthreads();
-  if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> global (j * 4 + kind) * Vt + x
+  if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> the table
     for (int i = threadIdx.x; i < nl; i += 256) {
       const int32_t v = dl[i];
       if (v) {
         const int jk = i / stride;
-        atomicAdd(&bw.deltas[(size_t)jk * Vt + (i - jk * stride)], v);
+        const int j = jk >> 2;
+        const BatchOp op{s_a[j], s_b[j], s_nid[j], max_len, Vt, 0, 0, stride, true, 0u, tlen, nlen, nullptr, table,
+                         aw.clean};
+        op.table_add(jk & 3, (uint32_t)(i - jk * stride), v);
       }
     }
   MSTAMP(KB_MI, 4);
 #undef KB_MI
 }
 
-// Apply a batch (k_apply_argmax's steps for each merge: rows own their entries), retire the
-// merged pairs after all adds, commit the batch (hash table, log, vcur) from workgroup 0, then
-// every changed row's best and second-best and this workgroup's BK best rows for the next
-// decision.  init: no batch, every row < vcur rescanned.
+// After a batch: retire the merged pairs, commit the batch (hash table, log, vcur) from
+// workgroup 0, then every changed row's best and second-best and this workgroup's BK best rows
+// for the next decision.  init: no batch, every row < vcur ranked.
 __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __restrict__ table, int Vt, ArgWs aw,
                                                                  BatchWs bw, uint32_t* __restrict__ tlen,
                                                                  LoopState* __restrict__ loop, LoopHash lh, int nrows,
                                                                  int init) {
   __shared__ unsigned long long wbest[APPLY_ROWS], wsec[APPLY_ROWS];
-  __shared__ int changed_w[APPLY_ROWS];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = init ? 0 : loop->bn;
   if (!init && (n == 0 || !loop->active)) return;
+#ifdef BPE_MERGE_STAMPS
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+  const int st_mi = loop->n_merges;
+  const bool st_on = !init && threadIdx.x == 0 && blockIdx.x < 256 && st_mi >= BPE_MERGE_STAMPS &&
+                     st_mi < BPE_MERGE_STAMPS + 64;
+#define ASTAMP(k)                                                                                           \
+  do {                                                                                                      \
+    if (st_on) g_apply_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+  if (st_on) g_apply_stamps[st_mi - BPE_MERGE_STAMPS][blockIdx.x][0] = t_entry;
+#else
+#define ASTAMP(k) do { } while (0)
+#endif
   int A[BK], B[BK], N[BK];
 #pragma unroll
   for (int j = 0; j < BK; ++j) {
@@ -1858,38 +1951,20 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   const int vcur = init ? loop->vcur : loop->bvcur;
   const int x0 = blockIdx.x * APPLY_ROWS;
   const int x = x0 + wave;
+  if (init && lane == 0 && x < vcur) atomicMax(&loop->maxtlen, (int)tlen[x]);
+  // rows the merges changed: clean[x] == 0 (k_merge_batch's adds through (x, a_j), (x, new_j)),
+  // and a_j, b_j, new_j
   int changed = 0;
-  if (lane == 0 && x < nrows) {   // (1) each wave's single entries (x, a_j) and (x, new_j)
-    uint32_t* row = table + (size_t)x * Vt;
-    for (int j = 0; j < n; ++j) {
-      int32_t* d = bw.deltas + (size_t)j * 4 * Vt;
-      int32_t v;
-      if ((v = d[x])) { row[A[j]] += (uint32_t)v; d[x] = 0; changed = 1; }
-      if ((v = d[Vt + x])) { row[N[j]] += (uint32_t)v; d[Vt + x] = 0; changed = 1; }
-    }
-  }
-  if (lane == 0) changed_w[wave] = changed;
-  __syncthreads();
-  for (int j = 0; j < n; ++j)     // (2) rows b_j and new_j entirely, by the workgroup owning them
-    for (int r = 0; r < 2; ++r) {
-      const int xr = r == 0 ? B[j] : N[j];
-      if (xr < x0 || xr >= x0 + APPLY_ROWS || xr >= nrows) continue;
-      int32_t* d = bw.deltas + ((size_t)j * 4 + 2 + r) * Vt;
-      uint32_t* row = table + (size_t)xr * Vt;
-      int anyr = 0;
-      for (int y = threadIdx.x; y < Vt; y += 64 * APPLY_ROWS) {
-        const int32_t v = d[y];
-        if (v) { row[y] += (uint32_t)v; d[y] = 0; anyr = 1; }
-      }
-      if (anyr) changed_w[xr - x0] = 1;
-    }
-  __syncthreads();
-  if (lane == 0 && x < nrows)     // (3) the merged pairs, after every add
-    for (int j = 0; j < n; ++j)
+#pragma unroll
+  for (int j = 0; j < BK; ++j) changed |= x == A[j] || x == B[j] || x == N[j];   // -1 past n
+  ASTAMP(1);
+  ASTAMP(2);
+  if (lane == 0 && x < nrows)     // the merged pairs (every add landed in the previous kernel)
+#pragma unroll
+    for (int j = 0; j < BK; ++j)
       if (x == A[j]) {
         table[(size_t)x * Vt + B[j]] = 0u;   // never re-picked
         tlen[N[j]] = tlen[A[j]] + tlen[B[j]];
-        changed_w[wave] = 1;
       }
   if (blockIdx.x == 0 && threadIdx.x == 0 && n > 0) {   // commit the batch (no other workgroup reads it)
     const uint64_t mask = (1ull << loop->log2cap) - 1;
@@ -1914,9 +1989,13 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     }
     loop->n_merges = nm;
     loop->vcur = vcur;
+    int mt = loop->maxtlen;
+    for (int j = 0; j < n; ++j) mt = max(mt, (int)loop->blen[j]);
+    loop->maxtlen = mt;
   }
   __syncthreads();
-  changed = init ? 1 : changed_w[wave];
+  ASTAMP(3);
+  changed |= init;
   unsigned long long best = 0, second = 0;
   if (x < nrows && x < vcur) {
     if (aw.clean[x] && !changed) {
@@ -1966,17 +2045,20 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   }
   if (lane == 0) { wbest[wave] = best; wsec[wave] = second; }
   __syncthreads();
-  if (threadIdx.x < BK) {   // this workgroup's BK best rows: thread k takes the k-th
-    const int k = threadIdx.x;
-    unsigned long long kb = 0, ks = 0;
-    for (int w = 0; w < APPLY_ROWS; ++w) {
-      int rank = 0;   // rows above w (keys are distinct unless 0)
-      for (int v = 0; v < APPLY_ROWS; ++v) rank += wbest[v] > wbest[w];
-      if (rank == k && wbest[w]) { kb = wbest[w]; ks = wsec[w]; }
+  ASTAMP(4);
+  if (threadIdx.x < APPLY_ROWS) {   // this workgroup's BK best rows, best first: row w goes to its rank
+    const int w = threadIdx.x;
+    const unsigned long long kw = wbest[w];
+    int rank = 0;   // rows above w (ties -- only empty rows -- by index)
+#pragma unroll
+    for (int v = 0; v < APPLY_ROWS; ++v) rank += wbest[v] > kw || (wbest[v] == kw && v < w);
+    if (rank < BK) {
+      bw.wgkey[(size_t)rank * batch_nwg(Vt) + blockIdx.x] = kw;   // the grid may cover fewer rows than Vt
+      bw.wgsec[(size_t)rank * batch_nwg(Vt) + blockIdx.x] = kw ? wsec[w] : 0ull;
     }
-    bw.wgkey[(size_t)k * batch_nwg(Vt) + blockIdx.x] = kb;   // the grid may cover fewer rows than Vt
-    bw.wgsec[(size_t)k * batch_nwg(Vt) + blockIdx.x] = ks;
   }
+  ASTAMP(5);
+#undef ASTAMP
 }
 
 // -------------------------------------------------- persistent merge loop --
@@ -2800,6 +2882,9 @@ static __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, i
 extern "C" int beast_debug_merge_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_stamps), sizeof(g_bpe_stamps)) == hipSuccess ? 0 : -2;
 }
+extern "C" int beast_debug_apply_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_apply_stamps), sizeof(g_apply_stamps)) == hipSuccess ? 0 : -2;
+}
 extern "C" int beast_debug_decide_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_dstamps), sizeof(g_bpe_dstamps)) == hipSuccess ? 0 : -2;
 }
@@ -2897,7 +2982,7 @@ static int loop_batch(LoopState* st, const LoopHash& lh, BatchWs bw, ArgWs aw, i
   const int agrid = (rows + APPLY_ROWS - 1) / APPLY_ROWS;
   for (int i = 0; i < n_steps; ++i) {
     hipLaunchKernelGGL(k_merge_batch<KM>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, tlen,
-                       max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, bw,
+                       max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, bw, table, aw,
                        (long long)beast::g_merge_lds_min);
     BEAST_LAUNCHED("k_merge_batch");
     hipLaunchKernelGGL(k_apply_batch, dim3(agrid), dim3(64 * APPLY_ROWS), 0, s, table, Vt, aw, bw, tlen, st, lh, rows, 0);
@@ -2925,7 +3010,7 @@ extern "C" int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_step
   const ArgWs aw = argws_view(argws, Vt);
   const BatchWs bw = batch_view(batch_ws, Vt);
   const int rows = std::min(Vt, std::max(vocab_size, 1));
-  if (init) {   // zero deltas, every row's best and second-best, the workgroups' best rows
+  if (init) {   // every row's best and second-best, the workgroups' best rows
     BEAST_HIP(hipMemsetAsync(batch_ws, 0, batch_ws_bytes(Vt), s), "batch workspace memset");
     hipLaunchKernelGGL(k_apply_batch, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s, table,
                        Vt, aw, bw, tlen, st, lh, rows, 1);

@@ -25,7 +25,7 @@ def build(m0):
     for f in sorted(os.listdir(_build.CSRC)):
         if f.endswith(".hip"):
             o = os.path.join(tempfile.gettempdir(), f"stamps_{f}.o")
-            subprocess.run([_build._hipcc(), *_build.CXXFLAGS, f"-DBPE_MERGE_STAMPS={m0}", "-c",
+            subprocess.run([_build._hipcc(), *_build.CXXFLAGS, f"-DBPE_MERGE_STAMPS={m0}", *os.environ.get("STAMPS_FLAGS", "").split(), "-c",
                             os.path.join(_build.CSRC, f), "-o", o], check=True)
             objs.append(o)
     subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o",
@@ -60,6 +60,12 @@ def run(mode):
         lib.beast_debug_decide_stamps.argtypes = [C.c_void_p]
         assert lib.beast_debug_decide_stamps(dbuf) == 0
         dst = np.frombuffer(dbuf, dtype=np.uint64).reshape(64, 8).astype(np.int64)
+    ast = None
+    if dst is not None and hasattr(lib, "beast_debug_apply_stamps"):
+        abuf = (C.c_ulonglong * (64 * 256 * 6))()
+        lib.beast_debug_apply_stamps.argtypes = [C.c_void_p]
+        assert lib.beast_debug_apply_stamps(abuf) == 0
+        ast = np.frombuffer(abuf, dtype=np.uint64).reshape(64, 256, 6).astype(np.int64)
     for m in range(64):
         s = st[m]
         ran = s[:, 0] > 0
@@ -74,7 +80,16 @@ def run(mode):
                "decide_us": [float(np.median(ph(0, 1))), float(ph(0, 1).max())]}
         if os.environ.get("BEAST_BPE_LOOP", "").startswith("batch"):
             rec["first_merge"] = m
-            rec["batch"] = int(s[0, 5])
+            rec["batch"] = int(s[0, 5] & 255)
+            nc = s[:, 5] >> 8   # candidates per workgroup
+            rec["cand_per_wg"] = [int(np.median(nc)), int(nc.max())]
+            if ast is not None:   # apply: single entries, full rows, retire+commit, rescan, top rows
+                a = ast[m]
+                a = a[(a[:, 0] > 0) & (a[:, 5] > 0)]
+                if len(a):
+                    ph = np.diff(a, axis=1) / 100.0
+                    rec["apply_us"] = [round(float(v), 2) for v in np.median(ph, axis=0)]
+                    rec["apply_span_us"] = round(float((a[:, 5].max() - a[:, 0].min()) / 100.0), 2)
             e = st[m][0, 0]   # workgroup 0: entry, loads, list merges, shuffle merges, probes, rules
             rec["decide_phases_us"] = [round(float(v), 2) for v in np.diff(np.r_[e, dst[m][:5]]) / 100.0]
         if done.any():
@@ -85,7 +100,14 @@ def run(mode):
                         "flush_us": [float(np.median((d[:, 4] - d[:, 3]) / 100.0)), float(((d[:, 4] - d[:, 3]) / 100.0).max())],
                         "last_exit_us": float((d[:, 4].max() - t0) / 100.0)})
         out.append(rec)
-    print(json.dumps({"mode": os.environ.get("BEAST_BPE_LOOP", mode), "merges": len(res.merges), "loop_s": res.stats["merge_loop_s"], "stamps": out}))
+    extra = {}
+    if hasattr(lib, "beast_debug_merge_stats"):   # built with STAMPS_FLAGS=-DBPE_MERGE_STATS
+        b4 = (C.c_ulonglong * 4)()
+        lib.beast_debug_merge_stats.argtypes = [C.c_void_p]
+        lib.beast_debug_merge_stats(b4)
+        extra["merge_stats"] = {"visited": b4[0], "changed": b4[1], "applications_or_syms": b4[2],
+                                "visited_syms": b4[3]}
+    print(json.dumps({**extra, "mode": os.environ.get("BEAST_BPE_LOOP", mode), "merges": len(res.merges), "loop_s": res.stats["merge_loop_s"], "stamps": out}))
 
 
 def run_persistent():
