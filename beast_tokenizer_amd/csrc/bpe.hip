@@ -1714,58 +1714,56 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       }
     }
     DSTAMP(KB_MI, 3);
-    int A[KM], B[KM], E[KM];
-    uint32_t Ln[KM];
-    unsigned long long H[KM], Kc[KM], Sc[KM];
+    // HF's stopping rules per merge and the batch rules (see above), every candidate on its own
+    // lane against the ones before it; the batch is the leading run of lanes that pass
+    const bool live = loop->active != 0;
+    const int target = loop->target, nm = loop->n_merges, maxm = loop->max_merges;
+    const unsigned long long minf = (unsigned long long)loop->min_freq;
+    const unsigned long long count = ckey >> 32;
+    bool ok = live && lane < KM && count >= 1 && count >= minf && vcur + lane < target && nm + lane < maxm;
+    if (lane > 0) ok &= exist < 0;   // only the first may re-use an id
+    unsigned long long sec = 0;
 #pragma unroll
-    for (int j = 0; j < KM; ++j) {
-      A[j] = __builtin_amdgcn_readlane(cand_a, j); B[j] = __builtin_amdgcn_readlane(cand_b, j);
-      E[j] = __builtin_amdgcn_readlane(exist, j); Ln[j] = (uint32_t)__builtin_amdgcn_readlane((int)clen, j);
-      H[j] = readlane_u64(ch, j); Kc[j] = readlane_u64(ckey, j); Sc[j] = readlane_u64(csec, j);
+    for (int i = 0; i < KM - 1; ++i) {
+      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
+      const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)clen, i);
+      const unsigned long long hi = readlane_u64(ch, i), si = readlane_u64(csec, i);
+      const bool ends = ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0);   // self-pair / re-use
+      if (i < lane)
+        ok &= !ends && cand_a != ai && cand_a != bi && cand_b != ai && cand_b != bi && !(ch == hi && clen == li);
+      if (i < lane) sec = umax64(sec, si);
     }
-    // HF's stopping rules per merge and the batch rules (see above); lane 0 decides
-    if (lane == 0) {
-      int n = 0;
-      unsigned long long sec = 0;
-      const bool live = loop->active != 0;
-      const int target = loop->target, nm = loop->n_merges, maxm = loop->max_merges;
-      const unsigned long long minf = (unsigned long long)loop->min_freq;
-#pragma unroll
-      for (int j = 0; j < KM; ++j) {
-        if (!live || n < j) break;
-        const unsigned long long count = Kc[j] >> 32;
-        if (count < 1 || count < minf || vcur + n >= target || nm + n >= maxm) break;
-        if (j > 0) {
-          bool stop = sec >= Kc[j] || E[j] >= 0;   // a taken row's second-best comes first / id re-use
-#pragma unroll
-          for (int i = 0; i < j; ++i)
-            stop |= A[j] == A[i] || A[j] == B[i] || B[j] == A[i] || B[j] == B[i] || (H[j] == H[i] && Ln[j] == Ln[i]);
-          if (stop) break;
-        }
-        const bool reused = j == 0 && E[0] >= 0;
-        s_a[n] = A[j];
-        s_b[n] = B[j];
-        s_nid[n] = reused ? E[0] : vcur + n;
-        s_len[n] = Ln[j];
-        s_need[n] = sig_bit((uint32_t)A[j]) | sig_bit((uint32_t)B[j]);
-        if (blockIdx.x == 0) {   // the record k_apply_batch applies and commits
-          loop->ba[n] = A[j]; loop->bb[n] = B[j]; loop->bnid[n] = s_nid[n];
-          loop->breused[n] = reused ? 1 : 0; loop->blen[n] = Ln[j]; loop->bh[n] = H[j];
-        }
-        sec = umax64(sec, Sc[j]);
-        ++n;
-        if (A[j] == B[j] || reused) break;   // a self-pair or a re-used id ends the batch
+    ok &= sec < ckey;   // a taken row's second-best would come first
+    const unsigned long long pass = __ballot(ok);
+    const int n = (int)__builtin_ctzll(~pass);   // leading lanes that pass (<= KM)
+    if (lane < n) {
+      const bool reused = lane == 0 && exist >= 0;
+      const int nid = reused ? exist : vcur + lane;
+      s_a[lane] = cand_a;
+      s_b[lane] = cand_b;
+      s_nid[lane] = nid;
+      s_len[lane] = clen;
+      s_need[lane] = sig_bit((uint32_t)cand_a) | sig_bit((uint32_t)cand_b);
+      if (blockIdx.x == 0) {   // the record k_apply_batch applies and commits
+        loop->ba[lane] = cand_a; loop->bb[lane] = cand_b; loop->bnid[lane] = nid;
+        loop->breused[lane] = reused ? 1 : 0; loop->blen[lane] = clen; loop->bh[lane] = ch;
       }
+    }
+    DSTAMP(KB_MI, 4);
+    if (lane == 0) {
       s_n = n;
-      DSTAMP(KB_MI, 4);
       // merges 0 .. kd-1 sum their changes in LDS: the frequent ones whose vectors fit
       const int stride = vcur + n;
       int kd = 0;
-      while (kd < n && (kd + 1) * 16 * stride <= BATCH_LDS && (long long)(Kc[kd] >> 32) >= lds_min) ++kd;
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (kd == j && j < n && (j + 1) * 16 * stride <= BATCH_LDS &&
+            (long long)(readlane_u64(ckey, j) >> 32) >= lds_min)
+          kd = j + 1;
       s_kd = kd;
       if (blockIdx.x == 0) {
         loop->bn = n;
-        loop->bvcur = vcur + n - ((n > 0 && E[0] >= 0) ? 1 : 0);
+        loop->bvcur = vcur + n - ((n > 0 && exist >= 0) ? 1 : 0);
         if (n == 0) loop->active = 0;
       }
     }
