@@ -397,7 +397,7 @@ def bpe_bench(dev, args, world, rank, reduce):
            "value": st["n_merges"] / el, "unit": "merges/s", "merges": st["n_merges"],
            "seconds": el, "seconds_runs": times, "trajectories": args.bpe_seqs - args.bpe_seqs % world,
            "vocab_size": args.bpe_vocab, "setup_s": st["setup_s"], "merge_loop_s": st["merge_loop_s"],
-           "us_per_merge": st["merge_loop_s"] / max(st["n_merges"], 1) * 1e6,
+           "us_per_merge": st["merge_loop_s"] / max(st["n_merges"], 1) * 1e6, "loop": st.get("loop"),
            "words": st["n_words"], "symbols": st["n_syms"], "distinct_words": st.get("n_distinct"),
            "corpus_sha256": sha}
     rb = bpe_bytes(st)
