@@ -42,10 +42,19 @@ constexpr int ST_OK = 0, ST_BELOW_MIN = 1, ST_ABOVE_MAX = 2, ST_NOT_UNICODE = 3,
               ST_NO_CLASS = 5, ST_TOO_LONG = 6;
 
 #ifdef BPE_STAMPS
-// tools/codec_stamps.py only (the product compiles these out): s_memtime at phase
-// boundaries of row 0
+// tools/codec/bpe_encode_phases.py only (the product compiles these out): s_memtime cycles of
+// each encode phase summed over every row (lane 0 of each wave); [0] counts the rows, [8] the
+// merge-map staging
 __device__ unsigned long long g_bpe_stamps[16];
-#define BPE_STAMP(k) do { if (r == 0 && lane == 0) g_bpe_stamps[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#define BPE_STAMP(k)                                                                          \
+  do {                                                                                        \
+    if (lane == 0) {                                                                          \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+      if ((k) > 0) atomicAdd(&g_bpe_stamps[k], t_ - t_prev);                                  \
+      else atomicAdd(&g_bpe_stamps[0], 1ull);                                                 \
+      t_prev = t_;                                                                            \
+    }                                                                                         \
+  } while (0)
 #else
 #define BPE_STAMP(k) do { } while (0)
 #endif
@@ -261,6 +270,9 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
 
 template <class Map>
 __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r, int lane) {
+#ifdef BPE_STAMPS
+  unsigned long long t_prev = 0;
+#endif
   BPE_STAMP(0);
   const int64_t r0 = a.row_off[r];
   const int n = (int)(a.row_off[r + 1] - r0);
@@ -488,6 +500,9 @@ template <bool MAP_LDS>
 __global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
   extern __shared__ __align__(16) char lds_raw[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef BPE_STAMPS
+  const unsigned long long t_stage = __builtin_amdgcn_s_memtime();
+#endif
   size_t row_base = 0;
   LdsMap lm;
   if constexpr (MAP_LDS) {
@@ -502,7 +517,7 @@ __global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
     __syncthreads();
   }
 #ifdef BPE_STAMPS
-  if (blockIdx.x == 0 && threadIdx.x == 0) g_bpe_stamps[8] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) atomicAdd(&g_bpe_stamps[8], __builtin_amdgcn_s_memtime() - t_stage);
 #endif
   EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S), a.Lc, a.S);
   for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
