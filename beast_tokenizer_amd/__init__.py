@@ -10,11 +10,11 @@ declared in include/beast_hip.h.  Build it with ``python -m beast_tokenizer_amd.
 """
 from .base_tokenizer import TokenizerBase
 from .beast_bspline_tokenizer import CONFIG_FILENAME, BEASTBsplineTokenizer
-from .beast_bspline_bpe_tokenizer import BEASTBsplineBPETokenizer
+from .beast_bspline_bpe_tokenizer import BEASTBsplineBPETokenizer, BpeIds
 from .beast_bpe_trainer import FIGBPE, FIGBPEState
 from .utils import continuous_to_discrete, denormalize_tensor, discrete_to_continuous, normalize_tensor
 
 __all__ = [
-    "TokenizerBase", "CONFIG_FILENAME", "BEASTBsplineTokenizer", "BEASTBsplineBPETokenizer", "FIGBPE", "FIGBPEState",
+    "TokenizerBase", "CONFIG_FILENAME", "BEASTBsplineTokenizer", "BEASTBsplineBPETokenizer", "BpeIds", "FIGBPE", "FIGBPEState",
     "continuous_to_discrete", "discrete_to_continuous", "normalize_tensor", "denormalize_tensor",
 ]

@@ -25,6 +25,7 @@ OPT_GENERIC_KERNELS = 1
 OPT_BLOCK_WAVES = 2
 OPT_MERGE_LDS_MIN = 3
 OPT_MERGE_LIST_RATIO = 4
+OPT_BPE_ENCODE_MODE = 5
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 

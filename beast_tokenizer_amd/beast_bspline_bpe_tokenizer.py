@@ -19,7 +19,7 @@ import json
 import numbers
 from dataclasses import dataclass
 from pathlib import Path
-from typing import TYPE_CHECKING, Any, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+from typing import TYPE_CHECKING, Any, Dict, Iterable, List, NamedTuple, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
@@ -28,6 +28,18 @@ from tokenizers import ByteLevelBPETokenizer
 from .beast_bspline_tokenizer import CONFIG_FILENAME, BEASTBsplineTokenizer
 
 TokenLike = Union[Sequence[int], torch.Tensor, np.ndarray]
+
+
+class BpeIds(NamedTuple):
+    """BPE ids of a batch as one device block: ``ids`` int64 [rows, width] padded with
+    ``bpe_codec.PAD_ID`` (a u32 no vocabulary holds: decoding skips it, as HF's does),
+    ``lengths`` int64 [rows]; ``to_lists()`` gives the reference's ``List[List[int]]``."""
+    ids: torch.Tensor
+    lengths: torch.Tensor
+
+    def to_lists(self) -> List[List[int]]:
+        ids, lens = self.ids.cpu().numpy(), self.lengths.cpu().numpy()
+        return [ids[i, :lens[i]].tolist() for i in range(ids.shape[0])]
 
 if TYPE_CHECKING:
     from .beast_bpe_trainer import FIGBPEState
@@ -175,9 +187,10 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
             self._bpe_gpu_owner = tokenizer   # keeps id(tokenizer) from being reused
         return self._bpe_gpu
 
-    def _discrete_to_bpe(self, discrete_tokens: TokenLike) -> List[List[int]]:
+    def _discrete_to_bpe(self, discrete_tokens: TokenLike, as_tensors: bool = False):
         """Reference :175-198, every row in one GPU launch (csrc/bpe_codec.hip k_bpe_encode):
-        same ids as HF's per-row ``encode(text, add_special_tokens=False)``, same errors."""
+        same ids as HF's per-row ``encode(text, add_special_tokens=False)``, same errors.
+        as_tensors: a ``BpeIds`` block (device ids padded with PAD_ID, lengths) instead of lists."""
         from .bpe_codec import rows_from_sequences, rows_from_tensor
         model = self._gpu_bpe()
         max_span = None if self.bpe_max_token is None else self.bpe_max_token - self.bpe_min_token
@@ -188,6 +201,8 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
         else:
             seqs = [np.asarray(s).reshape(-1).astype(np.int64) for s in self._as_sequence_list(discrete_tokens)]
             flat, off, width = rows_from_sequences(seqs, model.device)
+        if as_tensors:
+            return BpeIds(*model.encode_to_tensors(flat, off, width, self.bpe_min_token, max_span))
         return model.encode_to_lists(flat, off, width, self.bpe_min_token, max_span)
 
     def _bpe_to_discrete(self, tokens: Iterable[TokenLike]) -> torch.Tensor:
@@ -196,6 +211,8 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
         from .bpe_codec import ids_as_i32, rows_from_sequences, rows_from_tensor
         model = self._gpu_bpe()
         dev = model.device
+        if isinstance(tokens, BpeIds):   # padded block from encode(..., return_tensors=True)
+            tokens = tokens.ids
         if isinstance(tokens, (torch.Tensor, np.ndarray)):
             _rows(tokens, "BPE tokens")          # dimension check with the reference's message
             block = torch.as_tensor(tokens)
@@ -216,9 +233,12 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
                                             respect_llm_vocab_size=False)
 
     def encode(self, trajs: torch.Tensor, update_bounds: bool = False, *,
-               return_mp_tokens: bool = False) -> tuple:
+               return_mp_tokens: bool = False, return_tensors: bool = False) -> tuple:
+        """return_tensors (an extension): the BPE ids as ``BpeIds(ids, lengths)`` -- a device
+        block padded with ``PAD_ID`` that ``decode`` / ``bpe_to_mp_tokens`` take as is --
+        instead of ``List[List[int]]``; the ids are the same."""
         mp_tokens, params = self.encode_to_mp_tokens(trajs, update_bounds=update_bounds)
-        out = (self._discrete_to_bpe(mp_tokens), params)
+        out = (self._discrete_to_bpe(mp_tokens, as_tensors=return_tensors), params)
         return out + (mp_tokens,) if return_mp_tokens else out
 
     def bpe_to_mp_tokens(self, tokens: Iterable[TokenLike]) -> torch.Tensor:

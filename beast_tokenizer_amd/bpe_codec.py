@@ -28,6 +28,9 @@ from . import _lib
 from .pretok import bytes_to_unicode, class_lut
 
 MAX_SPECIAL, MAX_SPECIAL_LEN = 64, 64
+# padding of the tensor form of encoded rows: a u32 that is no vocabulary id, so HF's decode (and
+# ours, ids_as_i32 -> -1) skips it -- a padded row decodes to the row itself
+PAD_ID = 0xFFFFFFFF
 
 _ENC_ERRORS = {
     1: (ValueError, "Discrete tokens contain values smaller than the configured BPE minimum token."),
@@ -202,6 +205,26 @@ class GpuBpeModel:
         ids_np = ids_h.numpy()
         lens_np = ls[0]
         return [ids_np[i, :lens_np[i]].tolist() for i in range(R)]
+
+    def encode_to_tensors(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,
+                          max_span: Optional[int]):
+        """The ids as a device block instead of lists: (ids int64 [R, W] padded with PAD_ID,
+        lengths int64 [R]); one small device-to-host copy (the row status, for the reference's
+        errors) instead of the whole id block and a list build."""
+        ids, lens, status = self.encode_rows(tok, row_off, max_row, min_token, max_span)
+        R = lens.numel()
+        if R == 0:
+            return torch.empty((0, 0), dtype=torch.int64, device=self.device), lens.to(torch.int64)
+        # one copy of the status summary: worst status (first failing row's code) and the widest row
+        first_bad = torch.where(status != 0, torch.arange(R, device=self.device, dtype=torch.int32), R).min()
+        summ = torch.stack([first_bad, lens.max()]).cpu()
+        r_bad, w = int(summ[0]), int(summ[1])
+        if r_bad < R:
+            exc, msg = _ENC_ERRORS[int(status[r_bad])]
+            raise exc(msg)
+        out = ids[:, :w].to(torch.int64)
+        out.masked_fill_(torch.arange(w, device=self.device)[None, :] >= lens[:, None], PAD_ID)
+        return out, lens.to(torch.int64)
 
     # --------------------------------------------------------------- decode --
     def decode_rows(self, ids: torch.Tensor, row_off: torch.Tensor, L: int, min_token: int):

@@ -31,11 +31,15 @@ namespace {
 
 constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;
 constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
-constexpr int WAVES = 4;            // rows in flight per workgroup
+constexpr int WAVES = 4;            // rows in flight per workgroup (decode)
+constexpr int ENC_MAX_WAVES = 16;   // encode: as many rows per workgroup as the LDS holds, up to 16
 constexpr int BLOCK = 64 * WAVES;
 constexpr int MAX_SPECIAL = 64, MAX_SPECIAL_LEN = 64;
+constexpr int RM_PER = 8;           // symbol positions per lane of the round merge (rows <= 512 symbols)
+constexpr uint32_t RK_NONE = 0xFFFFFFFFu;
 constexpr int LDS_MAP_MAX_LOG2 = 13;   // stage maps of <= 8192 slots (64 KiB + rank table)
-constexpr size_t LDS_BUDGET = 160 * 1024;   // gfx950: one workgroup may declare all 160 KiB
+constexpr size_t LDS_BUDGET = 160 * 1024;
+constexpr size_t STATIC_LDS = 2048;         // k_bpe_encode's byte -> id table and LUT head   // gfx950: one workgroup may declare all 160 KiB
 
 // encode status per row (host maps them to the reference's exceptions)
 constexpr int ST_OK = 0, ST_BELOW_MIN = 1, ST_ABOVE_MAX = 2, ST_NOT_UNICODE = 3, ST_SURROGATE = 4,
@@ -176,18 +180,34 @@ struct EncLds {
   int16_t* nxt;       // [S]
   uint8_t* cls;       // [Lc]
   int32_t* misc;      // [4]: n_words
+  uint32_t* rk;       // [S] round merge: (rank << 16 | new id) of the pair starting here, RK_NONE: none
+  int16_t* wid;       // [S] word of each symbol
+  uint8_t* cand;      // [S] this round's merge candidates
+  uint8_t* dirty;     // [S] pair changed since its rank was read
+  uint32_t* wmin;     // [Lc] this round's lowest pair per word
 };
 
+// the heap (long rows) and the round merge's arrays (rows <= 64 * RM_PER symbols) share a region
+__host__ __device__ inline size_t enc_merge_bytes(int Lc, int S) {
+  const size_t heap = al16(sizeof(uint32_t) * 3 * (size_t)S);
+  const size_t rounds = al16(sizeof(uint32_t) * S) + al16(sizeof(uint32_t) * Lc) + 2 * al16(S);
+  return heap > rounds ? heap : rounds;
+}
 __host__ __device__ inline size_t enc_row_bytes(int Lc, int S) {
-  return al16(sizeof(uint32_t) * 3 * (size_t)S) + al16(sizeof(int32_t) * S) + al16(sizeof(int32_t) * Lc) +
+  return enc_merge_bytes(Lc, S) + al16(sizeof(int32_t) * S) + al16(sizeof(int32_t) * Lc) +
          2 * al16(sizeof(int32_t) * (Lc + 1)) + 2 * al16(sizeof(int32_t) * Lc) + 2 * al16(sizeof(int16_t) * S) +
-         al16(Lc) + 16;
+         al16(Lc) + 16 + al16(sizeof(int16_t) * S);
 }
 
 __device__ inline EncLds enc_carve(char* p, int Lc, int S) {
   EncLds L;
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
-  L.heap = (uint32_t*)take(sizeof(uint32_t) * 3 * (size_t)S);
+  char* merge = take(enc_merge_bytes(Lc, S));   // heap, or rk | wmin | cand | dirty
+  L.heap = (uint32_t*)merge;
+  L.rk = (uint32_t*)merge;
+  L.wmin = (uint32_t*)(merge + al16(sizeof(uint32_t) * S));
+  L.cand = (uint8_t*)(merge + al16(sizeof(uint32_t) * S) + al16(sizeof(uint32_t) * Lc));
+  L.dirty = L.cand + al16(S);
   L.c = (int32_t*)take(sizeof(int32_t) * S);
   L.cps = (int32_t*)take(sizeof(int32_t) * Lc);
   L.symoff = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
@@ -198,6 +218,7 @@ __device__ inline EncLds enc_carve(char* p, int Lc, int S) {
   L.nxt = (int16_t*)take(sizeof(int16_t) * S);
   L.cls = (uint8_t*)take(Lc);
   L.misc = (int32_t*)take(16);
+  L.wid = (int16_t*)take(sizeof(int16_t) * S);
   return L;
 }
 
@@ -219,6 +240,7 @@ struct EncArgs {
   MergeMap map;               // in HBM
   int n_merges;
   int map_in_lds;             // host choice: k_bpe_encode<true> stages the map
+  int heap_merge;             // BEAST_OPT_BPE_ENCODE_MODE bit 0: HF's heap per word instead of rounds
   const int32_t* spec_cps;    // [n_spec][MAX_SPECIAL_LEN]
   const int32_t* spec_len;
   const int32_t* spec_id;
@@ -268,8 +290,114 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
   return x - v;
 }
 
+// 4b. (see encode_row) the round merge of a row of <= 64 * RMP byte symbols
+template <int RMP, class Map>
+__device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, int nw, int lane) {
+    // Each step reads all of a lane's positions first (addresses clamped, loads in flight
+    // together) and then acts on them, so a step costs one LDS round trip, not one per position.
+    const int kmax = (npos + 63) >> 6;   // positions per lane in use (<= RMP)
+    for (int k = 0; k < kmax; ++k) {
+      const int s = lane + 64 * k;
+      if (s < npos) { L.dirty[s] = 1; L.cand[s] = 0; }
+    }
+    wave_sync();
+    const int last = npos > 0 ? npos - 1 : 0;
+#ifdef BPE_STAMPS
+    if (lane == 0) { atomicAdd(&g_bpe_stamps[10], (unsigned long long)npos); atomicAdd(&g_bpe_stamps[11], (unsigned long long)nw); }
+#endif
+    while (true) {
+#ifdef BPE_STAMPS
+      if (lane == 0) atomicAdd(&g_bpe_stamps[9], 1ull);
+#endif
+      for (int w = lane; w < nw; w += 64) L.wmin[w] = RK_NONE;
+      // (a) ranks of the pairs next to last round's merges
+      int ck[RMP], nk[RMP], dk[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        const int s = min(lane + 64 * k, last);
+        dk[k] = k < kmax && lane + 64 * k < npos ? L.dirty[s] : 0;
+        ck[k] = L.c[s];
+        nk[k] = L.nxt[s];
+      }
+      int cn[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) cn[k] = L.c[max(nk[k], 0)];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        if (!dk[k]) continue;
+        const int s = lane + 64 * k;
+        uint32_t v = RK_NONE;
+        if (ck[k] >= 0 && nk[k] >= 0) {
+          int nid;
+          const int rk = mm_find(mm, ck[k], cn[k], nid);
+          if (rk >= 0) v = ((uint32_t)rk << 16) | (uint32_t)nid;
+        }
+        L.rk[s] = v;
+        L.dirty[s] = 0;
+      }
+      wave_sync();
+      // (b) every word's lowest pair
+      bool live = false;
+      uint32_t rv[RMP];
+      int wv[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        const int s = min(lane + 64 * k, last);
+        rv[k] = (k < kmax && lane + 64 * k < npos) ? L.rk[s] : RK_NONE;
+        wv[k] = L.wid[s];
+        ck[k] = L.c[s];
+      }
+#pragma unroll
+      for (int k = 0; k < RMP; ++k)
+        if (ck[k] >= 0 && rv[k] != RK_NONE) {
+          atomicMin(&L.wmin[wv[k]], rv[k]);
+          live = true;
+        }
+      if (!__any(live)) break;
+      wave_sync();
+      // (c) candidates: the pairs equal to their word's lowest
+      uint32_t mv[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) mv[k] = L.wmin[wv[k]];
+      bool cd[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        cd[k] = ck[k] >= 0 && rv[k] != RK_NONE && rv[k] == mv[k];
+        if (k < kmax && lane + 64 * k < npos) L.cand[lane + 64 * k] = cd[k];
+      }
+      wave_sync();
+      // (d) each run's head applies its run (one merge unless a self-pair repeats)
+      int pk[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) pk[k] = L.prv[min(lane + 64 * k, last)];
+      int pc[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) pc[k] = L.cand[max(pk[k], 0)];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        if (!cd[k] || (pk[k] >= 0 && pc[k])) continue;
+        const int nid = (int)(rv[k] & 0xFFFFu);
+        int t = lane + 64 * k;
+        while (true) {
+          const int u = L.nxt[t], nn = L.nxt[u];
+          L.c[t] = nid;
+          L.c[u] = -1;
+          L.nxt[t] = (int16_t)nn;
+          if (nn >= 0) L.prv[nn] = (int16_t)t;
+          L.dirty[t] = 1;
+          const int pv = L.prv[t];
+          if (pv >= 0) L.dirty[pv] = 1;
+          if (!L.cand[u] || nn < 0 || !L.cand[nn]) break;   // the run of a self-pair goes on
+          t = nn;
+        }
+      }
+      wave_sync();
+    }
+}
+
 template <class Map>
-__device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r, int lane) {
+__device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r, int lane, const int32_t* b2i,
+                           const uint8_t* lut256) {
 #ifdef BPE_STAMPS
   unsigned long long t_prev = 0;
 #endif
@@ -280,10 +408,12 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
     if (lane == 0) { a.status[r] = ST_TOO_LONG; a.out_len[r] = 0; }
     return;
   }
-  // 1. code points, range checks (reference :181-192 order: below-min first), classes
+  // 1. code points, range checks (reference :181-192 order: below-min first), classes.  The
+  //    first 256 code points' loads are all in flight at once; classes of code points < 256
+  //    come from the workgroup's LDS copy of the LUT.
   int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
-  for (int i = lane; i < n; i += 64) {
-    const long long v = a.tok[r0 + i] - a.min_tok;
+  auto code_point = [&](int i, long long t) {
+    const long long v = t - a.min_tok;
     below |= v < 0;
     above |= (a.max_span >= 0 && v > a.max_span);
     notuni |= v > 0x10FFFF;
@@ -291,8 +421,16 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
     nocls |= v >= a.lut_n;
     const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
     L.cps[i] = cp;
-    L.cls[i] = (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
-  }
+    L.cls[i] = cp < 256 ? lut256[cp] : (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
+  };
+  constexpr int PF = 4;
+  long long tv[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) tv[k] = lane + 64 * k < n ? a.tok[r0 + lane + 64 * k] : 0;
+#pragma unroll
+  for (int k = 0; k < PF; ++k)
+    if (lane + 64 * k < n) code_point(lane + 64 * k, tv[k]);
+  for (int i = lane + 64 * PF; i < n; i += 64) code_point(i, a.tok[r0 + i]);
   BPE_STAMP(1);
   int st = ST_OK;
   if (__any(below)) st = ST_BELOW_MIN;
@@ -387,22 +525,24 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
   // 3. byte symbols as vocab ids
   for (int i = lane; i < n; i += 64) {
     const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
-    for (int q = 0; q < len; ++q) L.c[o + q] = a.byte2id[utf8_byte(cp, q)];
+    for (int q = 0; q < len; ++q) L.c[o + q] = b2i[utf8_byte(cp, q)];
   }
   wave_sync();
   const int nw = L.misc[0];
 
   BPE_STAMP(4);
-  // 4. one word per lane: BPE::merge_word + Word::merge_all
+  // 4a. one word per lane: special words, unknown chars (HF's unk / fuse_unk), the symbol list
+  const int npos = L.symoff[n];
   for (int w = lane; w < nw; w += 64) {
     const int sb = L.symoff[L.wcp[w]], se = L.symoff[L.wcp[w + 1]];
+    for (int s = sb; s < se; ++s) L.wid[s] = (int16_t)w;
     if (L.wspec[w] >= 0) {
       L.c[sb] = L.wspec[w];
+      L.nxt[sb] = -1;
+      L.prv[sb] = -1;
       for (int s = sb + 1; s < se; ++s) L.c[s] = -1;
-      L.wcnt[w] = 1;
       continue;
     }
-    // unknown chars: dropped (no unk token), or the unk id, fused if fuse_unk
     bool pending_unk = false;
     int last = -1;
     for (int s = sb; s < se; ++s) {
@@ -420,50 +560,68 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
       if (last >= 0) L.nxt[last] = (int16_t)s;
       last = s;
     }
-    uint32_t* hp = L.heap + 3 * (size_t)sb;
-    int hn = 0;
-    for (int s = sb; s < se; ++s) {
-      if (L.c[s] < 0 || L.nxt[s] < 0) continue;
-      int nid;
-      const int rk = mm_find(mm, L.c[s], L.c[L.nxt[s]], nid);
-      if (rk >= 0) heap_push(hp, hn, ((uint32_t)rk << 16) | (uint32_t)(s - sb));
-    }
-    int cnt = 0;
-    for (int s = sb; s < se; ++s) cnt += (L.c[s] >= 0);
-#ifdef BPE_SKIP_MERGE
-    hn = 0;
-#endif
-    while (hn > 0) {
-      const uint32_t top = heap_pop(hp, hn);
-      const int pos = sb + (int)(top & 0xFFFFu);
-      const int trank = (int)(top >> 16);
-      if (L.c[pos] < 0) continue;             // merged into its left neighbour
-      const int nx = L.nxt[pos];
-      if (nx < 0) continue;                   // last symbol
-      int new_id;
-      const int rk = mm_find(mm, L.c[pos], L.c[nx], new_id);
-      if (rk < 0) continue;
-      if (rk != trank && mm.rank2new[trank] != new_id) continue;   // expired entry
-      L.c[pos] = new_id;
-      L.c[nx] = -1;
-      --cnt;
-      const int nn = L.nxt[nx];
-      L.nxt[pos] = (int16_t)nn;
-      if (nn >= 0) L.prv[nn] = (int16_t)pos;
-      const int pv = L.prv[pos];
-      if (pv >= 0) {
-        int nid;
-        const int rp = mm_find(mm, L.c[pv], new_id, nid);
-        if (rp >= 0) heap_push(hp, hn, ((uint32_t)rp << 16) | (uint32_t)(pv - sb));
-      }
-      if (nn >= 0) {
-        int nid;
-        const int rn = mm_find(mm, new_id, L.c[nn], nid);
-        if (rn >= 0) heap_push(hp, hn, ((uint32_t)rn << 16) | (uint32_t)(pos - sb));
-      }
-    }
-    L.wcnt[w] = cnt;
   }
+  wave_sync();
+#ifndef BPE_SKIP_MERGE
+  if (npos <= 64 * RM_PER && !a.heap_merge) {
+    // 4b. BPE::merge_word + Word::merge_all for every word of the row at once.  HF pops the
+    //     lowest (rank, position) of the word's current pairs (stale heap entries skipped), so a
+    //     word's result is: repeatedly merge its lowest-rank pair, leftmost first.  One round
+    //     merges, in every word, all occurrences of that word's lowest pair (left to right in a
+    //     run of a self-pair: each run's head walks it), so rounds = distinct ranks applied per
+    //     word, and only pairs next to a merge are looked up again.
+    if (npos <= 64 * 4) round_merge<4>(mm, L, npos, nw, lane);
+    else round_merge<RM_PER>(mm, L, npos, nw, lane);
+  } else {
+    // 4b'. long rows: one word per lane with HF's (rank, pos) min-heap
+    for (int w = lane; w < nw; w += 64) {
+      if (L.wspec[w] >= 0) continue;
+      const int sb = L.symoff[L.wcp[w]], se = L.symoff[L.wcp[w + 1]];
+      uint32_t* hp = L.heap + 3 * (size_t)sb;
+      int hn = 0;
+      for (int s = sb; s < se; ++s) {
+        if (L.c[s] < 0 || L.nxt[s] < 0) continue;
+        int nid;
+        const int rk = mm_find(mm, L.c[s], L.c[L.nxt[s]], nid);
+        if (rk >= 0) heap_push(hp, hn, ((uint32_t)rk << 16) | (uint32_t)(s - sb));
+      }
+      while (hn > 0) {
+        const uint32_t top = heap_pop(hp, hn);
+        const int pos = sb + (int)(top & 0xFFFFu);
+        const int trank = (int)(top >> 16);
+        if (L.c[pos] < 0) continue;             // merged into its left neighbour
+        const int nx = L.nxt[pos];
+        if (nx < 0) continue;                   // last symbol
+        int new_id;
+        const int rk = mm_find(mm, L.c[pos], L.c[nx], new_id);
+        if (rk < 0) continue;
+        if (rk != trank && mm.rank2new[trank] != new_id) continue;   // expired entry
+        L.c[pos] = new_id;
+        L.c[nx] = -1;
+        const int nn = L.nxt[nx];
+        L.nxt[pos] = (int16_t)nn;
+        if (nn >= 0) L.prv[nn] = (int16_t)pos;
+        const int pv = L.prv[pos];
+        if (pv >= 0) {
+          int nid;
+          const int rp = mm_find(mm, L.c[pv], new_id, nid);
+          if (rp >= 0) heap_push(hp, hn, ((uint32_t)rp << 16) | (uint32_t)(pv - sb));
+        }
+        if (nn >= 0) {
+          int nid;
+          const int rn = mm_find(mm, new_id, L.c[nn], nid);
+          if (rn >= 0) heap_push(hp, hn, ((uint32_t)rn << 16) | (uint32_t)(pos - sb));
+        }
+      }
+    }
+    wave_sync();
+  }
+#endif
+  // symbols left per word
+  for (int w = lane; w < nw; w += 64) L.wcnt[w] = 0;
+  wave_sync();
+  for (int s = lane; s < npos; s += 64)
+    if (L.c[s] >= 0) atomicAdd(&L.wcnt[L.wid[s]], 1);
   wave_sync();
   BPE_STAMP(5);
   // 5. word offsets (wave scan), ids in order
@@ -497,12 +655,19 @@ struct LdsMap {
 };
 
 template <bool MAP_LDS>
-__global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
+__global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
   extern __shared__ __align__(16) char lds_raw[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ int32_t s_b2i[256];    // byte -> vocab id
+  __shared__ uint8_t s_lut[256];    // classes of code points < 256
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
 #ifdef BPE_STAMPS
   const unsigned long long t_stage = __builtin_amdgcn_s_memtime();
 #endif
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    s_b2i[i] = a.byte2id[i];
+    s_lut[i] = i < a.lut_n ? a.lut[i] : (uint8_t)CLS_OTHER;
+  }
+  if (!MAP_LDS) __syncthreads();
   size_t row_base = 0;
   LdsMap lm;
   if constexpr (MAP_LDS) {
@@ -510,8 +675,15 @@ __global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
     uint32_t* k = reinterpret_cast<uint32_t*>(lds_raw);
     uint32_t* v = k + cap;
     uint16_t* r2n = reinterpret_cast<uint16_t*>(lds_raw + al16(sizeof(uint32_t) * 2 * (size_t)cap));
-    for (int i = threadIdx.x; i < cap; i += BLOCK) { k[i] = a.map.keys[i]; v[i] = a.map.vals[i]; }
-    for (int i = threadIdx.x; i < a.n_merges; i += BLOCK) r2n[i] = a.map.rank2new[i];
+    // 16-byte copies (cap >= 64 is a multiple of 4; both halves are 16-byte aligned)
+    const uint4* gk = reinterpret_cast<const uint4*>(a.map.keys);
+    const uint4* gv = reinterpret_cast<const uint4*>(a.map.vals);
+    for (int i = threadIdx.x; i < cap / 4; i += blockDim.x) {
+      const uint4 x = gk[i], y = gv[i];
+      reinterpret_cast<uint4*>(k)[i] = x;
+      reinterpret_cast<uint4*>(v)[i] = y;
+    }
+    for (int i = threadIdx.x; i < a.n_merges; i += blockDim.x) r2n[i] = a.map.rank2new[i];
     lm.keys = k; lm.vals = v; lm.rank2new = r2n; lm.log2cap = a.map.log2cap;
     row_base = map_lds_bytes(a.map.log2cap, a.n_merges);
     __syncthreads();
@@ -520,9 +692,9 @@ __global__ __launch_bounds__(BLOCK) void k_bpe_encode(EncArgs a) {
   if (threadIdx.x == 0) atomicAdd(&g_bpe_stamps[8], __builtin_amdgcn_s_memtime() - t_stage);
 #endif
   EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S), a.Lc, a.S);
-  for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
-    if constexpr (MAP_LDS) encode_row(a, lm, L, r, lane);
-    else encode_row(a, a.map, L, r, lane);
+  for (int64_t r = (int64_t)blockIdx.x * nwv + wave; r < a.n_rows; r += (int64_t)gridDim.x * nwv) {
+    if constexpr (MAP_LDS) encode_row(a, lm, L, r, lane, s_b2i, s_lut);
+    else encode_row(a, a.map, L, r, lane, s_b2i, s_lut);
     wave_sync();
   }
 }
@@ -712,7 +884,9 @@ inline int log2_ceil(int64_t x) {
   return l;
 }
 
-int grid_for(int64_t n_rows) {
+// rows -> workgroups: at most the ones resident at once (per_cu from the occupancy of the launch:
+// each workgroup stages the merge map once and then loops over rows)
+int grid_for(int64_t n_rows, int per_cu = 4) {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0, v = 0;
@@ -720,7 +894,7 @@ int grid_for(int64_t n_rows) {
            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
   }
   const int64_t want = (n_rows + WAVES - 1) / WAVES;
-  const int64_t cap = (int64_t)cus * 4;
+  const int64_t cap = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
   return (int)(want < cap ? want : cap);
 }
 
@@ -774,8 +948,8 @@ extern "C" int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* m
   return BEAST_OK;
 }
 
-extern "C" size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms) {
-  return (size_t)WAVES * enc_row_bytes(max_row_cps, max_row_syms);
+extern "C" size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms) {   // per row (wave)
+  return enc_row_bytes(max_row_cps, max_row_syms);
 }
 
 extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
@@ -795,20 +969,27 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
   BEAST_REQUIRE(n_spec >= 0 && n_spec <= MAX_SPECIAL, "at most %d special tokens are supported", MAX_SPECIAL);
   BEAST_REQUIRE(n_spec == 0 || (spec_cps && spec_len && spec_id), "special-token arrays are null");
-  const size_t rows_lds = (size_t)WAVES * enc_row_bytes(max_row_cps, max_row_syms);
-  BEAST_REQUIRE_CODE(rows_lds <= LDS_BUDGET, BEAST_E_UNSUPPORTED,
+  const size_t row_b = enc_row_bytes(max_row_cps, max_row_syms);
+  BEAST_REQUIRE_CODE(row_b + STATIC_LDS <= LDS_BUDGET, BEAST_E_UNSUPPORTED,
                      "rows of %d code points / %d byte symbols need %zu B of LDS (> 160 KiB)", max_row_cps,
-                     max_row_syms, rows_lds);
+                     max_row_syms, row_b);
   EncArgs a;
   a.tok = reinterpret_cast<const long long*>(tok);
   a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
   a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
   a.map = map_view(map, n_merges);
   a.n_merges = n_merges;
+  // one workgroup per CU holding the merge map once and as many rows (waves) as fit beside it
+  // (BEAST_OPT_BPE_ENCODE_MODE bit 1: four waves per workgroup, as many workgroups as fit)
   const size_t map_lds = map_lds_bytes(a.map.log2cap, n_merges);
-  a.map_in_lds = (map_lds > 0 && rows_lds + map_lds <= LDS_BUDGET) ? 1 : 0;
+  const int want_w = (beast::g_bpe_encode_mode & 2) ? WAVES : ENC_MAX_WAVES;
+  a.map_in_lds = (map_lds > 0 && map_lds + row_b + STATIC_LDS <= LDS_BUDGET) ? 1 : 0;
+  const size_t room = LDS_BUDGET - STATIC_LDS - (a.map_in_lds ? map_lds : 0);
+  const int nwv = (int)std::max<size_t>(1, std::min<size_t>((size_t)want_w, room / row_b));
+  const size_t rows_lds = (size_t)nwv * row_b;
   a.spec_cps = spec_cps; a.spec_len = spec_len; a.spec_id = spec_id; a.n_spec = n_spec;
   a.unk_id = unk_id; a.fuse_unk = fuse_unk;
+  a.heap_merge = beast::g_bpe_encode_mode & 1;
   a.Lc = max_row_cps; a.S = max_row_syms;
   a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
   const size_t lds = rows_lds + (a.map_in_lds ? map_lds : 0);
@@ -817,10 +998,13 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   if (lds > 65536)
     BEAST_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
               "hipFuncSetAttribute(k_bpe_encode)");
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nwv, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
+  const int grid = (int)std::min<int64_t>((n_rows + nwv - 1) / nwv, (int64_t)grid_for(1 << 30, per_cu));
   if (a.map_in_lds)
-    hipLaunchKernelGGL(k_bpe_encode<true>, dim3(grid_for(n_rows)), dim3(BLOCK), lds, beast::as_stream(stream), a);
+    hipLaunchKernelGGL(k_bpe_encode<true>, dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
   else
-    hipLaunchKernelGGL(k_bpe_encode<false>, dim3(grid_for(n_rows)), dim3(BLOCK), lds, beast::as_stream(stream), a);
+    hipLaunchKernelGGL(k_bpe_encode<false>, dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
   BEAST_LAUNCHED("k_bpe_encode");
   return BEAST_OK;
 }

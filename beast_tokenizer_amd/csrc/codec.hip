@@ -1384,6 +1384,11 @@ extern "C" int beast_set_option(int option, int value) {
     beast::g_merge_lds_min = value;
     return BEAST_OK;
   }
+  if (option == BEAST_OPT_BPE_ENCODE_MODE) {
+    BEAST_REQUIRE(value >= 0 && value <= 3, "BEAST_OPT_BPE_ENCODE_MODE: %d is not 0..3", value);
+    beast::g_bpe_encode_mode = value;
+    return BEAST_OK;
+  }
   if (option == BEAST_OPT_MERGE_LIST_RATIO) {
     BEAST_REQUIRE(value >= 0, "BEAST_OPT_MERGE_LIST_RATIO: %d < 0", value);
     beast::g_merge_list_ratio = value;

@@ -497,10 +497,18 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     t0 = time.perf_counter()
     lists = model.encode_to_lists(flat, off, width, lo, span)
     t_api_enc = time.perf_counter() - t0
+    model.encode_to_tensors(flat, off, width, lo, span)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        blk = model.encode_to_tensors(flat, off, width, lo, span)
+    torch.cuda.synchronize()
+    t_api_tens = (time.perf_counter() - t0) / 10
+    assert blk[1].tolist() == [len(r) for r in lists]
     out.update({"rows": R, "ids_per_row": n_ids / R,
                 "encode_kernel_us": t_enc, "encode_rows_per_s_kernel": R / (t_enc * 1e-6),
                 "decode_kernel_us": t_dec, "decode_rows_per_s_kernel": R / (t_dec * 1e-6),
-                "encode_api_rows_per_s": R / t_api_enc,
+                "encode_api_rows_per_s": R / t_api_enc, "encode_api_tensors_rows_per_s": R / t_api_tens,
                 "encode_kernel_GBps": (R * width * 8 + n_ids * 4) / (t_enc * 1e-6) / 1e9,
                 "decode_kernel_GBps": (n_ids * 4 + R * width * 8) / (t_dec * 1e-6) / 1e9})
     if not args.no_cpu:

@@ -53,11 +53,14 @@ const char* beast_last_error(void);
  * BEAST_OPT_MERGE_LIST_RATIO = r: a pair-index merge walks its candidate list when the list is
  * shorter than (words / r), else it scans every word's Bloom signature (default 16; 0 = always
  * the list); results are identical.
- * Not thread-safe with concurrent launches. */
+ * Not thread-safe with concurrent launches. * BEAST_OPT_BPE_ENCODE_MODE = m (tests, measurements): beast_bpe_encode_rows' per-word merge by
+ * rounds (0, the default) or by HF's min-heap (1); m + 2 also launches one workgroup per 4 rows
+ * instead of only the resident ones.  Results are identical. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
 #define BEAST_OPT_MERGE_LDS_MIN 3
 #define BEAST_OPT_MERGE_LIST_RATIO 4
+#define BEAST_OPT_BPE_ENCODE_MODE 5
 int beast_set_option(int option, int value);
 
 /* ---------------------------------------------------------------- H1/H2 ---
@@ -340,8 +343,9 @@ int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* merge_b, con
  * max_row_syms.  byte2id[256]: vocab id of each byte-level char, -1 if absent (dropped, or
  * unk_id (fused when fuse_unk) if the model has an unk token).  Special tokens:
  * spec_cps[n_spec][64] code points, spec_len, spec_id.  Output: out_ids[r][0 .. out_len[r])
- * (row stride out_stride >= max_row_syms).  LDS per row: beast_bpe_encode_lds_bytes
- * (at most 160 KiB with the staged merge map, else BEAST_E_UNSUPPORTED). */
+ * (row stride out_stride >= max_row_syms).  LDS per row: beast_bpe_encode_lds_bytes (one row
+ * must fit 160 KiB, else BEAST_E_UNSUPPORTED); a workgroup holds the merge map once (when it
+ * fits beside a row) and as many rows as fit, up to 16. */
 size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms);
 int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
                           int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,

@@ -51,8 +51,17 @@ def decode_rows(model, id_rows, dev, L):
     return [out[i, :counts[i]].tolist() for i in range(len(seqs))], counts, status.cpu().numpy()
 
 
+@pytest.fixture(params=[0, 1, 3], ids=["rounds", "heap", "heap_wide_grid"])
+def encode_mode(request):
+    """k_bpe_encode's per-word merge (rounds by default, HF's heap) and its grid: same ids."""
+    from beast_tokenizer_amd import _lib
+    _lib.run("beast_set_option", _lib.OPT_BPE_ENCODE_MODE, request.param)
+    yield request.param
+    _lib.run("beast_set_option", _lib.OPT_BPE_ENCODE_MODE, 0)
+
+
 @pytest.mark.parametrize("case", sorted(CODEC))
-def test_encode_matches_hf_golden(case, gpu_device):
+def test_encode_matches_hf_golden(case, encode_mode, gpu_device):
     spec = CODEC[case]
     model = GpuBpeModel(hf_tokenizer(spec), gpu_device)
     rows = [cps for cps, _ in spec["encode"]]
@@ -75,7 +84,7 @@ def test_decode_matches_hf_golden(case, gpu_device):
 @pytest.mark.parametrize("span,rows,width,vocab", [(255, 3000, 140, 2048), (700, 1500, 60, 1500),
                                                     (3000, 800, 50, 4000), (127, 2000, 140, 800),
                                                     (255, 6000, 140, 6000)])
-def test_codec_matches_live_hf(span, rows, width, vocab, gpu_device):
+def test_codec_matches_live_hf(span, rows, width, vocab, encode_mode, gpu_device):
     """Train with HF (the reference's trainer), then every row of a fresh corpus -- including
     bins never seen in training -- encodes and decodes exactly as HF does."""
     from tokenizers import ByteLevelBPETokenizer

@@ -656,6 +656,23 @@ def test_bpe_tokenizer_end_to_end(gpu_device):
     back = tok.bpe_to_mp_tokens(bpe_ids)
     assert torch.equal(back.cpu(), mp.cpu())
     assert torch.equal(tok.decode(bpe_ids), BEASTBsplineTokenizer.decode(tok, mp))
+    # the tensor form: same ids, padded with PAD_ID, decodes as given (pads skipped, as HF skips them)
+    from beast_tokenizer_amd import BpeIds
+    from beast_tokenizer_amd.bpe_codec import PAD_ID
+    blk, params2 = tok.encode(x, return_tensors=True)
+    assert isinstance(blk, BpeIds) and blk.ids.device.type == "cuda" and params2.keys() == params.keys()
+    assert blk.to_lists() == bpe_ids
+    assert blk.lengths.tolist() == [len(r) for r in bpe_ids]
+    assert int(blk.ids.shape[1]) == max(len(r) for r in bpe_ids)
+    assert bool((blk.ids[torch.arange(blk.ids.shape[1], device=blk.ids.device)[None, :] >= blk.lengths[:, None]]
+                 == PAD_ID).all())
+    assert torch.equal(tok.bpe_to_mp_tokens(blk).cpu(), mp.cpu())
+    assert torch.equal(tok.bpe_to_mp_tokens(blk.ids).cpu(), mp.cpu())
+    assert torch.equal(tok.decode(blk), BEASTBsplineTokenizer.decode(tok, mp))
+    assert tok._require_bpe().decode([blk.ids[0, 0].item(), PAD_ID], skip_special_tokens=True) == \
+        tok._require_bpe().decode([blk.ids[0, 0].item()], skip_special_tokens=True)   # HF skips the pad id too
+    with pytest.raises(ValueError):   # out-of-range bins: the same error as the list form
+        tok._discrete_to_bpe(torch.full((2, 140), -5, dtype=torch.int64, device=gpu_device), as_tensors=True)
     # HF-trained reference on the same bins gives the same merges
     from tokenizers import ByteLevelBPETokenizer
     from tokenizers.trainers import BpeTrainer

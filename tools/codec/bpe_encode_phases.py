@@ -63,7 +63,8 @@ def run():
     n = max(d[0], 1)
     out = {"rows": d[0], "wall_us": el * 1e6,
            "cycles_per_row": {PHASES[k]: d[k] / n for k in range(1, 7)},
-           "staging_cycles_per_workgroup": d[8] / max(1, (4096 + 3) // 4)}
+           "staging_cycles_per_workgroup": d[8] / max(1, (4096 + 3) // 4),
+           "rounds_per_row": d[9] / n, "symbols_per_row": d[10] / n, "words_per_row": d[11] / n}
     print(json.dumps(out))
     del zero
 
