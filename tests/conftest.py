@@ -48,7 +48,7 @@ def gpu_device():
 
 
 KERNEL_MODES = {"specialised": (0, 0), "specialised_w4": (0, 4), "specialised_w7": (0, 7),
-                "specialised_w8": (0, 8), "generic": (1, 0)}
+                "specialised_w8": (0, 8), "specialised_w9": (0, 9), "generic": (1, 0)}
 
 
 def set_kernel_mode(mode):
@@ -60,11 +60,12 @@ def set_kernel_mode(mode):
     lib.beast_set_option(_lib.OPT_BLOCK_WAVES, waves)
 
 
-@pytest.fixture(params=["specialised", "specialised_w4", "specialised_w7", "specialised_w8", "generic"])
+@pytest.fixture(params=["specialised", "specialised_w4", "specialised_w7", "specialised_w8", "specialised_w9",
+                        "generic"])
 def kernel_mode(request):
     """Run a parity test on the shape-specialised kernels (the width the batch size picks,
-    the 4-wave width large batches use, the 7-wave one-pass encode and the 8-wave pipelined
-    encode forced at any batch) and on the runtime-shape ones."""
+    the 4-wave width large batches use, the 7-wave one-pass encode, the 8-wave pipelined
+    encode and the LDS-free direct encode forced at any batch) and on the runtime-shape ones."""
     set_kernel_mode(request.param)
     yield request.param
     set_kernel_mode("specialised")

@@ -211,7 +211,7 @@ def test_specialised_kernels_equal_generic(name, gpu_device):
     tok = make_tok(name, g, gpu_device)
     x = torch.from_numpy(synth_trajectories(1000, 50, CONFIGS[name]["num_dof"], seed=3, gripper_indices=gi))
     outs = []
-    for mode in ("generic", "specialised_w4", "specialised_w7", "specialised"):
+    for mode in ("generic", "specialised_w4", "specialised_w7", "specialised_w8", "specialised_w9", "specialised"):
         set_kernel_mode(mode)
         try:
             t, pd = tok.encode(x)

@@ -117,7 +117,7 @@ def test_options_validate_and_reset():
     lib = _lib.load()
     assert lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 1) == 0
     assert lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0) == 0
-    for w in (4, 7, 8, 0):
+    for w in (4, 7, 8, 9, 0):
         assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, w) == 0
     assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, 5) == _lib.BEAST_E_INVALID
     assert lib.beast_set_option(99, 0) == _lib.BEAST_E_INVALID
