@@ -540,6 +540,8 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
                  "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce,
                  "merge_mode": "pair_index" if getattr(ops, "_pair", None) is not None else "signature_scan",
                  "loop": getattr(ops, "loop_used", "steps")}
+        if os.environ.get("BEAST_BPE_STATS"):   # tools: distinct words that can still merge
+            stats["n_live_ge2"] = int((words["wlen"][:words["n_words"]] >= 2).sum())
         apps = getattr(ops, "last_apps", None)
         if apps is not None:
             stats["applications"] = apps.tolist()
