@@ -508,6 +508,11 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
             and ops.loop_supported(Vt)):
         # merges decided on the GPU; the host replays the log against the real strings
         try:
+            if os.environ.get("BEAST_BPE_STATS"):   # tools: word lengths before the loop
+                wl = words["wlen"][:words["n_words"]]
+                ops.wlen_start = {k: int((wl > k).sum()) for k in (8, 16, 32, 64, 128)}
+                ops.wlen_start["max"] = int(wl.max())
+                ops.wlen_start["syms_over_32"] = int(wl[wl > 32].sum())
             log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
         except _PersistentAbort:
             # workgroups were not all resident (another process on the GPU?): the launch-per-merge loop
@@ -542,6 +547,9 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
                  "loop": getattr(ops, "loop_used", "steps")}
         if os.environ.get("BEAST_BPE_STATS"):   # tools: distinct words that can still merge
             stats["n_live_ge2"] = int((words["wlen"][:words["n_words"]] >= 2).sum())
+            stats["wlen_end"] = {k: int((words["wlen"][:words["n_words"]] > k).sum()) for k in (8, 16, 32, 64, 128)}
+            stats["wlen_end"]["max"] = int(words["wlen"][:words["n_words"]].max())
+            stats["wlen_start"] = getattr(ops, "wlen_start", None)
         apps = getattr(ops, "last_apps", None)
         if apps is not None:
             stats["applications"] = apps.tolist()

@@ -15,11 +15,12 @@ def main():
     rows = bench.k5_corpus(dev, 500000, 0, 1, bench.k5_golden())
     flat, off = fixed_rows_to_device(rows)
     out = {}
-    for vs in (400, 700, 1000, 1400, 2048):
+    for vs in (2048,):
         res = train_bpe(flat, off, vs)
         st = res.stats
         out[vs] = {"merges": st["n_merges"], "words": st["n_words"], "distinct": st.get("n_distinct"),
-                   "live_words_ge2": st.get("n_live_ge2"), "loop_ms": st["merge_loop_s"] * 1e3}
+                   "live_words_ge2": st.get("n_live_ge2"), "loop_ms": st["merge_loop_s"] * 1e3,
+                   "wlen_start": st.get("wlen_start"), "wlen_end": st.get("wlen_end")}
         print(vs, out[vs], flush=True)
     print(json.dumps(out))
 
