@@ -85,6 +85,31 @@ def test_shape_validation():
     assert rc == _lib.BEAST_E_INVALID
 
 
+def test_batched_loop_validation():
+    """beast_bpe_loop_batch checks its pointers, the batch cap and the workspace size before any
+    HIP call; its workspace query is pure."""
+    lib = _lib.load()
+    fake = C.c_void_p(16)
+    nb = lib.beast_bpe_batch_workspace_bytes(2048)
+    assert nb >= 2048 * 8 and nb == lib.beast_bpe_batch_workspace_bytes(2048)
+    args = [fake, 2048, 8000, 1, 8, fake, fake, fake, fake, 100, fake, 10000, fake, fake, fake, fake, nb, 2048, 1,
+            None]
+    bad_null = list(args)
+    bad_null[12] = None                       # signatures are required by the batched loop
+    assert lib.beast_bpe_loop_batch(*bad_null) == _lib.BEAST_E_INVALID
+    bad_k = list(args)
+    bad_k[4] = 3                              # max_batch must be 2, 4 or 8
+    assert lib.beast_bpe_loop_batch(*bad_k) == _lib.BEAST_E_INVALID
+    small = list(args)
+    small[16] = nb - 256                      # workspace too small
+    assert lib.beast_bpe_loop_batch(*small) == _lib.BEAST_E_WORKSPACE
+    wide = list(args)
+    wide[1] = 8192                            # Vt beyond the batched loop's 4,096
+    assert lib.beast_bpe_loop_batch(*wide) == _lib.BEAST_E_UNSUPPORTED
+    assert lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, 4) == _lib.BEAST_E_INVALID
+    assert lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, 0) == 0
+
+
 def test_workspace_queries_are_pure():
     lib = _lib.load()
     assert lib.beast_quantile_hist_count(14, 2) == 14 * 2 * 2048 * 2
