@@ -489,9 +489,12 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         loop_reduce = no_reduce
     table = ops.count_pairs(words, Vt, len(id2str))
     loop_reduce(table, "sum")
+    # token lengths in HF's unit for max_token_length: characters of the byte-level string (every
+    # initial symbol counts 1: BpeTrainer::tokenize_words adds each char with len 1, Word::merge
+    # sums them), not UTF-8 bytes -- 'Â' (U+00C2) is one
     tlen = np.zeros(Vt, dtype=np.int64)
     for i, s in enumerate(id2str):
-        tlen[i] = len(s.encode("utf-8"))
+        tlen[i] = len(s)
     ops.new_state(Vt, tlen)
     if merge_mode is None:
         merge_mode = os.environ.get("BEAST_BPE_MERGE", "signature_scan")

@@ -442,6 +442,9 @@ __global__ __launch_bounds__(256) void k_count_pairs_lds(const uint16_t* __restr
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 __device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
 
+// Only pairs with a positive count are candidates (the table holds int32 counts in u32 cells): a
+// pair whose "+" was always blocked by max_token_length goes negative on its "-" updates, and HF
+// never queues it (BpeTrainer pushes a pair only when its count is > 0), so neither do we.
 // Incremental argmax.  ws layout (u64): [2 + parity] result slots, [4, 4+Vt) the best key of
 // each row, then u32 clean[Vt] (0 = never scanned: the zero-filled workspace starts
 // all-dirty).  Call k writes slot k & 1 and zeroes the other for call k + 1 (no memset).
@@ -592,7 +595,10 @@ struct MergeOp {
   int32_t* rowN;
   __device__ __forceinline__ void left(uint32_t p, int32_t cnt) const {     // HF: ((prev, a), -1), ((prev, new), +1)
     atomicAdd(&colA[p], -cnt);
-    if ((int)(tlen[p] + newlen) < max_len) atomicAdd(&colN[p], cnt);
+    // the left neighbour may be this merge's own new token ("a a a a" -> "n n"); its length is
+    // not in tlen until the apply
+    const uint32_t lp = p == (uint32_t)nid ? newlen : tlen[p];
+    if ((int)(lp + newlen) < max_len) atomicAdd(&colN[p], cnt);
   }
   __device__ __forceinline__ void right(uint32_t nx, int32_t cnt) const {   // HF: ((b, next), -1), ((new, next), +1)
     atomicAdd(&rowB[nx], -cnt);
@@ -1474,7 +1480,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_argmax(uint32_t* __re
             const int y = base + (k * 64 + lane) * 4 + q;
             const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
             const uint32_t cv = c[4 * k + q];
-            if (cv) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
+            if ((int32_t)cv > 0) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
           }
       }
       for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));
@@ -2021,7 +2027,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
             const uint32_t cv = c[4 * k + q];
             const int y = base + (k * 64 + lane) * 4 + q;
             const unsigned long long key =
-                cv ? ((unsigned long long)cv << 32) | (unsigned long long)(~((uint32_t)x * (uint32_t)Vt + (uint32_t)y))
+                (int32_t)cv > 0 ? ((unsigned long long)cv << 32) | (unsigned long long)(~((uint32_t)x * (uint32_t)Vt + (uint32_t)y))
                    : 0ull;
             const unsigned long long lo = umin64(key, best);
             best = umax64(key, best);
@@ -2164,7 +2170,7 @@ __global__ __launch_bounds__(PL_T) void k_bpe_loop(uint16_t* __restrict__ sym, c
           const int y = base + (k * 64 + lane) * 4 + q;
           const uint32_t idx = (uint32_t)x * (uint32_t)Vt + (uint32_t)y;
           const uint32_t cv = c[4 * k + q];
-          if (cv) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
+          if ((int32_t)cv > 0) best = umax64(best, ((unsigned long long)cv << 32) | (unsigned long long)(~idx));
         }
     }
     for (int o = 32; o > 0; o >>= 1) best = umax64(best, __shfl_xor(best, o));

@@ -93,7 +93,8 @@ class NumpyBpeOps:
                 if w[i] == a and i + 1 < len(w) and w[i + 1] == b:
                     if i > 0:
                         d[0, w[i - 1]] -= n
-                        if self.tlen[w[i - 1]] + nl < max_len:
+                        lp = nl if w[i - 1] == nid else self.tlen[w[i - 1]]   # "a a a a": the new token
+                        if lp + nl < max_len:
                             d[1, w[i - 1]] += n
                     w[i:i + 2] = [nid]
                     if i < len(w) - 1:

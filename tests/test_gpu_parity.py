@@ -775,3 +775,33 @@ def test_bpe_batched_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     assert res.stats.get("device_loop") is True and res.stats.get("loop") == loop
     assert [list(m) for m in res.merges] == ref[case]["merges"]
     assert res.vocab == ref[case]["vocab"]
+
+
+@pytest.mark.parametrize("loop", ["batch", "steps"])
+@pytest.mark.parametrize("special,max_len,min_freq", [
+    ((), 10000, 2), (("<pad>", "<eos>"), 10000, 2), ((), 3, 2), ((), 10000, 5), (("<s>",), 2, 3), ((), 4, 7)])
+def test_train_options_match_live_hf(special, max_len, min_freq, loop, gpu_device):
+    """HF's BpeTrainer options through the device loops against HF itself, live: special tokens
+    (ids first, never in words), max_token_length (the batched loop's length lookups, with new
+    tokens of the same batch as neighbours), min_frequency (a stop inside a batch)."""
+    from tokenizers import ByteLevelBPETokenizer
+    from tokenizers.trainers import BpeTrainer
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+    rng = np.random.default_rng(len(special) * 100 + max_len + min_freq)
+    base = rng.integers(0, 300, size=9)
+    arr = base[rng.integers(0, 9, size=(600, 48))]
+    arr[::7] = rng.integers(0, 300, size=(arr[::7].shape[0], 48))
+    lo, hi = int(arr.min()), int(arr.max())
+    bpe = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=1500, min_frequency=min_freq, show_progress=False, special_tokens=list(special),
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=max_len)
+    bpe._tokenizer.train_from_iterator(["".join(map(chr, r - lo)) for r in arr], trainer=tr)
+    m = json.loads(bpe._tokenizer.to_str())["model"]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    ops = GpuBpeOps(gpu_device)
+    ops._loop_kind = loop
+    res = train_bpe(flat, off, 1500, min_frequency=min_freq, special_tokens=special, max_token_length=max_len,
+                    ops=ops)
+    assert res.stats.get("loop") == loop
+    assert [list(x) for x in res.merges] == [list(x) for x in m["merges"]]
+    assert res.vocab == m["vocab"]
