@@ -90,14 +90,48 @@ __device__ __forceinline__ void burst(void* __restrict__ dst, const void* __rest
   }
 }
 
+// 16-byte output store with a cache policy SP: 0 plain (write-back L2), 1 nt, 2 sc1
+// (write-through).  A dependent kernel boundary pays for the bytes its predecessor leaves
+// dirty in L2 (MI355X_MICROARCH.md, "boundary": + B / 6 TB/s); in the latency regime (a tile or
+// two per CU, the bench's B = 4,096) write-through stores move that write-back inside the
+// kernel, under the other waves' work: encode -> reconstruct step 12.2 -> 10.5 us.  Bulk
+// launches keep write-back stores (write-through encode at B = 262,144: 227 -> 311 us).
+// BEAST_LAT_SP overrides the latency-regime policy (measurements).
+#ifndef BEAST_LAT_SP
+#define BEAST_LAT_SP 2
+#endif
+constexpr int LAT_SP = BEAST_LAT_SP;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+template <int SP>
+__device__ __forceinline__ void st16(void* p, u32x4_t v) {
+  if constexpr (SP == 1) {
+    __builtin_nontemporal_store(v, static_cast<u32x4_t*>(p));
+  } else if constexpr (SP == 2) {
+    // vector store, write-through to memory (vmcnt counts it like any store; s_nop 1 covers
+    // the store-data hazard of an inline-asm 128-bit store)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    *static_cast<u32x4_t*>(p) = v;
+  }
+}
+template <int SP>
+__device__ __forceinline__ void st16(void* p, float4 v) {
+  st16<SP>(p, u32x4_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)});
+}
+template <int SP>
+__device__ __forceinline__ void st16(void* p, long long a, long long b) {
+  st16<SP>(p, u32x4_t{(unsigned)a, (unsigned)((unsigned long long)a >> 32), (unsigned)b,
+                      (unsigned)((unsigned long long)b >> 32)});
+}
+
 // LDS -> global, float count
-template <int NT = NTHREADS>
+template <int NT = NTHREADS, int SP = 0>
 __device__ __forceinline__ void store_out(float* __restrict__ dst, const float* __restrict__ src, int count) {
   if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
     const int n4 = count >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (int i = threadIdx.x; i < n4; i += NT) d4[i] = s4[i];
+    for (int i = threadIdx.x; i < n4; i += NT) st16<SP>(d4 + i, s4[i]);
     for (int i = (n4 << 2) + threadIdx.x; i < count; i += NT) dst[i] = src[i];
   } else {
     for (int i = threadIdx.x; i < count; i += NT) dst[i] = src[i];
@@ -414,7 +448,8 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
     if (tile == blockIdx.x) STAMP(0, 4);
 
     // ---- epilogue: params (d n) and tokens (n d), both contiguous per tile
-    if (a.params_out != nullptr && (a.phases & 4)) store_out<NT>(a.params_out + b0 * DN, pb, nb * DN);
+    constexpr int SP = (S::W == 7) ? LAT_SP : 0;   // the 7-wave shape is the latency regime's
+    if (a.params_out != nullptr && (a.phases & 4)) store_out<NT, SP>(a.params_out + b0 * DN, pb, nb * DN);
     if (tile == blockIdx.x) STAMP(0, 5);
     if (quant && (a.phases & 8)) {
       // tokens in (n d) order: each thread quantises 4 consecutive tokens from the (d n)
@@ -449,9 +484,8 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
           }
-          longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
-          o2[0] = make_longlong2(beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
-          o2[1] = make_longlong2(beast::widen_bin(bin[2], off), beast::widen_bin(bin[3], off));
+          st16<SP>(tout + 4 * i, beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
+          st16<SP>(tout + 4 * i + 2, beast::widen_bin(bin[2], off), beast::widen_bin(bin[3], off));
         }
         done = n4 << 2;
       }
@@ -578,7 +612,7 @@ __device__ __forceinline__ void pipe_store(const EncArgs& a, const float* pb, co
     const int count = nb * per;
     if ((((uintptr_t)dst) & 15) == 0 && (per % 4) == 0) {
       for (int i = t; i < count / 4; i += nthr)
-        reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(pb)[i];
+        st16<LAT_SP>(reinterpret_cast<float4*>(dst) + i, reinterpret_cast<const float4*>(pb)[i]);
     } else {
       for (int i = t; i < count; i += nthr) dst[i] = pb[i];
     }
@@ -594,27 +628,27 @@ __device__ __forceinline__ void pipe_store(const EncArgs& a, const float* pb, co
   };
   int done = 0;
   if ((((uintptr_t)tout) & 15) == 0) {
-    const int n4 = total >> 2;
-    for (int i = t; i < n4; i += nthr) {
-      int bin[4], c[4], pj[4];
-      float pv[4];
-      float4 qv[4];
+    // two tokens per 16-byte store, consecutive pairs in consecutive lanes: a wave's store
+    // instruction covers one contiguous 1 KiB (whole lines for the write-through path)
+    const int n2 = total >> 1;
+    for (int i = t; i < n2; i += nthr) {
+      int bin[2], c[2], pj[2];
+      float pv[2];
+      float4 qv[2];
       bool ex = false;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) c[u] = col_of(4 * i + u, pj[u]);
+      for (int u = 0; u < 2; ++u) c[u] = col_of(2 * i + u, pj[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { pv[u] = pb[pj[u] + c[u]]; qv[u] = kq[c[u]]; }
+      for (int u = 0; u < 2; ++u) { pv[u] = pb[pj[u] + c[u]]; qv[u] = kq[c[u]]; }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin_k(pv[u], qv[u].x, qv[u].y, qv[u].z, vm1, ex);
+      for (int u = 0; u < 2; ++u) bin[u] = beast::quantize_bin_k(pv[u], qv[u].x, qv[u].y, qv[u].z, vm1, ex);
       if (ex) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
+        for (int u = 0; u < 2; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
       }
-      longlong2* o2 = reinterpret_cast<longlong2*>(tout + 4 * i);
-      o2[0] = make_longlong2(beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
-      o2[1] = make_longlong2(beast::widen_bin(bin[2], off), beast::widen_bin(bin[3], off));
+      st16<LAT_SP>(tout + 2 * i, beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
     }
-    done = n4 << 2;
+    done = n2 << 1;
   }
   for (int e = done + t; e < total; e += nthr) {
     int pj;
@@ -950,7 +984,8 @@ __device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const f
     for (int i = threadIdx.x; i < n4; i += S::W * 64) {
       const uint32_t e = 4 * i;
       const uint32_t j = div_by<S>(e, rowlen, a.fd_row);
-      reinterpret_cast<float4*>(gout)[i] = *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen));
+      st16<(S::W == 7) ? LAT_SP : 0>(reinterpret_cast<float4*>(gout) + i,
+                                     *reinterpret_cast<const float4*>(ob + j * RTR * ndo + (e - j * rowlen)));
     }
   } else {
     for (int e = threadIdx.x; e < nb * rowlen; e += S::W * 64) {

@@ -3,6 +3,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <vector>
 
 struct Args { char pad[224]; };
 
@@ -33,19 +35,28 @@ int main() {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   Args a;
   memset(&a, 0, sizeof(a));
-  const int n = 20000;
-  printf("{\"hipLaunchKernelGGL_512\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a); }, n));
-  printf("\"hipLaunchKernelGGL_1\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, s, a); }, n));
-  printf("\"hipLaunchKernelGGL_512_dynlds\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 40000, s, a); }, n));
-  void* args[] = {&a};
-  printf("\"hipLaunchKernel\": %.3f, ", host_us([&] { hipLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s); }, n));
+  const int n = 5000;
   hipFunction_t f;
   CK(hipGetFuncBySymbol(&f, (const void*)k_noop));
   size_t sz = sizeof(a);
+  void* args[] = {&a};
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  printf("\"hipModuleLaunchKernel_extra\": %.3f, ", host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, nullptr, cfg); }, n));
-  printf("\"hipModuleLaunchKernel_params\": %.3f, ", host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, args, nullptr); }, n));
-  printf("\"hipExtLaunchKernel\": %.3f, ", host_us([&] { hipExtLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s, nullptr, nullptr, 0); }, n));
+  // interleaved rounds: every entry point once per round, median over rounds
+  const char* names[] = {"hipLaunchKernelGGL_512", "hipLaunchKernel", "hipModuleLaunchKernel_extra",
+                         "hipModuleLaunchKernel_params", "hipExtLaunchKernel"};
+  std::vector<double> t[5];
+  for (int r = 0; r < 9; ++r) {
+    t[0].push_back(host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, s, a); }, n));
+    t[1].push_back(host_us([&] { hipLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s); }, n));
+    t[2].push_back(host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, nullptr, cfg); }, n));
+    t[3].push_back(host_us([&] { hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, args, nullptr); }, n));
+    t[4].push_back(host_us([&] { hipExtLaunchKernel((const void*)k_noop, dim3(512), dim3(256), args, 0, s, nullptr, nullptr, 0); }, n));
+  }
+  printf("{");
+  for (int i = 0; i < 5; ++i) {
+    std::sort(t[i].begin(), t[i].end());
+    printf("\"%s\": [%.3f, %.3f, %.3f], ", names[i], t[i][0], t[i][4], t[i][8]);
+  }
   // null stream
   printf("\"GGL_null_stream\": %.3f, ", host_us([&] { hipLaunchKernelGGL(k_noop, dim3(512), dim3(256), 0, 0, a); }, n));
   // graph of 2 kernels
