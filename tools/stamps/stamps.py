@@ -65,7 +65,8 @@ def main():
     import torch
     from beast_tokenizer_amd import BEASTBsplineTokenizer, _lib
     from beast_tokenizer_amd.synthetic import synth_trajectories
-    lib = C.CDLL(build())
+    so = os.path.join(HERE, "libbeast_stamps.so")   # built in the container (build()), travels along
+    lib = C.CDLL(so if os.path.exists(so) and not os.environ.get("STAMPS_REBUILD") else build())
     for name, (res, args) in _lib.SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
