@@ -28,6 +28,12 @@ CXXFLAGS = [
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}",
 ] + [f"-D{d}" for d in os.environ.get("BEAST_DEFINES", "").split()]
+# per-source extra flags.  codec.hip: kernel-argument preloading -- the latency-regime encode /
+# reconstruct kernels take their first DMA's operands (source rows, B, element size) as leading
+# scalar arguments, which the dispatcher then places in SGPRs, so a wave's first load does not
+# wait for a scalar load of the argument block (B = 4,096 reconstruct 5.20 -> 5.04 us, A/B in
+# profiles/r02/kernarg_preload_ab.log).  BEAST_CODEC_FLAGS replaces them (measurements).
+FILE_FLAGS = {"codec.hip": os.environ.get("BEAST_CODEC_FLAGS", "-mllvm -amdgpu-kernarg-preload-count=3").split()}
 
 
 def _hipcc() -> str:
@@ -81,6 +87,7 @@ def _fingerprint() -> str:
     import hashlib
     h = hashlib.sha256()
     h.update(" ".join(CXXFLAGS).encode())
+    h.update(repr(sorted(FILE_FLAGS.items())).encode())
     for p in _sources() + sorted(_deps()) + [__file__]:
         h.update(os.path.relpath(p, REPO).encode())
         with open(p, "rb") as f:
@@ -106,7 +113,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src):
         obj = os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
-        cmd = [hipcc, *CXXFLAGS, "-c", src, "-o", obj]
+        cmd = [hipcc, *CXXFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -676,8 +676,11 @@ __host__ __device__ constexpr PipeSmem pipe_smem() {
   return s;
 }
 
+// traj and B lead the argument list (the rest of EncArgs follows by value) so that a build with
+// kernarg preloading (-mllvm -amdgpu-kernarg-preload-count) has them in SGPRs at wave start and
+// the first DMA does not wait for a scalar load of the argument block.
 template <class S>
-__global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
+__global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(const float* __restrict__ traj, int64_t B, EncArgs a) {
   using PS = PipeShape<S>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ __attribute__((aligned(16))) float YA[PS::Y_OPS * PIPE_MT * 4];
@@ -699,15 +702,15 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(EncArgs a) {
   const bool quant = a.tokens_out != nullptr;
   const float vm1 = (float)(a.vocab - 1);
   const int64_t b0 = (int64_t)blockIdx.x * (2 * PIPE_SUB);
-  const int nbA = (int)min<int64_t>(PIPE_SUB, a.B - b0);
-  const int nbB = (int)max<int64_t>(0, min<int64_t>(PIPE_SUB, a.B - b0 - PIPE_SUB));
+  const int nbA = (int)min<int64_t>(PIPE_SUB, B - b0);
+  const int nbB = (int)max<int64_t>(0, min<int64_t>(PIPE_SUB, B - b0 - PIPE_SUB));
   constexpr int tile16 = PS::T * PS::DL / 4;   // float4 per trajectory
 
   if (mw) {
-    const float4* src = reinterpret_cast<const float4*>(a.traj);
+    const float4* src = reinterpret_cast<const float4*>(traj);
     // sources clamped to the sub-tile's own last vector (the padding re-reads a line this
     // workgroup already fetches, not the next workgroup's trajectories)
-    const int64_t last = a.B * tile16 - 1;
+    const int64_t last = B * tile16 - 1;
     dma16_fixed<PS::Y_OPS>(YA, src, b0 * tile16, min(last, (b0 + PIPE_SUB) * tile16 - 1));
     const int nk16 = ((m.nj < m.D) ? 2 : 1) * 4 * PS::Tp;
     dma16_fixed<PS::P_OPS>(P, reinterpret_cast<const float4*>(a.proj), 0, nk16 - 1);
@@ -861,6 +864,17 @@ constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divide
 constexpr int RT_REG = 4;       // row tiles (64 output rows) whose basis operands live in registers
 
 // token tile [nb][per] (int64, or fp32 normalised tokens) HBM -> LDS by DMA
+// rows [b0, b0 + tbt) of a [B][per] array of esz-byte elements HBM -> LDS by DMA
+template <int NT = NTHREADS>
+__device__ __forceinline__ void stage_rows(void* lds, const void* base, int64_t B, int esz, int64_t b0, int per,
+                                           int tbt) {
+  const int nb = (int)min<int64_t>(B - b0, tbt);
+  const char* src = static_cast<const char*>(base) + b0 * per * esz;
+  const int bytes = nb * per * esz;
+  if ((bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) dma16<NT>(lds, src, bytes >> 4);
+  else dma4<NT>(lds, src, bytes >> 2);
+}
+
 template <int NT = NTHREADS>
 __device__ __forceinline__ void stage_tokens(const RecArgs& a, void* lds, int64_t b0, int per) {
   const int nb = (int)min<int64_t>(a.B - b0, a.tbt);
@@ -995,8 +1009,11 @@ __device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const f
   }
 }
 
+// tsrc (the token rows: a.tokens, or a.ntokens with esz 4), B and esz lead the argument list for
+// kernarg preloading, as in k_encode_pipe: the first tile's DMA needs nothing else.
 template <int TBT, int KS, int RT, class S>
-__global__ __launch_bounds__(S::W * 64) void k_reconstruct(RecArgs a) {
+__global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restrict__ tsrc, int64_t B, int esz,
+                                                           RecArgs a) {
   static_assert(KS > 0, "shared-basis kernel");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NW = S::W, NT = NW * 64;
@@ -1024,7 +1041,8 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(RecArgs a) {
   BSTAMP(1, 0);
   // ---- prologue: the first token tile, the bounds and the DoF map by DMA; the basis
   //      operands (registers or LDS) by clamped loads -- all in flight together
-  if ((a.phases & 1) && blockIdx.x < a.ntiles) stage_tokens<NT>(a, smem + L.tok, (int64_t)blockIdx.x * TBT, per);
+  // the first tile (the grid never exceeds the tile count); BEAST_DEBUG_PHASES does not skip it
+  stage_rows<NT>(smem + L.tok, tsrc, B, esz, (int64_t)blockIdx.x * TBT, per, TBT);
   STAMP(1, 9);
   dma4<NT>(wlo, a.w_min, per);
   dma4<NT>(whi, a.w_max, per);
@@ -1385,7 +1403,7 @@ int launch_encode_pipe(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   a.g = make_geom<PIPE_SUB>(D, nj, N, T);
   a.ntiles = (a.B + 2 * PIPE_SUB - 1) / (2 * PIPE_SUB);
   constexpr PipeSmem L = pipe_smem<S>();
-  hipLaunchKernelGGL((k_encode_pipe<S>), dim3(a.ntiles), dim3(PIPE_W * 64), L.total, s, a);
+  hipLaunchKernelGGL((k_encode_pipe<S>), dim3(a.ntiles), dim3(PIPE_W * 64), L.total, s, a.traj, a.B, a);
   BEAST_LAUNCHED("k_encode_pipe");
   return BEAST_OK;
 }
@@ -1464,7 +1482,10 @@ int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
   if constexpr (KS == 0) hipLaunchKernelGGL((k_reconstruct_rows<TBT>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(S::W * 64), L.total, s, a);
+  else
+    hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(S::W * 64), L.total, s,
+                       a.ntokens ? static_cast<const void*>(a.ntokens) : static_cast<const void*>(a.tokens), a.B,
+                       a.ntokens ? 4 : 8, a);
   BEAST_LAUNCHED("k_reconstruct");
   return BEAST_OK;
 }
