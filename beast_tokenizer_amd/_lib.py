@@ -13,7 +13,8 @@ from typing import Optional
 import torch
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libbeast_hip.so")
+# BEAST_LIB: another build of the same library (tools/asan: the host-AddressSanitizer build)
+LIB_PATH = os.environ.get("BEAST_LIB") or os.path.join(_PKG, "libbeast_hip.so")
 
 BEAST_OK = 0
 BEAST_E_INVALID = -1
