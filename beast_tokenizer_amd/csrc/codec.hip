@@ -1398,14 +1398,32 @@ bool pipe_encode(int64_t ntiles) { return g_block_waves == 8 || (g_block_waves =
 // ... or the LDS-free one-wave-per-column-tile kernel (BEAST_OPT_BLOCK_WAVES 9 forces it)
 bool direct_encode(int64_t ntiles) { return g_block_waves == 9 || (g_block_waves == 0 && g_direct_default && wide_blocks(ntiles)); }
 
+// Host launch of a hot kernel through hipModuleLaunchKernel with a cached function handle (per
+// device): the runtime skips hipLaunchKernel's host-function lookup and the GGL template's
+// argument packing, ≈0.15 us of host time per launch (profiles/r02/launch_host_cost.json).
+template <class... Args>
+int launch_fn(const void* kernel, hipFunction_t (&cache)[16], unsigned grid, unsigned block, unsigned lds,
+              hipStream_t s, const char* what, Args... args) {
+  int dev = 0;
+  BEAST_HIP(hipGetDevice(&dev), what);
+  hipFunction_t f = (dev >= 0 && dev < 16) ? cache[dev] : nullptr;
+  if (f == nullptr) {
+    BEAST_HIP(hipGetFuncBySymbol(&f, kernel), what);
+    if (dev >= 0 && dev < 16) cache[dev] = f;
+  }
+  void* params[] = {static_cast<void*>(&args)...};
+  BEAST_HIP(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds, s, params, nullptr), what);
+  return BEAST_OK;
+}
+
 template <class S>
 int launch_encode_pipe(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   a.g = make_geom<PIPE_SUB>(D, nj, N, T);
   a.ntiles = (a.B + 2 * PIPE_SUB - 1) / (2 * PIPE_SUB);
   constexpr PipeSmem L = pipe_smem<S>();
-  hipLaunchKernelGGL((k_encode_pipe<S>), dim3(a.ntiles), dim3(PIPE_W * 64), L.total, s, a.traj, a.B, a);
-  BEAST_LAUNCHED("k_encode_pipe");
-  return BEAST_OK;
+  static hipFunction_t fn[16] = {};
+  return launch_fn(reinterpret_cast<const void*>(&k_encode_pipe<S>), fn, (unsigned)a.ntiles, PIPE_W * 64, L.total, s,
+                   "k_encode_pipe", a.traj, a.B, a);
 }
 
 template <class S>
@@ -1482,10 +1500,13 @@ int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
   BEAST_REQUIRE_CODE(L.total <= 160 * 1024, BEAST_E_UNSUPPORTED, "reconstruct tile needs %d B of LDS", L.total);
   const int64_t grid = grid_for(a.ntiles, L.total);
   if constexpr (KS == 0) hipLaunchKernelGGL((k_reconstruct_rows<TBT>), dim3(grid), dim3(NTHREADS), L.total, s, a);
-  else
-    hipLaunchKernelGGL((k_reconstruct<TBT, KS, RT, S>), dim3(grid), dim3(S::W * 64), L.total, s,
-                       a.ntokens ? static_cast<const void*>(a.ntokens) : static_cast<const void*>(a.tokens), a.B,
-                       a.ntokens ? 4 : 8, a);
+  else {
+    static hipFunction_t fn[16] = {};
+    return launch_fn(reinterpret_cast<const void*>(&k_reconstruct<TBT, KS, RT, S>), fn, (unsigned)grid, S::W * 64,
+                     L.total, s, "k_reconstruct",
+                     a.ntokens ? static_cast<const void*>(a.ntokens) : static_cast<const void*>(a.tokens), a.B,
+                     a.ntokens ? 4 : 8, a);
+  }
   BEAST_LAUNCHED("k_reconstruct");
   return BEAST_OK;
 }

@@ -11,6 +11,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -89,6 +90,35 @@ struct Plan {
     if (rc) fail(rc, "beast_reconstruct_f32");
     return py::cast(pos);
   }
+
+  // Diagnostic (tools/host_split.py): host microseconds per call of the pieces of encode, over n
+  // back-to-back calls each -- the two output allocations, the C-ABI call with preallocated
+  // outputs (validation + launch), and the whole fast-path call.
+  py::dict time_parts(const at::Tensor& x, int64_t stream, int64_t n) const {
+    using clk = std::chrono::steady_clock;
+    auto us = [&](clk::time_point t0) { return std::chrono::duration<double, std::micro>(clk::now() - t0).count() / n; };
+    const int64_t B = x.size(0), DN = D * N;
+    py::dict out;
+    auto t0 = clk::now();
+    for (int64_t i = 0; i < n; ++i) {
+      at::Tensor p = at::empty({B, DN}, x.options());
+      at::Tensor t = at::empty({B, DN}, x.options().dtype(at::kLong));
+    }
+    out["alloc2"] = us(t0);
+    at::Tensor params = at::empty({B, DN}, x.options());
+    at::Tensor tokens = at::empty({B, DN}, x.options().dtype(at::kLong));
+    t0 = clk::now();
+    for (int64_t i = 0; i < n; ++i)
+      enc(x.data_ptr<float>(), B, (int)T, x.stride(0), x.stride(1), x.stride(2), (int)x.size(2), (int)D, (int)nj,
+          reinterpret_cast<const int32_t*>(p_src), reinterpret_cast<const float*>(p_proj), (int)N,
+          reinterpret_cast<const float*>(p_wmn), reinterpret_cast<const float*>(p_wmx), (int)V, 0,
+          params.data_ptr<float>(), tokens.data_ptr<int64_t>(), reinterpret_cast<void*>(stream));
+    out["abi_call"] = us(t0);
+    t0 = clk::now();
+    for (int64_t i = 0; i < n; ++i) encode(x, 0, stream);
+    out["fast_encode_cpp"] = us(t0);
+    return out;
+  }
 };
 
 Plan make_plan(int64_t enc, int64_t rec, int64_t err, int64_t device, int64_t D, int64_t nj, int64_t N, int64_t T,
@@ -148,7 +178,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<Plan>(m, "Plan")
       .def("encode", &Plan::encode, py::arg("x"), py::arg("offset"), py::arg("stream"))
       .def("fit", &Plan::fit, py::arg("x"), py::arg("stream"))
-      .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"));
+      .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"))
+      .def("time_parts", &Plan::time_parts, py::arg("x"), py::arg("stream"), py::arg("n"));
   m.def("make_plan", &make_plan);
   m.def("rows_to_lists", &rows_to_lists, py::arg("ids"), py::arg("lens"));
 }

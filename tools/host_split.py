@@ -47,4 +47,8 @@ out = {
     "api_reconstruct": t(lambda: tok.reconstruct_traj(tokens)),
     "api_step": t(lambda: tok.reconstruct_traj(tok.encode(x)[0])),
 }
+for _ in range(2):
+    parts = p.fast.time_parts(x, s0, 4000)
+    torch.cuda.synchronize()
+out["cpp_parts"] = {k: round(v, 3) for k, v in parts.items()}
 print(json.dumps(out))
