@@ -68,7 +68,13 @@ def build_fastpath(force: bool = False, verbose: bool = False) -> str:
         return so
     from torch.utils.cpp_extension import load
     os.makedirs(FAST_DIR, exist_ok=True)
-    load(name=FAST_NAME, sources=[FAST_SRC], build_directory=FAST_DIR, extra_cflags=["-O3"], verbose=verbose)
+    import torch
+    tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    # the current-stream query (c10::hip) needs the HIP headers and libc10_hip
+    load(name=FAST_NAME, sources=[FAST_SRC], build_directory=FAST_DIR, extra_cflags=["-O3"],
+         extra_include_paths=[os.path.join(rocm, "include")],
+         extra_ldflags=[f"-L{tlib}", "-lc10_hip", f"-Wl,-rpath,{tlib}"], verbose=verbose)
     with open(stamp, "w") as f:
         f.write(digest + "\n")
     return so

@@ -89,7 +89,8 @@ class _Plan:
     bound tensors change (in-place updates of ``w_min`` / ``w_max`` keep it valid)."""
 
     __slots__ = ("dev", "idx", "version", "wmin", "wmax", "keep", "T", "min_din", "dkey", "pinned",
-                 "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec", "fast")
+                 "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec", "fast", "fast_addr",
+                 "fast_enc", "fast_rec")
 
     def __init__(self, tok: "BEASTBsplineTokenizer", dev: torch.device):
         lib = _lib.load()
@@ -109,7 +110,7 @@ class _Plan:
         self.p_wmn, self.p_wmx = wmn.data_ptr(), wmx.data_ptr()
         self.enc, self.rec = lib.beast_encode_f32, lib.beast_reconstruct_f32
         fp = _fastpath()
-        self.fast = None
+        self.fast = self.fast_addr = self.fast_enc = self.fast_rec = None
         if fp is not None and not tok._conditioned:
             import ctypes
             addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value   # noqa: E731
@@ -117,6 +118,10 @@ class _Plan:
                                      addr(lib.beast_last_error), dev.index, tok.num_dof, tok.joint_dof,
                                      tok.num_basis, self.T, tok.vocab_size, self.min_din, self.p_src, self.p_proj,
                                      self.p_wmn, self.p_wmx, self.p_phi, self.p_dst)
+            # CPython fastcall entry points (csrc/fastpath.cpp): (plan address, tensor, offset);
+            # self.fast keeps the plan they point at alive
+            self.fast_addr = self.fast.addr()
+            self.fast_enc, self.fast_rec = fp.fast_encode, fp.fast_reconstruct
 
     def cacheable(self) -> bool:
         # bounds living elsewhere were copied to the device: do not reuse the copy
@@ -591,10 +596,10 @@ class BEASTBsplineTokenizer(TokenizerBase):
         p = self._plan()
         offset = (self.llm_vocab_size - self.vocab_size
                   if respect_llm_vocab_size and self.llm_vocab_size is not None else 0)
-        if not update_bounds and p.fast is not None:
-            r = p.fast.encode(trajs, offset, torch._C._cuda_getCurrentRawStream(p.idx))
+        if not update_bounds and p.fast_enc is not None:
+            r = p.fast_enc(p.fast_addr, trajs, offset)   # (tokens, {"params": ..., conditions None})
             if r is not None:
-                return r[0], {"params": r[1], "init_pos": None, "init_vel": None, "end_pos": None, "end_vel": None}
+                return r
         if update_bounds:
             with torch.no_grad():
                 params, _ = self._fit(trajs, None, p)
@@ -736,8 +741,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
     def reconstruct_traj(self, tokens, times=None, **kwargs):
         """Positions [B, T, num_dof] from tokens (reference :498-536); kwargs: init_p [B, num_dof]."""
         p = self._plan()
-        if times is None and p.fast is not None and kwargs.get("init_p") is None:
-            r = p.fast.reconstruct(tokens, self._offset(True), torch._C._cuda_getCurrentRawStream(p.idx))
+        if times is None and p.fast_rec is not None and kwargs.get("init_p") is None:
+            r = p.fast_rec(p.fast_addr, tokens, self._offset(True))
             if r is not None:
                 return r
         tokens = self._token_rows(tokens, p.dev)

@@ -9,6 +9,8 @@
 // unusual (non-contiguous input, wrong device / dtype / shape) returns None and the caller
 // takes the general Python path, which raises the reference's exception types.
 #include <torch/extension.h>
+#include <torch/csrc/autograd/python_variable.h>
+#include <c10/hip/HIPStream.h>
 
 #include <algorithm>
 #include <chrono>
@@ -171,6 +173,105 @@ py::list rows_to_lists(const at::Tensor& ids, const at::Tensor& lens) {
   return py::reinterpret_steal<py::list>(out);
 }
 
+// The per-call entry points as CPython METH_FASTCALL functions: (plan address, tensor, offset),
+// the current stream of the plan's device taken here, the reference's return value built here
+// (encode: (tokens, params dict)).  A pybind11 method call, the Python-side stream query and
+// the dict / tuple building cost about as much host time as the C-ABI call's own validation.
+PyObject* g_keys[5] = {};   // "params", "init_pos", "init_vel", "end_pos", "end_vel"
+
+inline const Plan* plan_of(PyObject* addr) { return reinterpret_cast<const Plan*>(PyLong_AsVoidPtr(addr)); }
+
+PyObject* fast_encode(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "fast_encode(plan, x, offset)");
+    return nullptr;
+  }
+  const Plan* p = plan_of(args[0]);
+  const long long offset = PyLong_AsLongLong(args[2]);
+  if ((p == nullptr || offset == -1) && PyErr_Occurred()) return nullptr;
+  if (!THPVariable_Check(args[1])) Py_RETURN_NONE;
+  const at::Tensor& x = THPVariable_Unpack(args[1]);
+  if (!x.is_cuda() || x.get_device() != p->device || x.scalar_type() != at::kFloat || x.dim() != 3 ||
+      x.size(1) != p->T || x.size(2) < p->min_din || x.stride(2) != 1)
+    Py_RETURN_NONE;
+  at::Tensor params, tokens;
+  try {
+    const int64_t B = x.size(0), DN = p->D * p->N;
+    params = at::empty({B, DN}, x.options());
+    tokens = at::empty({B, DN}, x.options().dtype(at::kLong));
+    const hipStream_t st = c10::hip::getCurrentHIPStream(p->device).stream();
+    const int rc = p->enc(x.data_ptr<float>(), B, (int)p->T, x.stride(0), x.stride(1), x.stride(2), (int)x.size(2),
+                          (int)p->D, (int)p->nj, reinterpret_cast<const int32_t*>(p->p_src),
+                          reinterpret_cast<const float*>(p->p_proj), (int)p->N,
+                          reinterpret_cast<const float*>(p->p_wmn), reinterpret_cast<const float*>(p->p_wmx),
+                          (int)p->V, offset, params.data_ptr<float>(), tokens.data_ptr<int64_t>(),
+                          reinterpret_cast<void*>(st));
+    if (rc) p->fail(rc, "beast_encode_f32");
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+  PyObject* d = PyDict_New();
+  PyObject* po = THPVariable_Wrap(std::move(params));
+  PyObject* to = THPVariable_Wrap(std::move(tokens));
+  if (!d || !po || !to || PyDict_SetItem(d, g_keys[0], po) < 0) {
+    Py_XDECREF(d); Py_XDECREF(po); Py_XDECREF(to);
+    return nullptr;
+  }
+  Py_DECREF(po);
+  for (int i = 1; i < 5; ++i)
+    if (PyDict_SetItem(d, g_keys[i], Py_None) < 0) {
+      Py_DECREF(d); Py_DECREF(to);
+      return nullptr;
+    }
+  PyObject* r = PyTuple_New(2);
+  if (!r) { Py_DECREF(d); Py_DECREF(to); return nullptr; }
+  PyTuple_SET_ITEM(r, 0, to);
+  PyTuple_SET_ITEM(r, 1, d);
+  return r;
+}
+
+PyObject* fast_reconstruct(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "fast_reconstruct(plan, tokens, offset)");
+    return nullptr;
+  }
+  const Plan* p = plan_of(args[0]);
+  const long long offset = PyLong_AsLongLong(args[2]);
+  if ((p == nullptr || offset == -1) && PyErr_Occurred()) return nullptr;
+  if (!THPVariable_Check(args[1])) Py_RETURN_NONE;
+  const at::Tensor& tok = THPVariable_Unpack(args[1]);
+  if (!tok.is_cuda() || tok.get_device() != p->device || tok.scalar_type() != at::kLong || !tok.is_contiguous())
+    Py_RETURN_NONE;
+  const int64_t DN = p->D * p->N;
+  int64_t B;
+  if (tok.dim() == 2 && tok.size(1) == DN) B = tok.size(0);
+  else if (tok.dim() == 3 && tok.size(1) * tok.size(2) == DN) B = tok.size(0);
+  else Py_RETURN_NONE;
+  at::Tensor pos;
+  try {
+    pos = at::empty({B, p->T, p->D}, tok.options().dtype(at::kFloat));
+    const hipStream_t st = c10::hip::getCurrentHIPStream(p->device).stream();
+    const int rc = p->rec(tok.data_ptr<int64_t>(), B, (int)p->D, (int)p->nj, (int)p->N, (int)p->V, offset,
+                          reinterpret_cast<const float*>(p->p_wmn), reinterpret_cast<const float*>(p->p_wmx),
+                          reinterpret_cast<const float*>(p->p_phi), 0, (int)p->T,
+                          reinterpret_cast<const int32_t*>(p->p_dst), (int)p->D, nullptr, 0, nullptr, nullptr,
+                          pos.data_ptr<float>(), nullptr, reinterpret_cast<void*>(st));
+    if (rc) p->fail(rc, "beast_reconstruct_f32");
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+  return THPVariable_Wrap(std::move(pos));
+}
+
+PyMethodDef g_fast_defs[] = {
+    {"fast_encode", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_encode)), METH_FASTCALL,
+     "fast_encode(plan_addr, x, offset) -> (tokens, params dict) or None"},
+    {"fast_reconstruct", reinterpret_cast<PyCFunction>(reinterpret_cast<void*>(fast_reconstruct)), METH_FASTCALL,
+     "fast_reconstruct(plan_addr, tokens, offset) -> positions or None"},
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -179,7 +280,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("encode", &Plan::encode, py::arg("x"), py::arg("offset"), py::arg("stream"))
       .def("fit", &Plan::fit, py::arg("x"), py::arg("stream"))
       .def("reconstruct", &Plan::reconstruct, py::arg("tokens"), py::arg("offset"), py::arg("stream"))
-      .def("time_parts", &Plan::time_parts, py::arg("x"), py::arg("stream"), py::arg("n"));
+      .def("time_parts", &Plan::time_parts, py::arg("x"), py::arg("stream"), py::arg("n"))
+      .def("addr", [](const Plan& p) { return reinterpret_cast<intptr_t>(&p); });
   m.def("make_plan", &make_plan);
+  const char* keys[5] = {"params", "init_pos", "init_vel", "end_pos", "end_vel"};
+  for (int i = 0; i < 5; ++i) g_keys[i] = PyUnicode_InternFromString(keys[i]);   // held for the process
+  for (auto& def : g_fast_defs) {
+    PyObject* f = PyCFunction_NewEx(&def, nullptr, m.ptr());
+    if (!f) throw py::error_already_set();
+    m.add_object(def.ml_name, py::reinterpret_steal<py::object>(f));
+  }
   m.def("rows_to_lists", &rows_to_lists, py::arg("ids"), py::arg("lens"));
 }

@@ -41,8 +41,9 @@ out = {
     "raw_stream": t(lambda: raw(0)),
     "empty_tok_params": t(lambda: (torch.empty((4096, 140), dtype=torch.int64, device=dev),
                                    torch.empty((4096, 140), device=dev))),
-    "fast_encode": t(lambda: p.fast.encode(x, 0, s0)),
-    "fast_reconstruct": t(lambda: p.fast.reconstruct(tokens, 0, s0)),
+    "fast_encode": t(lambda: p.fast_enc(p.fast_addr, x, 0)),
+    "fast_reconstruct": t(lambda: p.fast_rec(p.fast_addr, tokens, 0)),
+    "pybind_encode": t(lambda: p.fast.encode(x, 0, s0)),
     "api_encode": t(lambda: tok.encode(x)),
     "api_reconstruct": t(lambda: tok.reconstruct_traj(tokens)),
     "api_step": t(lambda: tok.reconstruct_traj(tok.encode(x)[0])),
