@@ -611,7 +611,10 @@ __device__ __forceinline__ void pipe_store(const EncArgs& a, const float* pb, co
     float* dst = a.params_out + b0 * per;
     const int count = nb * per;
     if ((((uintptr_t)dst) & 15) == 0 && (per % 4) == 0) {
-      for (int i = t; i < count / 4; i += nthr)
+      // params from the highest threads, tokens (below) from the lowest: a sub-tile's 140 param
+      // vectors and 280 token pairs land on different waves instead of both on the first ones
+      // (encode 4.72 -> 4.66 us at B = 4,096, profiles/r02/encode_params_top_ab.log)
+      for (int i = nthr - 1 - t; i < count / 4; i += nthr)
         st16<LAT_SP>(reinterpret_cast<float4*>(dst) + i, reinterpret_cast<const float4*>(pb)[i]);
     } else {
       for (int i = t; i < count; i += nthr) dst[i] = pb[i];
