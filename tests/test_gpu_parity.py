@@ -232,19 +232,27 @@ def test_host_fastpath_equals_python_path(name, gpu_device):
     g = dict(load_npz(f"bspline_{name}.npz"))
     tok = make_tok(name, g, gpu_device, llm_vocab_size=32000)
     p = tok._plan()
-    assert p.fast is not None, "fast path not built / not loaded"
+    assert p.fast is not None and p.fast_enc is not None, "fast path not built / not loaded"
     x = torch.from_numpy(synth_trajectories(777, 50, CONFIGS[name]["num_dof"], seed=4, gripper_indices=gi))
     xd = x.to(gpu_device)
     t1, d1 = tok.encode(xd)
     r1 = tok.reconstruct_traj(t1)
-    fast = p.fast
-    p.fast = None
+    saved = (p.fast, p.fast_enc, p.fast_rec)
+    p.fast = p.fast_enc = p.fast_rec = None          # the Python / ctypes path
     try:
         t2, d2 = tok.encode(xd)
         r2 = tok.reconstruct_traj(t2)
     finally:
-        p.fast = fast
+        p.fast, p.fast_enc, p.fast_rec = saved
     assert torch.equal(t1, t2) and torch.equal(d1["params"], d2["params"]) and torch.equal(r1, r2)
+    assert list(d1) == list(d2) and all(d1[k] is None for k in d1 if k != "params")   # same dict as the reference
+    # the fastcall entry points run on a non-default current stream too
+    s = torch.cuda.Stream(device=gpu_device)
+    with torch.cuda.stream(s):
+        t6, _ = tok.encode(xd)
+        r6 = tok.reconstruct_traj(t6)
+    s.synchronize()
+    assert torch.equal(t6, t1) and torch.equal(r6, r1)
     # fall-through cases: host input, strided input, 3-D int32 tokens
     t3, _ = tok.encode(x)
     assert torch.equal(t3, t1)
