@@ -27,7 +27,8 @@ def build():
     objs = []
     for src in glob.glob(os.path.join(REPO, "beast_tokenizer_amd", "csrc", "*.hip")):
         o = os.path.join(HERE, os.path.basename(src) + ".o")
-        subprocess.run([_build._hipcc(), *_build.CXXFLAGS, "-DBEAST_STAMPS", "-c", src, "-o", o], check=True)
+        extra = _build.FILE_FLAGS.get(os.path.basename(src), [])
+        subprocess.run([_build._hipcc(), *_build.CXXFLAGS, *extra, "-DBEAST_STAMPS", "-c", src, "-o", o], check=True)
         objs.append(o)
     subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-o", so, *objs], check=True)
     return so
