@@ -187,22 +187,25 @@ struct EncLds {
   uint32_t* wmin;     // [Lc] this round's lowest pair per word
 };
 
-// the heap (long rows) and the round merge's arrays (rows <= 64 * RM_PER symbols) share a region
-__host__ __device__ inline size_t enc_merge_bytes(int Lc, int S) {
-  const size_t heap = al16(sizeof(uint32_t) * 3 * (size_t)S);
+// the heap (long rows, or heap mode) and the round merge's arrays (rows <= 64 * RM_PER symbols)
+// share a region; a launch that never takes the heap path sizes it for the rounds only.  The
+// per-word counts (wcnt, live in steps 2 and 5) alias the round merge's wmin (live in step 4).
+__host__ __device__ inline bool enc_needs_heap(int S, int heap_merge) { return heap_merge || S > 64 * RM_PER; }
+__host__ __device__ inline size_t enc_merge_bytes(int Lc, int S, bool heap) {
   const size_t rounds = al16(sizeof(uint32_t) * S) + al16(sizeof(uint32_t) * Lc) + 2 * al16(S);
-  return heap > rounds ? heap : rounds;
+  const size_t hp = heap ? al16(sizeof(uint32_t) * 3 * (size_t)S) : 0;
+  return hp > rounds ? hp : rounds;
 }
-__host__ __device__ inline size_t enc_row_bytes(int Lc, int S) {
-  return enc_merge_bytes(Lc, S) + al16(sizeof(int32_t) * S) + al16(sizeof(int32_t) * Lc) +
-         2 * al16(sizeof(int32_t) * (Lc + 1)) + 2 * al16(sizeof(int32_t) * Lc) + 2 * al16(sizeof(int16_t) * S) +
+__host__ __device__ inline size_t enc_row_bytes(int Lc, int S, bool heap) {
+  return enc_merge_bytes(Lc, S, heap) + al16(sizeof(int32_t) * S) + al16(sizeof(int32_t) * Lc) +
+         2 * al16(sizeof(int32_t) * (Lc + 1)) + al16(sizeof(int32_t) * Lc) + 2 * al16(sizeof(int16_t) * S) +
          al16(Lc) + 16 + al16(sizeof(int16_t) * S);
 }
 
-__device__ inline EncLds enc_carve(char* p, int Lc, int S) {
+__device__ inline EncLds enc_carve(char* p, int Lc, int S, bool heap) {
   EncLds L;
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
-  char* merge = take(enc_merge_bytes(Lc, S));   // heap, or rk | wmin | cand | dirty
+  char* merge = take(enc_merge_bytes(Lc, S, heap));   // heap, or rk | wmin | cand | dirty
   L.heap = (uint32_t*)merge;
   L.rk = (uint32_t*)merge;
   L.wmin = (uint32_t*)(merge + al16(sizeof(uint32_t) * S));
@@ -213,7 +216,7 @@ __device__ inline EncLds enc_carve(char* p, int Lc, int S) {
   L.symoff = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
   L.wcp = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
   L.wspec = (int32_t*)take(sizeof(int32_t) * Lc);
-  L.wcnt = (int32_t*)take(sizeof(int32_t) * Lc);
+  L.wcnt = (int32_t*)L.wmin;
   L.prv = (int16_t*)take(sizeof(int16_t) * S);
   L.nxt = (int16_t*)take(sizeof(int16_t) * S);
   L.cls = (uint8_t*)take(Lc);
@@ -691,7 +694,8 @@ __global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
 #ifdef BPE_STAMPS
   if (threadIdx.x == 0) atomicAdd(&g_bpe_stamps[8], __builtin_amdgcn_s_memtime() - t_stage);
 #endif
-  EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S), a.Lc, a.S);
+  const bool heap = enc_needs_heap(a.S, a.heap_merge);
+  EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S, heap), a.Lc, a.S, heap);
   for (int64_t r = (int64_t)blockIdx.x * nwv + wave; r < a.n_rows; r += (int64_t)gridDim.x * nwv) {
     if constexpr (MAP_LDS) encode_row(a, lm, L, r, lane, s_b2i, s_lut);
     else encode_row(a, a.map, L, r, lane, s_b2i, s_lut);
@@ -949,7 +953,7 @@ extern "C" int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* m
 }
 
 extern "C" size_t beast_bpe_encode_lds_bytes(int max_row_cps, int max_row_syms) {   // per row (wave)
-  return enc_row_bytes(max_row_cps, max_row_syms);
+  return enc_row_bytes(max_row_cps, max_row_syms, enc_needs_heap(max_row_syms, beast::g_bpe_encode_mode & 1));
 }
 
 extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
@@ -969,7 +973,7 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
   BEAST_REQUIRE(n_spec >= 0 && n_spec <= MAX_SPECIAL, "at most %d special tokens are supported", MAX_SPECIAL);
   BEAST_REQUIRE(n_spec == 0 || (spec_cps && spec_len && spec_id), "special-token arrays are null");
-  const size_t row_b = enc_row_bytes(max_row_cps, max_row_syms);
+  const size_t row_b = enc_row_bytes(max_row_cps, max_row_syms, enc_needs_heap(max_row_syms, beast::g_bpe_encode_mode & 1));
   BEAST_REQUIRE_CODE(row_b + STATIC_LDS <= LDS_BUDGET, BEAST_E_UNSUPPORTED,
                      "rows of %d code points / %d byte symbols need %zu B of LDS (> 160 KiB)", max_row_cps,
                      max_row_syms, row_b);
