@@ -56,15 +56,29 @@ def fastpath_so() -> str:
     return os.path.join(FAST_DIR, FAST_NAME + ".so")
 
 
+def _fastpath_digest() -> str:
+    import hashlib
+    with open(FAST_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def fastpath_current() -> bool:
+    """The in-tree fast-path library exists and was built from the current fastpath.cpp."""
+    so = fastpath_so()
+    stamp = so + ".sha256"
+    if not (os.path.exists(so) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == _fastpath_digest()
+
+
 def build_fastpath(force: bool = False, verbose: bool = False) -> str:
     """The host-side C++ fast path (csrc/fastpath.cpp, ATen only, no device code), built
     in-tree with torch.utils.cpp_extension so it travels with the repo."""
     so = fastpath_so()
-    import hashlib
-    with open(FAST_SRC, "rb") as f:
-        digest = hashlib.sha256(f.read()).hexdigest()
+    digest = _fastpath_digest()
     stamp = so + ".sha256"
-    if not force and os.path.exists(so) and os.path.exists(stamp) and open(stamp).read().strip() == digest:
+    if not force and fastpath_current():
         return so
     from torch.utils.cpp_extension import load
     os.makedirs(FAST_DIR, exist_ok=True)

@@ -25,7 +25,6 @@ ABI_VERSION = 1
 OPT_GENERIC_KERNELS = 1
 OPT_BLOCK_WAVES = 2
 OPT_MERGE_LDS_MIN = 3
-OPT_MERGE_LIST_RATIO = 4
 OPT_BPE_ENCODE_MODE = 5
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
@@ -49,9 +48,10 @@ SIGNATURES = {
     "beast_quantile_prepare": (_i32, [_vp, _i64, _i32, _i64, _i64, _i32, _vp, _vp, _sz, _vp]),
     "beast_quantile_prepare_segments": (_i32, [_vp, _i32, _i64, _i64, _i32, _i64, _i32, _vp, _vp, _sz, _vp]),
     "beast_quantile_hist_ptr": (_vp, [_vp, _i32, _i32]),
-    "beast_quantile_hist_count": (_i64, [_i32, _i32]),
-    "beast_quantile_hist": (_i32, [_i32, _i64, _i32, _i32, _vp, _vp]),
-    "beast_quantile_select": (_i32, [_i32, _i32, _i32, _vp, _vp]),
+    "beast_quantile_passes": (_i32, [_i32]),
+    "beast_quantile_hist_count": (_i64, [_i32, _i32, _i32, _i32]),
+    "beast_quantile_hist": (_i32, [_i32, _i64, _i32, _i32, _i32, _vp, _vp]),
+    "beast_quantile_select": (_i32, [_i32, _i32, _i32, _i32, _vp, _vp]),
     "beast_quantile_finalize": (_i32, [_i32, _i32, _vp, _vp, _vp]),
     "beast_quantile_f32": (_i32, [_vp, _i64, _i32, _i64, _i32, _vp, _vp, _vp, _sz, _vp]),
     "beast_i64_minmax": (_i32, [_vp, _i64, _vp, _vp]),
@@ -61,30 +61,18 @@ SIGNATURES = {
     "beast_exclusive_scan_i64": (_i32, [_vp, _vp, _i64, _vp, _vp]),
     "beast_bpe_pretok_emit": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_count_pairs": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp]),
+    "beast_bpe_word_signatures": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "beast_bpe_argmax_workspace_bytes": (_sz, [_i32]),
     "beast_bpe_argmax": (_i32, [_vp, _i32, _i32, _vp, _i32, _vp]),
-    "beast_bpe_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _i64,
-                               _vp]),
-    "beast_bpe_index_workspace_bytes": (_sz, [_i32, _i64]),
-    "beast_bpe_build_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp, _sz, _vp]),
-    "beast_bpe_word_signatures": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
-    "beast_bpe_apply_argmax": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i32, _vp]),
+    "beast_bpe_merge": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _i64, _vp]),
+    "beast_bpe_apply_argmax": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp]),
     "beast_bpe_loop_workspace_bytes": (_sz, [_i32, _i32]),
-    "beast_bpe_loop_init": (_i32, [_vp, _sz, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
-    "beast_bpe_loop_steps": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp,
-                                    _vp, _i32, _vp]),
-    "beast_bpe_loop_persistent_bytes": (_sz, []),
-    "beast_bpe_loop_persistent": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
-                                         _vp, _i32, _vp, _sz, _vp]),
+    "beast_bpe_loop_init": (_i32, [_vp, _sz, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp]),
     "beast_bpe_loop_state": (_i32, [_vp, _i32, _i32, _vp, _vp]),
     "beast_bpe_batch_workspace_bytes": (_sz, [_i32]),
-    "beast_bpe_loop_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp,
-                                    _vp, _sz, _i32, _i32, _vp]),
-    "beast_bpe_pair_index_bytes": (_sz, [_i32, _i64]),
-    "beast_bpe_build_pair_index": (_i32, [_vp, _vp, _vp, _i64, _i32, _i64, _vp, _sz, _vp]),
-    "beast_bpe_token_index_init": (_i32, [_vp, _sz, _i32, _vp]),
-    "beast_bpe_loop_steps_ix": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32,
-                                       _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "beast_bpe_batch_delta_count": (_sz, [_i32]),
+    "beast_bpe_loop_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
+                                    _vp, _vp, _sz, _i32, _vp, _vp, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),

@@ -22,8 +22,10 @@ Deliberate divergences:
   train/eval.py:34) is accepted.
 * ``reconstruct_traj_continuous`` implements the intent of ``denormalize_tensor``
   (beast/utils.py:42 raises TypeError in the reference).
-* ``init_cond_order`` / ``end_cond_order`` != 0 raise NotImplementedError
-  (BEAST's default is 0).
+* ``init_cond_order`` / ``end_cond_order`` != 0 run the same fit kernel with the
+  conditioned projection (``bspline.DeviceBasis``).  As the
+  reference's MP object does, the last fit's boundary conditions are kept and reused
+  by ``reconstruct_traj``.
 """
 from __future__ import annotations
 
@@ -66,19 +68,21 @@ _FAST = None
 
 
 def _fastpath():
-    """The in-tree C++ host fast path (csrc/fastpath.cpp) if it was built, else None."""
+    """The in-tree C++ host fast path (csrc/fastpath.cpp) if it was built from the current source
+    (its .sha256 stamp matches), else None: a library built from an older fastpath.cpp may lack
+    entry points the plan uses, so it is never loaded."""
     global _FAST
     if _FAST is None:
-        import importlib.util
-        import os
-        from . import _build
-        so = _build.fastpath_so()
         _FAST = False
-        if os.path.exists(so):
+        from . import _build
+        if _build.fastpath_current():
+            import importlib.util
+            so = _build.fastpath_so()
             spec = importlib.util.spec_from_file_location(_build.FAST_NAME, so)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
-            _FAST = mod
+            if all(hasattr(mod, f) for f in ("make_plan", "fast_encode", "fast_reconstruct")):
+                _FAST = mod
     return _FAST or None
 
 

@@ -26,10 +26,12 @@ corpus.  Data-parallel training therefore has two forms:
   own shard, the distinct words x counts are all-gathered once (a word repeated
   across shards simply appears once per shard with its shard count -- pair counts
   and merges are unchanged), and every rank runs the single-GPU device-driven loop
-  on the union with no per-merge collective.  The loop is latency-bound (tens of
-  microseconds per merge), so one gather beats a collective per merge;
-* **per-merge all-reduce**: the initial pair table is all-reduced once and the
-  four per-merge delta vectors ``[4][Vt]`` every merge.
+  on the union with no per-pass collective.  The loop is latency-bound (tens of
+  microseconds per pass), so one gather beats a collective per pass;
+* **sharded** (``replicate=False``): every rank keeps its shard of the words; the
+  setup pair table is all-reduced once and, per pass of the batched device loop,
+  the pair-count changes ``[8][4][Vt]`` between its merge and apply launches (the
+  host-driven loop: ``[4][Vt]`` per merge).
 
 Either way every rank holds the same table and takes the same decisions.
 """
@@ -85,10 +87,6 @@ class BPEResult:
     min_token: int
     max_token: int
     stats: Dict[str, float] = field(default_factory=dict)
-
-
-class _PersistentAbort(RuntimeError):
-    """The persistent merge loop's grid barrier timed out (workgroups not co-resident)."""
 
 
 class GpuBpeOps:
@@ -205,9 +203,7 @@ class GpuBpeOps:
         return self._repack(dict(words, n_syms=off), sym, ow, ol, oc, int(ow.numel()), off)
 
     def compact(self, words):
-        """Drop words with < 2 symbols left (they can no longer merge).  Word indices change,
-        so the inverted index is dropped (merges then visit every word)."""
-        self._index = None
+        """Drop words with < 2 symbols left (they can no longer merge)."""
         n = words["n_words"]
         if n == 0:
             return words
@@ -233,33 +229,6 @@ class GpuBpeOps:
                  n_sym or Vt, self.stream)
         return table
 
-    def build_index(self, words, Vt: int):
-        """Inverted symbol -> word index with room for the merges' appends."""
-        cap = int(words.get("n_syms_distinct", words["n_syms"])) + Vt + 2 * int(words["n_words"]) + 1024
-        nb = _lib.load().beast_bpe_index_workspace_bytes(Vt, cap)
-        self._index = torch.empty((nb + 3) // 4, dtype=torch.int32, device=self.device)
-        _lib.run("beast_bpe_build_index", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
-                 words["n_words"], Vt, self._index.data_ptr(), nb, self.stream)
-
-    def build_pair_index(self, words, n_sym: int, Vt: int):
-        """Candidate lists for the device loop (csrc/bpe.hip PairIndex): the CSR of distinct words
-        per setup-symbol pair and an empty token index for the merged tokens' word lists."""
-        lib = _lib.load()
-        n, ns = int(words["n_words"]), int(words.get("n_syms_distinct", words["n_syms"]))
-        if n_sym < 1 or n_sym > 4096 or 4 * Vt * 4 > 64 * 1024:
-            self._pair = None
-            return
-        nb = lib.beast_bpe_pair_index_bytes(n_sym, ns)
-        self._pair = torch.empty(nb, dtype=torch.uint8, device=self.device)
-        _lib.run("beast_bpe_build_pair_index", words["sym"].data_ptr(), words["wstart"].data_ptr(),
-                 words["wlen"].data_ptr(), n, n_sym, ns, self._pair.data_ptr(), nb, self.stream)
-        self._pair_nsym = n_sym
-        cap = max(24 * n, 1 << 21)      # in u32: 8-byte entries, ~2 per rewritten word
-        tb = lib.beast_bpe_index_workspace_bytes(Vt, cap)
-        self._tokix = torch.empty((tb + 3) // 4, dtype=torch.int32, device=self.device)
-        _lib.run("beast_bpe_token_index_init", self._tokix.data_ptr(), tb, Vt, self.stream)
-        self._claim = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
-
     def new_state(self, Vt: int, tlen: np.ndarray):
         nb = _lib.load().beast_bpe_argmax_workspace_bytes(Vt)
         self._argws = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=self.device)
@@ -267,6 +236,7 @@ class GpuBpeOps:
         self._deltas = torch.zeros(4 * Vt, dtype=torch.int32, device=self.device)
         self._tlen = torch.from_numpy(tlen.astype(np.int32)).to(self.device)
 
+    # -- host-driven loop (one merge per call; csrc/bpe_loop.hip k_merge + k_apply_argmax)
     def argmax(self, table: torch.Tensor, Vt: int, vcur: int) -> int:
         k = self._calls
         self._calls += 1
@@ -279,28 +249,39 @@ class GpuBpeOps:
         k = self._calls
         self._calls += 1
         _lib.run("beast_bpe_apply_argmax", table.data_ptr(), deltas.data_ptr(), Vt, vcur, a, b, nid,
-                 self._tlen.data_ptr(), _lib.ptr(getattr(self, "_index", None)), int(reused),
-                 self._argws.data_ptr(), k, self.stream)
+                 self._tlen.data_ptr(), self._argws.data_ptr(), k, self.stream)
         return self._read_i64(self._argws[2 + (k & 1):], 1)[0] & 0xFFFFFFFFFFFFFFFF
 
-    # -- device-driven merge loop (csrc/bpe.hip k_loop_step): no host round trip per merge
+    def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int, count: int = 1 << 62) -> torch.Tensor:
+        _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                 _lib.ptr(words.get("wcount")), words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len,
+                 self._deltas.data_ptr(), Vt, words["sig"].data_ptr(), int(count), self.stream)
+        return self._deltas
+
+    # -- device-driven batched loop (csrc/bpe_loop.hip k_merge_batch + k_apply_batch)
     LOOP_P = 0x9E3779B97F4A7C15   # odd multiplier of the token-string hash
+    # int32 words of the loop state (csrc/bpe_loop.hip LoopState)
+    ST_ACTIVE, ST_VCUR, ST_NMERGES, ST_PASSES = 0, 1, 2, 9
+    BATCH_INIT, BATCH_NO_MERGE, BATCH_NO_APPLY = 1, 2, 4
 
     def loop_kind(self) -> str:
-        """'batch' (the default: two launches per pass of up to 8 exact merges, csrc/bpe.hip
-        k_merge_batch; 'batch2' / 'batch4' cap a pass at 2 / 4), 'steps' (two launches per merge)
-        or 'persistent' (one launch for the whole loop, csrc/bpe.hip k_bpe_loop); BEAST_BPE_LOOP
-        overrides.  At K5: batch 36.6 ms, steps 58 ms."""
-        return os.environ.get("BEAST_BPE_LOOP", getattr(self, "_loop_kind", "batch"))
+        """'batch' (up to 8 exact merges per pass; 'batch2' / 'batch4' cap a pass at 2 / 4).  An
+        explicit ``_loop_kind`` wins over the BEAST_BPE_LOOP environment variable."""
+        kind = getattr(self, "_loop_kind", None) or os.environ.get("BEAST_BPE_LOOP", "batch")
+        if kind not in ("batch", "batch2", "batch4", "batch8"):
+            raise ValueError(f"unknown BPE loop kind {kind!r}")
+        return kind
 
     def loop_supported(self, Vt: int) -> bool:
-        return 4 * Vt * 4 <= 64 * 1024
+        return Vt <= 4096
 
     def loop_run(self, words, table, Vt: int, id2str, vocab_size: int, min_frequency: int, max_len: int,
-                 chunk: int = 64):
-        """Run the merge loop on the device from the current argmax; returns the merge log
-        [(a, b, nid, reused)] for the host to replay and verify."""
+                 reduce: Optional[Reducer] = None, chunk: int = 64, count_applications: bool = False):
+        """Run the merge loop on the device; returns the merge log [(a, b, nid, reused)] for the host
+        to replay and verify, and whether the log filled up.  ``reduce`` (sharded words): each pass's
+        pair-count changes are all-reduced between its merge and apply launches."""
         lib = _lib.load()
+        dev, s = self.device, self.stream
         n_tok = len(id2str)
         max_merges = 4 * max(vocab_size - n_tok, 0) + 1024
         P, M = self.LOOP_P, (1 << 64) - 1
@@ -311,107 +292,69 @@ class GpuBpeOps:
                 h = (h * P + byte) & M
                 pw = (pw * P) & M
             h0[i], p0[i] = h, pw
-        hp = torch.from_numpy(np.stack([h0, p0]).view(np.int64)).to(self.device)
+        hp = torch.from_numpy(np.stack([h0, p0]).view(np.int64)).to(dev)
+        max_tlen = int(max((len(t) for t in id2str), default=0))
         nb = lib.beast_bpe_loop_workspace_bytes(Vt, max_merges)
-        ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
-        parity = (self._calls - 1) & 1          # slot of the argmax that produced `key`
-        _lib.run("beast_bpe_loop_init", ws.data_ptr(), nb, Vt, max_merges, n_tok, vocab_size, min_frequency, parity,
-                 hp[0].data_ptr(), hp[1].data_ptr(), self._tlen.data_ptr(), self.stream)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        _lib.run("beast_bpe_loop_init", ws.data_ptr(), nb, Vt, max_merges, n_tok, vocab_size, min_frequency,
+                 hp[0].data_ptr(), hp[1].data_ptr(), self._tlen.data_ptr(), max_tlen, s)
         import ctypes
         st_p, log_p = ctypes.c_void_p(), ctypes.c_void_p()
         _lib.run("beast_bpe_loop_state", ws.data_ptr(), Vt, max_merges, ctypes.byref(st_p), ctypes.byref(log_p))
         st_off, log_off = st_p.value - ws.data_ptr(), log_p.value - ws.data_ptr()
-        state = ws[st_off:st_off + 32].view(torch.int32)     # active, a, b, nid, reused, vcur, parity, n
-        host = torch.empty(8, dtype=torch.int32, pin_memory=True)
-        vcur = n_tok
-        launched = False
-        if self.loop_kind() == "persistent" and getattr(self, "_pair", None) is None:
-            bb = lib.beast_bpe_loop_persistent_bytes()
-            bar = torch.empty(bb, dtype=torch.uint8, device=self.device)
-            try:
-                _lib.run("beast_bpe_loop_persistent", ws.data_ptr(), Vt, max_merges, max(vocab_size - n_tok, 0),
-                         words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
-                         _lib.ptr(words.get("wcount")), words["n_words"], self._tlen.data_ptr(), max_len,
-                         self._deltas.data_ptr(), _lib.ptr(words.get("sig")), table.data_ptr(),
-                         self._argws.data_ptr(), vocab_size, bar.data_ptr(), bb, self.stream)
-                launched = True
-            except NotImplementedError:     # too few CUs for the table rows: two launches per merge
-                pass
-        if launched:
-            self.loop_used = "persistent"
-            host.copy_(state, non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-            flag = bar[36:40].view(torch.int32).cpu()
-            if int(flag[0]):
-                raise _PersistentAbort("a grid barrier of the persistent merge loop timed out")
-            n = int(host[7])
-            log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
-            self.last_apps = None
-            return [tuple(int(v) for v in r) for r in log], n >= max_merges
-        pair = getattr(self, "_pair", None)
+        state = ws[st_off:st_off + 64].view(torch.int32)
+        host = torch.empty(16, dtype=torch.int32, pin_memory=True)
         kind = self.loop_kind()
-        if kind.startswith("batch") and pair is None and Vt <= 4096 and words.get("sig") is not None:
-            # several merges per pass (csrc/bpe.hip k_merge_batch): "batch" = up to 8, "batchK" = up to K
-            kmax = int(kind[5:] or 8)
-            self.loop_used = kind
-            bb = lib.beast_bpe_batch_workspace_bytes(Vt)
-            bws = torch.empty(bb, dtype=torch.uint8, device=self.device)
-            init = 1
+        kmax = int(kind[5:] or 8)
+        self.loop_used = kind
+        bb = lib.beast_bpe_batch_workspace_bytes(Vt)
+        bws = torch.empty(bb, dtype=torch.uint8, device=dev)
+        deltas = None
+        if reduce is not None:
+            deltas = torch.zeros(lib.beast_bpe_batch_delta_count(Vt), dtype=torch.int32, device=dev)
+        apps = torch.zeros(max_merges, dtype=torch.int32, device=dev) if count_applications else None
+
+        def run(n_steps, flags):
+            _lib.run("beast_bpe_loop_batch", ws.data_ptr(), Vt, max_merges, n_steps, kmax, flags,
+                     words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
+                     _lib.ptr(words.get("wcount")), words["n_words"], self._tlen.data_ptr(), max_len,
+                     words["sig"].data_ptr(), table.data_ptr(), self._argws.data_ptr(), bws.data_ptr(), bb,
+                     vocab_size, _lib.ptr(deltas), _lib.ptr(apps), s)
+
+        vcur = n_tok
+        if deltas is None:
+            flags = self.BATCH_INIT
             while True:
-                # a pass takes >= 1 merge; ~2.7 on average at K5, so half the remaining merges
+                # a pass takes >= 1 merge; ~3.3 on average at K5, so half the remaining merges
                 # bounds the passes left without many no-op launches past the end
                 steps = max(1, min(chunk, (vocab_size - vcur + 1) // 2))
-                _lib.run("beast_bpe_loop_batch", ws.data_ptr(), Vt, max_merges, steps, kmax, words["sym"].data_ptr(),
-                         words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
-                         words["n_words"], self._tlen.data_ptr(), max_len, _lib.ptr(words.get("sig")),
-                         table.data_ptr(), self._argws.data_ptr(), bws.data_ptr(), bb, vocab_size, init, self.stream)
-                init = 0
-                host.copy_(state, non_blocking=True)
-                torch.cuda.current_stream(self.device).synchronize()
-                active, vcur, n = int(host[0]), int(host[5]), int(host[7])
+                run(steps, flags)
+                flags = 0
+                host.copy_(state[:16], non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                active, vcur = int(host[self.ST_ACTIVE]), int(host[self.ST_VCUR])
                 if not active or vcur >= vocab_size:
                     break
-            self.last_apps = None
-            log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
-            return [tuple(int(v) for v in r) for r in log], n >= max_merges
-        self.loop_used = "steps"
-        apps = torch.zeros(2 * max_merges, dtype=torch.int32, device=self.device) if pair is not None else None
-        while True:
-            steps = max(1, min(chunk, vocab_size - vcur))
-            if pair is not None:
-                _lib.run("beast_bpe_loop_steps_ix", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
-                         words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
-                         words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
-                         pair.data_ptr(), self._pair_nsym, self._tokix.data_ptr(), self._claim.data_ptr(),
-                         _lib.ptr(words.get("sig")),
-                         table.data_ptr(),
-                         self._argws.data_ptr(), vocab_size, apps.data_ptr(), self.stream)
-            else:
-                _lib.run("beast_bpe_loop_steps", ws.data_ptr(), Vt, max_merges, steps, words["sym"].data_ptr(),
-                         words["wstart"].data_ptr(), words["wlen"].data_ptr(), _lib.ptr(words.get("wcount")),
-                         words["n_words"], self._tlen.data_ptr(), max_len, self._deltas.data_ptr(),
-                         _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)), table.data_ptr(),
-                         self._argws.data_ptr(), vocab_size, self.stream)
-            host.copy_(state, non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-            active, vcur, n = int(host[0]), int(host[5]), int(host[7])
-            if not active or vcur >= vocab_size:
-                break
-        full = n >= max_merges
-        self.last_apps = None
-        if apps is not None:
-            a = apps.cpu().numpy().astype(np.int64)
-            self.last_apps = a[:n]
-            self.last_visits = a[max_merges:max_merges + n]
+        else:
+            # sharded: every rank holds the same table and takes the same decisions, so every rank
+            # runs the same number of passes (and collectives)
+            run(0, self.BATCH_INIT)
+            while True:
+                steps = max(1, min(chunk, (vocab_size - vcur + 1) // 2))
+                for _ in range(steps):
+                    run(1, self.BATCH_NO_APPLY)
+                    reduce(deltas, "sum")
+                    run(1, self.BATCH_NO_MERGE)
+                host.copy_(state[:16], non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                active, vcur = int(host[self.ST_ACTIVE]), int(host[self.ST_VCUR])
+                if not active or vcur >= vocab_size:
+                    break
+        n = int(host[self.ST_NMERGES])
+        self.loop_passes = int(host[self.ST_PASSES])
+        self.last_apps = apps[:n].cpu().numpy().astype(np.int64) if apps is not None else None
         log = ws[log_off:log_off + 16 * n].view(torch.int32).reshape(n, 4).cpu().numpy() if n else np.zeros((0, 4))
-        return [tuple(int(v) for v in r) for r in log], full
-
-    def merge(self, words, a: int, b: int, nid: int, max_len: int, Vt: int, count: int = 1 << 62) -> torch.Tensor:
-        _lib.run("beast_bpe_merge", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
-                 _lib.ptr(words.get("wcount")), words["n_words"], a, b, nid, self._tlen.data_ptr(), max_len,
-                 self._deltas.data_ptr(), Vt, _lib.ptr(words.get("sig")), _lib.ptr(getattr(self, "_index", None)),
-                 int(count), self.stream)
-        return self._deltas
+        return [tuple(int(v) for v in r) for r in log], n >= max_merges
 
 
 def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special_tokens: Sequence[str]):
@@ -440,15 +383,17 @@ def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special
 def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
               special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
               initial_alphabet: Optional[Sequence[str]] = None, ops=None, reduce: Reducer = no_reduce,
-              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, use_index: bool = False,
-              device_loop: bool = True, replicate: bool = True, merge_mode: Optional[str] = None) -> BPEResult:
+              mn_mx: Optional[Tuple[int, int]] = None, compact_every: int = 0, device_loop: bool = True,
+              replicate: bool = True, count_applications: bool = False) -> BPEResult:
     """Train on int64 token sequences ``tokens[seq_off[s]:seq_off[s+1]]`` (this rank's shard).
 
-    Single process on the GPU ops: the merge loop runs device-driven (``GpuBpeOps.loop_run``,
-    no host round trip per merge).  Multi-rank with ``replicate`` (and a ``reduce.gather``):
-    the shards' distinct words are all-gathered after dedup and every rank runs that same
-    loop on the union.  Otherwise multi-rank is the host-driven loop below with a per-merge
-    delta all-reduce (also the CPU model's loop)."""
+    On the GPU ops the merge loop runs device-driven and batched (``GpuBpeOps.loop_run``: no
+    host round trip per merge).  Multi-rank with ``replicate`` (and a ``reduce.gather``): the
+    shards' distinct words are all-gathered after dedup and every rank runs that loop on the
+    union.  Multi-rank without it (sharded): every rank keeps its shard, the setup pair table is
+    all-reduced once and each pass's pair-count changes are all-reduced between its merge and
+    apply launches.  The host-driven loop below (one merge per call, per-merge all-reduce) runs
+    the CPU model, vocabularies above 4096, ``compact_every`` and the hash-collision fallback."""
     import time
     t0 = time.perf_counter()
     if ops is None:
@@ -496,35 +441,17 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     for i, s in enumerate(id2str):
         tlen[i] = len(s)
     ops.new_state(Vt, tlen)
-    if merge_mode is None:
-        merge_mode = os.environ.get("BEAST_BPE_MERGE", "signature_scan")
-    if use_index and hasattr(ops, "build_index"):
-        ops.build_index(words, Vt)
-    elif (merge_mode == "pair_index" and device_loop and loop_reduce is no_reduce and not compact_every
-          and hasattr(ops, "build_pair_index")):
-        ops.build_pair_index(words, len(id2str), Vt)   # candidate lists instead of signature scans
     max_len = int(max_token_length) if max_token_length is not None else 2 ** 31 - 1
     merges: List[Tuple[str, str]] = []
     t1 = time.perf_counter()
-    key = ops.argmax(table, Vt, len(id2str))
-    if (device_loop and loop_reduce is no_reduce and not compact_every and hasattr(ops, "loop_supported")
-            and ops.loop_supported(Vt)):
+    sharded = loop_reduce is not no_reduce
+    base_stats = {"n_words": n_words, "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words),
+                  "n_syms_distinct": words.get("n_syms_distinct"), "Vt": Vt, "replicated": loop_reduce is not reduce,
+                  "sharded": sharded}
+    if (device_loop and not compact_every and hasattr(ops, "loop_supported") and ops.loop_supported(Vt)):
         # merges decided on the GPU; the host replays the log against the real strings
-        try:
-            if os.environ.get("BEAST_BPE_STATS"):   # tools: word lengths before the loop
-                wl = words["wlen"][:words["n_words"]]
-                ops.wlen_start = {k: int((wl > k).sum()) for k in (8, 16, 32, 64, 128)}
-                ops.wlen_start["max"] = int(wl.max())
-                ops.wlen_start["syms_over_32"] = int(wl[wl > 32].sum())
-            log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len)
-        except _PersistentAbort:
-            # workgroups were not all resident (another process on the GPU?): the launch-per-merge loop
-            ops2 = type(ops)(ops.device)
-            ops2._loop_kind = "steps"
-            return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
-                             max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=ops2,
-                             reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, use_index=use_index,
-                             device_loop=device_loop, replicate=replicate, merge_mode=merge_mode)
+        log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len,
+                                 reduce=loop_reduce if sharded else None, count_applications=count_applications)
         for a, b, nid, reused in log:
             new_tok = id2str[a] + id2str[b]
             have = str2id.get(new_tok)
@@ -539,25 +466,16 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         if full:
             return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
                              max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=None,
-                             reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, use_index=use_index,
-                             device_loop=False, replicate=replicate)
+                             reduce=reduce, mn_mx=mn_mx, compact_every=compact_every, device_loop=False,
+                             replicate=replicate)
         t2 = time.perf_counter()
-        stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
-                 "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
-                 "n_syms_distinct": words.get("n_syms_distinct"),
-                 "Vt": Vt, "device_loop": True, "replicated": loop_reduce is not reduce,
-                 "merge_mode": "pair_index" if getattr(ops, "_pair", None) is not None else "signature_scan",
-                 "loop": getattr(ops, "loop_used", "steps")}
-        if os.environ.get("BEAST_BPE_STATS"):   # tools: distinct words that can still merge
-            stats["n_live_ge2"] = int((words["wlen"][:words["n_words"]] >= 2).sum())
-            stats["wlen_end"] = {k: int((words["wlen"][:words["n_words"]] > k).sum()) for k in (8, 16, 32, 64, 128)}
-            stats["wlen_end"]["max"] = int(words["wlen"][:words["n_words"]].max())
-            stats["wlen_start"] = getattr(ops, "wlen_start", None)
+        stats = dict(base_stats, setup_s=t1 - t0, merge_loop_s=t2 - t1, n_merges=len(merges), device_loop=True,
+                     loop=ops.loop_used, passes=getattr(ops, "loop_passes", None), n_live_end=words["n_words"])
         apps = getattr(ops, "last_apps", None)
         if apps is not None:
             stats["applications"] = apps.tolist()
-            stats["words_visited"] = ops.last_visits.tolist()
         return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
+    key = ops.argmax(table, Vt, len(id2str))
     while len(id2str) < vocab_size:
         count = key >> 32
         if count < 1 or count < min_frequency:
@@ -581,10 +499,8 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         if compact_every and len(merges) % compact_every == 0 and hasattr(ops, "compact"):
             words = ops.compact(words)
     t2 = time.perf_counter()
-    stats = {"setup_s": t1 - t0, "merge_loop_s": t2 - t1, "n_merges": len(merges), "n_words": n_words,
-             "n_syms": n_syms, "n_distinct": words.get("n_distinct", n_words), "n_live_end": words["n_words"],
-                 "n_syms_distinct": words.get("n_syms_distinct"),
-             "Vt": Vt, "replicated": loop_reduce is not reduce}
+    stats = dict(base_stats, setup_s=t1 - t0, merge_loop_s=t2 - t1, n_merges=len(merges), device_loop=False,
+                 loop="host", n_live_end=words["n_words"])
     return BPEResult(vocab=dict(str2id), merges=merges, min_token=int(mn), max_token=int(mx), stats=stats)
 
 

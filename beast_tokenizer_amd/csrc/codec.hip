@@ -18,6 +18,8 @@
 // [16*RT][Np], W to [Np]) so the loops are branch-free.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -761,90 +763,6 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(const float* __rest
   BSTAMP(0, 1);
 }
 
-// Encode in the latency regime without LDS (the bench's B = 4,096): one wave per MFMA column tile
-// of an 8-trajectory tile (16 (trajectory, DoF) columns of one basis kind), every operand loaded
-// straight into registers -- the DoF map by scalar loads, then the K-steps' trajectory values
-// and projection rows and the lane's quantiser bounds, all in flight together -- then k_encode's
-// MFMA chain (even / odd K-steps, the same f32 order), and each lane quantises its own four
-// accumulators and stores params (d n) and tokens (n d) itself.  No barrier, no LDS round trip;
-// bit-identical to k_encode / k_encode_pipe.
-constexpr int DIR_TB = 8;
-template <class S>
-struct DirShape {
-  static constexpr int NQ = (DIR_TB * S::NJ + 15) / 16 + (DIR_TB * (S::D - S::NJ) + 15) / 16;   // waves
-};
-
-template <class S>
-__global__ __launch_bounds__(64 * DirShape<S>::NQ) void k_encode_direct(EncArgs a) {
-  static_assert(S::fixed && S::T > 0 && S::DL > 0, "direct encode: fixed shape");
-  constexpr int T = S::T, DL = S::DL, D = S::D, N = S::N, NST = (S::T + 3) / 4, Tp = 4 * NST;
-  constexpr int per = D * N;
-  const Geom& g = a.g;
-  const Dims<S> m(g);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int64_t b0 = (int64_t)blockIdx.x * DIR_TB;
-  const int nb = (int)min<int64_t>(DIR_TB, a.B - b0);
-  int j, d, kind;
-  bool ok;
-  tile_col<DIR_TB>(g, m, wave, lr, j, d, kind, ok);
-  ok = ok && j < nb;
-  const int jj = min(j, nb - 1);
-  // the DoF map through the scalar cache (uniform addresses), selected per lane
-  const __attribute__((address_space(4))) int32_t* dmap = (const __attribute__((address_space(4))) int32_t*)a.dof_src;
-  int c = 0;
-#pragma unroll
-  for (int i = 0; i < D; ++i) c = (d == i) ? dmap[i] : c;
-  c = min(max(c, 0), DL - 1);
-  const float* yc = a.traj + (b0 + jj) * (int64_t)(T * DL) + c;
-  const float* pa = a.proj + (kind * 16 + lr) * Tp + lk;
-  float xa[NST], ya[NST];
-#pragma unroll
-  for (int st = 0; st < NST; ++st) {
-    xa[st] = pa[4 * st];
-    ya[st] = yc[min(4 * st + lk, T - 1) * DL];
-  }
-  const bool quant = a.tokens_out != nullptr;
-  float lo[4], hi[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k = d * N + min(lk * 4 + r, N - 1);
-    lo[r] = quant ? a.w_min[k] : 0.0f;
-    hi[r] = quant ? a.w_max[k] : 0.0f;
-  }
-  float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0;
-#pragma unroll
-  for (int st = 0; st < NST; ++st) {
-    if (st & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc1, 0, 0, 0);
-    else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc0, 0, 0, 0);
-  }
-  if (!ok) return;
-  const int64_t row = (b0 + j) * per;
-  const float vm1 = (float)(a.vocab - 1);
-  const unsigned long long off = (unsigned long long)a.tok_offset;
-  float p[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) p[r] = __fadd_rn(acc0[r], acc1[r]);
-  if (a.params_out != nullptr) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (lk * 4 + r < N) a.params_out[row + d * N + lk * 4 + r] = p[r];
-  }
-  if (!quant) return;
-  int bin[4];
-  bool ex = false;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    bin[r] = beast::quantize_bin_k(p[r], lo[r], hi[r], beast::quantize_scale(lo[r], hi[r], vm1), vm1, ex);
-  if (ex) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bin[r] = beast::quantize_bin(p[r], lo[r], hi[r], vm1);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (lk * 4 + r < N) a.tokens_out[row + (lk * 4 + r) * D + d] = beast::widen_bin(bin[r], off);
-}
-
 // ------------------------------------------------------------ reconstruct --
 struct RecArgs {
   const long long* tokens;
@@ -1174,89 +1092,6 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
 #endif
 }
 
-// Reconstruct in the latency regime without LDS: one wave per MFMA column tile (16 (trajectory,
-// DoF) columns) of an 8-trajectory tile; the DoF map by scalar loads, then the lane's tokens,
-// bounds and basis rows straight into registers (one round trip), dequantise in the lane
-// (t / (V - 1) IEEE-divided, as the LUT holds it), k_reconstruct's MFMA chain (same order)
-// and each lane stores its 16 outputs.  Bit-identical to k_reconstruct.
-template <class S>
-__global__ __launch_bounds__(64 * DirShape<S>::NQ) void k_reconstruct_direct(RecArgs a) {
-  static_assert(S::fixed && S::T > 0 && S::N > 0 && S::N <= 12, "direct reconstruct: fixed shape, N <= 12");
-  constexpr int KS = (S::N + 3) / 4, RT = (S::T + 15) / 16, D = S::D, N = S::N, NJ = S::NJ, T = S::T;
-  constexpr int per = D * N, ndo = S::DL;
-  const Geom& g = a.g;
-  const Dims<S> m(g);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int64_t b0 = (int64_t)blockIdx.x * DIR_TB;
-  const int nb = (int)min<int64_t>(DIR_TB, a.B - b0);
-  int j, d, kind;
-  bool ok;
-  tile_col<DIR_TB>(g, m, wave, lr, j, d, kind, ok);
-  ok = ok && j < nb;
-  const int jj = min(j, nb - 1);
-  const __attribute__((address_space(4))) int32_t* dmap = (const __attribute__((address_space(4))) int32_t*)a.dof_dst;
-  int dst = 0;
-#pragma unroll
-  for (int i = 0; i < D; ++i) dst = (d == i) ? dmap[i] : dst;
-  dst = min(max(dst, 0), ndo - 1);
-  // loads: tokens, bounds, basis rows (A operand: Phi_kind[t = rt * 16 + lr][n = lk * KS + ks])
-  long long tk[KS];
-  float lo[KS], hi[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int n = min(lk * KS + ks, N - 1);
-    tk[ks] = a.tokens[(b0 + jj) * per + n * D + d];
-    lo[ks] = a.w_min[d * N + n];
-    hi[ks] = a.w_max[d * N + n];
-  }
-  float phr[RT][KS];
-  const float* ph = a.basis + (int64_t)kind * T * N;
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int t = rt * 16 + lr, n = lk * KS + ks;
-      const float x = ph[min(t, T - 1) * N + min(n, N - 1)];
-      phr[rt][ks] = (t < T && n < N) ? x : 0.0f;
-    }
-  float init0 = 0.0f;
-  const bool use_init = a.init_p != nullptr && lk == 0 && ok && d < NJ;
-  if (use_init) init0 = a.init_p[(b0 + jj) * a.init_p_sb + a.init_p_src[d]];
-  // dequantise (beast/utils.py:20-25 discrete_to_continuous)
-  const float vm1 = (float)(a.vocab - 1);
-  float w[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const float nrm = __fdiv_rn((float)(tk[ks] - a.tok_offset), vm1);
-    w[ks] = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi[ks], lo[ks])), lo[ks]), lo[ks], hi[ks]);
-  }
-  if (a.params_out != nullptr && ok) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      if (lk * KS + ks < N) a.params_out[(b0 + j) * per + d * N + lk * KS + ks] = w[ks];
-  }
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) w[ks] = (ok && lk * KS + ks < N) ? w[ks] : 0.0f;
-  if (use_init) w[0] = init0;
-  float4_t acc[RT];
-#pragma unroll
-  for (int i = 0; i < RT; ++i) acc[i] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int i = 0; i < RT; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(phr[i][ks], w[ks], acc[i], 0, 0, 0);
-  if (!ok || a.pos_out == nullptr) return;
-  float* out = a.pos_out + (b0 + j) * (int64_t)(T * ndo) + dst;
-#pragma unroll
-  for (int i = 0; i < RT; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = i * 16 + lk * 4 + r;
-      if (t < T) out[t * ndo] = acc[i][r];
-    }
-}
-
 // Per-trajectory basis rows (custom times per row, KS == 0): decode W into LDS, then a
 // sequential fma over n per output (the MFMA chain's order) on the VALU; also the
 // decode-only path when no positions are requested.
@@ -1390,29 +1225,35 @@ bool g_generic_only = false;
 // fit 4 workgroups per CU where 7-wave ones fit 2.  beast_set_option(BEAST_OPT_BLOCK_WAVES,
 // 4 | 7) forces one (tests, measurements); 0 = by batch size.
 int g_block_waves = 0;
-bool g_direct_default = false;   // k_encode_direct as the latency-regime default (after measurement)
 bool wide_blocks(int64_t ntiles) {
-  if (g_block_waves == 4 || g_block_waves == 7 || g_block_waves == 8 || g_block_waves == 9) return g_block_waves != 4;
+  if (g_block_waves == 4 || g_block_waves == 7 || g_block_waves == 8) return g_block_waves != 4;
   return ntiles <= 2 * (int64_t)cu_count();
 }
 // Encode in the latency regime: the pipelined 8-wave kernel (default; BEAST_OPT_BLOCK_WAVES
 // 8 forces it at any batch), or k_encode's 7-wave one (BEAST_OPT_BLOCK_WAVES 7).
 bool pipe_encode(int64_t ntiles) { return g_block_waves == 8 || (g_block_waves == 0 && wide_blocks(ntiles)); }
-// ... or the LDS-free one-wave-per-column-tile kernel (BEAST_OPT_BLOCK_WAVES 9 forces it)
-bool direct_encode(int64_t ntiles) { return g_block_waves == 9 || (g_block_waves == 0 && g_direct_default && wide_blocks(ntiles)); }
 
 // Host launch of a hot kernel through hipModuleLaunchKernel with a cached function handle (per
 // device): the runtime skips hipLaunchKernel's host-function lookup and the GGL template's
 // argument packing, ≈0.15 us of host time per launch (profiles/r02/launch_host_cost.json).
+// The handle is the one of the STREAM's device: a tokenizer on cuda:1 may be called while another
+// device is current (hipGetFuncBySymbol resolves for the current device, so it is looked up under
+// a guard that makes the stream's device current).  Cache entries are atomics: the first launches
+// on a device may race from several host threads, and every racer stores the same handle.
 template <class... Args>
-int launch_fn(const void* kernel, hipFunction_t (&cache)[16], unsigned grid, unsigned block, unsigned lds,
-              hipStream_t s, const char* what, Args... args) {
+int launch_fn(const void* kernel, std::atomic<hipFunction_t> (&cache)[16], unsigned grid, unsigned block,
+              unsigned lds, hipStream_t s, const char* what, Args... args) {
   int dev = 0;
-  BEAST_HIP(hipGetDevice(&dev), what);
-  hipFunction_t f = (dev >= 0 && dev < 16) ? cache[dev] : nullptr;
+  BEAST_HIP(hipStreamGetDevice(s, &dev), what);
+  hipFunction_t f = (dev >= 0 && dev < 16) ? cache[dev].load(std::memory_order_acquire) : nullptr;
   if (f == nullptr) {
-    BEAST_HIP(hipGetFuncBySymbol(&f, kernel), what);
-    if (dev >= 0 && dev < 16) cache[dev] = f;
+    int cur = 0;
+    BEAST_HIP(hipGetDevice(&cur), what);
+    if (cur != dev) BEAST_HIP(hipSetDevice(dev), what);
+    const hipError_t e = hipGetFuncBySymbol(&f, kernel);
+    if (cur != dev) BEAST_HIP(hipSetDevice(cur), what);
+    BEAST_HIP(e, what);
+    if (dev >= 0 && dev < 16) cache[dev].store(f, std::memory_order_release);
   }
   void* params[] = {static_cast<void*>(&args)...};
   BEAST_HIP(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds, s, params, nullptr), what);
@@ -1424,18 +1265,9 @@ int launch_encode_pipe(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
   a.g = make_geom<PIPE_SUB>(D, nj, N, T);
   a.ntiles = (a.B + 2 * PIPE_SUB - 1) / (2 * PIPE_SUB);
   constexpr PipeSmem L = pipe_smem<S>();
-  static hipFunction_t fn[16] = {};
+  static std::atomic<hipFunction_t> fn[16] = {};
   return launch_fn(reinterpret_cast<const void*>(&k_encode_pipe<S>), fn, (unsigned)a.ntiles, PIPE_W * 64, L.total, s,
                    "k_encode_pipe", a.traj, a.B, a);
-}
-
-template <class S>
-int launch_encode_direct(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
-  a.g = make_geom<DIR_TB>(D, nj, N, T);
-  a.ntiles = (a.B + DIR_TB - 1) / DIR_TB;
-  hipLaunchKernelGGL((k_encode_direct<S>), dim3(a.ntiles), dim3(64 * DirShape<S>::NQ), 0, s, a);
-  BEAST_LAUNCHED("k_encode_direct");
-  return BEAST_OK;
 }
 
 template <int TBT, class S>
@@ -1473,10 +1305,6 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
                 "encode list: rows must be contiguous and rows per batch a multiple of %d", tbt);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
     const bool wide = wide_blocks((a.B + 7) / 8);
-    if (!a.traj_list && direct_encode((a.B + 7) / 8)) {
-      if (D == 14 && nj == 14) return launch_encode_direct<Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, s);
-      if (D == 14 && nj == 12) return launch_encode_direct<Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, s);
-    }
     if (!a.traj_list && pipe_encode((a.B + 7) / 8)) {
       if (D == 14 && nj == 14) return launch_encode_pipe<Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, s);
       if (D == 14 && nj == 12) return launch_encode_pipe<Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, s);
@@ -1504,21 +1332,13 @@ int launch_rec_ks(RecArgs a, int D, int nj, hipStream_t s) {
   const int64_t grid = grid_for(a.ntiles, L.total);
   if constexpr (KS == 0) hipLaunchKernelGGL((k_reconstruct_rows<TBT>), dim3(grid), dim3(NTHREADS), L.total, s, a);
   else {
-    static hipFunction_t fn[16] = {};
+    static std::atomic<hipFunction_t> fn[16] = {};
     return launch_fn(reinterpret_cast<const void*>(&k_reconstruct<TBT, KS, RT, S>), fn, (unsigned)grid, S::W * 64,
                      L.total, s, "k_reconstruct",
                      a.ntokens ? static_cast<const void*>(a.ntokens) : static_cast<const void*>(a.tokens), a.B,
                      a.ntokens ? 4 : 8, a);
   }
   BEAST_LAUNCHED("k_reconstruct");
-  return BEAST_OK;
-}
-
-template <class S>
-int launch_rec_direct(RecArgs a, hipStream_t s) {
-  a.ntiles = (a.B + DIR_TB - 1) / DIR_TB;
-  hipLaunchKernelGGL((k_reconstruct_direct<S>), dim3(a.ntiles), dim3(64 * DirShape<S>::NQ), 0, s, a);
-  BEAST_LAUNCHED("k_reconstruct_direct");
   return BEAST_OK;
 }
 
@@ -1546,10 +1366,6 @@ int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t
   if (a.Tout <= 16 * RT_REG) {
     if (!g_generic_only && N == 10 && a.Tout == 50 && a.ndo == D) {
       const bool wide = wide_blocks(a.ntiles);
-      if (TBT == DIR_TB && a.ntokens == nullptr && direct_encode(a.ntiles)) {
-        if (D == 14 && nj == 14) return launch_rec_direct<Shape<14, 14, 10, 50, 14>>(a, s);
-        if (D == 14 && nj == 12) return launch_rec_direct<Shape<14, 12, 10, 50, 14>>(a, s);
-      }
       if (D == 14 && nj == 14)
         return wide ? launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14, 7>>(a, D, nj, s)
                     : launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14>>(a, D, nj, s);
@@ -1649,8 +1465,8 @@ extern "C" int beast_set_option(int option, int value) {
     return BEAST_OK;
   }
   if (option == BEAST_OPT_BLOCK_WAVES) {
-    BEAST_REQUIRE(value == 0 || value == 4 || value == 7 || value == 8 || value == 9,
-                  "BEAST_OPT_BLOCK_WAVES: %d is not 0, 4, 7, 8 or 9", value);
+    BEAST_REQUIRE(value == 0 || value == 4 || value == 7 || value == 8,
+                  "BEAST_OPT_BLOCK_WAVES: %d is not 0, 4, 7 or 8", value);
     g_block_waves = value;
     return BEAST_OK;
   }
@@ -1662,11 +1478,6 @@ extern "C" int beast_set_option(int option, int value) {
   if (option == BEAST_OPT_BPE_ENCODE_MODE) {
     BEAST_REQUIRE(value >= 0 && value <= 3, "BEAST_OPT_BPE_ENCODE_MODE: %d is not 0..3", value);
     beast::g_bpe_encode_mode = value;
-    return BEAST_OK;
-  }
-  if (option == BEAST_OPT_MERGE_LIST_RATIO) {
-    BEAST_REQUIRE(value >= 0, "BEAST_OPT_MERGE_LIST_RATIO: %d < 0", value);
-    beast::g_merge_list_ratio = value;
     return BEAST_OK;
   }
   BEAST_REQUIRE(false, "unknown option %d", option);

@@ -15,9 +15,6 @@ namespace beast {
 void set_error(const char* fmt, ...);
 // BEAST_OPT_MERGE_LDS_MIN: pair count from which k_merge privatises its deltas in LDS
 extern int64_t g_merge_lds_min;
-// BEAST_OPT_MERGE_LIST_RATIO: a merge walks its candidate list when list * ratio < words,
-// else it scans the Bloom signatures of every word
-extern int g_merge_list_ratio;
 // BEAST_OPT_BPE_ENCODE_MODE: bit 0 = heap merge, bit 1 = one workgroup per 4 rows
 extern int g_bpe_encode_mode;
 int hip_fail(hipError_t e, const char* what);

@@ -3,15 +3,20 @@
 //
 // 1. k_keys      transpose x[rows][cols] (row-major params) into order-preserving
 //                uint32 keys [cols][rows] through a [KT_R][33] LDS tile (coalesced both ways)
-// 2. k_hist      per pass (digits of 11, 11, 10 bits from the top) and per target
-//                rank: LDS-privatised 2048-bin histograms of the keys whose
-//                higher bits equal the target's prefix, flushed with u64 atomics.
-//                Multi-GPU: the caller all-reduces the histogram between hist and
-//                select; every rank then selects the same bucket.
+// 2. k_hist      per pass (digits of 11, 11, 10 bits from the top, or 11, 7, 7, 7 -- the
+//                radix the caller picks) and per target rank: LDS-privatised histograms
+//                of the keys whose higher bits equal the target's prefix, flushed with
+//                u32 atomics into a target-major [target][column][bins] array.
+//                Multi-GPU: the caller all-reduces the pass's live slice of it between
+//                hist and select (pass 0: target 0 only, every target shares the empty
+//                prefix); every rank then selects the same bucket.  With ranks the 7-bit
+//                digits keep the later slices small (1.15 MB, then 3 x 0.29 MB for 140
+//                columns x 4 targets, against 3 x 9.2 MB of u64 [column][target] histograms
+//                before) for one extra key pass; one GPU takes 11 bits (three passes).
 // 3. k_select    one thread per (column, target): walk the histogram to the bucket
 //                holding the remaining rank, extend the prefix.
 // 4. k_finalize  numpy's float32 _lerp between ranks floor(vi) and floor(vi)+1.
-// HBM traffic: rows*cols*4 (read x) + 4*rows*cols*4 (write keys, 3 key passes).
+// HBM traffic: rows*cols*4 (read x) + (1 + passes)*rows*cols*4 (write keys, 3 or 4 key passes).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -23,7 +28,7 @@ namespace {
 
 constexpr int MAXQ = 4;
 constexpr int MAXTG = 2 * MAXQ;
-constexpr int NBIN = 2048;
+constexpr int NBIN = 2048;   // bins of the widest digit (11 bits)
 constexpr int HIST_THREADS = 256;
 constexpr int64_t HIST_CHUNK = 32768;  // keys per workgroup per pass
 
@@ -53,7 +58,7 @@ inline WsLayout ws_layout(int64_t rows, int cols, int n_q) {
   w.hdr = o;   o += al(sizeof(QHeader));
   w.state = o; o += al(sizeof(QState) * (size_t)cols * ntg);
   w.nan = o;   o += al(sizeof(uint32_t) * (size_t)cols);
-  w.hist = o;  o += al(sizeof(uint64_t) * (size_t)cols * ntg * NBIN);
+  w.hist = o;  o += al(sizeof(uint32_t) * (size_t)cols * ntg * NBIN);
   w.keys = o;  o += al(sizeof(uint32_t) * (size_t)cols * (size_t)rows);
   w.total = o;
   return w;
@@ -69,10 +74,18 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float(u);
 }
 
-__device__ __forceinline__ void pass_geom(int pass, int& shift, int& bits) {
-  // 11 + 11 + 10 bits from the most significant end
-  shift = (pass == 0) ? 21 : (pass == 1) ? 10 : 0;
-  bits = (pass == 2) ? 10 : 11;
+// digits from the most significant end: radix 11 -> 11 + 11 + 10 bits, radix 7 -> 11 + 7 + 7 + 7
+// (the first digit is 11 bits either way: its last bucket holds exactly the NaN keys)
+__host__ __device__ inline int n_passes(int radix) { return radix == 11 ? 3 : 4; }
+__host__ __device__ inline int hist_stride(int pass, int radix) { return (radix == 11 || pass == 0) ? NBIN : 128; }
+__host__ __device__ inline void pass_geom(int pass, int radix, int& shift, int& bits) {
+  if (radix == 11) {
+    shift = (pass == 0) ? 21 : (pass == 1) ? 10 : 0;
+    bits = (pass == 2) ? 10 : 11;
+  } else {
+    shift = (pass == 0) ? 21 : 21 - 7 * pass;
+    bits = (pass == 0) ? 11 : 7;
+  }
 }
 
 // A workgroup moves a KT_R x 32 tile (16 KiB in, 16 KiB out; 16 loads in flight per thread):
@@ -163,13 +176,14 @@ __device__ __forceinline__ void run_add(uint32_t* h, uint32_t& bin, uint32_t& cn
 }
 
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restrict__ keys, int64_t rows, int ntg,
-                                                       int pass, const QState* __restrict__ st,
-                                                       uint64_t* __restrict__ hist) {
-  extern __shared__ uint32_t h_raw[];   // [nh][NBIN / 2] packed 16-bit bins
-  uint32_t (*h)[NBIN / 2] = reinterpret_cast<uint32_t (*)[NBIN / 2]>(h_raw);
-  const int c = blockIdx.y;
+                                                       int pass, int radix, const QState* __restrict__ st,
+                                                       uint32_t* __restrict__ hist) {
+  extern __shared__ uint32_t h_raw[];   // [nh][nb / 2] packed 16-bit bins
+  const int c = blockIdx.y, cols = gridDim.y;
   int shift, bits;
-  pass_geom(pass, shift, bits);
+  pass_geom(pass, radix, shift, bits);
+  const int nb = hist_stride(pass, radix), nb2 = nb / 2;
+  auto h = [&](int t) { return h_raw + t * nb2; };
   const uint32_t mask = (1u << bits) - 1u;
   const int hi_shift = shift + bits;  // bits above the digit are known
   // targets that need their own histogram (pass 0: one shared histogram)
@@ -180,7 +194,7 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restric
     rbin[t] = 0;
     rcnt[t] = 0;
   }
-  for (int i = threadIdx.x; i < nh * NBIN / 2; i += HIST_THREADS) (&h[0][0])[i] = 0;
+  for (int i = threadIdx.x; i < nh * nb2; i += HIST_THREADS) h_raw[i] = 0;
   __syncthreads();
   const uint32_t* kc = keys + (int64_t)c * rows;
   const int64_t chunk = HIST_CHUNK;
@@ -189,12 +203,12 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restric
   auto add = [&](uint32_t k) {
     const uint32_t dg = (k >> shift) & mask;
     if (pass == 0) {
-      run_add(h[0], rbin[0], rcnt[0], dg);
+      run_add(h(0), rbin[0], rcnt[0], dg);
     } else {
       const uint32_t hk = k >> hi_shift;
 #pragma unroll
       for (int t = 0; t < MAXTG; ++t)
-        if (t < nh && hk == pref[t]) run_add(h[t], rbin[t], rcnt[t], dg);
+        if (t < nh && hk == pref[t]) run_add(h(t), rbin[t], rcnt[t], dg);
     }
   };
   // column c's keys start at c * rows: 16-B aligned only if rows % 4 == 0 -> scalar head
@@ -218,13 +232,14 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restric
   for (int64_t i = a0 + 4 * nv + threadIdx.x; i < i1; i += HIST_THREADS) add(kc[i]);
 #pragma unroll
   for (int t = 0; t < MAXTG; ++t)
-    if (rcnt[t]) bin_add(h[t], rbin[t], rcnt[t]);
+    if (rcnt[t]) bin_add(h(t), rbin[t], rcnt[t]);
   __syncthreads();
-  uint64_t* hc = hist + (int64_t)c * ntg * NBIN;
-  for (int i = threadIdx.x; i < nh * NBIN / 2; i += HIST_THREADS) {
-    const uint32_t v = (&h[0][0])[i];
-    if (v & 0xFFFFu) atomicAdd(reinterpret_cast<unsigned long long*>(hc + 2 * i), (unsigned long long)(v & 0xFFFFu));
-    if (v >> 16) atomicAdd(reinterpret_cast<unsigned long long*>(hc + 2 * i + 1), (unsigned long long)(v >> 16));
+  for (int i = threadIdx.x; i < nh * nb2; i += HIST_THREADS) {
+    const uint32_t v = h_raw[i];
+    const int t = i / nb2, b = 2 * (i - t * nb2);
+    uint32_t* hc = hist + ((int64_t)t * cols + c) * nb;   // target-major: pass 0's live slice is contiguous
+    if (v & 0xFFFFu) atomicAdd(hc + b, v & 0xFFFFu);
+    if (v >> 16) atomicAdd(hc + b + 1, v >> 16);
   }
 }
 
@@ -232,14 +247,15 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const uint32_t* __restric
 // the thread whose bins hold the remaining rank extends the prefix.
 constexpr int SEL_T = 256;
 __global__ __launch_bounds__(SEL_T) void k_select(QState* __restrict__ st, uint32_t* __restrict__ nanf,
-                                                  const uint64_t* __restrict__ hist, int ntg, int pass) {
+                                                  const uint32_t* __restrict__ hist, int ntg, int pass, int radix,
+                                                  int cols) {
   __shared__ uint64_t wsum[SEL_T / 64];
   const int i = blockIdx.x;  // (column, target)
   const int c = i / ntg, t = i % ntg;
   int shift, bits;
-  pass_geom(pass, shift, bits);
+  pass_geom(pass, radix, shift, bits);
   const int nbins = 1 << bits;
-  const uint64_t* h = hist + ((int64_t)c * ntg + (pass == 0 ? 0 : t)) * NBIN;
+  const uint32_t* h = hist + ((int64_t)(pass == 0 ? 0 : t) * cols + c) * hist_stride(pass, radix);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   constexpr int PER = NBIN / SEL_T;  // 8
   uint64_t v[PER], sum = 0;
@@ -273,7 +289,8 @@ __global__ __launch_bounds__(SEL_T) void k_select(QState* __restrict__ st, uint3
       cum += v[k];
     }
   }
-  if (pass == 0 && t == 0 && tid == SEL_T - 1 && v[PER - 1] != 0) nanf[c] = 1;  // bucket 2047: NaN keys only
+  // the last bucket of pass 0 (11 bits) holds the NaN keys (0xFFFFFFFF) and no number's key
+  if (pass == 0 && t == 0 && tid == SEL_T - 1 && v[PER - 1] != 0) nanf[c] = 1;
 }
 
 // numpy _lerp in float32 (lib/_function_base_impl.py): a + d*g, or b - d*(1-g) when g >= 0.5
@@ -311,12 +328,16 @@ extern "C" size_t beast_quantile_workspace_bytes(int64_t rows, int cols, int n_q
   return ws_layout(rows, cols, n_q).total;
 }
 
-extern "C" uint64_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q) {
+extern "C" uint32_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q) {
   const WsLayout w = ws_layout(0, cols, n_q);
-  return reinterpret_cast<uint64_t*>(static_cast<unsigned char*>(workspace) + w.hist);
+  return reinterpret_cast<uint32_t*>(static_cast<unsigned char*>(workspace) + w.hist);
 }
 
-extern "C" int64_t beast_quantile_hist_count(int cols, int n_q) { return (int64_t)cols * 2 * n_q * NBIN; }
+extern "C" int beast_quantile_passes(int radix_bits) { return radix_bits == 11 ? 3 : radix_bits == 7 ? 4 : 0; }
+
+extern "C" int64_t beast_quantile_hist_count(int pass, int cols, int n_q, int radix_bits) {
+  return (int64_t)(pass == 0 ? 1 : 2 * n_q) * cols * hist_stride(pass, radix_bits);
+}
 
 extern "C" int beast_quantile_prepare(const float* x, int64_t rows, int cols, int64_t row_stride, int64_t n_total,
                                       int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream) {
@@ -326,6 +347,7 @@ extern "C" int beast_quantile_prepare(const float* x, int64_t rows, int cols, in
                 (long long)rows, (long long)n_total);
   BEAST_REQUIRE(rows == 0 || x, "beast_quantile_prepare: null x");
   BEAST_REQUIRE(rows < (int64_t(1) << 31), "rows per rank must be < 2^31");
+  BEAST_REQUIRE(n_total < (int64_t(1) << 32), "n_total must be < 2^32 (uint32 histogram counts)");
   const WsLayout w = ws_layout(rows, cols, n_q);
   BEAST_REQUIRE_CODE(ws_bytes >= w.total, BEAST_E_WORKSPACE, "quantile workspace %zu < %zu", ws_bytes, w.total);
   QHeader h;
@@ -383,33 +405,39 @@ extern "C" int beast_quantile_prepare_segments(const void* seg_table, int nseg, 
   return BEAST_OK;
 }
 
-extern "C" int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream) {
-  BEAST_REQUIRE(workspace && pass >= 0 && pass <= 2 && n_q >= 1 && n_q <= MAXQ, "beast_quantile_hist: bad args");
+extern "C" int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, int radix_bits, void* workspace,
+                                   void* stream) {
+  BEAST_REQUIRE(radix_bits == 11 || radix_bits == 7, "beast_quantile_hist: radix_bits must be 11 or 7");
+  BEAST_REQUIRE(workspace && pass >= 0 && pass < n_passes(radix_bits) && n_q >= 1 && n_q <= MAXQ,
+                "beast_quantile_hist: bad args");
   const WsLayout w = ws_layout(rows, cols, n_q);
   unsigned char* ws = static_cast<unsigned char*>(workspace);
   hipStream_t s = beast::as_stream(stream);
   const int ntg = 2 * n_q;
-  BEAST_HIP(hipMemsetAsync(ws + w.hist, 0, sizeof(uint64_t) * (size_t)cols * ntg * NBIN, s), "hist memset");
+  BEAST_HIP(hipMemsetAsync(ws + w.hist, 0, sizeof(uint32_t) * beast_quantile_hist_count(pass, cols, n_q, radix_bits),
+                           s), "hist memset");
   if (rows > 0) {
     const int64_t chunk = HIST_CHUNK;
     dim3 grid((unsigned)((rows + chunk - 1) / chunk), (unsigned)cols);
-    const size_t lds = sizeof(uint32_t) * (NBIN / 2) * (pass == 0 ? 1 : ntg);
+    const size_t lds = sizeof(uint32_t) * (hist_stride(pass, radix_bits) / 2) * (pass == 0 ? 1 : ntg);
     hipLaunchKernelGGL(k_hist, grid, dim3(HIST_THREADS), lds, s, reinterpret_cast<const uint32_t*>(ws + w.keys), rows,
-                       ntg, pass, reinterpret_cast<const QState*>(ws + w.state),
-                       reinterpret_cast<uint64_t*>(ws + w.hist));
+                       ntg, pass, radix_bits, reinterpret_cast<const QState*>(ws + w.state),
+                       reinterpret_cast<uint32_t*>(ws + w.hist));
     BEAST_LAUNCHED("k_hist");
   }
   return BEAST_OK;
 }
 
-extern "C" int beast_quantile_select(int pass, int cols, int n_q, void* workspace, void* stream) {
-  BEAST_REQUIRE(workspace && pass >= 0 && pass <= 2 && n_q >= 1 && n_q <= MAXQ, "beast_quantile_select: bad args");
+extern "C" int beast_quantile_select(int pass, int cols, int n_q, int radix_bits, void* workspace, void* stream) {
+  BEAST_REQUIRE(radix_bits == 11 || radix_bits == 7, "beast_quantile_select: radix_bits must be 11 or 7");
+  BEAST_REQUIRE(workspace && pass >= 0 && pass < n_passes(radix_bits) && n_q >= 1 && n_q <= MAXQ,
+                "beast_quantile_select: bad args");
   const WsLayout w = ws_layout(0, cols, n_q);
   unsigned char* ws = static_cast<unsigned char*>(workspace);
   const int n = cols * 2 * n_q;
   hipLaunchKernelGGL(k_select, dim3(n), dim3(SEL_T), 0, beast::as_stream(stream),
                      reinterpret_cast<QState*>(ws + w.state), reinterpret_cast<uint32_t*>(ws + w.nan),
-                     reinterpret_cast<const uint64_t*>(ws + w.hist), 2 * n_q, pass);
+                     reinterpret_cast<const uint32_t*>(ws + w.hist), 2 * n_q, pass, radix_bits, cols);
   BEAST_LAUNCHED("k_select");
   return BEAST_OK;
 }
@@ -430,9 +458,9 @@ extern "C" int beast_quantile_f32(const float* x, int64_t rows, int cols, int64_
                                   const float* host_q, float* out, void* workspace, size_t ws_bytes, void* stream) {
   BEAST_REQUIRE(rows >= 1, "np.quantile of an empty array is undefined (rows=0)");
   int rc = beast_quantile_prepare(x, rows, cols, row_stride, rows, n_q, host_q, workspace, ws_bytes, stream);
-  for (int p = 0; rc == BEAST_OK && p < 3; ++p) {
-    rc = beast_quantile_hist(p, rows, cols, n_q, workspace, stream);
-    if (rc == BEAST_OK) rc = beast_quantile_select(p, cols, n_q, workspace, stream);
+  for (int p = 0; rc == BEAST_OK && p < n_passes(11); ++p) {
+    rc = beast_quantile_hist(p, rows, cols, n_q, 11, workspace, stream);
+    if (rc == BEAST_OK) rc = beast_quantile_select(p, cols, n_q, 11, workspace, stream);
   }
   if (rc == BEAST_OK) rc = beast_quantile_finalize(cols, n_q, workspace, out, stream);
   return rc;

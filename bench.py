@@ -78,9 +78,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--windows", type=int, default=5, help="timed windows of --steps steps (median reported)")
+    ap.add_argument("--windows", type=int, default=None,
+                    help="timed windows of --steps steps (median reported); default: enough for >= 2,000 timed "
+                         "steps, at least 5")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--no-bpe", action="store_true")
+    ap.add_argument("--no-bpe-api", action="store_true", help="skip the fit_from_trajectories API leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fit", action="store_true")
     ap.add_argument("--no-large", action="store_true")
@@ -386,11 +389,11 @@ def bpe_bench(dev, args, world, rank, reduce):
     el = times[-1]
     st = res.stats
     if world == 1:
-        # §8d's byte count needs the pair occurrences every merge rewrote: an untimed rerun on the
-        # pair-index loop (same corpus -> same merges) records them
+        # §8d's byte count needs the pair occurrences every merge rewrote: an untimed rerun of the
+        # same loop that counts them (same corpus -> same merges)
         flat, off = fixed_rows_to_device(allrows)
-        rec = train_bpe(flat, off, args.bpe_vocab, reduce=reduce, merge_mode="pair_index")
-        assert rec.merges == res.merges, "pair-index loop and signature-scan loop disagree"
+        rec = train_bpe(flat, off, args.bpe_vocab, reduce=reduce, count_applications=True)
+        assert rec.merges == res.merges, "the counting rerun's merges differ"
         st = dict(st, applications=rec.stats.get("applications"))
         del flat, off
     out = {"metric": "BPE merges/sec (fit_from_trajectories core: pretokenise + count + merge loop)",
@@ -413,7 +416,18 @@ def bpe_bench(dev, args, world, rank, reduce):
         same = got == golden["merges"] and res.vocab == golden["vocab"]
         out["parity"] = {"golden": os.path.relpath(K5_GOLDEN, REPO), "merges_equal_hf": bool(same),
                          "corpus_sha256_equal": (sha == golden["corpus_sha256"]) if sha else None,
-                         "hf": golden.get("hf_version")}
+                         "hf": golden.get("hf_version"),
+                         "scope": "bit-exact vs HF BpeTrainer given identical bins (this corpus: the GPU encode of "
+                                  "the K5 trajectories)",
+                         # the configured pipeline against the reference's own encode of the same trajectories:
+                         # its fp32 LU fit moves a few bins across .5 ties, and HF on that corpus picks a
+                         # different pair at a count tie from merge 114 on (tests/golden/gen_k5.py)
+                         "merges_equal_on_reference_corpus": golden.get("merges_equal_on_reference_corpus"),
+                         "first_differing_merge_on_reference_corpus":
+                             golden.get("first_differing_merge_on_reference_corpus"),
+                         "corpus_token_flips_vs_reference": golden.get("gpu_vs_reference_token_flips"),
+                         "corpus_tokens": golden.get("tokens"),
+                         "corpus_flip_max_tie_distance": golden.get("gpu_vs_reference_max_tie_distance")}
         assert same, "K5 merges differ from the golden HF BpeTrainer merges of the same corpus"
     else:
         out["parity"] = {"golden": None, "note": "no K5 golden for this corpus size / vocab (parity unpinned)"}
@@ -421,6 +435,42 @@ def bpe_bench(dev, args, world, rank, reduce):
         out["cpu_baseline"] = hf_bpe_same_sample(allrows[:args.bpe_sample], args.bpe_vocab)
     out["codec"] = bpe_codec_bench(res, allrows[:args.batch], dev, args)
     del allrows
+    if not args.no_bpe_api:
+        out["api"] = bpe_api_bench(dev, args, world, rank, golden, res)
+    return out
+
+
+def bpe_api_bench(dev, args, world, rank, golden, core):
+    """Config K5 end to end through the drop-in API (reference beast_bspline_bpe_tokenizer.py:111-146):
+    BEASTBsplineBPETokenizer.fit_from_trajectories over the K5 trajectories resident in HBM, in
+    batches of 8,192 -- the encode of every batch, the row gather, the trainer and the HF wrapper
+    build.  Merges compared with the trainer-core leg's (same trajectories, same bounds)."""
+    from beast_tokenizer_amd import BEASTBsplineBPETokenizer
+    per_rank = args.bpe_seqs // world
+    x = synth_trajectories_device(per_rank, T, D, seed=7, start=rank * per_rank, device=dev)
+    loader = [{"actions": x[s:s + K5_CHUNK]} for s in range(0, per_rank, K5_CHUNK)]
+    tok = BEASTBsplineBPETokenizer(num_dof=D, num_basis=N, seq_len=T, vocab_size=V, bpe_vocab_size=args.bpe_vocab,
+                                   device=str(dev))
+    if golden is not None:
+        tok.w_min.copy_(torch.tensor(golden["w_min"], dtype=torch.float32))
+        tok.w_max.copy_(torch.tensor(golden["w_max"], dtype=torch.float32))
+    pg = True if world > 1 else None
+    times, st = [], None
+    for _ in range(2):            # the first run pays allocator growth; report the second
+        sync(world)
+        t0 = time.perf_counter()
+        st = tok.fit_from_trajectories(loader, show_progress=False, process_group=pg)
+        torch.cuda.synchronize()
+        times.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+    res = tok._last_bpe_result
+    el = times[-1]
+    out = {"metric": "BPE merges/sec through BEASTBsplineBPETokenizer.fit_from_trajectories (encode + gather + "
+                     "train + HF wrapper)", "value": len(res.merges) / el, "unit": "merges/s",
+           "trajectories_per_s": per_rank * world / el, "seconds": el, "seconds_runs": times,
+           "batches": len(loader), "batch": K5_CHUNK, "train_s": res.stats["setup_s"] + res.stats["merge_loop_s"],
+           "merges_equal_core": [list(m) for m in res.merges] == [list(m) for m in core.merges],
+           "state": {"min_token": st.min_token, "max_token": st.max_token}}
+    del x, loader
     return out
 
 
@@ -540,6 +590,8 @@ def dump_k5(dev, args):
 
 def main():
     args = parse()
+    if args.windows is None:
+        args.windows = max(5, -(-2000 // max(args.steps, 1)))
     torch.set_num_threads(_host_threads())
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -641,6 +693,8 @@ def main():
                        "median_gpu_event_us_per_step": float(np.median(gpu_ms)) / args.steps * 1e3},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "token_parity": parity,
             "host": host_info(), "fit": fitb, "bpe": bpe,
+            "dist": {"world_size": world, "backend": torch.distributed.get_backend() if world > 1 else None,
+                     "device": str(dev), "ranks_on_one_device": os.environ.get("BEAST_BENCH_ONE_DEVICE") == "1"},
         }
         if cpu and cpu.get("value"):
             line["gpu_over_cpu"] = value / cpu["value"]

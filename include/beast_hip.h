@@ -50,16 +50,13 @@ const char* beast_last_error(void);
  * identical.
  * BEAST_OPT_MERGE_LDS_MIN = n: BPE merges of pairs counted >= n privatise their pair-count deltas
  * in LDS (default 4096; below, global atomics); results are identical.
- * BEAST_OPT_MERGE_LIST_RATIO = r: a pair-index merge walks its candidate list when the list is
- * shorter than (words / r), else it scans every word's Bloom signature (default 16; 0 = always
- * the list); results are identical.
- * Not thread-safe with concurrent launches. * BEAST_OPT_BPE_ENCODE_MODE = m (tests, measurements): beast_bpe_encode_rows' per-word merge by
+ * BEAST_OPT_BPE_ENCODE_MODE = m (tests, measurements): beast_bpe_encode_rows' per-word merge by
  * rounds (0, the default) or by HF's min-heap (1); m + 2 also launches one workgroup per 4 rows
- * instead of only the resident ones.  Results are identical. */
+ * instead of only the resident ones.  Results are identical.
+ * Options are process-wide and not synchronised: set them before launching, not concurrently. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
 #define BEAST_OPT_MERGE_LDS_MIN 3
-#define BEAST_OPT_MERGE_LIST_RATIO 4
 #define BEAST_OPT_BPE_ENCODE_MODE 5
 int beast_set_option(int option, int value);
 
@@ -149,23 +146,27 @@ int beast_colminmax_f32(const float* x, int64_t rows, int cols, int64_t row_stri
                         float* out_max, void* workspace, size_t ws_bytes, void* stream);
 
 /* Exact per-column quantiles with numpy 'linear' semantics in float32
- * (np.quantile(params, q, axis=0), :213-214) by 3-pass 11/11/10-bit radix
- * select on order-preserving keys.  Multi-GPU: call prepare, then for pass in
- * 0..2 { hist; all-reduce(SUM, uint64) of beast_quantile_hist_ptr; select },
- * then finalize.  n_total = rows summed over all ranks.  n_q <= 4 (host_q). */
+ * (np.quantile(params, q, axis=0), :213-214) by radix select on order-preserving keys:
+ * radix_bits 11 (three passes: 11/11/10 bits) or 7 (four passes: 11/7/7/7 bits; smaller histograms
+ * to all-reduce for one more pass over the keys).  Multi-GPU: call
+ * prepare, then for pass in 0 .. beast_quantile_passes(radix_bits) - 1 { hist; all-reduce(SUM,
+ * uint32) of the first beast_quantile_hist_count(pass, ...) elements at beast_quantile_hist_ptr;
+ * select }, then finalize (every rank selects the same order statistics).  n_total = rows summed
+ * over all ranks (< 2^32).  n_q <= 4 (host_q). */
 size_t beast_quantile_workspace_bytes(int64_t rows, int cols, int n_q);
 int beast_quantile_prepare(const float* x, int64_t rows, int cols, int64_t row_stride, int64_t n_total,
                            int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream);
-uint64_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q);
-int64_t beast_quantile_hist_count(int cols, int n_q);
+uint32_t* beast_quantile_hist_ptr(void* workspace, int cols, int n_q);
+int beast_quantile_passes(int radix_bits);
+int64_t beast_quantile_hist_count(int pass, int cols, int n_q, int radix_bits);
 /* prepare over a list of row-major segments instead of one matrix (fit_parameters' per-batch
  * params without a concatenation): seg_table = device array of nseg {const float* ptr;
  * int64_t first_row; int64_t row_stride} (24 B each, first_row ascending from 0), rows = the
  * total, max_seg_rows = the largest segment. */
 int beast_quantile_prepare_segments(const void* seg_table, int nseg, int64_t max_seg_rows, int64_t rows, int cols,
                                     int64_t n_total, int n_q, const float* host_q, void* workspace, size_t ws_bytes, void* stream);
-int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, void* workspace, void* stream);
-int beast_quantile_select(int pass, int cols, int n_q, void* workspace, void* stream);
+int beast_quantile_hist(int pass, int64_t rows, int cols, int n_q, int radix_bits, void* workspace, void* stream);
+int beast_quantile_select(int pass, int cols, int n_q, int radix_bits, void* workspace, void* stream);
 int beast_quantile_finalize(int cols, int n_q, void* workspace, float* out, void* stream);
 /* single-GPU convenience: all of the above. out [n_q][cols]. */
 int beast_quantile_f32(const float* x, int64_t rows, int cols, int64_t row_stride, int n_q, const float* host_q,
@@ -197,7 +198,18 @@ int beast_bpe_pretok_emit(const int64_t* tok, const int64_t* seq_off, int64_t n_
 int beast_bpe_count_pairs(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
                           const uint32_t* wcount, int64_t n_words, uint32_t* table, int Vt, int n_sym,
                           void* stream);
-/* max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)) (0 if the table is empty)
+/* sig[w] = OR over word w's symbols x of two bits of x (a 64-bit Bloom mask, csrc/bpe_common.h
+ * sig_bit).  The merges use it to skip words that cannot contain a pair without reading their
+ * symbols, and keep it current for the words they rewrite. */
+int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
+                              uint64_t* sig, void* stream);
+
+/* -- the merge loop (csrc/bpe_loop.hip), replacing the loop of HF BpeTrainer::do_train as called
+ * from beast/beast_bpe_trainer.py:61-74.  Two forms over the same words:
+ *
+ * Host-driven, one merge per call (vocabularies above 4096, the host fallback on a string-hash
+ * collision, the per-merge all-reduce form):
+ * max over table[x][y], x,y < vcur, of (count << 32 | ~(x*Vt+y)) (0 if the table is empty)
  * into ws[2 + (call & 1)], where call = 0, 1, 2, ... numbers the calls on this workspace
  * (each call zeroes the other slot for the next one: no memset per call).  Incremental:
  * ws caches each row's best; a row is rescanned only when beast_bpe_apply_argmax changed it
@@ -209,95 +221,54 @@ int beast_bpe_argmax(const uint32_t* table, int Vt, int vcur, uint64_t* ws, int 
  * HF's pair-count changes, per word times wcount (NULL = 1):
  * [0]: (x,a)  [1]: (x,new)  [2]: (b,y)  [3]: (new,y).
  * are accumulated into deltas[4][Vt] int32 (multi-GPU: all-reduce them, then
- * beast_bpe_apply_argmax).  sig: see beast_bpe_word_signatures (nullable).  pair_count: the pair's
- * count from beast_bpe_argmax (a hint choosing LDS-privatised or direct delta atomics). */
+ * beast_bpe_apply_argmax).  sig: beast_bpe_word_signatures.  pair_count: the pair's count from
+ * beast_bpe_argmax (a hint choosing LDS-privatised or direct delta atomics). */
 int beast_bpe_merge(uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
                     int64_t n_words, int a, int b, int new_id, const uint32_t* tlen, int max_token_length,
-                    int32_t* deltas, int Vt, uint64_t* sig, void* index, int64_t pair_count, void* stream);
-/* Inverted index symbol -> words (HF's where_to_update): the merge visits only the words on
- * the shorter list of a and b, and appends the words it rewrote as the list of new_id
- * (committed by beast_bpe_apply_argmax).  index: beast_bpe_index_workspace_bytes(Vt, capacity) with
- * capacity >= (symbols of the words) + Vt + room for appends; when it runs out, lists become
- * unknown and merges fall back to visiting every word (results never change).  Nullable. */
-size_t beast_bpe_index_workspace_bytes(int Vt, int64_t pool_capacity);
-int beast_bpe_build_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
-                          int Vt, void* index, size_t index_bytes, void* stream);
-/* sig[w] = OR of 1 << (symbol & 63) over word w (a Bloom mask of its symbols).  Passed to
- * beast_bpe_merge (nullable), it lets the merge skip words that cannot contain the pair
- * without reading their symbols; the merge keeps it current for the words it rewrites. */
-int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
-                              uint64_t* sig, void* stream);
+                    int32_t* deltas, int Vt, uint64_t* sig, int64_t pair_count, void* stream);
 /* The step after a merge, fused with the next argmax: table += deltas (deltas consumed are
- * zeroed), table[a][b] = 0 (merged pair retired), tlen[new_id] = tlen[a] + tlen[b], with an
- * index commit new_id's word list (new_id_reused != 0: new_id already existed, its list
- * becomes unknown); then the argmax of beast_bpe_argmax (same ws, next call index) over
- * x, y < vcur (vcur counting new_id). */
+ * zeroed), table[a][b] = 0 (merged pair retired), tlen[new_id] = tlen[a] + tlen[b]; then the
+ * argmax of beast_bpe_argmax (same ws, next call index) over x, y < vcur (vcur counting new_id). */
 int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, int a, int b, int new_id,
-                           uint32_t* tlen, void* index, int new_id_reused, uint64_t* ws, int call, void* stream);
+                           uint32_t* tlen, uint64_t* ws, int call, void* stream);
 
-/* Device-driven merge loop: the next merge is decided on the GPU from the previous argmax
- * (stop when vocab_size is reached, the count drops below min_frequency, or the log is full),
- * its id by a (64-bit string hash, byte length) table of the vocabulary (HF's id reuse), and
- * merge + apply_argmax read it from the loop record -- no host round trip per merge.
+/* Device-driven, batched (the default): merges are decided on the GPU, several per pass and
+ * exactly HF's sequence -- each pass takes the table's top pairs in HF order while they are
+ * symbol-disjoint, the last taken is not a self-pair, no string re-uses an id (only the first
+ * may) and no taken row's second-best pair ranks above the next (csrc/bpe_loop.hip, "batched
+ * merges", has the proof); stop rules: vocab_size reached, count below min_frequency, log full.
+ * Ids of new strings come from a (64-bit string hash, byte length) table of the vocabulary
+ * (HF's id reuse); the host replays the log against the real strings.
  * tok_hash / tok_pow: per initial token, h = sum bytes[i] * P^(n-1-i) and P^n (mod 2^64) of its
- * UTF-8 string, tlen its byte length (the same tlen array merge / apply_argmax maintain);
- * argmax_parity: the `call & 1` of the beast_bpe_argmax that produced the first pair.
- * beast_bpe_loop_steps enqueues n_steps (step, merge, apply_argmax) triples (index: see
- * beast_bpe_build_index, nullable); steps after
- * the loop stopped are no-ops.  beast_bpe_loop_state returns device pointers to the record
- * {int32 active, a, b, nid, reused, vcur, parity, n_merges, ...} and the log
- * [max_merges][4] int32 {a, b, nid, reused} for the host to read and verify. */
+ * UTF-8 string; tlen its length in HF units (characters of the byte-level string), max_tlen
+ * the largest.  beast_bpe_loop_state returns device pointers to the state {int32 active, vcur,
+ * n_merges, ...} and the log [max_merges][4] int32 {a, b, nid, reused} for the host to read. */
 size_t beast_bpe_loop_workspace_bytes(int Vt, int max_merges);
 int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_merges, int n_tokens, int vocab_size,
-                        int min_frequency, int argmax_parity, const uint64_t* tok_hash, const uint64_t* tok_pow,
-                        const uint32_t* tlen, void* stream);
-int beast_bpe_loop_steps(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
-                         uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen, int max_token_length,
-                         int32_t* deltas, uint64_t* sig, void* index, uint32_t* table, uint64_t* argws,
-                         int vocab_size, void* stream);
-/* The same loop as ONE launch (one resident workgroup per CU; merge, grid barrier, apply +
- * argmax, grid barrier per merge; no kernel boundary per merge).  bar_ws: at least
- * beast_bpe_loop_persistent_bytes(); its first word group holds the barrier counters and the
- * abort flag (uint32 at byte offset 36: nonzero = a barrier timed out, the loop state is then
- * undefined and the caller reruns on beast_bpe_loop_steps).  Vt <= 4096. */
-size_t beast_bpe_loop_persistent_bytes(void);
-int beast_bpe_loop_persistent(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
-                              uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
-                              int max_token_length, int32_t* deltas, uint64_t* sig, uint32_t* table,
-                              uint64_t* argws, int vocab_size, void* bar_ws, size_t bar_bytes, void* stream);
+                        int min_frequency, const uint64_t* tok_hash, const uint64_t* tok_pow, const uint32_t* tlen,
+                        int max_tlen, void* stream);
 int beast_bpe_loop_state(const void* ws, int Vt, int max_merges, const void** state, const void** log);
-/* The same loop with several merges per (merge, apply) pair of launches, exactly HF's sequence:
- * each pass takes the table's top pairs in HF order while they are symbol-disjoint, the last
- * taken is not a self-pair, no string re-uses an id (only the first may) and no taken row's
- * second-best pair ranks above the next (csrc/bpe.hip, "batched merges", has the proof);
- * max_batch (2, 4 or 8) caps a pass; sig (beast_bpe_word_signatures) is required.  batch_ws: beast_bpe_batch_workspace_bytes(Vt); init = 1 on
- * the first call after beast_bpe_loop_init (zeroes batch_ws and ranks every row).  Vt <= 4096. */
+/* n_steps passes of (merge the decided batch over every word, apply + rank + decide the next),
+ * two launches each; passes after the loop stopped are no-ops.  max_batch (2, 4 or 8) caps a
+ * pass.  argws: beast_bpe_argmax_workspace_bytes(Vt), zero-filled; batch_ws:
+ * beast_bpe_batch_workspace_bytes(Vt).  flags: BEAST_BPE_BATCH_INIT ranks every row and decides
+ * the first batch before the passes (first call after beast_bpe_loop_init); _NO_MERGE / _NO_APPLY
+ * leave out one launch of each pass -- the sharded form: each rank holds a shard of the words,
+ * its merge launch writes the pair-count changes into deltas [beast_bpe_batch_delta_count(Vt)]
+ * int32 (zero-filled once) instead of the table, the caller all-reduces (SUM) them, and the apply
+ * launch adds them to every rank's identical table (deltas NULL: one GPU, the changes go straight
+ * into the table).  apps (nullable, accounting): apps[m] += the pair occurrences merge m
+ * rewrote in the distinct words.  Vt <= 4096. */
+#define BEAST_BPE_BATCH_INIT 1
+#define BEAST_BPE_BATCH_NO_MERGE 2
+#define BEAST_BPE_BATCH_NO_APPLY 4
 size_t beast_bpe_batch_workspace_bytes(int Vt);
-int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_batch, uint16_t* sym,
+size_t beast_bpe_batch_delta_count(int Vt);
+int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_batch, int flags, uint16_t* sym,
                          const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount, int64_t n_words,
                          uint32_t* tlen, int max_token_length, uint64_t* sig, uint32_t* table, uint64_t* argws,
-                         void* batch_ws, size_t batch_ws_bytes, int vocab_size, int init, void* stream);
-/* Pair index for the device-driven loop (replaces the per-merge signature scan): a CSR of
- * the distinct words holding each pair of two setup symbols (ids < n_sym), built once from the
- * distinct words (n_symbols = their total symbol count bounds the entries), plus a token index
- * (beast_bpe_index_workspace_bytes(Vt, capacity), initialised by beast_bpe_token_index_init)
- * that receives the words each merge rewrote -- the candidates of any later pair with that
- * merged token.  beast_bpe_loop_steps_ix is beast_bpe_loop_steps over these candidate lists
- * (pair_index nullable: every merge then visits every word); a merge whose list is long scans
- * the words' Bloom signatures instead (sig: beast_bpe_word_signatures, nullable = lists only;
- * BEAST_OPT_MERGE_LIST_RATIO).  word_claim[n_words] (zeroed by the caller before the first step)
- * marks the words a merge visited.  apps[2][max_merges] (nullable, zeroed by the caller) receives
- * per merge the pair occurrences it rewrote in distinct words, then the words it visited.
- * Replaces the loop of HF BpeTrainer::do_train as called from beast/beast_bpe_trainer.py:61-74. */
-size_t beast_bpe_pair_index_bytes(int n_sym, int64_t n_symbols);
-int beast_bpe_build_pair_index(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
-                               int n_sym, int64_t n_symbols, void* ws, size_t ws_bytes, void* stream);
-int beast_bpe_token_index_init(void* index, size_t index_bytes, int Vt, void* stream);
-int beast_bpe_loop_steps_ix(void* ws, int Vt, int max_merges, int n_steps, uint16_t* sym, const uint32_t* wstart,
-                            uint32_t* wlen, const uint32_t* wcount, int64_t n_words, uint32_t* tlen,
-                            int max_token_length, int32_t* deltas, const void* pair_index, int n_sym,
-                            void* token_index, uint32_t* word_claim, uint64_t* sig, uint32_t* table,
-                            uint64_t* argws, int vocab_size, uint32_t* apps, void* stream);
+                         void* batch_ws, size_t batch_ws_bytes, int vocab_size, int32_t* deltas, uint32_t* apps,
+                         void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

@@ -48,7 +48,7 @@ def gpu_device():
 
 
 KERNEL_MODES = {"specialised": (0, 0), "specialised_w4": (0, 4), "specialised_w7": (0, 7),
-                "specialised_w8": (0, 8), "specialised_w9": (0, 9), "generic": (1, 0)}
+                "specialised_w8": (0, 8), "generic": (1, 0)}
 
 
 def set_kernel_mode(mode):
@@ -60,8 +60,7 @@ def set_kernel_mode(mode):
     lib.beast_set_option(_lib.OPT_BLOCK_WAVES, waves)
 
 
-@pytest.fixture(params=["specialised", "specialised_w4", "specialised_w7", "specialised_w8", "specialised_w9",
-                        "generic"])
+@pytest.fixture(params=["specialised", "specialised_w4", "specialised_w7", "specialised_w8", "generic"])
 def kernel_mode(request):
     """Run a parity test on the shape-specialised kernels (the width the batch size picks,
     the 4-wave width large batches use, the 7-wave one-pass encode, the 8-wave pipelined

@@ -16,7 +16,12 @@ from oracle import bpe_oracle
 
 
 class NumpyBpeOps:
+    """``batched=True`` also models the batched device loop (``loop_run``), else ``train_bpe`` runs
+    its host-driven loop on these ops."""
     device = torch.device("cpu")
+
+    def __init__(self, batched: bool = False, kmax: int = 8):
+        self.batched, self.kmax = batched, kmax
 
     def minmax(self, tokens):
         return torch.tensor([int(tokens.min()), int(tokens.max())], dtype=torch.int64)
@@ -109,6 +114,71 @@ class NumpyBpeOps:
         self.apply(table, deltas, Vt, a, b, nid)
         return self.argmax(table, Vt, vcur)
 
+    # -- the batched device loop (csrc/bpe_loop.hip k_merge_batch + k_apply_batch), restated
+    def loop_supported(self, Vt):
+        return self.batched and Vt <= 4096
+
+    def loop_run(self, words, table, Vt, id2str, vocab_size, min_frequency, max_len, reduce=None, chunk=64,
+                 count_applications=False):
+        """Per pass: the table's top pairs in HF order (count, then smallest (a, b)) while the batch
+        rules hold -- symbol-disjoint from the batch, the previous one neither a self-pair nor an id
+        re-use, a new string distinct within the batch, count >= max(1, min_frequency), room in the
+        vocabulary; the merges applied in order to every word; the pass's changes [n][4][Vt] summed
+        (all-reduced when sharded) and added to the table, then the merged pairs retired.  The exact
+        global order stands in for the kernels' per-row best / second-best bookkeeping (the rule it
+        enforces: the batch is a prefix of that order)."""
+        tb = table.numpy().reshape(Vt, Vt)
+        strings = {t: i for i, t in enumerate(id2str)}
+        ntok, log, passes = len(id2str), [], 0
+        km = self.kmax
+        while ntok < vocab_size:
+            sub = tb[:ntok, :ntok].astype(np.int64).ravel()
+            pos = np.flatnonzero(sub > 0)
+            order = pos[np.lexsort((pos, -sub[pos]))][:km]
+            batch, used, made = [], set(), set()
+            for r, p in enumerate(order):
+                c = int(sub[p])
+                x, y = divmod(int(p), ntok)
+                t = id2str[x] + id2str[y] if x < len(id2str) and y < len(id2str) else None
+                if r > 0:
+                    pa, pb, _, pre = batch[-1]
+                    if pa == pb or pre or x in used or y in used:
+                        break
+                exist = strings.get(t) if t is not None else None
+                if (r > 0 and (exist is not None or t in made)) or c < max(1, min_frequency) or \
+                        ntok + len(batch) - (1 if batch and batch[0][3] else 0) >= vocab_size:
+                    break
+                nid = exist if exist is not None else ntok + len(batch)
+                batch.append((x, y, nid, exist is not None))
+                used |= {x, y}
+                made.add(t)
+            if not batch:
+                break
+            passes += 1
+            D = np.zeros((km, 4, Vt), dtype=np.int64)
+            for j, (a, b, nid, reused) in enumerate(batch):
+                if not reused:
+                    t = id2str[a] + id2str[b]
+                    strings[t] = nid
+                    id2str = id2str + [t]
+                    self.tlen[nid] = self.tlen[a] + self.tlen[b]
+                D[j] = self.merge(words, a, b, nid, max_len, Vt).numpy().reshape(4, Vt)
+            dt = torch.from_numpy(D.reshape(-1).astype(np.int32))
+            if reduce is not None:
+                reduce(dt, "sum")
+            D = dt.numpy().reshape(km, 4, Vt).astype(np.int64)
+            for j, (a, b, nid, reused) in enumerate(batch):
+                tb[:, a] += D[j, 0].astype(tb.dtype)
+                tb[:, nid] += D[j, 1].astype(tb.dtype)
+                tb[b, :] += D[j, 2].astype(tb.dtype)
+                tb[nid, :] += D[j, 3].astype(tb.dtype)
+            for a, b, nid, reused in batch:
+                tb[a, b] = 0
+                log.append((a, b, nid, int(reused)))
+            ntok += sum(1 for *_, reused in batch if not reused)
+        self.loop_used, self.loop_passes, self.last_apps = "batch", passes, None
+        return log, False
+
     def apply(self, table, deltas, Vt, a, b, nid):
         tb = table.numpy().reshape(Vt, Vt)
         d = deltas.numpy().reshape(4, Vt)
@@ -135,7 +205,10 @@ def _ranks(n, q):
 
 
 class NumpyQuantileOps:
-    GEOM = [(21, 11), (10, 11), (0, 10)]
+    """The radix select of csrc/quantile.hip: digits from the top (11/11/10 or 11/7/7/7 bits),
+    uint32 histograms in a target-major [target][column][bins] layout, pass 0 with target 0's
+    slice only (every target shares the empty prefix) -- the slices the driver all-reduces."""
+    GEOMS = {11: [(21, 11), (10, 11), (0, 10)], 7: [(21, 11), (14, 7), (7, 7), (0, 7)]}
 
     def prepare(self, x, n_total, qs):
         self.x = np.concatenate([b.numpy() for b in x]) if isinstance(x, (list, tuple)) else x.numpy()
@@ -152,34 +225,45 @@ class NumpyQuantileOps:
         self.rank = np.tile(np.array(tg, dtype=np.int64), (self.cols, 1))
         self.prefix = np.zeros((self.cols, self.ntg), dtype=np.uint64)
         self.nan = np.zeros(self.cols, dtype=bool)
-        self._hist = torch.zeros(self.cols * self.ntg * 2048, dtype=torch.int64)
 
-    def hist_tensor(self):
-        return self._hist
+    def set_radix(self, radix_bits):
+        self.radix, self.geom = radix_bits, self.GEOMS[radix_bits]
+        self._slices = []
+        for p in range(len(self.geom)):
+            stride = 2048 if (p == 0 or radix_bits == 11) else 128
+            self._slices.append((torch.zeros((1 if p == 0 else self.ntg) * self.cols * stride, dtype=torch.int32),
+                                 stride))
+        return len(self.geom)
+
+    def hist_tensor(self, p):
+        return self._slices[p][0]
 
     def hist(self, p):
-        shift, bits = self.GEOM[p]
-        h = np.zeros((self.cols, self.ntg, 2048), dtype=np.int64)
+        shift, bits = self.geom[p]
+        t_out, stride = self._slices[p]
+        nt = 1 if p == 0 else self.ntg
+        h = np.zeros((nt, self.cols, stride), dtype=np.int64)
         for c in range(self.cols):
             k = self.keys[c]
             dg = (k >> np.uint64(shift)) & np.uint64((1 << bits) - 1)
             if p == 0:
-                h[c, 0] = np.bincount(dg.astype(np.int64), minlength=2048)
+                h[0, c] = np.bincount(dg.astype(np.int64), minlength=stride)
             else:
                 hs = shift + bits
                 for t in range(self.ntg):
                     m = (k >> np.uint64(hs)) == (self.prefix[c, t] >> np.uint64(hs))
-                    h[c, t] = np.bincount(dg[m].astype(np.int64), minlength=2048)
-        self._hist.copy_(torch.from_numpy(h.reshape(-1)))
+                    h[t, c] = np.bincount(dg[m].astype(np.int64), minlength=stride)
+        t_out.copy_(torch.from_numpy(h.reshape(-1).astype(np.int32)))
 
     def select(self, p):
-        shift, bits = self.GEOM[p]
-        h = self._hist.numpy().reshape(self.cols, self.ntg, 2048)
+        shift, bits = self.geom[p]
+        t_in, stride = self._slices[p]
+        h = t_in.numpy().view(np.uint32).astype(np.int64).reshape(1 if p == 0 else self.ntg, self.cols, stride)
         for c in range(self.cols):
-            if p == 0 and h[c, 0, 2047]:
+            if p == 0 and h[0, c, 2047]:
                 self.nan[c] = True
             for t in range(self.ntg):
-                hh = h[c, 0 if p == 0 else t, : 1 << bits]
+                hh = h[0 if p == 0 else t, c, : 1 << bits]
                 cum = np.cumsum(hh)
                 b = int(np.searchsorted(cum, self.rank[c, t], side="right"))
                 b = min(b, (1 << bits) - 1)

@@ -42,8 +42,12 @@ def _worker(rank, world, port, case, q):
             arr = np.load(os.path.join(HERE, "golden", "bpe_corpora.npz"))[case[1]]
             shard = arr[rank::world]
             flat, off = fixed_rows_to_device(torch.from_numpy(shard.astype(np.int64)))
-            res = train_bpe(flat, off, case[2], ops=NumpyBpeOps(), reduce=red, replicate=case[3])
-            assert res.stats["replicated"] == case[3]
+            mode = case[3]
+            res = train_bpe(flat, off, case[2], ops=NumpyBpeOps(batched=mode != "per_merge_allreduce"), reduce=red,
+                            replicate=mode == "gather_words")
+            assert res.stats["replicated"] == (mode == "gather_words")
+            assert res.stats["sharded"] == (mode != "gather_words")
+            assert res.stats["device_loop"] == (mode != "per_merge_allreduce")
             q.put((rank, res.vocab, [list(m) for m in res.merges], res.min_token, res.max_token))
         else:
             from beast_tokenizer_amd.quantile import column_quantiles
@@ -71,14 +75,15 @@ def _run(case, world=2):
     return sorted(out, key=lambda t: t[0])
 
 
-@pytest.mark.parametrize("replicate", [True, False], ids=["gather_words", "per_merge_allreduce"])
+@pytest.mark.parametrize("mode", ["gather_words", "sharded_batched", "per_merge_allreduce"])
 @pytest.mark.parametrize("cname,vs", [("rand256", 700), ("skew", 2048), ("runs", 700)])
-def test_bpe_two_ranks_matches_hf(cname, vs, replicate):
-    """Both multi-rank forms: the shards' distinct words all-gathered once then a local
-    loop on every rank, and the per-merge delta all-reduce."""
+def test_bpe_two_ranks_matches_hf(cname, vs, mode):
+    """Every multi-rank form: the shards' distinct words all-gathered once then the batched loop
+    on every rank; sharded words with the batched loop's per-pass delta all-reduce; sharded words
+    with the host-driven loop's per-merge delta all-reduce."""
     import json
     ref = json.load(open(os.path.join(HERE, "golden", "bpe_hf.json")))[f"{cname}/{vs}"]
-    (r0, v0, m0, lo0, hi0), (r1, v1, m1, lo1, hi1) = _run(("bpe", cname, vs, replicate))
+    (r0, v0, m0, lo0, hi0), (r1, v1, m1, lo1, hi1) = _run(("bpe", cname, vs, mode))
     assert v0 == v1 and m0 == m1 and (lo0, hi0) == (lo1, hi1)
     assert (lo0, hi0) == (ref["min_token"], ref["max_token"])
     assert v0 == ref["vocab"]

@@ -1,7 +1,8 @@
 """Multi-rank BPE training on the GPU kernels: two processes share cuda:0 over gloo (the
 box has one GPU; RCCL needs one GPU per rank), each training on its half of a golden
-corpus, both multi-rank forms of ``train_bpe`` (words all-gathered then a device-driven
-loop on every rank, and the per-merge delta all-reduce); the result must be HF's."""
+corpus, every multi-rank form of ``train_bpe`` (words all-gathered then the batched device loop
+on every rank; sharded words with the batched loop's per-pass delta all-reduce; sharded words
+with the host-driven loop's per-merge all-reduce); the result must be HF's."""
 import json
 import os
 import socket
@@ -21,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, cname, vs, replicate, q):
+def _worker(rank, world, port, cname, vs, mode, q):
     sys.path.insert(0, os.path.dirname(HERE))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -34,27 +35,28 @@ def _worker(rank, world, port, cname, vs, replicate, q):
         arr = np.load(os.path.join(HERE, "golden", "bpe_corpora.npz"))[cname]
         shard = torch.from_numpy(arr[rank::world].astype(np.int64)).to(dev)
         flat, off = fixed_rows_to_device(shard)
-        res = train_bpe(flat, off, vs, reduce=torch_dist_reducer(), replicate=replicate)
+        res = train_bpe(flat, off, vs, reduce=torch_dist_reducer(), replicate=mode == "gather_words",
+                        device_loop=mode != "sharded_host")
         torch.cuda.synchronize()
         q.put((rank, res.vocab, [list(m) for m in res.merges], res.stats.get("replicated"),
-               res.stats.get("device_loop", False)))
+               res.stats.get("device_loop", False), res.stats.get("sharded")))
     except BaseException as e:  # report instead of hanging the parent
-        q.put((rank, repr(e), None, None, None))
+        q.put((rank, repr(e), None, None, None, None))
         raise
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("replicate", [True, False], ids=["gather_words", "per_merge_allreduce"])
-def test_bpe_two_ranks_gpu_matches_hf(gpu_device, replicate):
+@pytest.mark.parametrize("mode", ["gather_words", "sharded_batched", "sharded_host"])
+def test_bpe_two_ranks_gpu_matches_hf(gpu_device, mode):
     import multiprocessing as mp
     cname, vs = "skew", 2048
     ref = json.load(open(os.path.join(HERE, "golden", "bpe_hf.json")))[f"{cname}/{vs}"]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, cname, vs, replicate, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cname, vs, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -64,9 +66,10 @@ def test_bpe_two_ranks_gpu_matches_hf(gpu_device, replicate):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for rank, vocab, merges, replicated, device_loop in out:
+    for rank, vocab, merges, replicated, device_loop, sharded in out:
         assert merges is not None, vocab
-        assert replicated == replicate and device_loop == replicate
+        assert replicated == (mode == "gather_words") and sharded == (mode != "gather_words")
+        assert device_loop == (mode != "sharded_host")
         assert vocab == ref["vocab"]
         assert merges == ref["merges"]
 

@@ -5,8 +5,9 @@ Contracts:
   * params: |gpu - ref| <= 1e-5 * max(1, |ref row|_inf) (the reference's own fp32
     LU error is ~2e-6 of that scale); vs the float64 oracle fit: within the fp32
     fma-chain bound (T + 8) * 2^-24 * sum_t |P[n,t] y[t]|;
-  * tokens end-to-end: equal to the reference except where the reference's
-    normalised value lies within 1e-3 of a .5 rounding tie (counted);
+  * tokens end-to-end: equal to the reference except where the exact fit's
+    normalised value lies within TIE_TOL = 5e-4 of a .5 rounding tie (counted; observed
+    at most 4.0e-4 over the 7e7 tokens of the K5 corpus, 2.0e-4 at B = 4,096);
   * positions: |gpu - ref| <= 1e-5 * max(1, |ref|_inf per trajectory).
 """
 import hashlib
@@ -29,7 +30,7 @@ from oracle import beast_oracle as O  # noqa: E402
 sys.path.insert(0, GOLDEN)
 from kat_inputs import quantile_inputs  # noqa: E402
 
-TIE_TOL = 1e-3
+TIE_TOL = 5e-4   # observed max 4.0e-4 (K5 census, tests/golden/k5_bpe.json), 2.0e-4 at K2/K3
 
 
 def make_tok(name, g, dev, cls=BEASTBsplineTokenizer, **kw):
@@ -197,7 +198,8 @@ def test_flip_census_4096(name, gpu_device, kernel_mode):
     g["w_min"], g["w_max"] = z["w_min"], z["w_max"]
     tok = make_tok(name, g, gpu_device)
     tokens, _ = tok.encode(torch.from_numpy(x))
-    n = check_token_flips(tokens.cpu().numpy(), z["tokens"].astype(np.int64), x, g, name, max_flips=60)
+    # observed: 21 flips of 573,440 tokens at K2 (bench token census); about twice that is the bar
+    n = check_token_flips(tokens.cpu().numpy(), z["tokens"].astype(np.int64), x, g, name, max_flips=45)
     print(f"{name}: {n} tie flips of {tokens.numel()} tokens")
 
 
@@ -211,7 +213,7 @@ def test_specialised_kernels_equal_generic(name, gpu_device):
     tok = make_tok(name, g, gpu_device)
     x = torch.from_numpy(synth_trajectories(1000, 50, CONFIGS[name]["num_dof"], seed=3, gripper_indices=gi))
     outs = []
-    for mode in ("generic", "specialised_w4", "specialised_w7", "specialised_w8", "specialised_w9", "specialised"):
+    for mode in ("generic", "specialised_w4", "specialised_w7", "specialised_w8", "specialised"):
         set_kernel_mode(mode)
         try:
             t, pd = tok.encode(x)
@@ -331,11 +333,19 @@ def test_update_bounds(name, golden, gpu_device):
     assert np.array_equal(tokens.cpu().numpy(), want.reshape(B, D, 10).transpose(0, 2, 1).reshape(B, -1))
 
 
-def test_quantile_kat(gpu_device):
-    from beast_tokenizer_amd.quantile import column_quantiles
+def _identity_reduce(t, op):
+    """A one-rank stand-in for an all-reduce: column_quantiles then takes the multi-rank radix
+    (11/7/7/7-bit digits, small histogram slices)."""
+    return None
+
+
+@pytest.mark.parametrize("reduce", [None, _identity_reduce], ids=["radix11", "radix7"])
+def test_quantile_kat(gpu_device, reduce):
+    from beast_tokenizer_amd.quantile import column_quantiles, no_reduce
+    reduce = reduce or no_reduce
     z = load_npz("quantile_kat.npz")
     for k, x in quantile_inputs().items():
-        q = column_quantiles(torch.from_numpy(x).to(gpu_device), [0.01, 0.99]).cpu().numpy()
+        q = column_quantiles(torch.from_numpy(x).to(gpu_device), [0.01, 0.99], reduce).cpu().numpy()
         assert np.array_equal(q[0], z[k + "_lo"].astype(np.float32)), k
         assert np.array_equal(q[1], z[k + "_hi"].astype(np.float32)), k
     # row blocks read in place (fit_parameters' per-batch params) == one matrix
@@ -344,12 +354,12 @@ def test_quantile_kat(gpu_device):
             continue
         cuts = [0, 3, x.shape[0] // 2, x.shape[0] // 2, x.shape[0]]
         blocks = [torch.from_numpy(x[a:b]).to(gpu_device) for a, b in zip(cuts[:-1], cuts[1:])]
-        q = column_quantiles(blocks, [0.01, 0.99]).cpu().numpy()
+        q = column_quantiles(blocks, [0.01, 0.99], reduce).cpu().numpy()
         assert np.array_equal(q[0], z[k + "_lo"].astype(np.float32)), k
         assert np.array_equal(q[1], z[k + "_hi"].astype(np.float32)), k
     xn = quantile_inputs()["n101"].copy()
     xn[7, 3] = np.nan
-    q = column_quantiles(torch.from_numpy(xn).to(gpu_device), [0.01, 0.99]).cpu().numpy()
+    q = column_quantiles(torch.from_numpy(xn).to(gpu_device), [0.01, 0.99], reduce).cpu().numpy()
     ref = np.quantile(xn, [0.01, 0.99], axis=0)
     assert np.array_equal(np.isnan(q), np.isnan(ref)) and np.isnan(q[:, 3]).all()
     assert np.array_equal(q[~np.isnan(q)], ref[~np.isnan(ref)].astype(np.float32))
@@ -460,90 +470,28 @@ def test_bpe_train_matches_hf(case, bpe_golden, gpu_device):
     assert st.tokenizer.decode(ids) == text
 
 
-@pytest.mark.parametrize("index_mode", ["index", "tiny_pool", "no_index", "compact"])
 @pytest.mark.parametrize("case", ["skew/2048", "rand256/700", "traj_k3/2048"])
-def test_bpe_merge_paths_match_hf(case, index_mode, bpe_golden, gpu_device):
-    """The merge loop's fallbacks give HF's merges too: an index pool that overflows (lists
-    unknown -> every word visited), no index at all, and periodic compaction."""
-    from beast_tokenizer_amd import _lib
-    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+def test_bpe_host_loop_and_compaction_match_hf(case, bpe_golden, gpu_device):
+    """The host-driven loop (one merge per call: the fallback for vocabularies above 4,096 and on a
+    string-hash collision), with and without periodic compaction of the words that cannot merge
+    any more, gives HF's merges."""
+    from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
     ref, corpora = bpe_golden
     cname, vs = case.split("/")
-    arr = corpora[cname]
-
-    class Ops(GpuBpeOps):
-        def build_index(self, words, Vt):
-            if index_mode == "index":
-                return GpuBpeOps.build_index(self, words, Vt)
-            if index_mode == "no_index":
-                self._index = None
-                return
-            nb = _lib.load().beast_bpe_index_workspace_bytes(Vt, Vt + 64)
-            self._index = torch.empty((nb + 3) // 4, dtype=torch.int32, device=self.device)
-            _lib.run("beast_bpe_build_index", words["sym"].data_ptr(), words["wstart"].data_ptr(),
-                     words["wlen"].data_ptr(), words["n_words"], Vt, self._index.data_ptr(), nb, self.stream)
-    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
-    res = train_bpe(flat, off, int(vs), ops=Ops(gpu_device) if index_mode != "compact" else None,
-                    compact_every=3 if index_mode == "compact" else 0, use_index=index_mode != "compact")
-    assert res.vocab == ref[case]["vocab"]
-    assert [list(m) for m in res.merges] == ref[case]["merges"]
-
-
-@pytest.mark.parametrize("mode", ["pair_index", "lists_always", "pair_index_tiny_pool", "no_pair_lists",
-                                  "reuse_flag", "signature_scan"])
-@pytest.mark.parametrize("case", ["skew/2048", "rand256/700", "traj_k2/2048", "repeat700/300", "wide3000/2048"])
-def test_bpe_merge_modes_match_hf(case, mode, bpe_golden, gpu_device):
-    """The device loop's candidate sources all give HF's merges: the pair index (setup-pair CSR +
-    merged-token word lists), a token pool too small for the lists (lists INEXACT -> those merges
-    visit every word), a loop without the setup-pair CSR (every merge visits every word), and the
-    Bloom-signature scan of round 1.  The per-merge rewrite counts are consistent."""
-    from beast_tokenizer_amd import _lib
-    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
-    ref, corpora = bpe_golden
-    cname, vs = case.split("/")
-
-    class Ops(GpuBpeOps):
-        def build_pair_index(self, words, n_sym, Vt):
-            GpuBpeOps.build_pair_index(self, words, n_sym, Vt)
-            if mode == "pair_index_tiny_pool":
-                tb = _lib.load().beast_bpe_index_workspace_bytes(Vt, 16)
-                self._tokix = torch.empty((tb + 3) // 4, dtype=torch.int32, device=self.device)
-                _lib.run("beast_bpe_token_index_init", self._tokix.data_ptr(), tb, Vt, self.stream)
-            if mode == "reuse_flag":     # as after an id re-use: every merge scans
-                self._tokix[2 * Vt + 3] = 1
     flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
-    ops = Ops(gpu_device)
-    if mode == "no_pair_lists":
-        ops._pair_nsym = 0
-        orig = ops.build_pair_index
-
-        def no_csr(words, n_sym, Vt):
-            orig(words, n_sym, Vt)
-            ops._pair = torch.empty(0, dtype=torch.uint8, device=gpu_device)   # non-None, null CSR below
-        ops.build_pair_index = no_csr
-    lib = _lib.load()
-    assert lib.beast_set_option(_lib.OPT_MERGE_LIST_RATIO, 0 if mode == "lists_always" else 16) == 0
-    try:
-        res = train_bpe(flat, off, int(vs), ops=ops,
-                        merge_mode="signature_scan" if mode == "signature_scan" else "pair_index")
-    finally:
-        lib.beast_set_option(_lib.OPT_MERGE_LIST_RATIO, 16)
-    assert res.vocab == ref[case]["vocab"]
-    assert [list(m) for m in res.merges] == ref[case]["merges"]
-    if mode != "signature_scan":
-        apps = np.asarray(res.stats["applications"])
-        visits = np.asarray(res.stats["words_visited"])
-        assert len(apps) == len(res.merges) and (apps >= 1).all()
-        assert apps.sum() <= res.stats["n_syms_distinct"] and (visits >= 1).all()
-        if mode in ("reuse_flag", "no_pair_lists"):
-            assert (visits == res.stats["n_distinct"]).all()
+    for compact in (0, 3):
+        res = train_bpe(flat, off, int(vs), device_loop=False, compact_every=compact)
+        assert res.stats["loop"] == "host"
+        assert res.vocab == ref[case]["vocab"]
+        assert [list(m) for m in res.merges] == ref[case]["merges"]
 
 
 @pytest.mark.parametrize("lds_min", [0, 1 << 30])
 @pytest.mark.parametrize("case", ["skew/2048", "traj_k3/2048"])
 def test_bpe_delta_paths_match_hf(case, lds_min, bpe_golden, gpu_device):
-    """k_merge's pair-count deltas privatised in LDS for every merge (threshold 0) and by global
-    atomics for every merge (threshold 2^30) both give HF's merges (default: LDS from 4,096)."""
+    """The merge kernels' pair-count changes summed in LDS first for every merge (threshold 0) and
+    by global atomics for every merge (threshold 2^30) both give HF's merges (default: LDS from
+    4,096), in the batched device loop and the host-driven loop."""
     from beast_tokenizer_amd import _lib
     from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
     ref, corpora = bpe_golden
@@ -553,10 +501,12 @@ def test_bpe_delta_paths_match_hf(case, lds_min, bpe_golden, gpu_device):
     assert lib.beast_set_option(_lib.OPT_MERGE_LDS_MIN, lds_min) == 0
     try:
         res = train_bpe(flat, off, int(vs))
+        res2 = train_bpe(flat, off, int(vs), device_loop=False)
     finally:
         lib.beast_set_option(_lib.OPT_MERGE_LDS_MIN, 4096)
-    assert res.vocab == ref[case]["vocab"]
-    assert [list(m) for m in res.merges] == ref[case]["merges"]
+    for r in (res, res2):
+        assert r.vocab == ref[case]["vocab"]
+        assert [list(m) for m in r.merges] == ref[case]["merges"]
 
 
 def test_bpe_pretok_words_match_hf(gpu_device):
@@ -739,7 +689,7 @@ def test_conditions_match_reference(case, gpu_device):
         tok.reconstruct_traj(torch.from_numpy(rt[:5]).to(gpu_device))    # conditions fitted on 32 rows
 
 
-@pytest.mark.parametrize("loop", ["steps", "persistent", "batch"])
+@pytest.mark.parametrize("loop", ["batch"])
 @pytest.mark.parametrize("case", ["traj_k2/2048", "skew/700", "wide3000/2048", "repeat700/300", "runs/2048"])
 def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     """The device-driven merge loop (merges decided on the GPU, ids by string hash, replayed and
@@ -750,7 +700,7 @@ def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     cname, vs = case.split("/")
     flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(gpu_device))
     ops = GpuBpeOps(gpu_device)
-    ops._loop_kind = loop            # one launch for the whole loop, or two per merge
+    ops._loop_kind = loop
     res = train_bpe(flat, off, int(vs), ops=ops)
     assert res.stats.get("device_loop") is True and res.stats.get("loop") == loop
     assert res.vocab == ref[case]["vocab"]
@@ -785,7 +735,7 @@ def test_bpe_batched_loop_matches_hf(case, loop, bpe_golden, gpu_device):
     assert res.vocab == ref[case]["vocab"]
 
 
-@pytest.mark.parametrize("loop", ["batch", "steps"])
+@pytest.mark.parametrize("loop", ["batch", "host"])
 @pytest.mark.parametrize("special,max_len,min_freq", [
     ((), 10000, 2), (("<pad>", "<eos>"), 10000, 2), ((), 3, 2), ((), 10000, 5), (("<s>",), 2, 3), ((), 4, 7)])
 def test_train_options_match_live_hf(special, max_len, min_freq, loop, gpu_device):
@@ -807,9 +757,8 @@ def test_train_options_match_live_hf(special, max_len, min_freq, loop, gpu_devic
     m = json.loads(bpe._tokenizer.to_str())["model"]
     flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
     ops = GpuBpeOps(gpu_device)
-    ops._loop_kind = loop
     res = train_bpe(flat, off, 1500, min_frequency=min_freq, special_tokens=special, max_token_length=max_len,
-                    ops=ops)
+                    ops=ops, device_loop=loop != "host")
     assert res.stats.get("loop") == loop
     assert [list(x) for x in res.merges] == [list(x) for x in m["merges"]]
     assert res.vocab == m["vocab"]

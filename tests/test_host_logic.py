@@ -22,15 +22,23 @@ from beast_tokenizer_amd.quantile import column_quantiles
 
 
 # ------------------------------------------------------------ BPE driver ----
-@pytest.mark.parametrize("case", ["rand256/700", "skew/2048", "runs/700", "wide3000/2048", "traj_k3/700"])
-def test_train_bpe_single_rank_matches_hf(case):
+@pytest.mark.parametrize("batched", [False, True], ids=["host_loop", "batched_model"])
+@pytest.mark.parametrize("case", ["rand256/700", "skew/2048", "runs/700", "wide3000/2048", "traj_k3/700",
+                                  "repeat700/300", "repeat700/2048"])
+def test_train_bpe_single_rank_matches_hf(case, batched):
+    """The driver on the numpy model of the host-driven loop and of the batched device loop
+    (batch rules: disjoint top pairs, self-pair / id re-use ends a batch, min_frequency stop)."""
     ref = load_json("bpe_hf.json").get(case)
     if ref is None:
         pytest.skip(f"no golden {case}")
     cname, vs = case.split("/")
     arr = load_npz("bpe_corpora.npz")[cname]
     flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)))
-    res = train_bpe(flat, off, int(vs), ops=NumpyBpeOps())
+    ops = NumpyBpeOps(batched=batched)
+    res = train_bpe(flat, off, int(vs), ops=ops)
+    assert res.stats["device_loop"] == batched
+    if batched:
+        assert res.stats["passes"] < len(res.merges) or len(res.merges) < 2
     assert (res.min_token, res.max_token) == (ref["min_token"], ref["max_token"])
     assert res.vocab == ref["vocab"]
     assert [list(m) for m in res.merges] == ref["merges"]
@@ -60,10 +68,11 @@ def test_train_bpe_options_match_hf(special, max_len, min_freq):
     alpha = [chr(i) for i in range(hi - lo + 1)]
     v_ref, m_ref = _hf_train(strings, alpha, 1200, min_freq, special, max_len)
     flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)))
-    res = train_bpe(flat, off, 1200, min_frequency=min_freq, special_tokens=special, max_token_length=max_len,
-                    ops=NumpyBpeOps())
-    assert res.vocab == v_ref
-    assert [list(m) for m in res.merges] == m_ref
+    for batched in (False, True):
+        res = train_bpe(flat, off, 1200, min_frequency=min_freq, special_tokens=special, max_token_length=max_len,
+                        ops=NumpyBpeOps(batched=batched))
+        assert res.vocab == v_ref
+        assert [list(m) for m in res.merges] == m_ref
 
 
 def test_train_bpe_vocab_smaller_than_alphabet():
@@ -104,8 +113,14 @@ def test_fixed_rows_to_device():
 
 
 # ------------------------------------------------------- quantile driver ----
+def _identity_reduce(t, op):
+    """One rank standing in for an all-reduce: the driver then takes the multi-rank radix."""
+    return None
+
+
+@pytest.mark.parametrize("reduce", [None, _identity_reduce], ids=["radix11", "radix7"])
 @pytest.mark.parametrize("rows", [1, 2, 3, 7, 100, 1001])
-def test_column_quantiles_driver(rows):
+def test_column_quantiles_driver(rows, reduce):
     rng = np.random.default_rng(rows)
     x = rng.standard_normal((rows, 5)).astype(np.float32)
     x[:, 1] = 0.5                               # constant column
@@ -113,7 +128,8 @@ def test_column_quantiles_driver(rows):
     if rows > 3:
         x[1, 3] = np.nan                        # NaN propagates as in np.quantile
     x[:, 4] = np.round(x[:, 4])                 # many duplicates
-    out = column_quantiles(torch.from_numpy(x), [0.01, 0.99], ops=NumpyQuantileOps()).numpy()
+    from beast_tokenizer_amd.bpe_train import no_reduce
+    out = column_quantiles(torch.from_numpy(x), [0.01, 0.99], reduce or no_reduce, ops=NumpyQuantileOps()).numpy()
     # the reference calls np.quantile with a scalar q (beast_bspline_tokenizer.py:213-214): float32 result
     ref = np.stack([np.quantile(x, q, axis=0) for q in (0.01, 0.99)])
     assert ref.dtype == np.float32

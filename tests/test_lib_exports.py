@@ -86,22 +86,28 @@ def test_shape_validation():
 
 
 def test_batched_loop_validation():
-    """beast_bpe_loop_batch checks its pointers, the batch cap and the workspace size before any
-    HIP call; its workspace query is pure."""
+    """beast_bpe_loop_batch checks its pointers, the batch cap, the flags and the workspace size
+    before any HIP call; its workspace queries are pure."""
     lib = _lib.load()
     fake = C.c_void_p(16)
     nb = lib.beast_bpe_batch_workspace_bytes(2048)
     assert nb >= 2048 * 8 and nb == lib.beast_bpe_batch_workspace_bytes(2048)
-    args = [fake, 2048, 8000, 1, 8, fake, fake, fake, fake, 100, fake, 10000, fake, fake, fake, fake, nb, 2048, 1,
-            None]
+    assert lib.beast_bpe_batch_delta_count(2048) == 8 * 4 * 2048
+    # ws, Vt, max_merges, n_steps, max_batch, flags, sym, wstart, wlen, wcount, n_words, tlen, max_len, sig,
+    # table, argws, batch_ws, batch_ws_bytes, vocab_size, deltas, apps, stream
+    args = [fake, 2048, 8000, 1, 8, 1, fake, fake, fake, fake, 100, fake, 10000, fake, fake, fake, fake, nb, 2048,
+            None, None, None]
     bad_null = list(args)
-    bad_null[12] = None                       # signatures are required by the batched loop
+    bad_null[13] = None                       # signatures are required by the batched loop
     assert lib.beast_bpe_loop_batch(*bad_null) == _lib.BEAST_E_INVALID
     bad_k = list(args)
     bad_k[4] = 3                              # max_batch must be 2, 4 or 8
     assert lib.beast_bpe_loop_batch(*bad_k) == _lib.BEAST_E_INVALID
+    bad_flags = list(args)
+    bad_flags[5] = 8                          # unknown flag bit
+    assert lib.beast_bpe_loop_batch(*bad_flags) == _lib.BEAST_E_INVALID
     small = list(args)
-    small[16] = nb - 256                      # workspace too small
+    small[17] = nb - 256                      # workspace too small
     assert lib.beast_bpe_loop_batch(*small) == _lib.BEAST_E_WORKSPACE
     wide = list(args)
     wide[1] = 8192                            # Vt beyond the batched loop's 4,096
@@ -112,7 +118,11 @@ def test_batched_loop_validation():
 
 def test_workspace_queries_are_pure():
     lib = _lib.load()
-    assert lib.beast_quantile_hist_count(14, 2) == 14 * 2 * 2048 * 2
+    assert lib.beast_quantile_hist_count(0, 14, 2, 11) == 14 * 2048            # pass 0: target 0's slice
+    assert lib.beast_quantile_hist_count(1, 14, 2, 11) == 4 * 14 * 2048
+    assert lib.beast_quantile_hist_count(0, 14, 2, 7) == 14 * 2048
+    assert lib.beast_quantile_hist_count(2, 14, 2, 7) == 4 * 14 * 128
+    assert (lib.beast_quantile_passes(11), lib.beast_quantile_passes(7), lib.beast_quantile_passes(8)) == (3, 4, 0)
     assert lib.beast_quantile_workspace_bytes(1000, 14, 2) > 1000 * 14 * 4
     assert lib.beast_scan_workspace_bytes(1 << 20) > 0
     assert lib.beast_colminmax_workspace_bytes(10 ** 6, 14) > 0
@@ -142,9 +152,10 @@ def test_options_validate_and_reset():
     lib = _lib.load()
     assert lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 1) == 0
     assert lib.beast_set_option(_lib.OPT_GENERIC_KERNELS, 0) == 0
-    for w in (4, 7, 8, 9, 0):
+    for w in (4, 7, 8, 0):
         assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, w) == 0
-    assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, 5) == _lib.BEAST_E_INVALID
+    for w in (5, 9):
+        assert lib.beast_set_option(_lib.OPT_BLOCK_WAVES, w) == _lib.BEAST_E_INVALID
     assert lib.beast_set_option(99, 0) == _lib.BEAST_E_INVALID
     assert b"option" in lib.beast_last_error()
 
@@ -159,3 +170,18 @@ def test_encode_list_validation():
     assert lib.beast_encode_list_f32(fake, 3, 4096, 49, 7, 7, 7, fake, fake, 10, fake, None) == _lib.BEAST_E_INVALID
     assert lib.beast_encode_list_f32(fake, -1, 4096, 50, 14, 14, 14, fake, fake, 10, fake, None) == _lib.BEAST_E_INVALID
     assert lib.beast_encode_list_f32(fake, 0, 4096, 50, 14, 14, 14, fake, fake, 10, fake, None) == 0
+
+
+def test_stale_fastpath_is_not_loaded(monkeypatch):
+    """A host fast-path library whose .sha256 stamp does not match csrc/fastpath.cpp is never
+    loaded (it may lack entry points the plan binds); the tokenizer then runs the ctypes path."""
+    from beast_tokenizer_amd import _build
+    from beast_tokenizer_amd import beast_bspline_tokenizer as bt
+    saved = bt._FAST
+    try:
+        monkeypatch.setattr(_build, "_fastpath_digest", lambda: "0" * 64)
+        bt._FAST = None
+        assert not _build.fastpath_current()
+        assert bt._fastpath() is None
+    finally:
+        bt._FAST = saved
