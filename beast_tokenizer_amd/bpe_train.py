@@ -168,7 +168,7 @@ class GpuBpeOps:
         on = torch.empty(1, dtype=torch.int64, device=dev)
         ws = torch.empty(_lib.load().beast_bpe_repack_workspace_bytes(nu), dtype=torch.uint8, device=dev)
         m = max(nu, 1)
-        sym2 = torch.empty(max(cap, 1), dtype=torch.int16, device=dev)
+        sym2 = torch.empty(max(cap + 3 * nu, 1), dtype=torch.int16, device=dev)   # spans rounded up to 4
         w2, l2, c2 = (torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3))
         _lib.run("beast_bpe_repack_words", sym.data_ptr(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), nu,
                  ws.data_ptr(), ws.numel(), sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), c2.data_ptr(),
@@ -178,14 +178,15 @@ class GpuBpeOps:
         sym2 = sym2[:max(ns, 1)].clone()
         sig = torch.empty(m, dtype=torch.int64, device=dev)
         _lib.run("beast_bpe_word_signatures", sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), nu, sig.data_ptr(), s)
+        live = int(l2[:nu].sum()) if nu else 0
         return dict(words, sym=sym2, wstart=w2, wlen=l2, wcount=c2, sig=sig, n_words=nu, n_distinct=nu,
-                    n_syms_distinct=ns)
+                    n_syms_distinct=live, n_syms_padded=ns)
 
     def gather_words(self, words, gather):
         """Every rank's distinct words x counts on every rank (one all-gather per array),
         repacked for the merge loop.  Ranks are concatenated in rank order, so all ranks
         hold identical word arrays."""
-        n, ns = words["n_words"], words.get("n_syms_distinct", 0)
+        n, ns = words["n_words"], words.get("n_syms_padded", 0)
         syms = gather(words["sym"][:ns].to(torch.int32))      # RCCL has no int16
         starts = gather(words["wstart"][:n].contiguous())
         lens = gather(words["wlen"][:n].contiguous())

@@ -30,7 +30,7 @@
 namespace {
 
 constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;
-constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
+[[maybe_unused]] constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
 constexpr int WAVES = 4;            // rows in flight per workgroup (decode)
 constexpr int ENC_MAX_WAVES = 16;   // encode: as many rows per workgroup as the LDS holds, up to 16
 constexpr int BLOCK = 64 * WAVES;

@@ -117,10 +117,22 @@ __device__ __forceinline__ uint32_t merge_global(uint16_t* __restrict__ s, uint3
   return o;
 }
 
-// a word of L <= MERGE_REG symbols in registers (sentinels past the end)
+// A word of L <= MERGE_REG symbols in registers (sentinels past the end).  Words start at a
+// multiple of 4 symbols and own their span rounded up to 4 (beast_bpe_repack_words), so the word
+// is read as 8-byte units -- at most 8 loads in flight, not 32 two-byte ones.
 __device__ __forceinline__ void load_word(const uint16_t* __restrict__ s, uint32_t L, uint32_t (&v)[MERGE_REG + 2]) {
+  const uint2* __restrict__ p = reinterpret_cast<const uint2*>(s);
 #pragma unroll
-  for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? (uint32_t)s[i] : 0xFFFFFFFFu;
+  for (int q = 0; q < MERGE_REG / 4; ++q) {
+    uint2 u = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    if ((uint32_t)(4 * q) < L) u = p[q];
+    v[4 * q] = u.x & 0xFFFFu;
+    v[4 * q + 1] = u.x >> 16;
+    v[4 * q + 2] = u.y & 0xFFFFu;
+    v[4 * q + 3] = u.y >> 16;
+  }
+#pragma unroll
+  for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? v[i] : 0xFFFFFFFFu;
   v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
 }
 __device__ __forceinline__ bool word_has_pair(const uint32_t (&v)[MERGE_REG + 2], uint32_t a, uint32_t b) {
@@ -129,13 +141,16 @@ __device__ __forceinline__ bool word_has_pair(const uint32_t (&v)[MERGE_REG + 2]
   for (int i = 0; i < MERGE_REG - 1; ++i) hit |= (v[i] == a) & (v[i + 1] == b);
   return hit;
 }
-// the merge of a word held in v (which holds the pair) written back to s
+// The merge of a word held in v (which holds the pair), written back to s as 8-byte units: the
+// output symbols collect in a 64-bit accumulator that is stored whenever it holds four (the
+// units past the new length are the word's own dead span).
 template <class Op>
 __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2], uint32_t L, uint16_t* __restrict__ s,
                                                int32_t cnt, const Op& m, unsigned long long& g, uint32_t& napp) {
   const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
+  uint2* __restrict__ out = reinterpret_cast<uint2*>(s);
   uint32_t o = 0, last = 0, skip = 0;
-  unsigned long long sg = 0;
+  unsigned long long sg = 0, acc = 0;
 #pragma unroll
   for (int i = 0; i < MERGE_REG; ++i) {
     if ((uint32_t)i < L) {
@@ -151,11 +166,17 @@ __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2
         skip = 1;
         ++napp;
       }
-      s[o++] = (uint16_t)y;
+      acc |= (unsigned long long)y << (16 * (o & 3u));
+      ++o;
+      if ((o & 3u) == 0) {
+        out[(o >> 2) - 1] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
+        acc = 0;
+      }
       last = y;
       sg |= sig_bit(y);
     }
   }
+  if (o & 3u) out[o >> 2] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
   g = sg;
   return o;
 }
@@ -394,8 +415,9 @@ constexpr int BATCH_LDS = 32768;      // bytes of LDS delta vectors per workgrou
 constexpr int BATCH_WG_LANE = 4;      // apply-workgroup lists per lane of the deciding wave (Vt <= 4096)
 
 // The loop's device state: counters, the string hash table's geometry and the batch the next
-// k_merge_batch applies.  Everything but `ticket` is written by ONE thread: the deciding lane of
-// k_apply_batch (or k_loop_init); every other kernel only reads it, after a kernel boundary.
+// k_merge_batch applies.  The batch record (b*) is written by the deciding wave of k_apply_batch
+// (or k_loop_init); the counters (vcur, n_merges, maxtlen) by workgroup 0 of k_merge_batch when
+// it commits the batch; every other reader is in a later kernel.
 struct LoopState {
   int32_t active;        // 0 once the loop has stopped (later launches are no-ops)
   int32_t vcur;          // vocabulary size (committed merges)
@@ -407,8 +429,9 @@ struct LoopState {
   int32_t maxtlen;       // longest committed token (HF length units)
   uint32_t ticket;       // k_apply_batch workgroups arrived in this launch
   int32_t passes;        // batches decided
-  // the batch the next k_merge_batch applies
+  // the batch the next k_merge_batch applies (and commits: its workgroup 0)
   int32_t bn;            // merges (0: none; the loop has stopped)
+  int32_t bv0, bnm0;     // vocabulary size and merges logged before the batch
   int32_t bvcur;         // vocabulary size after the batch
   int32_t bkd;           // merges 0 .. bkd-1 sum their pair-count changes in LDS first
   int32_t bmt;           // longest token a word can hold during the batch (its new ones included)
@@ -422,35 +445,45 @@ struct LoopState {
 // (h, len) -> id; equal strings always collide (HF reuses the id), different strings collide
 // with probability ~2^-64 -- the host re-checks every logged merge against the real strings
 // and reruns on the host-driven loop if it ever finds one (beast_tokenizer_amd/bpe_train.py).
-constexpr uint32_t LOOP_EMPTY = 0xFFFFFFFFu;
+// A slot is two 8-byte words loaded together (one round trip per probe step): the hash, and
+// (length << 32 | id), all ones while the slot is free.
+constexpr unsigned long long LOOP_EMPTY = ~0ull;
 struct LoopHash {
   unsigned long long* key;   // [cap] h
-  uint32_t* klen;            // [cap] byte length, LOOP_EMPTY = free slot
-  int32_t* kid;              // [cap]
+  unsigned long long* lid;   // [cap] byte length << 32 | id, LOOP_EMPTY = free slot
   unsigned long long* th;    // [Vt] token hash
   unsigned long long* tp;    // [Vt] P^len
   int32_t* log;              // [max_merges][4] a, b, nid, reused
 };
+__device__ __forceinline__ unsigned long long lid_of(uint32_t len, int id) {
+  return ((unsigned long long)len << 32) | (uint32_t)id;
+}
 
 __device__ __forceinline__ uint64_t loop_slot(unsigned long long h, uint32_t len, int log2cap) {
   return ((h ^ ((unsigned long long)len * 0x9E3779B97F4A7C15ull)) * 0xbf58476d1ce4e5b9ull) >> (64 - log2cap);
 }
 
+constexpr int KR = 4;   // candidate pairs per table row: its KR best, in HF order
+// Each row's cached keys: rowtop[x][0 .. RT_K) descending (0 past them) are exactly the row's keys
+// >= rowtop[x][RT_F] (the floor; 1 when they are all its positive keys).  A batch changes a row
+// outside b_j / new_j only at known columns, so re-reading those keeps the invariant; the row is
+// re-ranked in full only when fewer than KR + 1 keys stay above a floor > 1.
+constexpr int RT_K = 12, RT_F = 15, RT_STRIDE = 16;
 struct BatchWs {
-  unsigned long long* rowsecond;      // [Vt]
-  unsigned long long* wgkey;          // [BK][nwg] each apply workgroup's BK best rows, best first (k-major:
-  unsigned long long* wgsec;          // [BK][nwg]  the deciding wave reads them coalesced) and their second-best
+  unsigned long long* rowtop;         // [Vt][RT_STRIDE]: the row caches above
+  unsigned long long* wgkey;          // [BK][nwg] each apply workgroup's BK best candidates, best first (k-major:
+  unsigned long long* wgsec;          // [BK][nwg]  the deciding wave reads them coalesced) and their rows' bounds
 };
 __host__ __device__ inline int batch_nwg(int Vt) { return (Vt + APPLY_ROWS - 1) / APPLY_ROWS; }
 __host__ __device__ inline size_t batch_ws_bytes(int Vt) {
-  return ((size_t)Vt * 8 + (size_t)batch_nwg(Vt) * BK * 2 * 8 + 255) & ~size_t(255);
+  return ((size_t)Vt * RT_STRIDE * 8 + (size_t)batch_nwg(Vt) * BK * 2 * 8 + 255) & ~size_t(255);
 }
 __host__ __device__ inline BatchWs batch_view(void* ws, int Vt) {
   BatchWs v;
   char* p = static_cast<char*>(ws);
   const size_t nt = (size_t)batch_nwg(Vt) * BK;
-  v.rowsecond = reinterpret_cast<unsigned long long*>(p);
-  v.wgkey = v.rowsecond + Vt;
+  v.rowtop = reinterpret_cast<unsigned long long*>(p);
+  v.wgkey = v.rowtop + (size_t)Vt * RT_STRIDE;
   v.wgsec = v.wgkey + nt;
   return v;
 }
@@ -547,6 +580,146 @@ __device__ __forceinline__ void top_merge(unsigned long long (&K)[KM], unsigned 
       }
 }
 
+// The row's RT_K best keys (descending, 0 past its positive pairs) and its floor, by the whole
+// wave, into out[RT_STRIDE] (LDS).  A key is count << 32 | ~(x * Vt + y): larger = earlier in HF
+// order.  Lane `lane` holds columns i * 64 + lane of each 2,048-column stretch (neighbouring ids
+// -- frequent tokens often are -- on different lanes); it keeps its best two by (count desc,
+// column asc) -- its columns rise with i, so a strict '>' keeps the first of equal counts -- and
+// wave-max rounds pop the owner's current one.  A lane popped past its second rescans its counts below the last one
+// (registers for one stretch; Vt <= 4,096 is two).  RT_K rounds: the cache outlives many batches.
+constexpr int ROW_STRETCH = 2048;
+__device__ __forceinline__ void row_counts(const uint32_t* __restrict__ row, int Vt, int vcur, int lane, int base,
+                                           int32_t (&c)[32]) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int y = base + i * 64 + lane;
+    c[i] = y < vcur ? (int32_t)row[y] : 0;
+  }
+}
+__device__ __forceinline__ int row_col(int idx, int lane) {   // idx = stretch * 32 + i
+  return (idx >> 5) * ROW_STRETCH + (idx & 31) * 64 + lane;
+}
+__device__ __forceinline__ unsigned long long row_key(int32_t cnt, int x, int Vt, int y) {
+  return cnt > 0 ? ((unsigned long long)(uint32_t)cnt << 32) | (unsigned long long)(~((uint32_t)x * (uint32_t)Vt + (uint32_t)y))
+                 : 0ull;
+}
+__device__ __forceinline__ int key_col(unsigned long long k, int x, int Vt) {
+  return (int)(~(uint32_t)k - (uint32_t)x * (uint32_t)Vt);
+}
+
+__device__ __forceinline__ void rank_row_top(const uint32_t* __restrict__ row, int x, int Vt, int vcur, int lane,
+                                             unsigned long long* __restrict__ out) {
+  const int nst = (vcur + ROW_STRETCH - 1) / ROW_STRETCH;
+  int32_t c[32];
+  int32_t c1 = 0, c2 = 0;
+  int i1 = -1, i2 = -1;
+  for (int st = 0; st < nst; ++st) {
+    row_counts(row, Vt, vcur, lane, st * ROW_STRETCH, c);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int32_t v = c[i];
+      const int idx = st * 32 + i;
+      const bool g1 = v > c1, g2 = v > c2;
+      c2 = g1 ? c1 : (g2 ? v : c2);
+      i2 = g1 ? i1 : (g2 ? idx : i2);
+      c1 = g1 ? v : c1;
+      i1 = g1 ? idx : i1;
+    }
+  }
+  int32_t cc = c1;
+  int ci = i1;
+  bool second = true;   // (c2, i2) is the lane's next
+  unsigned long long w = 0ull;
+#pragma unroll 1
+  for (int r = 0; r < RT_K; ++r) {   // rolled: one copy of the body stays in the instruction cache
+    const unsigned long long k = row_key(cc, x, Vt, row_col(ci, lane));
+    w = wave_max_u64(k);
+    if (lane == 0) out[r] = w;
+    if (r + 1 < RT_K && w != 0ull && k == w) {   // the owner (keys are distinct) moves to its next
+      if (second) {
+        cc = c2;
+        ci = i2;
+        second = false;
+      } else {   // rare: its best below (cc, ci)
+        int32_t nc = 0;
+        int ni = -1;
+        for (int st = 0; st < nst; ++st) {
+          if (nst > 1) row_counts(row, Vt, vcur, lane, st * ROW_STRETCH, c);
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            const int32_t v = c[i];
+            const int idx = st * 32 + i;
+            const bool take = ((v < cc) | ((v == cc) & (idx > ci))) & (v > nc);   // no short-circuit branches
+            nc = take ? v : nc;
+            ni = take ? idx : ni;
+          }
+        }
+        cc = nc;
+        ci = ni;
+      }
+    }
+  }
+  if (lane == 0) out[RT_F] = w != 0ull ? w : 1ull;
+}
+
+// A row outside b_j / new_j after a batch: only its columns a_j (less), new_j (more) and, for
+// x = a_j, b_j (retired) changed.  The cached keys at those columns are dropped, their current
+// keys >= the floor added (lanes 32 + 8t + j: column t of merge j, a repeat column once), and the
+// candidates ranked by one pass over them: still exactly the row's keys >= the floor.  The top
+// RT_K are kept (the floor rises to the last kept when some are cut).  Returns false (a full
+// re-rank is needed) when fewer than KR + 1 remain above a floor > 1.  The wave calls it together.
+__device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row, const unsigned long long* __restrict__ g,
+                                               int x, int Vt, int lane, int n, const int (&A)[BK], const int (&B)[BK],
+                                               const int (&N)[BK], unsigned long long* __restrict__ out) {
+  int col[3 * BK];   // uniform: the changed columns, -1 unused
+#pragma unroll
+  for (int j = 0; j < BK; ++j) {
+    col[j] = j < n ? A[j] : -1;
+    col[BK + j] = j < n ? N[j] : -1;
+    col[2 * BK + j] = j < n && A[j] == x ? B[j] : -1;
+  }
+  const unsigned long long F = g[RT_F];
+  unsigned long long k = 0ull;
+  if (lane < RT_K) {
+    k = g[lane];
+    const int y = key_col(k, x, Vt);
+    bool drop = false;
+#pragma unroll
+    for (int t = 0; t < 3 * BK; ++t) drop |= y == col[t];
+    k = drop ? 0ull : k;
+  } else if (lane >= 32 && lane < 32 + 3 * BK) {
+    const int sl = lane - 32;
+    int y = -1;
+#pragma unroll
+    for (int t = 0; t < 3 * BK; ++t) y = t == sl ? col[t] : y;
+    bool rep = false;
+#pragma unroll
+    for (int t = 0; t < 3 * BK; ++t) rep |= t < sl && col[t] == y;
+    if (y >= 0 && !rep) {
+      k = row_key((int32_t)row[y], x, Vt, y);
+      k = k >= F ? k : 0ull;
+    }
+  }
+  unsigned long long m = __builtin_amdgcn_ballot_w64(k != 0ull);
+  const int cnt = __builtin_popcountll(m);
+  if (cnt < KR + 1 && F > 1ull) return false;
+  int rank = 0;
+  while (m) {   // uniform
+    const int c = __builtin_ctzll(m);
+    m &= m - 1;
+    rank += readlane_u64(k, c) > k;
+  }
+  if (k != 0ull && rank < RT_K) out[rank] = k;
+  if (lane >= cnt && lane < RT_K) out[lane] = 0ull;
+  unsigned long long f = F;
+  if (cnt > RT_K) {   // cut: the floor is the last kept key
+    const unsigned long long last = __builtin_amdgcn_ballot_w64(k != 0ull && rank == RT_K - 1);
+    f = readlane_u64(k, __builtin_ctzll(last));
+  }
+  if (lane == 0) out[RT_F] = f;
+  return true;
+}
+
 // Per-pass phase stamps (tools builds with -DBPE_MERGE_STAMPS=<first pass>; the product library
 // compiles them out): s_memrealtime (100 MHz) of thread 0 of the first 1024 merge workgroups at
 // entry, after the record, after the scan, before the delta flush and at exit, and of the
@@ -554,6 +727,12 @@ __device__ __forceinline__ void top_merge(unsigned long long (&K)[KM], unsigned 
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][6];
 __device__ unsigned long long g_bpe_dstamps[64][8];
+__device__ unsigned long long g_apply_stamps[64][256][12];
+#define ASTAMP(pi, k)                                                                                     \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && (pi) >= BPE_MERGE_STAMPS && (pi) < BPE_MERGE_STAMPS + 64)  \
+      g_apply_stamps[(pi) - BPE_MERGE_STAMPS][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();           \
+  } while (0)
 #define MSTAMP(pi, k)                                                                                     \
   do {                                                                                                    \
     if (threadIdx.x == 0 && blockIdx.x < 1024 && (pi) >= BPE_MERGE_STAMPS && (pi) < BPE_MERGE_STAMPS + 64) \
@@ -567,6 +746,7 @@ __device__ unsigned long long g_bpe_dstamps[64][8];
 #else
 #define MSTAMP(pi, k) do { } while (0)
 #define DSTAMP(pi, k) do { } while (0)
+#define ASTAMP(pi, k) do { } while (0)
 #endif
 
 // The merges of the batch the last k_apply_batch decided, over every word: one scan of the word
@@ -578,17 +758,24 @@ __device__ unsigned long long g_bpe_dstamps[64][8];
 // rewritten per merge, unweighted, at apps[n_merges + j].
 __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                      uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
-                                                     int64_t nw, const uint32_t* __restrict__ tlen, int max_len,
+                                                     int64_t nw, uint32_t* __restrict__ tlen, int max_len,
                                                      int Vt, unsigned long long* __restrict__ sig,
-                                                     const LoopState* __restrict__ loop, uint32_t* __restrict__ table,
-                                                     uint32_t* __restrict__ clean, int32_t* __restrict__ deltas,
-                                                     uint32_t* __restrict__ apps) {
+                                                     LoopState* __restrict__ loop, LoopHash lh,
+                                                     uint32_t* __restrict__ table, uint32_t* __restrict__ clean,
+                                                     int32_t* __restrict__ deltas, uint32_t* __restrict__ apps) {
   __shared__ __attribute__((aligned(16))) int32_t dl[BATCH_LDS / 4];
   __shared__ uint32_t clist[BATCH_CLIST];
   __shared__ int cn, touched;
   __shared__ int s_a[BK], s_b[BK], s_nid[BK];
   __shared__ uint32_t s_len[BK], s_apps[BK];
   __shared__ unsigned long long s_need[BK];
+#ifdef BPE_MERGE_STAMPS
+  const int st_pi = loop->passes;
+#define KB_PI st_pi
+#else
+#define KB_PI 0
+#endif
+  MSTAMP(KB_PI, 0);
   // the batch record (threads < BK), then the first signature batch of the two-phase scan
   int ra = 0, rb = 0, rn = 0;
   uint32_t rl = 0;
@@ -607,14 +794,35 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     sgv[u] = w < nw ? sig[w] : 0ull;
   }
   if (n == 0) return;   // the loop has stopped (uniform)
-#ifdef BPE_MERGE_STAMPS
-  const int st_pi = loop->passes;
-#define KB_PI st_pi
-#else
-#define KB_PI 0
-#endif
-  MSTAMP(KB_PI, 0);
-  const int vcur = loop->vcur, kd = loop->bkd, mt = loop->bmt;
+  const int vcur = loop->bv0, kd = loop->bkd, mt = loop->bmt, nm0 = loop->bnm0;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // commit the batch, merge j on lane j: its string into the hash table (distinct strings, so
+    // concurrent inserts only race for free slots), the new token's hash / P^len / length, its log
+    // entry; then the counters.  No other workgroup of this launch reads what this writes: they
+    // take the vocabulary before the batch from bv0 and the new tokens' lengths from the record.
+    const int j = threadIdx.x;
+    if (j < n) {
+      const int reused = loop->breused[j];
+      if (!reused) {
+        const unsigned long long h = loop->bh[j];
+        const unsigned long long pa = lh.tp[ra], pb = lh.tp[rb];
+        const uint64_t hmask = (1ull << loop->log2cap) - 1;
+        uint64_t sl = loop_slot(h, rl, loop->log2cap);
+        while (atomicCAS(&lh.lid[sl], LOOP_EMPTY, lid_of(rl, rn)) != LOOP_EMPTY) sl = (sl + 1) & hmask;
+        lh.key[sl] = h;
+        lh.th[rn] = h;
+        lh.tp[rn] = pa * pb;
+        tlen[rn] = rl;
+      }
+      int32_t* lg = lh.log + 4 * (int64_t)(nm0 + j);
+      lg[0] = ra; lg[1] = rb; lg[2] = rn; lg[3] = reused;
+    }
+    if (j == 0) {
+      loop->n_merges = nm0 + n;
+      loop->vcur = loop->bvcur;
+      loop->maxtlen = mt;
+    }
+  }
   if (threadIdx.x < BK) {
     s_a[threadIdx.x] = ra;
     s_b[threadIdx.x] = rb;
@@ -643,7 +851,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   };
   // the batch's merges in order on one word; its symbols are read once (a rare second merge
   // in the same word re-reads them)
-  auto visit = [&](int64_t w, unsigned long long sgw) {
+  auto visit = [&](int64_t w) {
     uint32_t L = wlen[w];
     uint16_t* s = sym + wstart[w];
     const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
@@ -655,10 +863,8 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       load_word(s, L, v);
       uint32_t hits = 0;
 #pragma unroll 1
-      for (int j = 0; j < n; ++j) {
-        const unsigned long long nd = s_need[j];
-        if ((sgw & nd) == nd && word_has_pair(v, (uint32_t)s_a[j], (uint32_t)s_b[j])) hits |= 1u << j;
-      }
+      for (int j = 0; j < n; ++j)
+        if (word_has_pair(v, (uint32_t)s_a[j], (uint32_t)s_b[j])) hits |= 1u << j;
       if (!hits) return;
       // one merge_regs pass per set bit: lanes of a wave holding different merges share it
       // (the op is per lane), so a wave runs as many passes as its lanes' most merges (~1)
@@ -674,6 +880,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       }
       changed = true;
     } else {
+      const unsigned long long sgw = sig[w];
 #pragma unroll 1
       for (int j = 0; j < n; ++j) {
         const unsigned long long nd = s_need[j];
@@ -695,43 +902,44 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     sig[w] = g;
   };
   // two-phase scan: a word is a candidate if its signature holds some merge's pair.  Rounds of
-  // MERGE_SCAN signatures per thread append to the LDS list; it is processed once at the end, or
-  // earlier when another round could overflow it (visit is inlined once).
-  for (int64_t c0 = blockIdx.x;; c0 += (int64_t)MERGE_SCAN * gridDim.x) {
-    const bool more = c0 < nchunks;   // uniform
-    if (more) {
-      if (c0 != blockIdx.x) {
-#pragma unroll
-        for (int u = 0; u < MERGE_SCAN; ++u) {
-          const int64_t w = (c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
-          sgv[u] = w < nw ? sig[w] : 0ull;
-        }
-      }
+  // MERGE_SCAN signatures per thread append to the LDS list, the next round's loads in flight
+  // while this round is tested; the list is processed once at the end, or earlier when another
+  // round could overflow it (visit is inlined once).
+  const int64_t step = (int64_t)MERGE_SCAN * gridDim.x;
+  for (int64_t c0 = blockIdx.x; c0 < nchunks; c0 += step) {   // uniform
+    unsigned long long nxt[MERGE_SCAN];
+    const bool ahead = c0 + step < nchunks;
+    if (ahead) {
 #pragma unroll
       for (int u = 0; u < MERGE_SCAN; ++u) {
-        bool hit = false;
-#pragma unroll
-        for (int j = 0; j < BK; ++j) hit |= (sgv[u] & need[j]) == need[j];
-        if (hit) clist[atomicAdd(&cn, 1)] = (uint32_t)((c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x);
+        const int64_t w = (c0 + step + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
+        nxt[u] = w < nw ? sig[w] : 0ull;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < MERGE_SCAN; ++u) {
+      bool hit = false;
+#pragma unroll
+      for (int j = 0; j < BK; ++j) hit |= (sgv[u] & need[j]) == need[j];
+      if (hit) clist[atomicAdd(&cn, 1)] = (uint32_t)((c0 + (int64_t)u * gridDim.x) * 256 + threadIdx.x);
     }
     __syncthreads();
     const int nc = cn;
-    if (!more || nc > BATCH_CLIST - 256 * MERGE_SCAN) {
+    if (!ahead || nc > BATCH_CLIST - 256 * MERGE_SCAN) {
       MSTAMP(KB_PI, 2);
-      for (int k = threadIdx.x; k < nc; k += 256) {
-        const int64_t w = clist[k];
-        visit(w, sig[w]);
-      }
+      for (int k = threadIdx.x; k < nc; k += 256) visit(clist[k]);
       __syncthreads();
       if (threadIdx.x == 0) cn = 0;
       __syncthreads();
     }
-    if (!more) break;
+    if (ahead) {
+#pragma unroll
+      for (int u = 0; u < MERGE_SCAN; ++u) sgv[u] = nxt[u];
+    }
   }
   MSTAMP(KB_PI, 3);
   if (apps != nullptr && threadIdx.x < n && s_apps[threadIdx.x])
-    atomicAdd(&apps[loop->n_merges + threadIdx.x], s_apps[threadIdx.x]);
+    atomicAdd(&apps[nm0 + threadIdx.x], s_apps[threadIdx.x]);
   if (kd == 0) { MSTAMP(KB_PI, 4); return; }
   if (any) touched = 1;
   __syncthreads();
@@ -767,9 +975,15 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
                                                                  LoopState* __restrict__ loop, LoopHash lh, int nrows,
                                                                  int init, int32_t* __restrict__ deltas,
                                                                  long long lds_min) {
-  __shared__ unsigned long long wbest[APPLY_ROWS], wsec[APPLY_ROWS];
-  __shared__ int changed_w[APPLY_ROWS];
+  __shared__ unsigned long long s_top[APPLY_ROWS][RT_STRIDE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef BPE_MERGE_STAMPS
+  const int st_pi = loop->passes;
+#define KA_PI st_pi
+#else
+#define KA_PI 0
+#endif
+  ASTAMP(KA_PI, 0);
   const int n = init ? 0 : loop->bn;
   if (!init && (n == 0 || !loop->active)) return;   // uniform over the grid
   int A[BK], B[BK], N[BK];
@@ -782,21 +996,26 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   const int vcur = init ? loop->vcur : loop->bvcur;
   const int x0 = blockIdx.x * APPLY_ROWS;
   const int x = x0 + wave;
-  // rows the merges changed: clean[x] == 0 (k_merge_batch's adds through (x, a_j), (x, new_j)),
-  // and a_j, b_j, new_j
-  int changed = init;
+  // rows the merges changed: b_j, new_j entirely (re-ranked); other rows x only at columns a_j,
+  // new_j (k_merge_batch's adds: clean[x] == 0; or the sharded deltas: touched) and, for x = a_j,
+  // b_j (retired below)
+  int full = init, in_a = 0;
 #pragma unroll
-  for (int j = 0; j < BK; ++j) changed |= x == A[j] || x == B[j] || x == N[j];   // -1 past n
+  for (int j = 0; j < BK; ++j) {   // -1 past n
+    full |= x == B[j] || x == N[j];
+    in_a |= x == A[j];
+  }
+  int touched = 0;
   if (deltas != nullptr && n > 0) {
     // sharded: the all-reduced changes.  (1) each wave's entries (x, a_j), (x, new_j)
     if (lane == 0 && x < nrows)
       for (int j = 0; j < n; ++j) {
         int32_t* d = deltas + (size_t)j * 4 * Vt;
         int32_t v;
-        if ((v = d[x])) { atomicAdd(&table[(size_t)x * Vt + A[j]], (uint32_t)v); d[x] = 0; changed = 1; }
-        if ((v = d[Vt + x])) { atomicAdd(&table[(size_t)x * Vt + N[j]], (uint32_t)v); d[Vt + x] = 0; changed = 1; }
+        if ((v = d[x])) { atomicAdd(&table[(size_t)x * Vt + A[j]], (uint32_t)v); d[x] = 0; touched = 1; }
+        if ((v = d[Vt + x])) { atomicAdd(&table[(size_t)x * Vt + N[j]], (uint32_t)v); d[Vt + x] = 0; touched = 1; }
       }
-    changed = __builtin_amdgcn_readfirstlane(changed);   // the wave ranks its row together
+    touched = __builtin_amdgcn_readfirstlane(touched);   // the wave ranks its row together
     // (2) rows b_j and new_j entirely, by the workgroup that owns them (distinct rows: a batch
     //     of more than one merge has fresh ids and symbol-disjoint pairs)
     for (int j = 0; j < n; ++j)
@@ -816,94 +1035,87 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #pragma unroll
     for (int j = 0; j < BK; ++j)
       if (x == A[j]) table[(size_t)x * Vt + B[j]] = 0u;   // never re-picked
-  unsigned long long best = 0, second = 0;
+  // every row's KR best keys and its bound, in LDS: cached when the row did not change
+  unsigned long long* rt = s_top[wave];
   if (x < nrows && x < vcur) {
-    if (aw.clean[x] && !changed) {
-      best = aw.rowbest[x];
-      second = bw.rowsecond[x];
+    unsigned long long* g = bw.rowtop + (size_t)x * RT_STRIDE;
+    const uint32_t* row = table + (size_t)x * Vt;
+    if (!full && !touched && !in_a && aw.clean[x]) {
+      if (lane <= KR) rt[lane] = g[lane];
     } else {
-      rank_row(table + (size_t)x * Vt, x, Vt, vcur, lane, best, second);
-      if (lane == 0) {
-        aw.rowbest[x] = best;
-        bw.rowsecond[x] = second;
-        aw.clean[x] = 1u;
+#ifdef BPE_MERGE_STAMPS
+      const bool st_on = lane == 0 && blockIdx.x < 256 && KA_PI >= BPE_MERGE_STAMPS && KA_PI < BPE_MERGE_STAMPS + 64;
+      unsigned long long* st_a = st_on ? g_apply_stamps[KA_PI - BPE_MERGE_STAMPS][blockIdx.x] : nullptr;
+      if (st_on) atomicMax(&st_a[4], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      const bool upd = !full && row_top_update(row, g, x, Vt, lane, n, A, B, N, rt);
+      if (st_on) atomicMax(&st_a[5], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+      if (!upd) {   // the row's first stretch loaded and used, then the rank (cache hits)
+        int32_t cw[32];
+        row_counts(row, Vt, vcur, lane, 0, cw);
+        int acc = 0;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc += cw[i];
+        if (acc == 0x7fffffff) atomicAdd(&st_a[9], 1ull);
+        if (st_on) atomicMax(&st_a[8], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        rank_row_top(row, x, Vt, vcur, lane, rt);
       }
+      if (st_on) {
+        atomicMax(&st_a[6], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        atomicAdd(&st_a[7], upd ? 1ull : 1ull << 32);
+      }
+#else
+      if (full || !row_top_update(row, g, x, Vt, lane, n, A, B, N, rt)) rank_row_top(row, x, Vt, vcur, lane, rt);
+#endif
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < RT_K || lane == RT_F) g[lane] = rt[lane];
+      if (lane == 0) aw.clean[x] = 1u;
+#ifdef BPE_MERGE_STAMPS
+      if (lane == 0 && blockIdx.x < 256 && KA_PI >= BPE_MERGE_STAMPS && KA_PI < BPE_MERGE_STAMPS + 64)
+        atomicAdd(&g_apply_stamps[KA_PI - BPE_MERGE_STAMPS][blockIdx.x][3], 1ull);   // rows re-ranked
+#endif
     }
+  } else if (lane <= KR) {
+    rt[lane] = 0ull;
   }
-  if (lane == 0) { wbest[wave] = best; wsec[wave] = second; }
   __syncthreads();
+  ASTAMP(KA_PI, 1);
   if (wave != 0) return;
   const int nwg = batch_nwg(Vt);
-  if (lane < APPLY_ROWS) {   // this workgroup's BK best rows, best first: row w goes to its rank
-    const int w = lane;
-    const unsigned long long kw = wbest[w];
-    int rank = 0;   // rows above w (ties -- only empty rows -- by index)
-#pragma unroll
-    for (int v = 0; v < APPLY_ROWS; ++v) rank += wbest[v] > kw || (wbest[v] == kw && v < w);
+  {   // this workgroup's BK best of its APPLY_ROWS x KR candidates, best first, with their rows' bounds
+    const int w = lane / KR, r = lane % KR;   // 64 lanes = 16 rows x 4
+    const unsigned long long kw = s_top[w][r];
+    int rank = 0;   // candidates above this one (keys are distinct; empty ones by lane)
+    for (int v = 0; v < APPLY_ROWS * KR; ++v) {
+      const unsigned long long kv = s_top[v / KR][v % KR];
+      rank += kv > kw || (kv == kw && v < lane);
+    }
     if (rank < BK) {
       st_agent(&bw.wgkey[(size_t)rank * nwg + blockIdx.x], kw);   // the grid may cover fewer rows than Vt
-      st_agent(&bw.wgsec[(size_t)rank * nwg + blockIdx.x], kw ? wsec[w] : 0ull);
+      st_agent(&bw.wgsec[(size_t)rank * nwg + blockIdx.x], kw ? s_top[w][KR] : 0ull);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   uint32_t t = 0;
   if (lane == 0) t = __hip_atomic_fetch_add(&loop->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+  ASTAMP(KA_PI, 2);
   if (t != gridDim.x - 1) return;
   // ---- the last workgroup's wave 0: commit the batch just applied, decide the next one
-#ifdef BPE_MERGE_STAMPS
-  const int st_pi = loop->passes;
-#define KA_PI st_pi
-#else
-#define KA_PI 0
-#endif
   DSTAMP(KA_PI, 0);
-  // the loop state in registers (uniform): this wave writes it below and never re-reads it
+  // the loop state in registers (uniform): this wave writes only the record below.  The batch
+  // just applied was committed by k_merge_batch's workgroup 0 (a kernel boundary ago).
   const int log2cap = loop->log2cap, target = loop->target, maxm = loop->max_merges;
   const unsigned long long minf = (unsigned long long)loop->min_freq;
-  int nm = loop->n_merges, mt = loop->maxtlen;
-  const int vnow = vcur;   // the vocabulary once this batch is committed
-  if (n > 0) {
-    if (lane == 0) {
-      const uint64_t mask = (1ull << log2cap) - 1;
-      for (int j = 0; j < n; ++j) {
-        const int reused = loop->breused[j];
-        const uint32_t len = loop->blen[j];
-        if (!reused) {
-          const unsigned long long h = loop->bh[j];
-          uint64_t sl = loop_slot(h, len, log2cap);
-          while (ld_agent(&lh.klen[sl]) != LOOP_EMPTY) sl = (sl + 1) & mask;
-          st_agent(&lh.key[sl], h);
-          st_agent(&lh.kid[sl], N[j]);
-          st_agent(&lh.klen[sl], len);
-          st_agent(&lh.th[N[j]], h);
-          st_agent(&lh.tp[N[j]], ld_agent(&lh.tp[A[j]]) * ld_agent(&lh.tp[B[j]]));
-          st_agent(&tlen[N[j]], len);
-        }
-        int32_t* lg = lh.log + 4 * (int64_t)(nm + j);
-        lg[0] = A[j]; lg[1] = B[j]; lg[2] = N[j]; lg[3] = reused;
-      }
-    }
-    for (int j = 0; j < n; ++j) mt = max(mt, (int)loop->blen[j]);
-    nm += n;
-    if (lane == 0) {
-      loop->n_merges = nm;
-      loop->vcur = vnow;
-      loop->maxtlen = mt;
-    }
-  }
-  if (lane == 0) st_agent(&loop->ticket, 0u);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // lane 0's commit before the other lanes' probes
-  __builtin_amdgcn_wave_barrier();
-  // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
-  // rows each), then KM wave-max rounds hand it out
-  unsigned long long K[KM], S[KM];
-#pragma unroll
-  for (int i = 0; i < KM; ++i) K[i] = S[i] = 0ull;
-#pragma unroll
-  for (int t0 = 0; t0 < BATCH_WG_LANE; t0 += 2) {
-    if (t0 * 64 >= nwg) break;
-    unsigned long long LK[2][KM], LS[2][KM];
+  const int nm = loop->n_merges;
+  int mt = loop->maxtlen;
+  const int vnow = loop->vcur;
+  const uint64_t hmask = (1ull << log2cap) - 1;
+  // the workgroups' lists (the first 128: the whole table up to Vt = 2,048) first: they do not
+  // depend on the commit, so their round trip overlaps it
+  unsigned long long LK[2][KM], LS[2][KM];
+  auto load_lists = [&](int t0) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int g = (t0 + t) * 64 + lane;
@@ -913,6 +1125,17 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
         LS[t][i] = g < nwg ? ld_agent(&bw.wgsec[(size_t)i * nwg + g]) : 0ull;
       }
     }
+  };
+  load_lists(0);
+  if (lane == 0) st_agent(&loop->ticket, 0u);
+  // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
+  // rows each), then KM wave-max rounds hand it out
+  unsigned long long K[KM], S[KM];
+#pragma unroll
+  for (int i = 0; i < KM; ++i) K[i] = S[i] = 0ull;
+  for (int t0 = 0; t0 < BATCH_WG_LANE; t0 += 2) {
+    if (t0 * 64 >= nwg) break;
+    if (t0 > 0) load_lists(t0);
 #pragma unroll
     for (int t = 0; t < 2; ++t) top_merge<KM>(K, S, LK[t], LS[t]);
   }
@@ -945,12 +1168,12 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     cand_b = (int)(idx % (uint32_t)Vt);
     ch = ld_agent(&lh.th[cand_a]) * ld_agent(&lh.tp[cand_b]) + ld_agent(&lh.th[cand_b]);
     clen = ld_agent(&tlen[cand_a]) + ld_agent(&tlen[cand_b]);
-    const uint64_t mask = (1ull << log2cap) - 1;
     uint64_t sl = loop_slot(ch, clen, log2cap);
-    uint32_t kl;
-    while ((kl = ld_agent(&lh.klen[sl])) != LOOP_EMPTY) {
-      if (kl == clen && ld_agent(&lh.key[sl]) == ch) { exist = ld_agent(&lh.kid[sl]); break; }
-      sl = (sl + 1) & mask;
+    while (true) {
+      const unsigned long long li = ld_agent(&lh.lid[sl]), ki = ld_agent(&lh.key[sl]);
+      if (li == LOOP_EMPTY) break;
+      if ((uint32_t)(li >> 32) == clen && ki == ch) { exist = (int)(uint32_t)li; break; }
+      sl = (sl + 1) & hmask;
     }
   }
   DSTAMP(KA_PI, 3);
@@ -966,8 +1189,9 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)clen, i);
     const unsigned long long hi = readlane_u64(ch, i), si = readlane_u64(csec, i);
     const bool ends = ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0);   // self-pair / re-use
-    if (i < lane)
-      ok &= !ends && cand_a != ai && cand_a != bi && cand_b != ai && cand_b != bi && !(ch == hi && clen == li);
+    // a later pair must not chain onto an earlier one (b_j == a_i: (x, a_i) loses count; a_j ==
+    // b_i: (b_i, y) does); sharing a_i as its left or b_i as its right symbol is fine
+    if (i < lane) ok &= !ends && cand_b != ai && cand_a != bi && !(ch == hi && clen == li);
     if (i < lane) sec = umax64(sec, si);
   }
   ok &= sec < ckey;   // a taken row's second-best would come first
@@ -996,6 +1220,8 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   }
   if (lane == 0) {
     loop->bn = nb;
+    loop->bv0 = vnow;
+    loop->bnm0 = nm;
     loop->bvcur = vnow + nb - (reused0 ? 1 : 0);
     loop->bkd = kd;
     loop->bmt = mt;
@@ -1018,8 +1244,8 @@ __global__ void k_loop_init(LoopState* st, LoopState init, LoopHash lh, int n_to
   const uint64_t mask = (1ull << log2cap) - 1;
   uint64_t sl = loop_slot(h, tlen[i], log2cap);
   while (true) {   // the initial tokens are distinct strings
-    const uint32_t prev = atomicCAS(&lh.klen[sl], LOOP_EMPTY, tlen[i]);
-    if (prev == LOOP_EMPTY) { lh.key[sl] = h; lh.kid[sl] = i; break; }
+    const unsigned long long prev = atomicCAS(&lh.lid[sl], LOOP_EMPTY, lid_of(tlen[i], i));
+    if (prev == LOOP_EMPTY) { lh.key[sl] = h; break; }
     sl = (sl + 1) & mask;
   }
 }
@@ -1102,7 +1328,7 @@ static int loop_log2cap(int Vt) {
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct LoopLayout {
-  size_t st, key, klen, kid, th, tp, log, total;
+  size_t st, key, lid, th, tp, log, total;
 };
 
 static LoopLayout loop_layout(int Vt, int max_merges) {
@@ -1111,8 +1337,7 @@ static LoopLayout loop_layout(int Vt, int max_merges) {
   size_t o = 0;
   L.st = o;   o += al256(sizeof(LoopState));
   L.key = o;  o += al256(cap * 8);
-  L.klen = o; o += al256(cap * 4);
-  L.kid = o;  o += al256(cap * 4);
+  L.lid = o;  o += al256(cap * 8);
   L.th = o;   o += al256((size_t)Vt * 8);
   L.tp = o;   o += al256((size_t)Vt * 8);
   L.log = o;  o += al256((size_t)max_merges * 16);
@@ -1125,8 +1350,7 @@ static LoopHash loop_hash_view(void* ws, int Vt, int max_merges) {
   unsigned char* w = static_cast<unsigned char*>(ws);
   LoopHash lh;
   lh.key = reinterpret_cast<unsigned long long*>(w + L.key);
-  lh.klen = reinterpret_cast<uint32_t*>(w + L.klen);
-  lh.kid = reinterpret_cast<int32_t*>(w + L.kid);
+  lh.lid = reinterpret_cast<unsigned long long*>(w + L.lid);
   lh.th = reinterpret_cast<unsigned long long*>(w + L.th);
   lh.tp = reinterpret_cast<unsigned long long*>(w + L.tp);
   lh.log = reinterpret_cast<int32_t*>(w + L.log);
@@ -1139,6 +1363,9 @@ extern "C" int beast_debug_merge_stamps(unsigned long long* host) {
 }
 extern "C" int beast_debug_decide_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_dstamps), sizeof(g_bpe_dstamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int beast_debug_apply_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_apply_stamps), sizeof(g_apply_stamps)) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -1156,7 +1383,7 @@ extern "C" int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_me
   BEAST_REQUIRE_CODE(ws_bytes >= L.total, BEAST_E_WORKSPACE, "loop workspace %zu < %zu", ws_bytes, L.total);
   hipStream_t s = beast::as_stream(stream);
   unsigned char* w = static_cast<unsigned char*>(ws);
-  BEAST_HIP(hipMemsetAsync(w + L.klen, 0xFF, L.kid - L.klen, s), "loop hash memset");
+  BEAST_HIP(hipMemsetAsync(w + L.lid, 0xFF, L.th - L.lid, s), "loop hash memset");
   LoopState init{};
   init.active = 1;
   init.vcur = n_tokens;
@@ -1233,7 +1460,7 @@ extern "C" int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_step
   for (int i = 0; i < n_steps; ++i) {
     if (!(flags & BEAST_BPE_BATCH_NO_MERGE)) {
       hipLaunchKernelGGL(k_merge_batch, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, tlen,
-                         max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, table, aw.clean,
+                         max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, table, aw.clean,
                          deltas, apps);
       BEAST_LAUNCHED("k_merge_batch");
     }

@@ -21,7 +21,7 @@
 
 namespace {
 
-constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
+[[maybe_unused]] constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
 
 // ------------------------------------------------------------- min / max --
 __global__ void k_minmax(const long long* __restrict__ x, int64_t n, long long* __restrict__ out) {
@@ -597,7 +597,9 @@ __global__ __launch_bounds__(256) void k_compact_words(const uint32_t* __restric
 // ------------------------------------------------------------ word repack --
 // Distinct words copied into one contiguous symbol array ordered by length (bucket
 // min(L, 255)): a wave's words are neighbours in memory and of similar length, so the
-// merge scan is coalesced and its per-thread loops stay in step.
+// merge scan is coalesced and its per-thread loops stay in step.  Each word starts at a
+// multiple of 4 symbols and owns its span rounded up to 4: the merge loop reads and writes
+// a word as 8-byte units that no other word shares.
 constexpr int RP_WPB = 2048;   // words per workgroup in the bucket scatter
 
 __global__ __launch_bounds__(256) void k_len_hist(const uint32_t* __restrict__ wlen, int64_t nw,
@@ -652,7 +654,7 @@ __global__ __launch_bounds__(256) void k_gather_lens(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ oc) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t w = order[i];
-    lens[i] = wlen[w];
+    lens[i] = (wlen[w] + 3u) & ~3u;   // the word's span: 4-symbol (8-byte) units of its own
     ol[i] = wlen[w];
     oc[i] = wcount ? wcount[w] : 1u;
   }
@@ -668,6 +670,7 @@ __global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__
     const uint16_t* src = sym + wstart[w];
     uint16_t* dst = osym + offs[i];
     for (uint32_t k = 0; k < L; ++k) dst[k] = src[k];
+    for (uint32_t k = L; k & 3u; ++k) dst[k] = 0;   // the span's padding (never a symbol of the word)
     ow[i] = (uint32_t)offs[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *out_nsym = offs[nw];

@@ -279,9 +279,11 @@ size_t beast_bpe_dedup_workspace_bytes(int64_t n_words);
 int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
                           void* workspace, size_t ws_bytes, uint32_t* out_wstart, uint32_t* out_wlen,
                           uint32_t* out_wcount, int64_t* out_n, void* stream);
-/* Copy words into one contiguous symbol array ordered by length (min(L, 255) buckets,
- * order inside a bucket unspecified): out_sym capacity >= sum of wlen (e.g. the corpus
- * symbol count); *out_nsym (device int64) = symbols written. wcount may be NULL. */
+/* Copy words into one symbol array ordered by length (min(L, 255) buckets, order inside a
+ * bucket unspecified); each word starts at a multiple of 4 symbols (8 bytes) and owns its length
+ * rounded up to 4 (the padding is zero): the layout the merge loops read and write in 8-byte
+ * units.  out_sym capacity >= sum of round_up(wlen, 4); *out_nsym (device int64) = symbols of
+ * the padded layout.  wcount may be NULL. */
 size_t beast_bpe_repack_workspace_bytes(int64_t n_words);
 int beast_bpe_repack_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, const uint32_t* wcount,
                            int64_t n_words, void* workspace, size_t ws_bytes, uint16_t* out_sym,

@@ -20,8 +20,13 @@ class NumpyBpeOps:
     its host-driven loop on these ops."""
     device = torch.device("cpu")
 
-    def __init__(self, batched: bool = False, kmax: int = 8):
-        self.batched, self.kmax = batched, kmax
+    def __init__(self, batched: bool = False, kmax: int = 8, chain_rule: bool = True, row_top: int = 0):
+        # chain_rule: a later member may share a symbol with an earlier one unless it chains onto
+        # it (b_j == a_i or a_j == b_i); False: fully symbol-disjoint batches.
+        # row_top = k > 0: candidates come as the kernels see them -- each row's k best pairs, in
+        # order, and a batch stops where a taken row's (k+1)-th best would come first; 0: the exact
+        # global order
+        self.batched, self.kmax, self.chain_rule, self.row_top = batched, kmax, chain_rule, row_top
 
     def minmax(self, tokens):
         return torch.tensor([int(tokens.min()), int(tokens.max())], dtype=torch.int64)
@@ -134,7 +139,29 @@ class NumpyBpeOps:
         while ntok < vocab_size:
             sub = tb[:ntok, :ntok].astype(np.int64).ravel()
             pos = np.flatnonzero(sub > 0)
-            order = pos[np.lexsort((pos, -sub[pos]))][:km]
+            order = pos[np.lexsort((pos, -sub[pos]))]
+            if self.row_top:
+                # per row its k best (HF order); the (k+1)-th of every row bounds what may follow
+                rows_seen, cand, nxt = {}, [], {}
+                for p in order:
+                    x = int(p) // ntok
+                    c = rows_seen.get(x, 0)
+                    if c < self.row_top:
+                        cand.append(p)
+                    elif c == self.row_top:
+                        nxt[x] = p
+                    rows_seen[x] = c + 1
+                # keep the prefix of cand before which no taken row's next pair ranks
+                rank = {int(p): i for i, p in enumerate(order)}
+                keep, taken = [], set()
+                for p in cand:
+                    bound = min((rank[int(nxt[x])] for x in taken if x in nxt), default=len(order))
+                    if rank[int(p)] > bound:
+                        break
+                    keep.append(p)
+                    taken.add(int(p) // ntok)
+                order = np.array(keep, dtype=np.int64)
+            order = order[:km]
             batch, used, made = [], set(), set()
             for r, p in enumerate(order):
                 c = int(sub[p])
@@ -142,7 +169,11 @@ class NumpyBpeOps:
                 t = id2str[x] + id2str[y] if x < len(id2str) and y < len(id2str) else None
                 if r > 0:
                     pa, pb, _, pre = batch[-1]
-                    if pa == pb or pre or x in used or y in used:
+                    if self.chain_rule:
+                        clash = any(y == ai or x == bi for ai, bi, _, _ in batch)
+                    else:
+                        clash = x in used or y in used
+                    if pa == pb or pre or clash:
                         break
                 exist = strings.get(t) if t is not None else None
                 if (r > 0 and (exist is not None or t in made)) or c < max(1, min_frequency) or \

@@ -586,7 +586,8 @@ def test_bpe_dedup_and_compact_match_counter(gpu_device):
     lens = u["wlen"].cpu().numpy()[: u["n_words"]]
     assert np.all(np.diff(np.minimum(lens, 255)) >= 0)                     # length-ordered
     ws = u["wstart"].cpu().numpy()[: u["n_words"]]
-    assert np.array_equal(ws[1:], ws[:-1] + lens[:-1])                      # contiguous
+    assert np.array_equal(ws[1:], ws[:-1] + (lens[:-1] + 3) // 4 * 4)       # contiguous 4-symbol-aligned spans
+    assert u["n_syms_distinct"] == int(lens.sum()) and u["n_syms_padded"] == int(((lens + 3) // 4 * 4).sum())
     # shorten some words to length 1 / 0 and compact
     wl = u["wlen"].clone()
     wl[::3] = 1

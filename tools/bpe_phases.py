@@ -1,0 +1,130 @@
+"""Phase timeline of the batched BPE merge loop from in-kernel stamps (tools only).
+
+    python tools/bpe_phases.py build P0     # here: tools/libbpe_stamps.so with -DBPE_MERGE_STAMPS=P0
+    python tools/bpe_phases.py run [json]   # on the box: K5 training on that library, passes P0 .. P0+63
+
+Per pass (s_memrealtime, 100 MHz, microseconds from the merge kernel's first workgroup entry):
+merge kernel -- workgroup entry spread, record + LDS clear done, last candidate visit start, scan
+done, exit (median / max over workgroups); apply kernel -- entry, ranks done, ticket taken (median
+/ max), the deciding workgroup's commit + list merge, wave-max rounds, probes, decision written."""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+LIB = os.path.join(HERE, "libbpe_stamps.so")
+
+
+def build(p0: int) -> None:
+    from beast_tokenizer_amd import _build
+    objs = []
+    for f in sorted(os.listdir(_build.CSRC)):
+        if f.endswith(".hip"):
+            o = os.path.join(tempfile.gettempdir(), f"phases_{f}.o")
+            subprocess.run([_build._hipcc(), *_build.CXXFLAGS, *_build.FILE_FLAGS.get(f, []),
+                            f"-DBPE_MERGE_STAMPS={p0}", "-c", os.path.join(_build.CSRC, f), "-o", o], check=True)
+            objs.append(o)
+    subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", LIB, *objs],
+                   check=True)
+    print("built", LIB)
+
+
+def _read(lib, name, shape):
+    buf = (C.c_ulonglong * int(np.prod(shape)))()
+    fn = getattr(lib, name)
+    fn.argtypes = [C.c_void_p]
+    assert fn(buf) == 0, name
+    return np.frombuffer(buf, dtype=np.uint64).reshape(shape).astype(np.int64)
+
+
+def run(out_json=None) -> None:
+    os.environ["BEAST_LIB"] = LIB
+    import torch
+    import bench
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, fixed_rows_to_device, train_bpe
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    rows = bench.k5_corpus(dev, 500000, 0, 1, bench.k5_golden())
+    flat, off = fixed_rows_to_device(rows)
+    seen = {}
+
+    class Ops(GpuBpeOps):   # keeps the word arrays to count the words that can still merge
+        def loop_run(self, words, *a, **kw):
+            wl0 = words["wlen"][:words["n_words"]].clone()
+            out = GpuBpeOps.loop_run(self, words, *a, **kw)
+            wl1 = words["wlen"][:words["n_words"]]
+            seen.update({"distinct_words": int(words["n_words"]), "words_ge2_start": int((wl0 >= 2).sum()),
+                         "words_ge2_end": int((wl1 >= 2).sum()), "symbols_start": int(wl0.sum()),
+                         "symbols_end": int(wl1.sum())})
+            return out
+    res = train_bpe(flat, off, 2048, ops=Ops(dev))
+    torch.cuda.synchronize()
+    ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 6))
+    ds = _read(lib, "beast_debug_decide_stamps", (64, 8))
+    aps = _read(lib, "beast_debug_apply_stamps", (64, 256, 12))
+    us = lambda v: round(float(v) / 100.0, 2)   # noqa: E731
+    passes = []
+    for p in range(64):
+        m = ms[p]
+        ran = m[:, 0] > 0
+        if not ran.any():
+            continue
+        m = m[ran]
+        t0 = m[:, 0].min()
+        a = aps[p]
+        a = a[a[:, 0] > 0]
+        rec = {"wg": int(ran.sum()),
+               "merge_entry_spread": us(m[:, 0].max() - t0),
+               "merge_record_med": us(np.median(m[:, 1] - m[:, 0])),
+               "merge_visit_start_med": us(np.median(m[:, 2] - t0)),
+               "merge_scan_done_med": us(np.median(m[:, 3] - t0)), "merge_scan_done_max": us(m[:, 3].max() - t0),
+               "merge_exit_med": us(np.median(m[:, 4] - t0)), "merge_exit_max": us(m[:, 4].max() - t0)}
+        if len(a):
+            rec.update({"apply_entry_first": us(a[:, 0].min() - t0), "apply_entry_last": us(a[:, 0].max() - t0),
+                        "apply_ranked_med": us(np.median(a[:, 1] - t0)), "apply_ranked_max": us(a[:, 1].max() - t0),
+                        "apply_ticket_med": us(np.median(a[:, 2] - t0)), "apply_ticket_max": us(a[:, 2].max() - t0)})
+            rk = (a[:, 1] - a[:, 0]) / 100.0   # per-workgroup ranking time, by rows re-ranked
+            nr = a[:, 3]
+            rec.update({"apply_wg": int(len(a)), "apply_rows_reranked": int(nr.sum()),
+                        "apply_rank_us_wg_reranking_max": float(rk[nr > 0].max()) if (nr > 0).any() else 0.0,
+                        "apply_rank_us_wg_reranking_med": float(np.median(rk[nr > 0])) if (nr > 0).any() else 0.0,
+                        "apply_rank_us_wg_cached_max": float(rk[nr == 0].max()) if (nr == 0).any() else 0.0,
+                        "apply_rank_us_argmax_wg": int(np.argmax(rk)), "apply_rank_us_argmax_rows": int(nr[np.argmax(rk)])})
+            rr = a[nr > 0]
+            if len(rr):   # re-ranking workgroups: their waves' last flags loaded / update tried / ranked
+                rec.update({"apply_rr_flags_med": us(np.median(rr[:, 4] - rr[:, 0])),
+                            "apply_rr_update_med": us(np.median(rr[:, 5] - rr[:, 0])),
+                            "apply_rr_loaded_med": us(np.median(rr[rr[:, 8] > 0, 8] - rr[rr[:, 8] > 0, 0])),
+                            "apply_rr_ranked_med": us(np.median(rr[:, 6] - rr[:, 0])),
+                            "apply_rr_ranked_max": us((rr[:, 6] - rr[:, 0]).max()),
+                            "apply_rows_incremental": int((rr[:, 7] & 0xFFFFFFFF).sum()),
+                            "apply_rows_full": int((rr[:, 7] >> 32).sum())})
+        d = ds[p]
+        if d[0] > 0:
+            rec.update({"decide_start": us(d[0] - t0), "decide_lists_merged": us(d[1] - t0),
+                        "decide_rounds": us(d[2] - t0), "decide_probed": us(d[3] - t0), "decide_end": us(d[4] - t0)})
+        passes.append(rec)
+    keys = [k for k in passes[0] if k != "wg"]
+    summary = {k: float(np.median([r[k] for r in passes if k in r])) for k in keys}
+    out = {"merges": len(res.merges), "passes": res.stats.get("passes"), "passes_stamped": len(passes),
+           "median_over_passes_us": summary, "words": seen, "per_pass": passes, "loop_s": res.stats["merge_loop_s"]}
+    print(json.dumps({k: out[k] for k in ("merges", "passes", "loop_s", "words")}))
+    print(json.dumps(summary, indent=1))
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(int(sys.argv[2]))
+    else:
+        run(sys.argv[2] if len(sys.argv) > 2 else None)

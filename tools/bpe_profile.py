@@ -1,4 +1,7 @@
-"""BPE training at bench scale (5e5 trajectories, vocab 2048) for rocprofv3 / timing."""
+"""The K5 BPE training (bench.py's bpe leg: 5e5 trajectories, vocab 2048) once or twice, for
+rocprofv3 kernel traces / PMC passes (tools/bpe_trace.sh, tools/bpe_pmc.sh).
+
+    python tools/bpe_profile.py [reps] [--apps]     # --apps: also count pair applications per merge"""
 import json
 import os
 import sys
@@ -8,30 +11,19 @@ import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-from beast_tokenizer_amd import BEASTBsplineTokenizer  # noqa: E402
+import bench  # noqa: E402
 from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe  # noqa: E402
-from beast_tokenizer_amd.synthetic import synth_trajectories  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 500000
-ce = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-ix = bool(int(sys.argv[3])) if len(sys.argv) > 3 else False
-if len(sys.argv) > 4:   # BEAST_OPT_MERGE_LDS_MIN
-    from beast_tokenizer_amd import _lib
-    _lib.load().beast_set_option(_lib.OPT_MERGE_LDS_MIN, int(sys.argv[4]))
+reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1
+apps = "--apps" in sys.argv
 dev = torch.device("cuda", 0)
-tok = BEASTBsplineTokenizer(num_dof=14, device="cuda:0")
-fit = [{"actions": torch.from_numpy(synth_trajectories(4096, 50, 14, seed=1, start=4096 * i))} for i in range(2)]
-tok.fit_parameters(fit, verbose=False)
-rows = []
-for s in range(0, n, 8192):
-    b = min(8192, n - s)
-    rows.append(tok.encode(torch.from_numpy(synth_trajectories(b, 50, 14, seed=7, start=s)).to(dev))[0])
-allrows = torch.cat(rows)
+rows = bench.k5_corpus(dev, 500000, 0, 1, bench.k5_golden())
 torch.cuda.synchronize()
-for rep in range(2):
+for rep in range(reps):
     t0 = time.perf_counter()
-    flat, off = fixed_rows_to_device(allrows)
-    res = train_bpe(flat, off, 2048, compact_every=ce, use_index=ix)
+    flat, off = fixed_rows_to_device(rows)
+    res = train_bpe(flat, off, 2048, count_applications=apps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    print(json.dumps({"rep": rep, "seconds": el, "merges_per_s": res.stats["n_merges"] / el, **res.stats}))
+    st = {k: v for k, v in res.stats.items() if isinstance(v, (int, float, str, bool))}
+    print(json.dumps({"rep": rep, "seconds": el, "merges_per_s": len(res.merges) / el, **st}), flush=True)

@@ -6,4 +6,4 @@ TAG="${1:-bpetrace}"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/$TAG" -o bpe \
-  -- python3 "$R/tools/bpe_profile.py" 500000 0 0 > "$R/gpurun_out/$TAG.log" 2>&1
+  -- python3 "$R/tools/bpe_profile.py" 1 > "$R/gpurun_out/$TAG.log" 2>&1
