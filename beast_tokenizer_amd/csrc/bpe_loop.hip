@@ -60,8 +60,13 @@ __host__ __device__ inline ArgWs argws_view(void* ws, int Vt) {
 // the new length (0: the word holds no (a, b)), the new Bloom signature in g and the occurrences
 // merged in napp.  Words of <= MERGE_REG symbols are read once into registers (all loads in
 // flight together) and rewritten there: the in-place loop over global memory made every symbol a
-// dependent round trip, and a merge waits for its slowest word.
-constexpr int MERGE_REG = 32;
+// dependent round trip, and a merge waits for its slowest word.  48 holds nearly every K5 word
+// (1,050 of 4.85 M exceed 32 symbols, the longest 58; 99.9% <= 27); 64 would cost k_merge_batch
+// a wave per SIMD (174 VGPRs) and measured slower.
+#ifndef BPE_MERGE_REG
+#define BPE_MERGE_REG 48
+#endif
+constexpr int MERGE_REG = BPE_MERGE_REG;
 struct MergeOp {
   int a, b, nid, max_len;
   uint32_t newlen;
@@ -135,49 +140,67 @@ __device__ __forceinline__ void load_word(const uint16_t* __restrict__ s, uint32
   for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? v[i] : 0xFFFFFFFFu;
   v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
 }
-__device__ __forceinline__ bool word_has_pair(const uint32_t (&v)[MERGE_REG + 2], uint32_t a, uint32_t b) {
+// Wave-uniform exit from the unrolled sweeps once no active lane's word reaches position i.
+#define WORD_SWEEP_EXIT(i, L)                                                                  \
+  if (((i) & 7) == 0 && (i) > 0 && __builtin_amdgcn_ballot_w64((uint32_t)(i) < (L)) == 0ull) \
+    break
+__device__ __forceinline__ bool word_has_pair(const uint32_t (&v)[MERGE_REG + 2], uint32_t L, uint32_t a, uint32_t b) {
   bool hit = false;
 #pragma unroll
-  for (int i = 0; i < MERGE_REG - 1; ++i) hit |= (v[i] == a) & (v[i + 1] == b);
+  for (int i = 0; i < MERGE_REG - 1; ++i) {
+    WORD_SWEEP_EXIT(i, L);
+    hit |= (v[i] == a) & (v[i + 1] == b);
+  }
   return hit;
 }
 // The merge of a word held in v (which holds the pair), written back to s as 8-byte units: the
 // output symbols collect in a 64-bit accumulator that is stored whenever it holds four (the
-// units past the new length are the word's own dead span).
+// units past the new length are the word's own dead span).  The sweep is branch-free and marks
+// the occurrences (HF's left-to-right, non-overlapping rule); the pair-count changes then go one
+// occurrence at a time in a rolled loop -- the left neighbour is new when an occurrence starts
+// two symbols before, else v[i - 1], the right one v[i + 2] -- so the code that adds them exists
+// once, not once per position (the unrolled form overflowed the instruction cache).
 template <class Op>
 __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2], uint32_t L, uint16_t* __restrict__ s,
                                                int32_t cnt, const Op& m, unsigned long long& g, uint32_t& napp) {
   const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
   uint2* __restrict__ out = reinterpret_cast<uint2*>(s);
-  uint32_t o = 0, last = 0, skip = 0;
-  unsigned long long sg = 0, acc = 0;
+  uint32_t o = 0;
+  bool skip = false;
+  unsigned long long sg = 0, acc = 0, occ = 0;
 #pragma unroll
   for (int i = 0; i < MERGE_REG; ++i) {
-    if ((uint32_t)i < L) {
-      uint32_t y = v[i];
-      if (skip) {
-        skip = 0;
-        continue;
-      }
-      if (v[i] == a && v[i + 1] == b) {   // v[i + 1] is the sentinel past the end
-        if (o > 0) m.left(last, cnt);
-        if (v[i + 2] != 0xFFFFFFFFu) m.right(v[i + 2], cnt);
-        y = nid;
-        skip = 1;
-        ++napp;
-      }
+    WORD_SWEEP_EXIT(i, L);
+    const bool emit = ((uint32_t)i < L) & !skip;
+    const bool hit = emit & (v[i] == a) & (v[i + 1] == b);   // v[i + 1] is the sentinel past the end
+    occ |= (unsigned long long)hit << i;
+    skip = hit;
+    const uint32_t y = hit ? nid : v[i];
+    if (emit) {
       acc |= (unsigned long long)y << (16 * (o & 3u));
+      sg |= sig_bit(y);
       ++o;
       if ((o & 3u) == 0) {
         out[(o >> 2) - 1] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
         acc = 0;
       }
-      last = y;
-      sg |= sig_bit(y);
     }
   }
   if (o & 3u) out[o >> 2] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
   g = sg;
+  napp += (uint32_t)__builtin_popcountll(occ);
+  for (unsigned long long rest = occ; rest; rest &= rest - 1) {
+    const int i = __builtin_ctzll(rest);
+    uint32_t lv = nid, rv = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < MERGE_REG; ++k) {
+      lv = k + 1 == i ? v[k] : lv;
+      rv = k == i + 2 ? v[k] : rv;
+    }
+    if (i >= 2 && ((occ >> (i - 2)) & 1ull)) lv = nid;
+    if (i > 0) m.left(lv, cnt);
+    if (rv != 0xFFFFFFFFu) m.right(rv, cnt);
+  }
   return o;
 }
 
@@ -188,7 +211,7 @@ __device__ __forceinline__ uint32_t merge_symbols(uint16_t* __restrict__ s, uint
   if (L <= (uint32_t)MERGE_REG) {
     uint32_t v[MERGE_REG + 2];
     load_word(s, L, v);
-    if (!word_has_pair(v, a, b)) return 0;
+    if (!word_has_pair(v, L, a, b)) return 0;
     return merge_regs(v, L, s, wcount ? (int32_t)wcount[w] : 1, m, g, napp);
   }
   return merge_global(s, L, wcount, w, m, g, napp);
@@ -725,8 +748,9 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
 // entry, after the record, after the scan, before the delta flush and at exit, and of the
 // deciding apply workgroup at its phases, for 64 passes.
 #ifdef BPE_MERGE_STAMPS
-__device__ unsigned long long g_bpe_stamps[64][1024][6];
+__device__ unsigned long long g_bpe_stamps[64][1024][8];
 __device__ unsigned long long g_bpe_dstamps[64][8];
+__device__ unsigned long long g_bpe_batch[1024][2];   // every pass: merges decided, why the batch ended
 __device__ unsigned long long g_apply_stamps[64][256][12];
 #define ASTAMP(pi, k)                                                                                     \
   do {                                                                                                    \
@@ -855,16 +879,21 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     uint32_t L = wlen[w];
     uint16_t* s = sym + wstart[w];
     const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+    const unsigned long long sgw = sig[w];
     unsigned long long g = 0;
     bool changed = false;
     if (L < 2) return;
     if (L <= (uint32_t)MERGE_REG) {
       uint32_t v[MERGE_REG + 2];
       load_word(s, L, v);
+      uint32_t cand = 0;   // the merges whose pair the signature admits (need[j] = ~0 past n)
+#pragma unroll
+      for (int j = 0; j < BK; ++j) cand |= (uint32_t)((sgw & need[j]) == need[j]) << j;
       uint32_t hits = 0;
-#pragma unroll 1
-      for (int j = 0; j < n; ++j)
-        if (word_has_pair(v, (uint32_t)s_a[j], (uint32_t)s_b[j])) hits |= 1u << j;
+      for (; cand; cand &= cand - 1) {
+        const int j = __builtin_ctz(cand);
+        if (word_has_pair(v, L, (uint32_t)s_a[j], (uint32_t)s_b[j])) hits |= 1u << j;
+      }
       if (!hits) return;
       // one merge_regs pass per set bit: lanes of a wave holding different merges share it
       // (the op is per lane), so a wave runs as many passes as its lanes' most merges (~1)
@@ -880,7 +909,6 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       }
       changed = true;
     } else {
-      const unsigned long long sgw = sig[w];
 #pragma unroll 1
       for (int j = 0; j < n; ++j) {
         const unsigned long long nd = s_need[j];
@@ -897,6 +925,10 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       }
     }
     if (!changed) return;
+#ifdef BPE_MERGE_STAMPS
+    if (blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64)
+      atomicAdd(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][6], 1ull);   // words rewritten
+#endif
     any = true;
     wlen[w] = L;
     sig[w] = g;
@@ -927,6 +959,10 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     const int nc = cn;
     if (!ahead || nc > BATCH_CLIST - 256 * MERGE_SCAN) {
       MSTAMP(KB_PI, 2);
+#ifdef BPE_MERGE_STAMPS
+      if (threadIdx.x == 0 && blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64)
+        g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][5] += nc;   // candidates visited
+#endif
       for (int k = threadIdx.x; k < nc; k += 256) visit(clist[k]);
       __syncthreads();
       if (threadIdx.x == 0) cn = 0;
@@ -1197,6 +1233,26 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   ok &= sec < ckey;   // a taken row's second-best would come first
   const unsigned long long pass = __ballot(ok);
   const int nb = (int)__builtin_ctzll(~pass);   // leading lanes that pass (<= KM)
+#ifdef BPE_MERGE_STAMPS
+  {   // why the batch ended: the first failing lane's rules (bit 0 list end, 1 HF stop, 2 re-use,
+      // 3 after a self-pair / re-use, 4 chaining, 5 same string, 6 a taken row's bound)
+    uint32_t why = lane >= KM ? 1u : 0u;
+    why |= !(count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm) ? 2u : 0u;
+    why |= lane > 0 && exist >= 0 ? 4u : 0u;
+    for (int i = 0; i < KM - 1 && i < lane; ++i) {
+      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
+      why |= ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0) ? 8u : 0u;
+      why |= cand_b == ai || cand_a == bi ? 16u : 0u;
+      why |= ch == readlane_u64(ch, i) && clen == (uint32_t)__builtin_amdgcn_readlane((int)clen, i) ? 32u : 0u;
+    }
+    why |= !(sec < ckey) ? 64u : 0u;
+    const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
+    if (lane == 0 && KA_PI < 1024) {
+      g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
+      g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
+    }
+  }
+#endif
   // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
   const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
   if (lane < nb) {
@@ -1363,6 +1419,9 @@ extern "C" int beast_debug_merge_stamps(unsigned long long* host) {
 }
 extern "C" int beast_debug_decide_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_dstamps), sizeof(g_bpe_dstamps)) == hipSuccess ? 0 : -2;
+}
+extern "C" int beast_debug_batch_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_batch), sizeof(g_bpe_batch)) == hipSuccess ? 0 : -2;
 }
 extern "C" int beast_debug_apply_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_apply_stamps), sizeof(g_apply_stamps)) == hipSuccess ? 0 : -2;

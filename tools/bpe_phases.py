@@ -22,18 +22,19 @@ sys.path.insert(0, REPO)
 LIB = os.path.join(HERE, "libbpe_stamps.so")
 
 
-def build(p0: int) -> None:
+def build(p0: int, lib: str = LIB, extra=()) -> None:
     from beast_tokenizer_amd import _build
     objs = []
     for f in sorted(os.listdir(_build.CSRC)):
         if f.endswith(".hip"):
             o = os.path.join(tempfile.gettempdir(), f"phases_{f}.o")
             subprocess.run([_build._hipcc(), *_build.CXXFLAGS, *_build.FILE_FLAGS.get(f, []),
-                            f"-DBPE_MERGE_STAMPS={p0}", "-c", os.path.join(_build.CSRC, f), "-o", o], check=True)
+                            f"-DBPE_MERGE_STAMPS={p0}", *extra, "-c", os.path.join(_build.CSRC, f), "-o", o],
+                           check=True)
             objs.append(o)
-    subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", LIB, *objs],
+    subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
                    check=True)
-    print("built", LIB)
+    print("built", lib)
 
 
 def _read(lib, name, shape):
@@ -45,7 +46,7 @@ def _read(lib, name, shape):
 
 
 def run(out_json=None) -> None:
-    os.environ["BEAST_LIB"] = LIB
+    os.environ.setdefault("BEAST_LIB", LIB)
     import torch
     import bench
     from beast_tokenizer_amd import _lib
@@ -61,13 +62,16 @@ def run(out_json=None) -> None:
             wl0 = words["wlen"][:words["n_words"]].clone()
             out = GpuBpeOps.loop_run(self, words, *a, **kw)
             wl1 = words["wlen"][:words["n_words"]]
+            q = torch.quantile(wl0.float(), torch.tensor([0.5, 0.9, 0.99, 0.999], device=wl0.device)).tolist()
+            seen.update({"wlen_q50_90_99_999": q, "wlen_max": int(wl0.max()), "words_gt16": int((wl0 > 16).sum()),
+                         "words_gt32": int((wl0 > 32).sum()), "symbols_in_words_gt32": int(wl0[wl0 > 32].sum())})
             seen.update({"distinct_words": int(words["n_words"]), "words_ge2_start": int((wl0 >= 2).sum()),
                          "words_ge2_end": int((wl1 >= 2).sum()), "symbols_start": int(wl0.sum()),
                          "symbols_end": int(wl1.sum())})
             return out
     res = train_bpe(flat, off, 2048, ops=Ops(dev))
     torch.cuda.synchronize()
-    ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 6))
+    ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 8))
     ds = _read(lib, "beast_debug_decide_stamps", (64, 8))
     aps = _read(lib, "beast_debug_apply_stamps", (64, 256, 12))
     us = lambda v: round(float(v) / 100.0, 2)   # noqa: E731
@@ -86,7 +90,11 @@ def run(out_json=None) -> None:
                "merge_record_med": us(np.median(m[:, 1] - m[:, 0])),
                "merge_visit_start_med": us(np.median(m[:, 2] - t0)),
                "merge_scan_done_med": us(np.median(m[:, 3] - t0)), "merge_scan_done_max": us(m[:, 3].max() - t0),
-               "merge_exit_med": us(np.median(m[:, 4] - t0)), "merge_exit_max": us(m[:, 4].max() - t0)}
+               "merge_exit_med": us(np.median(m[:, 4] - t0)), "merge_exit_max": us(m[:, 4].max() - t0),
+               "merge_candidates": int(m[:, 5].sum()), "merge_words_rewritten": int(m[:, 6].sum()),
+               "merge_candidates_wg_max": int(m[:, 5].max())}
+        if p + 1 < 64 and (ms[p + 1][:, 0] > 0).any():
+            rec["pass_period"] = us(ms[p + 1][ms[p + 1][:, 0] > 0, 0].min() - t0)
         if len(a):
             rec.update({"apply_entry_first": us(a[:, 0].min() - t0), "apply_entry_last": us(a[:, 0].max() - t0),
                         "apply_ranked_med": us(np.median(a[:, 1] - t0)), "apply_ranked_max": us(a[:, 1].max() - t0),
@@ -112,19 +120,27 @@ def run(out_json=None) -> None:
             rec.update({"decide_start": us(d[0] - t0), "decide_lists_merged": us(d[1] - t0),
                         "decide_rounds": us(d[2] - t0), "decide_probed": us(d[3] - t0), "decide_end": us(d[4] - t0)})
         passes.append(rec)
-    keys = [k for k in passes[0] if k != "wg"]
+    keys = list(dict.fromkeys(k for r in passes for k in r if k != "wg"))
     summary = {k: float(np.median([r[k] for r in passes if k in r])) for k in keys}
     out = {"merges": len(res.merges), "passes": res.stats.get("passes"), "passes_stamped": len(passes),
            "median_over_passes_us": summary, "words": seen, "per_pass": passes, "loop_s": res.stats["merge_loop_s"]}
     print(json.dumps({k: out[k] for k in ("merges", "passes", "loop_s", "words")}))
     print(json.dumps(summary, indent=1))
+    bs = _read(lib, "beast_debug_batch_stamps", (1024, 2))[:min(int(res.stats.get("passes") or 0), 1024)]
+    why = {}   # batch-end reasons over every pass (bits: see k_apply_batch)
+    names = ["list_end", "hf_stop", "reuse", "after_self_or_reuse", "chaining", "same_string", "row_bound"]
+    for bit, nm in enumerate(names):
+        why[nm] = int(((bs[:, 1] >> bit) & 1).sum())
+    out["batch_end"] = why
+    out["batch_n_hist"] = np.bincount(bs[:, 0]).tolist()
+    print(json.dumps({"batch_end": why, "batch_n_hist": out["batch_n_hist"]}))
     if out_json:
         with open(out_json, "w") as f:
             json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "build":
-        build(int(sys.argv[2]))
+    if sys.argv[1] == "build":   # build P0 [lib -Dflags ...]
+        build(int(sys.argv[2]), *(sys.argv[3:4] or [LIB]), extra=sys.argv[4:])
     else:
         run(sys.argv[2] if len(sys.argv) > 2 else None)
