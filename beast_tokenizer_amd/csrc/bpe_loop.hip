@@ -221,6 +221,8 @@ constexpr int MERGE_SCAN = 8;       // signature loads in flight per thread (two
 constexpr int MERGE_CLIST = 2048;   // LDS candidate list per workgroup (k_merge)
 constexpr int BATCH_CLIST = 2 * 256 * MERGE_SCAN;   // k_merge_batch's list: two scan rounds
 
+__device__ const uint32_t k_one_u32 = 1u;   // the count of every word when wcount is null
+
 // One merge (a, b) -> nid over every word (the host-driven loop).  Deltas go to LDS (LDS = true,
 // 4*Vt int32 <= 64 KiB) and are flushed once per workgroup into deltas[] with contiguous
 // atomics, or straight to deltas[] by global atomics (rare pairs: the per-workgroup LDS clear
@@ -748,7 +750,7 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
 // entry, after the record, after the scan, before the delta flush and at exit, and of the
 // deciding apply workgroup at its phases, for 64 passes.
 #ifdef BPE_MERGE_STAMPS
-__device__ unsigned long long g_bpe_stamps[64][1024][8];
+__device__ unsigned long long g_bpe_stamps[64][1024][12];
 __device__ unsigned long long g_bpe_dstamps[64][8];
 __device__ unsigned long long g_bpe_batch[1024][2];   // every pass: merges decided, why the batch ended
 __device__ unsigned long long g_apply_stamps[64][256][12];
@@ -809,7 +811,8 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     rn = loop->bnid[threadIdx.x];
     rl = loop->blen[threadIdx.x];
   }
-  const int n = loop->bn;
+  // the record's fields all in one round trip (no load waits on the n == 0 test)
+  const int n = loop->bn, vcur = loop->bv0, kd = loop->bkd, mt = loop->bmt, nm0 = loop->bnm0;
   unsigned long long sgv[MERGE_SCAN];
   const int64_t nchunks = (nw + 255) / 256;
 #pragma unroll
@@ -817,8 +820,9 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     const int64_t w = (blockIdx.x + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
     sgv[u] = w < nw ? sig[w] : 0ull;
   }
+  // the LDS delta vectors cleared whole while the record is in flight (16-byte stores)
+  for (int i = threadIdx.x; i < BATCH_LDS / 16; i += 256) reinterpret_cast<int4*>(dl)[i] = make_int4(0, 0, 0, 0);
   if (n == 0) return;   // the loop has stopped (uniform)
-  const int vcur = loop->bv0, kd = loop->bkd, mt = loop->bmt, nm0 = loop->bnm0;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // commit the batch, merge j on lane j: its string into the hash table (distinct strings, so
     // concurrent inserts only race for free slots), the new token's hash / P^len / length, its log
@@ -857,8 +861,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   }
   if (threadIdx.x == 0) { cn = 0; touched = 0; }
   const int stride = vcur + n;
-  const int nl = kd * 4 * stride;   // LDS entries in use
-  for (int i = threadIdx.x; i < nl; i += 256) dl[i] = 0;
+  const int nl = kd * 4 * stride;   // LDS entries in use (<= BATCH_LDS / 4: the decider's rule)
   __syncthreads();
   MSTAMP(KB_PI, 1);
   const int vbase = s_nid[0] == vcur ? vcur : vcur + 1;   // first new id (merge 0 may re-use one)
@@ -876,16 +879,31 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   // the batch's merges in order on one word; its symbols are read once (a rare second merge
   // in the same word re-reads them)
   auto visit = [&](int64_t w) {
+    // the word's four metadata loads in one round trip: no branch between them (a null wcount
+    // reads the constant 1)
+    const uint32_t* wc = wcount != nullptr ? wcount + w : &k_one_u32;
     uint32_t L = wlen[w];
-    uint16_t* s = sym + wstart[w];
-    const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
+    const uint32_t st = wstart[w];
+    const int32_t cnt = (int32_t)*wc;
     const unsigned long long sgw = sig[w];
+    // used together here, so the compiler cannot sink three of the loads below the L < 2 exit
+    asm volatile("" ::"v"(L), "v"(st), "v"(cnt), "v"((uint32_t)sgw), "v"((uint32_t)(sgw >> 32)));
+    uint16_t* s = sym + st;
     unsigned long long g = 0;
     bool changed = false;
     if (L < 2) return;
+#ifdef BPE_MERGE_STAMPS
+    const bool vst = blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64;
+    if (vst && (sgw >> 63) != 2u)   // uses sgw and L: the metadata has arrived
+      atomicMax(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][7], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     if (L <= (uint32_t)MERGE_REG) {
       uint32_t v[MERGE_REG + 2];
       load_word(s, L, v);
+#ifdef BPE_MERGE_STAMPS
+      if (vst && v[0] != 0xFFFFFFFEu)   // the word has arrived
+        atomicMax(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][8], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
       uint32_t cand = 0;   // the merges whose pair the signature admits (need[j] = ~0 past n)
 #pragma unroll
       for (int j = 0; j < BK; ++j) cand |= (uint32_t)((sgw & need[j]) == need[j]) << j;
@@ -926,8 +944,10 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     }
     if (!changed) return;
 #ifdef BPE_MERGE_STAMPS
-    if (blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64)
+    if (blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64) {
       atomicAdd(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][6], 1ull);   // words rewritten
+      atomicMax(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 #endif
     any = true;
     wlen[w] = L;
@@ -963,7 +983,14 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       if (threadIdx.x == 0 && blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64)
         g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][5] += nc;   // candidates visited
 #endif
-      for (int k = threadIdx.x; k < nc; k += 256) visit(clist[k]);
+      for (int k = threadIdx.x; k < nc; k += 256) {
+        visit(clist[k]);
+#ifdef BPE_MERGE_STAMPS
+        if (blockIdx.x < 1024 && KB_PI >= BPE_MERGE_STAMPS && KB_PI < BPE_MERGE_STAMPS + 64)
+          atomicMax(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][10],
+                    (unsigned long long)__builtin_amdgcn_s_memrealtime());   // any visit done
+#endif
+      }
       __syncthreads();
       if (threadIdx.x == 0) cn = 0;
       __syncthreads();
@@ -1120,12 +1147,14 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   if (wave != 0) return;
   const int nwg = batch_nwg(Vt);
   {   // this workgroup's BK best of its APPLY_ROWS x KR candidates, best first, with their rows' bounds
+    static_assert(APPLY_ROWS * KR == 64, "one candidate per lane of the wave");
     const int w = lane / KR, r = lane % KR;   // 64 lanes = 16 rows x 4
     const unsigned long long kw = s_top[w][r];
-    int rank = 0;   // candidates above this one (keys are distinct; empty ones by lane)
+    int rank = 0;   // candidates above this one (keys are distinct; empty ones by lane), in registers
+#pragma unroll
     for (int v = 0; v < APPLY_ROWS * KR; ++v) {
-      const unsigned long long kv = s_top[v / KR][v % KR];
-      rank += kv > kw || (kv == kw && v < lane);
+      const unsigned long long kv = readlane_u64(kw, v);
+      rank += (kv > kw) | ((kv == kw) & (v < lane));
     }
     if (rank < BK) {
       st_agent(&bw.wgkey[(size_t)rank * nwg + blockIdx.x], kw);   // the grid may cover fewer rows than Vt

@@ -1,6 +1,7 @@
 """Phase timeline of the batched BPE merge loop from in-kernel stamps (tools only).
 
-    python tools/bpe_phases.py build P0     # here: tools/libbpe_stamps.so with -DBPE_MERGE_STAMPS=P0
+    python tools/bpe_phases.py build P0 [lib -Dflags..]   # here: tools/libbpe_stamps.so with -DBPE_MERGE_STAMPS=P0
+                                                         # (P0 < 0: no stamps, an A/B build of the product)
     python tools/bpe_phases.py run [json]   # on the box: K5 training on that library, passes P0 .. P0+63
 
 Per pass (s_memrealtime, 100 MHz, microseconds from the merge kernel's first workgroup entry):
@@ -29,7 +30,8 @@ def build(p0: int, lib: str = LIB, extra=()) -> None:
         if f.endswith(".hip"):
             o = os.path.join(tempfile.gettempdir(), f"phases_{f}.o")
             subprocess.run([_build._hipcc(), *_build.CXXFLAGS, *_build.FILE_FLAGS.get(f, []),
-                            f"-DBPE_MERGE_STAMPS={p0}", *extra, "-c", os.path.join(_build.CSRC, f), "-o", o],
+                            *([f"-DBPE_MERGE_STAMPS={p0}"] if p0 >= 0 else []), *extra, "-c",
+                            os.path.join(_build.CSRC, f), "-o", o],
                            check=True)
             objs.append(o)
     subprocess.run([_build._hipcc(), f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", lib, *objs],
@@ -71,7 +73,7 @@ def run(out_json=None) -> None:
             return out
     res = train_bpe(flat, off, 2048, ops=Ops(dev))
     torch.cuda.synchronize()
-    ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 8))
+    ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 12))
     ds = _read(lib, "beast_debug_decide_stamps", (64, 8))
     aps = _read(lib, "beast_debug_apply_stamps", (64, 256, 12))
     us = lambda v: round(float(v) / 100.0, 2)   # noqa: E731
@@ -93,6 +95,19 @@ def run(out_json=None) -> None:
                "merge_exit_med": us(np.median(m[:, 4] - t0)), "merge_exit_max": us(m[:, 4].max() - t0),
                "merge_candidates": int(m[:, 5].sum()), "merge_words_rewritten": int(m[:, 6].sum()),
                "merge_candidates_wg_max": int(m[:, 5].max())}
+        vt = m[:, 3] - m[:, 2]   # visit phase per workgroup
+        for k, nm in ((7, "meta"), (8, "word"), (9, "merged"), (10, "any_done")):   # last visit's metadata / word
+            # in, last rewriting visit done, last visit of any kind done
+            ok = m[:, k] > 0
+            if ok.any():
+                rec["merge_visit_" + nm + "_med"] = us(np.median(m[ok, k] - m[ok, 2]))
+        slow = int(np.argmax(m[:, 3]))
+        rec.update({"merge_visit_med": us(np.median(vt)), "merge_visit_max": us(vt.max()),
+                    "merge_slowest_wg_candidates": int(m[slow, 5]), "merge_slowest_wg_rewritten": int(m[slow, 6]),
+                    "merge_slowest_wg_visit": us(vt[slow]), "merge_slowest_wg_scan": us(m[slow, 2] - m[slow, 1]),
+                    "merge_median_wg_candidates": float(np.median(m[:, 5])),
+                    "merge_corr_visit_candidates": round(float(np.corrcoef(vt, m[:, 5])[0, 1]), 3),
+                    "merge_corr_visit_rewritten": round(float(np.corrcoef(vt, m[:, 6])[0, 1]), 3)})
         if p + 1 < 64 and (ms[p + 1][:, 0] > 0).any():
             rec["pass_period"] = us(ms[p + 1][ms[p + 1][:, 0] > 0, 0].min() - t0)
         if len(a):

@@ -9,7 +9,7 @@ from collections import defaultdict
 
 def summarise(root, kernels=("k_encode", "k_reconstruct")):
     acc = defaultdict(lambda: defaultdict(list))
-    for f in sorted(glob.glob(os.path.join(root, "*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         per = defaultdict(float)   # (dispatch, kernel, counter) -> summed over dims
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
@@ -23,4 +23,5 @@ def summarise(root, kernels=("k_encode", "k_reconstruct")):
 
 
 if __name__ == "__main__":
-    print(json.dumps(summarise(sys.argv[1]), indent=1))
+    # python tools/pmc_summary.py ROOT [kernel-name substrings ...]
+    print(json.dumps(summarise(sys.argv[1], tuple(sys.argv[2:]) or ("k_encode", "k_reconstruct")), indent=1))
