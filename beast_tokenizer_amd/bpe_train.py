@@ -324,18 +324,36 @@ class GpuBpeOps:
 
         vcur = n_tok
         if deltas is None:
-            flags = self.BATCH_INIT
-            while True:
-                # a pass takes >= 1 merge; ~3.3 on average at K5, so half the remaining merges
-                # bounds the passes left without many no-op launches past the end
-                steps = max(1, min(chunk, (vocab_size - vcur + 1) // 2))
+            # two chunks of passes in flight: the host reads the state the older one left (an event,
+            # not a stream sync) while the GPU runs the newer, so the GPU never waits for the host.
+            # A pass takes at most kmax merges, so ceil(remaining / kmax) passes never overshoot the
+            # vocabulary; the state read is one chunk old, so the chunk still in flight is counted
+            # at 4 merges a pass (K5 averages 4.8) and few launches run past the end.
+            stage = [torch.empty(16, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+            inflight = []   # (event, stage index, passes), oldest first
+
+            def launch(steps, flags):
                 run(steps, flags)
-                flags = 0
-                host.copy_(state[:16], non_blocking=True)
-                torch.cuda.current_stream(dev).synchronize()
+                bi = 1 - inflight[-1][1] if inflight else 0
+                stage[bi].copy_(state[:16], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))   # the stream the launches and the copy use
+                inflight.append((ev, bi, steps))
+
+            launch(max(1, min(chunk, -(-(vocab_size - vcur) // kmax))), self.BATCH_INIT)
+            while True:
+                left = vocab_size - vcur - 4 * sum(p for _, _, p in inflight)
+                if left > 0:
+                    launch(min(chunk, -(-left // kmax)), 0)
+                ev, bi, _ = inflight.pop(0)
+                ev.synchronize()
+                host.copy_(stage[bi])
                 active, vcur = int(host[self.ST_ACTIVE]), int(host[self.ST_VCUR])
                 if not active or vcur >= vocab_size:
                     break
+                if not inflight:   # the estimate held back: keep one chunk going
+                    launch(1, 0)
+            torch.cuda.current_stream(dev).synchronize()
         else:
             # sharded: every rank holds the same table and takes the same decisions, so every rank
             # runs the same number of passes (and collectives)
