@@ -1,16 +1,20 @@
 """k_bpe_encode on the bench's codec workload through the product library (tools only, for
-rocprofv3 --pmc / --kernel-trace): trains the K5 model, then encodes 4,096 rows x 140 bins N times.
-    python tools/codec/bpe_encode_run.py [N]
+rocprofv3 --pmc / --kernel-trace and A/B timing): trains the K5 model, then encodes 4,096 rows x
+140 bins.
+    python tools/codec/bpe_encode_run.py [N]     # N launches (profilers)
+    python tools/codec/bpe_encode_run.py time    # event-timed launches per merge mode + the list API
 """
+import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 
 
-def main(n):
+def setup():
     import torch
     import bench
     from beast_tokenizer_amd.beast_bpe_trainer import tokenizer_from_result
@@ -23,11 +27,59 @@ def main(n):
     model = GpuBpeModel(tokenizer_from_result(res), dev)
     lo, span = res.min_token, res.max_token - res.min_token
     rf, ro, w = rows_from_tensor(rows[:4096], dev)
+    return dev, model, (rf, ro, w, lo, span)
+
+
+def timed(n_launch=50):
+    import torch
+    from beast_tokenizer_amd import _lib
+    dev, model, args = setup()
+    lib = _lib.load()
+    out = {}
+    ref = None
+    for mode, name in ((4, "rounds"), (0, "default"), (1, "heap")):
+        lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, mode)
+        r = model.encode_rows(*args)
+        torch.cuda.synchronize()
+        got = (r[0].cpu(), r[1].cpu())
+        if ref is None:
+            ref = got
+        same = torch.equal(ref[1], got[1]) and all(
+            torch.equal(ref[0][i, :int(ref[1][i])], got[0][i, :int(got[1][i])]) for i in range(0, 4096, 97))
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n_launch):
+            model.encode_rows(*args)
+        e.record()
+        torch.cuda.synchronize()
+        out[name] = {"us_per_launch": s.elapsed_time(e) * 1e3 / n_launch, "same_as_first": bool(same)}
+    lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, 0)
+    model.encode_to_lists(*args)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        lists = model.encode_to_lists(*args)
+    out["encode_to_lists_rows_per_s"] = 5 * 4096 / (time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        model.encode_to_tensors(*args)
+    torch.cuda.synchronize()
+    out["encode_to_tensors_rows_per_s"] = 10 * 4096 / (time.perf_counter() - t0)
+    out["rows"] = len(lists)
+    print(json.dumps(out))
+
+
+def main(n):
+    import torch
+    dev, model, args = setup()
     for _ in range(n):
-        model.encode_rows(rf, ro, w, lo, span)
+        model.encode_rows(*args)
     torch.cuda.synchronize()
     print("encoded", n, "x 4096 rows")
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 20)
+    if len(sys.argv) > 1 and sys.argv[1] == "time":
+        timed()
+    else:
+        main(int(sys.argv[1]) if len(sys.argv) > 1 else 20)
