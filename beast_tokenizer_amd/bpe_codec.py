@@ -67,6 +67,7 @@ class GpuBpeModel:
         model = spec["model"]
         vocab: Dict[str, int] = model["vocab"]
         self.device = device
+        self._host_blk = None   # pinned staging of encode_to_lists
         lib = _lib.load()
         if vocab and max(vocab.values()) >= 65536:
             raise NotImplementedError("BPE vocabularies with ids >= 65536 are not supported on the GPU")
@@ -191,19 +192,29 @@ class GpuBpeModel:
         R = lens.numel()
         if R == 0:
             return []
-        ls = torch.stack([lens, status]).cpu().numpy()
-        bad = np.nonzero(ls[1])[0]
-        if bad.size:
-            exc, msg = _ENC_ERRORS[int(ls[1][bad[0]])]
+        # one wait: the id block, the lengths and the status land in one reused pinned buffer by
+        # asynchronous copies (the id block whole: a slice to the widest row would need the
+        # lengths first, i.e. a second round trip)
+        W = ids.shape[1]
+        need = R * W + 2 * R
+        if self._host_blk is None or self._host_blk.numel() < need:
+            self._host_blk = torch.empty(need, dtype=torch.int32, pin_memory=True)
+        blk = self._host_blk
+        ids_h = blk[:R * W].view(R, W)
+        lens_h, st_h = blk[R * W:R * W + R], blk[R * W + R:need]
+        ids_h.copy_(ids, non_blocking=True)
+        lens_h.copy_(lens, non_blocking=True)
+        st_h.copy_(status, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        st_np = st_h.numpy()
+        if st_np.any():
+            exc, msg = _ENC_ERRORS[int(st_np[np.flatnonzero(st_np)[0]])]
             raise exc(msg)
-        w = int(ls[0].max())
-        ids_h = ids[:, :w].contiguous().cpu()
         from .beast_bspline_tokenizer import _fastpath
         fp = _fastpath()
         if fp is not None:   # host C++ list builder (csrc/fastpath.cpp)
-            return fp.rows_to_lists(ids_h, torch.from_numpy(np.ascontiguousarray(ls[0], dtype=np.int32)))
-        ids_np = ids_h.numpy()
-        lens_np = ls[0]
+            return fp.rows_to_lists(ids_h, lens_h)
+        ids_np, lens_np = ids_h.numpy(), lens_h.numpy()
         return [ids_np[i, :lens_np[i]].tolist() for i in range(R)]
 
     def encode_to_tensors(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,

@@ -293,6 +293,62 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
   return x - v;
 }
 
+// 2. (see encode_row) the word starts of a row from e[i], the end of the regex word that would
+// start at code point i: the chain 0 -> e[0] -> e[e[0]] -> ... < n.  Lane-parallel instead of one
+// lane following ~n / 2 dependent links: lane s walks the chain from the start of its segment
+// [s G, s G + G) (G = ceil(n / 64)), marking what it visits (vis, one byte per code point), and
+// records where it leaves the segment.  The true chain enters segment s where it left segment
+// s - 1; a marked entry means lane s's walk already is the true chain from there (the chain is a
+// function of the position), an entry past the segment means the segment holds no start, and
+// any other entry (rare: regex words self-synchronise within a word) makes the lane re-walk its
+// segment from it -- repeated until no exit changes.  Starts = marked positions at or past
+// their segment's entry, written in order by a wave scan.
+__device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, EncLds& L, int n, int lane) {
+  const int G = (n + 63) >> 6;
+  const int sb = min(lane * G, n), se = min(sb + G, n);
+  for (int i = lane; i < n; i += 64) vis[i] = 0;
+  wave_sync();
+  int ex = sb;   // exit: the first chain position >= se (n past the end)
+  if (sb < se) {
+    int p = sb;
+    while (p < se) { vis[p] = 1; p = e[p]; }
+    ex = p;
+  }
+  int entry = 0;
+  while (true) {
+    const int prev = __shfl_up(ex, 1);
+    const int en = lane == 0 ? 0 : prev;
+    int nex = ex;
+    bool changed = false;
+    if (sb < se) {
+      if (en >= se) {
+        nex = en;                 // the chain jumps this segment
+      } else if (en >= sb && !vis[en]) {
+        for (int i = en; i < se; ++i) vis[i] = 0;   // re-walk from the true entry
+        int p = en;
+        while (p < se) { vis[p] = 1; p = e[p]; }
+        nex = p;
+        changed = true;
+      }
+    } else {
+      nex = en > sb ? en : sb;   // empty segment (past n): pass the exit on
+    }
+    changed |= nex != ex || en != entry;
+    ex = nex;
+    entry = en;
+    if (!__any(changed)) break;
+  }
+  wave_sync();
+  int cnt = 0;
+  for (int i = max(sb, entry); i < se; ++i) cnt += vis[i];
+  int tot;
+  int o = wave_excl_scan(cnt, lane, tot);
+  for (int i = max(sb, entry); i < se; ++i)
+    if (vis[i]) { L.wcp[o] = i; L.wspec[o] = -1; ++o; }
+  if (lane == 0) { L.wcp[tot] = n; L.misc[0] = tot; }
+  wave_sync();
+}
+
 // 4b. (see encode_row) the round merge of a row of <= 64 * RMP byte symbols
 template <int RMP, class Map>
 __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, int nw, int lane) {
@@ -471,16 +527,7 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
 #ifndef BPE_SERIAL_PRETOK
     int32_t* e = L.wcnt;   // scratch until step 4
     for (int i = lane; i < n; i += 64) e[i] = regex_word(L.cps, L.cls, i, n);
-    wave_sync();
-    if (lane == 0) {
-      int nw = 0, p = 0;
-      while (p < n) {
-        L.wcp[nw] = p; L.wspec[nw] = -1; ++nw;
-        p = e[p];
-      }
-      L.wcp[nw] = n;
-      L.misc[0] = nw;
-    }
+    word_starts(e, L.cand, L, n, lane);
 #else
     if (lane == 0) {
       int nw = 0, p = 0;

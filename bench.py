@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--dump-k5", default=None, help="write the K5 corpus (uint8 bins, npz) and exit")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
                     help="per-launch HBM bytes from rocprofv3 --pmc (tools/gpu_pmc.sh)")
+    ap.add_argument("--bpe-counters", default=os.path.join(REPO, "profiles", "r03", "bpe_loop_counters.json"),
+                    help="per-pass HBM bytes of the BPE merge loop (tools/make_bpe_counters.py)")
     ap.add_argument("--pmc-mfma", default=os.path.join(REPO, "profiles", "pmc_mfma.json"),
                     help="per-launch MFMA instruction counts from rocprofv3 --pmc SQ_INSTS_MFMA")
     return ap.parse_args()
@@ -409,6 +411,22 @@ def bpe_bench(dev, args, world, rank, reduce):
                    "frac": rb["algo_bytes"] / el / HBM_PEAK, "bound": "hbm",
                    "note": "§8d counts a full scan of the live symbols per merge; the kernels visit only "
                            "candidate words, so this is an effective rate, not bytes moved"})
+    # measured beside it: the HBM bytes the loop's two kernels move per pass (rocprofv3 FETCH_SIZE +
+    # WRITE_SIZE of k_merge_batch and k_apply_batch at K5, profiles/r03/bpe_loop_counters.json)
+    # times the passes this run took, over the live loop time
+    if os.path.exists(args.bpe_counters) and st.get("passes"):
+        with open(args.bpe_counters) as f:
+            cnt = json.load(f)
+        pp = cnt.get("per_pass", {})
+        if pp.get("bytes"):
+            moved = pp["bytes"] * st["passes"]
+            rb["counters"] = {"source": os.path.relpath(args.bpe_counters, REPO), "bytes_per_pass": pp["bytes"],
+                              "passes": st["passes"], "traffic": moved,
+                              "achieved_GBps": moved / st["merge_loop_s"] / 1e9,
+                              "frac": moved / st["merge_loop_s"] / HBM_PEAK,
+                              "in_kernel_GBps": pp.get("hbm_GBps_in_kernels"),
+                              "note": "counter bytes over the whole loop (launch gaps and the decision chain "
+                                      "included); in_kernel_GBps is over the two kernels' own time"}
     out["roofline"] = rb
     if golden is not None and golden.get("merges") is not None and args.bpe_seqs == golden["trajectories"] \
             and args.bpe_vocab == golden["vocab_size"]:
