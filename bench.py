@@ -247,9 +247,9 @@ def cpu_baseline(x_np: np.ndarray, gpu_tokens: np.ndarray, tok_bounds, seconds: 
     parity = {"tokens": int(gpu_tokens.size), "flips": int(diff.sum()),
               "max_flip_tie_distance": float(dist.max()) if diff.any() else None,
               "max_flip_size": int(np.abs(gpu_tokens[diff] - ref_tok[diff]).max()) if diff.any() else 0,
-              "contract": "every flip within 1e-3 of a .5 rounding tie of the exact fit, by one bin "
+              "contract": "every flip within 5e-4 of a .5 rounding tie of the exact fit, by one bin "
                           "(tests/test_gpu_parity.py TIE_TOL)"}
-    parity["ok"] = bool(not diff.any() or (dist.max() < 1e-3 and parity["max_flip_size"] == 1))
+    parity["ok"] = bool(not diff.any() or (dist.max() < 5e-4 and parity["max_flip_size"] == 1))
     return {"value": B / med, "unit": "trajectories/s", "cores": torch.get_num_threads(), "kind": "port",
             "seconds_per_batch_median": med, "repetitions": len(reps),
             "sample": f"{len(reps)} x the bench's own B={B} batch (D=14,T=50,N=10,V=256), encode+reconstruct via "
@@ -561,10 +561,14 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
         dec["r"] = model.decode_rows(dflat, doff, width, lo)
     t_dec = kernel_time_us(launch_dec, stream, reps=20, rounds=3)
     assert torch.equal(dec["r"][0], rows), "BPE decode(encode(rows)) != rows"
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    lists = model.encode_to_lists(flat, off, width, lo, span)
-    t_api_enc = time.perf_counter() - t0
+    lists = model.encode_to_lists(flat, off, width, lo, span)   # warm-up (pinned staging allocated)
+    api_runs = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lists = model.encode_to_lists(flat, off, width, lo, span)
+        api_runs.append(time.perf_counter() - t0)
+    t_api_enc = sorted(api_runs)[len(api_runs) // 2]
     model.encode_to_tensors(flat, off, width, lo, span)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
