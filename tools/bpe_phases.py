@@ -137,7 +137,23 @@ def run(out_json=None) -> None:
         passes.append(rec)
     keys = list(dict.fromkeys(k for r in passes for k in r if k != "wg"))
     summary = {k: float(np.median([r[k] for r in passes if k in r])) for k in keys}
-    out = {"merges": len(res.merges), "passes": res.stats.get("passes"), "passes_stamped": len(passes),
+    raw = {}   # per-workgroup merge stamps (us from the pass's first entry) of four passes, for straggler analysis
+    for p in (10, 20, 30, 40):
+        m = ms[p]
+        ran = m[:, 0] > 0
+        if ran.any():
+            t0 = m[ran, 0].min()
+            raw[str(p)] = {"wg": np.flatnonzero(ran).tolist(),
+                           "entry": ((m[ran, 0] - t0) / 100.0).round(2).tolist(),
+                           "visit_start": ((m[ran, 2] - t0) / 100.0).round(2).tolist(),
+                           "scan_done": ((m[ran, 3] - t0) / 100.0).round(2).tolist(),
+                           "exit": ((m[ran, 4] - t0) / 100.0).round(2).tolist(),
+                           "candidates": m[ran, 5].tolist(), "rewritten": m[ran, 6].tolist(),
+                           "meta": ((m[ran, 7] - t0) / 100.0).round(2).tolist(),
+                           "word": ((m[ran, 8] - t0) / 100.0).round(2).tolist(),
+                           "merged": ((m[ran, 9] - t0) / 100.0).round(2).tolist(),
+                           "any_done": ((m[ran, 10] - t0) / 100.0).round(2).tolist()}
+    out = {"merges": len(res.merges), "passes": res.stats.get("passes"), "passes_stamped": len(passes), "raw": raw,
            "median_over_passes_us": summary, "words": seen, "per_pass": passes, "loop_s": res.stats["merge_loop_s"]}
     print(json.dumps({k: out[k] for k in ("merges", "passes", "loop_s", "words")}))
     print(json.dumps(summary, indent=1))
