@@ -927,6 +927,9 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
       }
       changed = true;
     } else {
+#ifdef BPE_MERGE_STAMPS
+      if (vst) atomicAdd(&g_bpe_stamps[KB_PI - BPE_MERGE_STAMPS][blockIdx.x][11], 1ull);   // long-word visits
+#endif
 #pragma unroll 1
       for (int j = 0; j < n; ++j) {
         const unsigned long long nd = s_need[j];

@@ -94,7 +94,7 @@ def run(out_json=None) -> None:
                "merge_scan_done_med": us(np.median(m[:, 3] - t0)), "merge_scan_done_max": us(m[:, 3].max() - t0),
                "merge_exit_med": us(np.median(m[:, 4] - t0)), "merge_exit_max": us(m[:, 4].max() - t0),
                "merge_candidates": int(m[:, 5].sum()), "merge_words_rewritten": int(m[:, 6].sum()),
-               "merge_candidates_wg_max": int(m[:, 5].max())}
+               "merge_candidates_wg_max": int(m[:, 5].max()), "merge_long_word_visits": int(m[:, 11].sum())}
         vt = m[:, 3] - m[:, 2]   # visit phase per workgroup
         for k, nm in ((7, "meta"), (8, "word"), (9, "merged"), (10, "any_done")):   # last visit's metadata / word
             # in, last rewriting visit done, last visit of any kind done
@@ -152,7 +152,8 @@ def run(out_json=None) -> None:
                            "meta": ((m[ran, 7] - t0) / 100.0).round(2).tolist(),
                            "word": ((m[ran, 8] - t0) / 100.0).round(2).tolist(),
                            "merged": ((m[ran, 9] - t0) / 100.0).round(2).tolist(),
-                           "any_done": ((m[ran, 10] - t0) / 100.0).round(2).tolist()}
+                           "any_done": ((m[ran, 10] - t0) / 100.0).round(2).tolist(),
+                           "long_words": m[ran, 11].tolist()}
     out = {"merges": len(res.merges), "passes": res.stats.get("passes"), "passes_stamped": len(passes), "raw": raw,
            "median_over_passes_us": summary, "words": seen, "per_pass": passes, "loop_s": res.stats["merge_loop_s"]}
     print(json.dumps({k: out[k] for k in ("merges", "passes", "loop_s", "words")}))
