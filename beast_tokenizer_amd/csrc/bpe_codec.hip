@@ -36,6 +36,7 @@ constexpr int ENC_MAX_WAVES = 16;   // encode: as many rows per workgroup as the
 constexpr int BLOCK = 64 * WAVES;
 constexpr int MAX_SPECIAL = 64, MAX_SPECIAL_LEN = 64;
 constexpr int RM_PER = 8;           // symbol positions per lane of the round merge (rows <= 512 symbols)
+constexpr int RM_NARROW = 6;        // ... in the narrow kernel (rows <= 384 symbols)
 constexpr uint32_t RK_NONE = 0xFFFFFFFFu;
 constexpr int LDS_MAP_MAX_LOG2 = 13;   // stage maps of <= 8192 slots (64 KiB + rank table)
 constexpr size_t LDS_BUDGET = 160 * 1024;
@@ -46,18 +47,15 @@ constexpr int ST_OK = 0, ST_BELOW_MIN = 1, ST_ABOVE_MAX = 2, ST_NOT_UNICODE = 3,
               ST_NO_CLASS = 5, ST_TOO_LONG = 6;
 
 #ifdef BPE_STAMPS
-// tools/codec/bpe_encode_phases.py only (the product compiles these out): s_memtime cycles of
-// each encode phase summed over every row (lane 0 of each wave); [0] counts the rows, [8] the
-// merge-map staging
-__device__ unsigned long long g_bpe_stamps[16];
+// tools/codec/bpe_encode_phases.py only (the product compiles these out): per row r < 4096,
+// s_memrealtime (100 MHz) at each phase boundary [0, 7), then merge rounds, byte symbols, words
+// and the workgroup's map-staging start / end -- plain stores by lane 0, one slot per row, so
+// the stamps add no atomics and no shared address
+constexpr int BPE_RS = 4096;
+__device__ unsigned long long g_bpe_rs[BPE_RS][12];
 #define BPE_STAMP(k)                                                                          \
   do {                                                                                        \
-    if (lane == 0) {                                                                          \
-      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
-      if ((k) > 0) atomicAdd(&g_bpe_stamps[k], t_ - t_prev);                                  \
-      else atomicAdd(&g_bpe_stamps[0], 1ull);                                                 \
-      t_prev = t_;                                                                            \
-    }                                                                                         \
+    if (lane == 0 && r < BPE_RS) g_bpe_rs[r][k] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 #else
 #define BPE_STAMP(k) do { } while (0)
@@ -72,10 +70,10 @@ __device__ __forceinline__ void wave_sync() {
 __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // ------------------------------------------------------------- merge map --
-// layout: keys u32[cap] | vals u32[cap] ((rank + 1) << 16 | new_id, 0 = unset) | rank2new u16[n]
+// layout: kv uint2[cap] (key a << 16 | b, EMPTY_KEY = free; value (rank + 1) << 16 | new_id, 0 =
+// unset) | rank2new u16[n].  Key and value side by side: a probe is one 8-byte load.
 struct MergeMap {
-  const uint32_t* keys;
-  const uint32_t* vals;
+  const uint2* kv;
   const uint16_t* rank2new;
   int log2cap;
 };
@@ -84,25 +82,26 @@ __device__ __forceinline__ uint32_t mm_hash(uint32_t key, int log2cap) {
   return (key * 0x9E3779B1u) >> (32 - log2cap);
 }
 
-__global__ void k_mergemap_clear(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int cap) {
+__global__ void k_mergemap_clear(uint2* __restrict__ kv, int cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < cap) { keys[i] = EMPTY_KEY; vals[i] = 0u; }
+  if (i < cap) kv[i] = make_uint2(EMPTY_KEY, 0u);
 }
 
 __global__ void k_mergemap_build(const int32_t* __restrict__ ma, const int32_t* __restrict__ mb,
-                                 const int32_t* __restrict__ mnew, int n, uint32_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals, uint16_t* __restrict__ rank2new, int log2cap) {
+                                 const int32_t* __restrict__ mnew, int n, uint2* __restrict__ kv,
+                                 uint16_t* __restrict__ rank2new, int log2cap) {
+  uint32_t* const w = reinterpret_cast<uint32_t*>(kv);   // slot h: key at 2h, value at 2h + 1
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = ((uint32_t)ma[i] << 16) | (uint32_t)mb[i];
   const uint32_t mask = (1u << log2cap) - 1u;
   uint32_t h = mm_hash(key, log2cap);
   while (true) {
-    const uint32_t prev = atomicCAS(&keys[h], EMPTY_KEY, key);
+    const uint32_t prev = atomicCAS(&w[2 * h], EMPTY_KEY, key);
     if (prev == EMPTY_KEY || prev == key) break;
     h = (h + 1) & mask;
   }
-  atomicMax(&vals[h], ((uint32_t)(i + 1) << 16) | (uint32_t)mnew[i]);   // later rank wins
+  atomicMax(&w[2 * h + 1], ((uint32_t)(i + 1) << 16) | (uint32_t)mnew[i]);   // later rank wins
   rank2new[i] = (uint16_t)mnew[i];
 }
 
@@ -113,13 +112,12 @@ __device__ __forceinline__ int mm_find(const Map& m, int a, int b, int& new_id) 
   const uint32_t mask = (1u << m.log2cap) - 1u;
   uint32_t h = mm_hash(key, m.log2cap);
   while (true) {
-    const uint32_t k = m.keys[h];
-    if (k == key) {
-      const uint32_t v = m.vals[h];
-      new_id = (int)(v & 0xFFFFu);
-      return (int)(v >> 16) - 1;
+    const uint2 e = m.kv[h];
+    if (e.x == key) {
+      new_id = (int)(e.y & 0xFFFFu);
+      return (int)(e.y >> 16) - 1;
     }
-    if (k == EMPTY_KEY) return -1;
+    if (e.x == EMPTY_KEY) return -1;
     h = (h + 1) & mask;
   }
 }
@@ -361,12 +359,11 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
     }
     wave_sync();
     const int last = npos > 0 ? npos - 1 : 0;
+    // every round with a live pair merges at least one (each word's lowest pair has a head), so
+    // npos rounds bound the loop: a broken invariant ends it instead of hanging the wave
+    for (int round = 0; round < npos; ++round) {
 #ifdef BPE_STAMPS
-    if (lane == 0) { atomicAdd(&g_bpe_stamps[10], (unsigned long long)npos); atomicAdd(&g_bpe_stamps[11], (unsigned long long)nw); }
-#endif
-    while (true) {
-#ifdef BPE_STAMPS
-      if (lane == 0) atomicAdd(&g_bpe_stamps[9], 1ull);
+      if (lane == 0) L.misc[1] += 1;
 #endif
       for (int w = lane; w < nw; w += 64) L.wmin[w] = RK_NONE;
       // (a) ranks of the pairs next to last round's merges
@@ -381,18 +378,35 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
       int cn[RMP];
 #pragma unroll
       for (int k = 0; k < RMP; ++k) cn[k] = L.c[max(nk[k], 0)];
+      // the dirty pairs' first probes all in flight together (one 8-byte load each), then the
+      // rare collision chains per position
+      const uint32_t mmask = (1u << mm.log2cap) - 1u;
+      constexpr int PG = RMP < 4 ? RMP : 4;   // positions probed together (registers)
 #pragma unroll
-      for (int k = 0; k < RMP; ++k) {
-        if (!dk[k]) continue;
-        const int s = lane + 64 * k;
-        uint32_t v = RK_NONE;
-        if (ck[k] >= 0 && nk[k] >= 0) {
-          int nid;
-          const int rk = mm_find(mm, ck[k], cn[k], nid);
-          if (rk >= 0) v = ((uint32_t)rk << 16) | (uint32_t)nid;
+      for (int k0 = 0; k0 < RMP; k0 += PG) {
+        uint32_t key[PG], hs[PG];
+        uint2 e[PG];
+        bool q[PG];   // a live pair to look up (a dead symbol's key may equal EMPTY_KEY)
+#pragma unroll
+        for (int i = 0; i < PG; ++i) {
+          const int k = min(k0 + i, RMP - 1);   // RMP need not be a multiple of PG
+          q[i] = k0 + i < RMP && dk[k] && ck[k] >= 0 && nk[k] >= 0;
+          key[i] = ((uint32_t)ck[k] << 16) | (uint32_t)cn[k];
+          hs[i] = mm_hash(key[i], mm.log2cap);
+          e[i] = q[i] ? mm.kv[hs[i]] : make_uint2(EMPTY_KEY, 0u);
         }
-        L.rk[s] = v;
-        L.dirty[s] = 0;
+#pragma unroll
+        for (int i = 0; i < PG; ++i) {
+          const int k = min(k0 + i, RMP - 1);
+          if (k0 + i >= RMP || !dk[k]) continue;
+          while (q[i] && e[i].x != key[i] && e[i].x != EMPTY_KEY) {
+            hs[i] = (hs[i] + 1) & mmask;
+            e[i] = mm.kv[hs[i]];
+          }
+          // (rank + 1) << 16 | new_id  ->  rank << 16 | new_id
+          L.rk[lane + 64 * k] = (q[i] && e[i].x == key[i]) ? e[i].y - 0x10000u : RK_NONE;
+          L.dirty[lane + 64 * k] = 0;
+        }
       }
       wave_sync();
       // (b) every word's lowest pair
@@ -432,11 +446,39 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
       int pc[RMP];
 #pragma unroll
       for (int k = 0; k < RMP; ++k) pc[k] = L.cand[max(pk[k], 0)];
+      // the heads' first merges: their reads all issued before any write (no head writes what
+      // another head's first merge reads: nxt / cand of its own pair only, prv of the symbol
+      // after it -- read here only as the head's own left neighbour, which marks the same live
+      // pair dirty either way), then the rare self-pair runs one step at a time
+      bool hd[RMP];
+      int uk[RMP], nnk[RMP], cuk[RMP];
 #pragma unroll
       for (int k = 0; k < RMP; ++k) {
-        if (!cd[k] || (pk[k] >= 0 && pc[k])) continue;
+        hd[k] = cd[k] && !(pk[k] >= 0 && pc[k]);
+        uk[k] = hd[k] ? L.nxt[lane + 64 * k] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        nnk[k] = hd[k] ? L.nxt[uk[k]] : -1;
+        cuk[k] = hd[k] ? L.cand[uk[k]] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        if (!hd[k]) continue;
         const int nid = (int)(rv[k] & 0xFFFFu);
-        int t = lane + 64 * k;
+        const int t = lane + 64 * k, u = uk[k], nn = nnk[k];
+        L.c[t] = nid;
+        L.c[u] = -1;
+        L.nxt[t] = (int16_t)nn;
+        if (nn >= 0) L.prv[nn] = (int16_t)t;
+        L.dirty[t] = 1;
+        if (pk[k] >= 0) L.dirty[pk[k]] = 1;
+      }
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        if (!hd[k] || !cuk[k] || nnk[k] < 0 || !L.cand[nnk[k]]) continue;
+        const int nid = (int)(rv[k] & 0xFFFFu);
+        int t = nnk[k];   // the run of a self-pair goes on
         while (true) {
           const int u = L.nxt[t], nn = L.nxt[u];
           L.c[t] = nid;
@@ -446,7 +488,7 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
           L.dirty[t] = 1;
           const int pv = L.prv[t];
           if (pv >= 0) L.dirty[pv] = 1;
-          if (!L.cand[u] || nn < 0 || !L.cand[nn]) break;   // the run of a self-pair goes on
+          if (!L.cand[u] || nn < 0 || !L.cand[nn]) break;
           t = nn;
         }
       }
@@ -454,11 +496,14 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
     }
 }
 
-template <class Map>
+// RMX: the widest round merge compiled in.  RM_NARROW (rows of <= 384 byte symbols, e.g. 140 bins
+// of 2-byte code points) keeps the kernel at ~109 VGPRs with nothing spilled; the RM_PER form
+// needs 128 and spills ~16 to scratch.  The host launches the narrow kernel whenever every row fits.
+template <int RMX, class Map>
 __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r, int lane, const int32_t* b2i,
                            const uint8_t* lut256) {
 #ifdef BPE_STAMPS
-  unsigned long long t_prev = 0;
+  if (lane == 0) L.misc[1] = 0;
 #endif
   BPE_STAMP(0);
   const int64_t r0 = a.row_off[r];
@@ -620,8 +665,12 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
     //     merges, in every word, all occurrences of that word's lowest pair (left to right in a
     //     run of a self-pair: each run's head walks it), so rounds = distinct ranks applied per
     //     word, and only pairs next to a merge are looked up again.
-    if (npos <= 64 * 4) round_merge<4>(mm, L, npos, nw, lane);
-    else round_merge<RM_PER>(mm, L, npos, nw, lane);
+    if (npos <= 64 * 4) {
+      round_merge<4>(mm, L, npos, nw, lane);
+    } else {
+      if constexpr (RMX == RM_NARROW) round_merge<RM_NARROW>(mm, L, npos, nw, lane);
+      else round_merge<RM_PER>(mm, L, npos, nw, lane);
+    }
   } else {
     // 4b'. long rows: one word per lane with HF's (rank, pos) min-heap
     for (int w = lane; w < nw; w += 64) {
@@ -694,24 +743,30 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
   }
   if (lane == 0) { a.out_len[r] = carry; a.status[r] = ST_OK; }
   BPE_STAMP(6);
+#ifdef BPE_STAMPS
+  if (lane == 0 && r < BPE_RS) {
+    g_bpe_rs[r][7] = (unsigned long long)L.misc[1];
+    g_bpe_rs[r][8] = (unsigned long long)npos;
+    g_bpe_rs[r][9] = (unsigned long long)nw;
+  }
+#endif
 }
 
 // the merge map staged in LDS: offsets from the dynamic LDS base, so every probe is a ds_read
 struct LdsMap {
-  const uint32_t* keys;
-  const uint32_t* vals;
+  const uint2* kv;
   const uint16_t* rank2new;
   int log2cap;
 };
 
-template <bool MAP_LDS>
+template <bool MAP_LDS, int RMX>
 __global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
   extern __shared__ __align__(16) char lds_raw[];
   __shared__ int32_t s_b2i[256];    // byte -> vocab id
   __shared__ uint8_t s_lut[256];    // classes of code points < 256
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
 #ifdef BPE_STAMPS
-  const unsigned long long t_stage = __builtin_amdgcn_s_memtime();
+  const unsigned long long t_stage = __builtin_amdgcn_s_memrealtime();
 #endif
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     s_b2i[i] = a.byte2id[i];
@@ -722,30 +777,27 @@ __global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
   LdsMap lm;
   if constexpr (MAP_LDS) {
     const int cap = 1 << a.map.log2cap;
-    uint32_t* k = reinterpret_cast<uint32_t*>(lds_raw);
-    uint32_t* v = k + cap;
+    uint2* kv = reinterpret_cast<uint2*>(lds_raw);
     uint16_t* r2n = reinterpret_cast<uint16_t*>(lds_raw + al16(sizeof(uint32_t) * 2 * (size_t)cap));
-    // 16-byte copies (cap >= 64 is a multiple of 4; both halves are 16-byte aligned)
-    const uint4* gk = reinterpret_cast<const uint4*>(a.map.keys);
-    const uint4* gv = reinterpret_cast<const uint4*>(a.map.vals);
-    for (int i = threadIdx.x; i < cap / 4; i += blockDim.x) {
-      const uint4 x = gk[i], y = gv[i];
-      reinterpret_cast<uint4*>(k)[i] = x;
-      reinterpret_cast<uint4*>(v)[i] = y;
-    }
+    // 16-byte copies (cap >= 64 slots of 8 bytes, 16-byte aligned)
+    const uint4* g = reinterpret_cast<const uint4*>(a.map.kv);
+    for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) reinterpret_cast<uint4*>(kv)[i] = g[i];
     for (int i = threadIdx.x; i < a.n_merges; i += blockDim.x) r2n[i] = a.map.rank2new[i];
-    lm.keys = k; lm.vals = v; lm.rank2new = r2n; lm.log2cap = a.map.log2cap;
+    lm.kv = kv; lm.rank2new = r2n; lm.log2cap = a.map.log2cap;
     row_base = map_lds_bytes(a.map.log2cap, a.n_merges);
     __syncthreads();
   }
 #ifdef BPE_STAMPS
-  if (threadIdx.x == 0) atomicAdd(&g_bpe_stamps[8], __builtin_amdgcn_s_memtime() - t_stage);
+  if (lane == 0) {
+    const int64_t r0 = (int64_t)blockIdx.x * nwv + wave;
+    if (r0 < BPE_RS) { g_bpe_rs[r0][10] = t_stage; g_bpe_rs[r0][11] = __builtin_amdgcn_s_memrealtime(); }
+  }
 #endif
   const bool heap = enc_needs_heap(a.S, a.heap_merge);
   EncLds L = enc_carve(lds_raw + row_base + (size_t)wave * enc_row_bytes(a.Lc, a.S, heap), a.Lc, a.S, heap);
   for (int64_t r = (int64_t)blockIdx.x * nwv + wave; r < a.n_rows; r += (int64_t)gridDim.x * nwv) {
-    if constexpr (MAP_LDS) encode_row(a, lm, L, r, lane, s_b2i, s_lut);
-    else encode_row(a, a.map, L, r, lane, s_b2i, s_lut);
+    if constexpr (MAP_LDS) encode_row<RMX>(a, lm, L, r, lane, s_b2i, s_lut);
+    else encode_row<RMX>(a, a.map, L, r, lane, s_b2i, s_lut);
     wave_sync();
   }
 }
@@ -952,8 +1004,8 @@ int grid_for(int64_t n_rows, int per_cu = 4) {
 }  // namespace
 
 #ifdef BPE_STAMPS
-extern "C" int beast_debug_bpe_stamps(unsigned long long* host16) {
-  return hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_bpe_stamps), sizeof(g_bpe_stamps)) == hipSuccess ? 0 : -2;
+extern "C" int beast_debug_bpe_stamps(unsigned long long* host) {   // [4096][12]
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_rs), sizeof(g_bpe_rs)) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -971,8 +1023,7 @@ static MergeMap map_view(const void* map, int n_merges) {
   MergeMap m;
   m.log2cap = beast_bpe_mergemap_log2cap(n_merges);
   const size_t cap = size_t(1) << m.log2cap;
-  m.keys = reinterpret_cast<const uint32_t*>(map);
-  m.vals = m.keys + cap;
+  m.kv = reinterpret_cast<const uint2*>(map);
   m.rank2new = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(map) + al16(cap * 2 * sizeof(uint32_t)));
   return m;
 }
@@ -987,13 +1038,11 @@ extern "C" int beast_bpe_mergemap_build(const int32_t* merge_a, const int32_t* m
   const MergeMap m = map_view(map, n_merges);
   const int cap = 1 << m.log2cap;
   hipStream_t s = beast::as_stream(stream);
-  hipLaunchKernelGGL(k_mergemap_clear, dim3((cap + 255) / 256), dim3(256), 0, s, const_cast<uint32_t*>(m.keys),
-                     const_cast<uint32_t*>(m.vals), cap);
+  hipLaunchKernelGGL(k_mergemap_clear, dim3((cap + 255) / 256), dim3(256), 0, s, const_cast<uint2*>(m.kv), cap);
   BEAST_LAUNCHED("k_mergemap_clear");
   if (n_merges > 0) {
     hipLaunchKernelGGL(k_mergemap_build, dim3((n_merges + 255) / 256), dim3(256), 0, s, merge_a, merge_b, merge_new,
-                       n_merges, const_cast<uint32_t*>(m.keys), const_cast<uint32_t*>(m.vals),
-                       const_cast<uint16_t*>(m.rank2new), m.log2cap);
+                       n_merges, const_cast<uint2*>(m.kv), const_cast<uint16_t*>(m.rank2new), m.log2cap);
     BEAST_LAUNCHED("k_mergemap_build");
   }
   return BEAST_OK;
@@ -1044,18 +1093,25 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   a.Lc = max_row_cps; a.S = max_row_syms;
   a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
   const size_t lds = rows_lds + (a.map_in_lds ? map_lds : 0);
-  const void* fn = a.map_in_lds ? reinterpret_cast<const void*>(&k_bpe_encode<true>)
-                                : reinterpret_cast<const void*>(&k_bpe_encode<false>);
+  const bool narrow = max_row_syms <= 64 * RM_NARROW;   // every row fits the narrow kernel's round merge
+  const void* fn = a.map_in_lds ? (narrow ? reinterpret_cast<const void*>(&k_bpe_encode<true, RM_NARROW>)
+                                          : reinterpret_cast<const void*>(&k_bpe_encode<true, RM_PER>))
+                                : (narrow ? reinterpret_cast<const void*>(&k_bpe_encode<false, RM_NARROW>)
+                                          : reinterpret_cast<const void*>(&k_bpe_encode<false, RM_PER>));
   if (lds > 65536)
     BEAST_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
               "hipFuncSetAttribute(k_bpe_encode)");
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * nwv, lds) != hipSuccess || per_cu <= 0) per_cu = 1;
   const int grid = (int)std::min<int64_t>((n_rows + nwv - 1) / nwv, (int64_t)grid_for(1 << 30, per_cu));
-  if (a.map_in_lds)
-    hipLaunchKernelGGL(k_bpe_encode<true>, dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
+  if (a.map_in_lds && narrow)
+    hipLaunchKernelGGL((k_bpe_encode<true, RM_NARROW>), dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
+  else if (a.map_in_lds)
+    hipLaunchKernelGGL((k_bpe_encode<true, RM_PER>), dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
+  else if (narrow)
+    hipLaunchKernelGGL((k_bpe_encode<false, RM_NARROW>), dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
   else
-    hipLaunchKernelGGL(k_bpe_encode<false>, dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
+    hipLaunchKernelGGL((k_bpe_encode<false, RM_PER>), dim3(grid), dim3(64 * nwv), lds, beast::as_stream(stream), a);
   BEAST_LAUNCHED("k_bpe_encode");
   return BEAST_OK;
 }

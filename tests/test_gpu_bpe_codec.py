@@ -83,7 +83,7 @@ def test_decode_matches_hf_golden(case, gpu_device):
 
 @pytest.mark.parametrize("span,rows,width,vocab", [(255, 3000, 140, 2048), (700, 1500, 60, 1500),
                                                     (3000, 800, 50, 4000), (127, 2000, 140, 800),
-                                                    (255, 6000, 140, 6000)])
+                                                    (255, 6000, 140, 6000), (3000, 600, 140, 4000)])
 def test_codec_matches_live_hf(span, rows, width, vocab, encode_mode, gpu_device):
     """Train with HF (the reference's trainer), then every row of a fresh corpus -- including
     bins never seen in training -- encodes and decodes exactly as HF does."""

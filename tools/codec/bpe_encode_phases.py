@@ -1,6 +1,7 @@
-"""Where k_bpe_encode's time goes (tools only): a -DBPE_STAMPS build sums s_memtime cycles of each
-per-row phase over every row, on the bench's K5-model codec workload (4,096 rows x 140 bins).
-    python tools/codec/bpe_encode_phases.py build | run
+"""Where k_bpe_encode's time goes (tools only): a -DBPE_STAMPS build stores s_memrealtime at each
+per-row phase boundary (one slot per row, no atomics), on the bench's K5-model codec workload
+(4,096 rows x 140 bins).
+    python tools/codec/bpe_encode_phases.py build | run [out.json]
 """
 import ctypes as C
 import json
@@ -14,9 +15,6 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 LIB = os.path.join(HERE, "lib_bpestamps.so")
-PHASES = ["rows", "code points + checks", "utf-8 offsets", "word boundaries", "byte ids", "merges (heap)",
-          "output", "-", "map staging (per workgroup)"]
-
 
 def build():
     from beast_tokenizer_amd import _build
@@ -48,25 +46,41 @@ def run():
     rf, ro, w = rows_from_tensor(rows[:4096], dev)
     model.encode_rows(rf, ro, w, lo, span)
     torch.cuda.synchronize()
-    zero = (C.c_ulonglong * 16)()
-    buf = (C.c_ulonglong * 16)()
+    import numpy as np
+    buf = (C.c_ulonglong * (4096 * 12))()
     fn = lib.beast_debug_bpe_stamps
     fn.argtypes = [C.c_void_p]
-    assert fn(buf) == 0
-    before = list(buf)
     t0 = time.perf_counter()
     model.encode_rows(rf, ro, w, lo, span)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     assert fn(buf) == 0
-    d = [b - a for a, b in zip(before, buf)]
-    n = max(d[0], 1)
-    out = {"rows": d[0], "wall_us": el * 1e6,
-           "cycles_per_row": {PHASES[k]: d[k] / n for k in range(1, 7)},
-           "staging_cycles_per_workgroup": d[8] / max(1, (4096 + 3) // 4),
-           "rounds_per_row": d[9] / n, "symbols_per_row": d[10] / n, "words_per_row": d[11] / n}
-    print(json.dumps(out))
-    del zero
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 12).astype(np.int64)
+    ok = st[:, 0] > 0
+    st = st[ok]
+    t00 = st[st[:, 10] > 0, 10].min()
+    us = lambda v: np.round(v / 100.0, 2)   # noqa: E731  (100 MHz)
+    names = ["code points + checks", "utf-8 offsets", "word boundaries", "byte ids", "symbol lists + merges",
+             "output"]
+    ph = {names[k]: st[:, k + 1] - st[:, k] for k in range(6)}
+    q = lambda v: [float(x) for x in us(np.percentile(v, [50, 90, 99, 100]))]   # noqa: E731
+    out = {"rows": int(ok.sum()), "wall_us": el * 1e6,
+           "phase_us_p50_p90_p99_max": {k: q(v) for k, v in ph.items()},
+           "row_start_us_p50_max": [float(x) for x in us(np.percentile(st[:, 0] - t00, [50, 100]))],
+           "row_end_us_p50_max": [float(x) for x in us(np.percentile(st[:, 6] - t00, [50, 100]))],
+           "row_total_us_p50_p90_max": [float(x) for x in us(np.percentile(st[:, 6] - st[:, 0], [50, 90, 100]))],
+           "staging_us_p50_max": [float(x) for x in us(np.percentile(st[st[:, 11] > 0, 11] - st[st[:, 11] > 0, 10], [50, 100]))],
+           "rounds_p50_max": [float(np.median(st[:, 7])), int(st[:, 7].max())],
+           "symbols_p50_max": [float(np.median(st[:, 8])), int(st[:, 8].max())],
+           "words_p50_max": [float(np.median(st[:, 9])), int(st[:, 9].max())]}
+    slow = np.argsort(-(st[:, 6] - t00))[:5]
+    out["slowest_rows"] = [{"end_us": float(us(st[i, 6] - t00)), "start_us": float(us(st[i, 0] - t00)),
+                            **{k: float(us(v[i])) for k, v in ph.items()}, "rounds": int(st[i, 7]),
+                            "symbols": int(st[i, 8]), "words": int(st[i, 9])} for i in slow]
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 2:
+        with open(sys.argv[2], "w") as f:
+            json.dump(out, f, indent=1)
 
 
 if __name__ == "__main__":
