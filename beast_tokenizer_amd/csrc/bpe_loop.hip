@@ -693,9 +693,10 @@ __device__ __forceinline__ void rank_row_top(const uint32_t* __restrict__ row, i
 // candidates ranked by one pass over them: still exactly the row's keys >= the floor.  The top
 // RT_K are kept (the floor rises to the last kept when some are cut).  Returns false (a full
 // re-rank is needed) when fewer than KR + 1 remain above a floor > 1.  The wave calls it together.
-__device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row, const unsigned long long* __restrict__ g,
-                                               int x, int Vt, int lane, int n, const int (&A)[BK], const int (&B)[BK],
-                                               const int (&N)[BK], unsigned long long* __restrict__ out) {
+__device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row, unsigned long long F,
+                                               unsigned long long kc, int x, int Vt, int lane, int n,
+                                               const int (&A)[BK], const int (&B)[BK], const int (&N)[BK],
+                                               unsigned long long* __restrict__ out) {
   int col[3 * BK];   // uniform: the changed columns, -1 unused
 #pragma unroll
   for (int j = 0; j < BK; ++j) {
@@ -703,10 +704,10 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
     col[BK + j] = j < n ? N[j] : -1;
     col[2 * BK + j] = j < n && A[j] == x ? B[j] : -1;
   }
-  const unsigned long long F = g[RT_F];
+  // F = the cached floor, kc = the lane's cached key (lanes < RT_K), loaded by the caller
   unsigned long long k = 0ull;
   if (lane < RT_K) {
-    k = g[lane];
+    k = kc;
     const int y = key_col(k, x, Vt);
     bool drop = false;
 #pragma unroll
@@ -1050,6 +1051,20 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #define KA_PI 0
 #endif
   ASTAMP(KA_PI, 0);
+  // rows interleaved over the workgroups (x = blockIdx + wave * grid): the rows a batch touches
+  // -- neighbours of its pairs, often a run of early, frequent ids -- spread over the grid
+  // instead of filling a few workgroups' waves (a workgroup re-ranking 14 of its 16 rows was the
+  // pass's last ticket, 8.4 us against 4.4 for the median re-ranking one)
+  const int x = (int)blockIdx.x + wave * (int)gridDim.x;
+  // the row's clean flag and cached keys do not depend on the batch record: in flight with it
+  uint32_t pre_clean = 0u;
+  unsigned long long pre_k = 0ull, pre_F = 0ull;
+  if (x < nrows) {
+    const unsigned long long* g = bw.rowtop + (size_t)x * RT_STRIDE;
+    pre_clean = aw.clean[x];
+    pre_k = lane < RT_K ? g[lane] : 0ull;
+    pre_F = g[RT_F];
+  }
   const int n = init ? 0 : loop->bn;
   if (!init && (n == 0 || !loop->active)) return;   // uniform over the grid
   int A[BK], B[BK], N[BK];
@@ -1060,11 +1075,6 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     N[j] = j < n ? loop->bnid[j] : -1;
   }
   const int vcur = init ? loop->vcur : loop->bvcur;
-  // rows interleaved over the workgroups (x = blockIdx + wave * grid): the rows a batch touches
-  // -- neighbours of its pairs, often a run of early, frequent ids -- spread over the grid
-  // instead of filling a few workgroups' waves (a workgroup re-ranking 14 of its 16 rows was the
-  // pass's last ticket, 8.4 us against 4.4 for the median re-ranking one)
-  const int x = (int)blockIdx.x + wave * (int)gridDim.x;
   // rows the merges changed: b_j, new_j entirely (re-ranked); other rows x only at columns a_j,
   // new_j (k_merge_batch's adds: clean[x] == 0; or the sharded deltas: touched) and, for x = a_j,
   // b_j (retired below)
@@ -1109,14 +1119,14 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   if (x < nrows && x < vcur) {
     unsigned long long* g = bw.rowtop + (size_t)x * RT_STRIDE;
     const uint32_t* row = table + (size_t)x * Vt;
-    if (!full && !touched && !in_a && aw.clean[x]) {
-      if (lane <= KR) rt[lane] = g[lane];
+    if (!full && !touched && !in_a && pre_clean) {
+      if (lane <= KR) rt[lane] = pre_k;
     } else {
 #ifdef BPE_MERGE_STAMPS
       const bool st_on = lane == 0 && blockIdx.x < 256 && KA_PI >= BPE_MERGE_STAMPS && KA_PI < BPE_MERGE_STAMPS + 64;
       unsigned long long* st_a = st_on ? g_apply_stamps[KA_PI - BPE_MERGE_STAMPS][blockIdx.x] : nullptr;
       if (st_on) atomicMax(&st_a[4], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-      const bool upd = !full && row_top_update(row, g, x, Vt, lane, n, A, B, N, rt);
+      const bool upd = !full && row_top_update(row, pre_F, pre_k, x, Vt, lane, n, A, B, N, rt);
       if (st_on) atomicMax(&st_a[5], (unsigned long long)__builtin_amdgcn_s_memrealtime());
       if (!upd) {   // the row's first stretch loaded and used, then the rank (cache hits)
         int32_t cw[32];
@@ -1133,7 +1143,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
         atomicAdd(&st_a[7], upd ? 1ull : 1ull << 32);
       }
 #else
-      if (full || !row_top_update(row, g, x, Vt, lane, n, A, B, N, rt)) rank_row_top(row, x, Vt, vcur, lane, rt);
+      if (full || !row_top_update(row, pre_F, pre_k, x, Vt, lane, n, A, B, N, rt)) rank_row_top(row, x, Vt, vcur, lane, rt);
 #endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
