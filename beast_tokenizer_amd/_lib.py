@@ -40,6 +40,9 @@ SIGNATURES = {
                                 _i32, _i64, _vp, _vp, _vp]),
     "beast_encode_list_f32": (_i32, [_vp, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp]),
     "beast_quantize_f32": (_i32, [_vp, _i64, _i32, _i32, _vp, _vp, _i32, _i64, _i32, _vp, _vp, _vp]),
+    "beast_cond_fixed_f32": (_i32, [_vp, _i64, _i32, _i64, _i64, _i64, _vp, _i32, _vp, _vp, _i32, _i32, _f32, _i32,
+                                    _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "beast_cond_add_f32": (_i32, [_vp, _i64, _i32, _i32, _vp, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     "beast_reconstruct_f32": (_i32, [_vp, _i64, _i32, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _i64, _i32, _vp, _i32,
                                      _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "beast_colminmax_workspace_bytes": (_sz, [_i64, _i32]),

@@ -319,16 +319,42 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if rc:
             _lib.check(rc, "beast_encode_f32")
         if self._conditioned:
-            self._store_conditions(trajs)
+            self._store_conditions(trajs, p)
         return params, tokens
 
-    def _store_conditions(self, trajs: torch.Tensor) -> None:
+    def _cond_consts(self, dev: torch.device):
+        """(joint DoF map int32, time grid fp32, joint knot vector) on dev for csrc/cond.hip."""
+        key = (dev, self._times_version)
+        cache = getattr(self, "_cond_cache", {})
+        c = cache.get(key)
+        if c is None:
+            c = (torch.tensor(self.joint_indices, dtype=torch.int32, device=dev),
+                 self.times.to(dev, torch.float32).reshape(-1).contiguous(),
+                 self._basis.knots(dev, 0).to(torch.float32).contiguous())
+            self._cond_cache = {key: c}
+        return c
+
+    def _store_conditions(self, trajs: torch.Tensor, p) -> None:
         """init / end conditions of the joint MP from this batch (uni_bspline.py:499-550), kept
-        for the next reconstruct as the reference's MP object keeps them."""
-        yj = trajs[..., self.joint_indices]
-        t = self.times.to(trajs.device, torch.float32).reshape(-1)
-        ip, iv, ep, ev, p_init, p_end = self._basis.fixed_ctrl(yj, t[1] - t[0])
-        self._cond_state = {"B": trajs.shape[0], "init_pos": ip, "init_vel": iv, "end_pos": ep, "end_vel": ev,
+        for the next reconstruct as the reference's MP object keeps them: one launch of
+        k_cond_fixed (csrc/cond.hip) over trajs [B, T, D] (fp32 on the plan's device)."""
+        jidx, t, kv = self._cond_consts(p.dev)
+        B, T = trajs.shape[0], trajs.shape[1]
+        dj, ic, ec = jidx.numel(), self._basis.ic, self._basis.ec
+
+        def out(*shape):
+            return torch.empty(shape, dtype=torch.float32, device=p.dev)
+        ip = iv = ep = ev = p_init = p_end = None
+        if ic:
+            ip, iv, p_init = out(B, dj), out(B, dj), out(B, dj, ic)
+        if ec:
+            ep, ev, p_end = out(B, dj), out(B, dj), out(B, dj, abs(ec))
+        st = trajs.stride()
+        _lib.run("beast_cond_fixed_f32", trajs.data_ptr(), B, T, st[0], st[1], st[2], jidx.data_ptr(), dj,
+                 t.data_ptr(), kv.data_ptr(), self._basis.degrees[0], self._basis.n_ctrl, float(self._basis.tau),
+                 ic, ec, *map(_lib.ptr, (ip, iv, ep, ev, p_init, p_end)),
+                 _lib.stream_of(p.dev))
+        self._cond_state = {"B": B, "init_pos": ip, "init_vel": iv, "end_pos": ep, "end_vel": ev,
                             "params_init": p_init, "params_end": p_end}
 
     def _cond_dict(self) -> dict:
@@ -354,9 +380,15 @@ class BEASTBsplineTokenizer(TokenizerBase):
                 self._full_basis = {key: self._basis.full_basis_at(self.times.to(dev).reshape(-1))}
                 full = self._full_basis[key]
         else:   # [T] or per-row [B, T] grids -> [T, C] / [B, T, C]
-            full = self._basis.full_basis_at(times.to(dev, dtype=torch.float32))
-        bias = self._basis.fixed_term(full, st["params_init"], st["params_end"], st["init_pos"], fit=False)
-        pos[..., self.joint_indices] += bias
+            full = self._basis.full_basis_at(times.to(dev, dtype=torch.float32)).contiguous()
+        if full.dim() not in (2, 3) or full.shape[-2] != pos.shape[1]:
+            raise ValueError(f"times grid {tuple(full.shape[:-1])} does not match positions {tuple(pos.shape)}")
+        jidx = self._cond_consts(dev)[0]
+        _lib.run("beast_cond_add_f32", pos.data_ptr(), B, pos.shape[1], pos.shape[2], jidx.data_ptr(), jidx.numel(),
+                 full.data_ptr(), 0 if full.dim() == 2 else full.shape[-2] * full.shape[-1], self._basis.n_ctrl,
+                 self._basis.ic, self._basis.ec, _lib.ptr(st["params_init"]), _lib.ptr(st["params_end"]),
+                 _lib.ptr(st["init_pos"]),
+                 _lib.stream_of(dev))
         return pos
 
     # ===============================================

@@ -114,7 +114,10 @@ class DeviceBasis:
 
     def fixed_ctrl(self, y: torch.Tensor, dt: torch.Tensor):
         """Boundary control points from trajectories y [..., T, Dj] (uni_bspline.py:499-550,
-        uni_bspline_basis.py:192-301, not goal_basis), in y's dtype and the reference's op order.
+        uni_bspline_basis.py:192-301, not goal_basis) -- here only for the float64 conditioned
+        projection built once per grid (conditioned_projection); every encode / reconstruct runs
+        csrc/cond.hip instead (k_cond_fixed / k_cond_add).  Same arithmetic, in y's dtype and the
+        reference's op order.
         Returns (init_pos, init_vel, end_pos_abs, end_vel, params_init [..., Dj, ic],
         params_end [..., Dj, |ec|]), entries None where the reference has None."""
         p = self.degrees[0]

@@ -137,6 +137,31 @@ int beast_reconstruct_f32(const int64_t* tokens, int64_t B, int D, int n_joint, 
                           const float* init_p, int64_t init_p_sb, const int32_t* init_p_src,
                           float* params_out, float* pos_out, const float* ntokens, void* stream);
 
+/* ---------------------------------------------------- §8f rank 4: conditions ---
+ * init_cond_order / end_cond_order != 0 (init_order in 0..2, end_order in -1..2, not both 0).
+ * beast_cond_fixed_f32 replaces the per-fit condition step of UniBSpline.learn
+ * (MP_lite_PyTorch/mp_pytorch/mp/uni_bspline.py:499-550 calling compute_init_params /
+ * compute_end_params, basis_gn/uni_bspline_basis.py:192-301): for trajectories traj
+ * [B][T][*] (element strides sb, st, sd) and the joint DoFs joint_idx[dj], with
+ * dt = times[1] - times[0] and the knot steps knots[1+degree] - knots[1] /
+ * knots[n_ctrl-1+degree] - knots[n_ctrl-1] of the joint spline (n_ctrl control points):
+ *   init_pos, init_vel [B][dj], params_init [B][dj][init_order]   (init_order > 0)
+ *   end_pos, end_vel [B][dj], params_end [B][dj][|end_order|]     (end_order != 0)
+ * in the reference's fp32 op order.  T >= 2.
+ * beast_cond_add_f32 replaces the fixed control points' part of UniBSpline.get_traj_pos
+ * (uni_bspline.py:126-166): pos [B][T][D] (contiguous, the fitted columns' positions from
+ * beast_reconstruct_f32) gains, at the joint DoFs, sum_k full_basis[t][k] * fixed[k] (+ init_pos
+ * when init_order > 0) over the fixed columns k (the first init_order, the last |end_order|;
+ * end order -1 subtracts params_end from column n_ctrl-2).  full_basis [T][n_ctrl] with
+ * full_sb = 0, or per trajectory [B][T][n_ctrl] with full_sb = T * n_ctrl. */
+int beast_cond_fixed_f32(const float* traj, int64_t B, int T, int64_t sb, int64_t st, int64_t sd,
+                         const int32_t* joint_idx, int dj, const float* times, const float* knots, int degree,
+                         int n_ctrl, float tau, int init_order, int end_order, float* init_pos, float* init_vel,
+                         float* end_pos, float* end_vel, float* params_init, float* params_end, void* stream);
+int beast_cond_add_f32(float* pos, int64_t B, int T, int D, const int32_t* joint_idx, int dj,
+                       const float* full_basis, int64_t full_sb, int n_ctrl, int init_order, int end_order,
+                       const float* params_init, const float* params_end, const float* init_pos, void* stream);
+
 /* ------------------------------------------------------------------ H13 ---
  * Column min / max with NaN propagation (torch.min/max(dim=0)), used by
  * update_weights_bounds / update_weights_bounds_per_batch (:362-389).

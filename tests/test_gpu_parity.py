@@ -690,6 +690,41 @@ def test_conditions_match_reference(case, gpu_device):
         tok.reconstruct_traj(torch.from_numpy(rt[:5]).to(gpu_device))    # conditions fitted on 32 rows
 
 
+@pytest.mark.parametrize("ic,ec", [(1, 0), (2, 0), (0, 1), (0, 2), (0, -1), (1, 1), (2, 2), (2, -1), (1, -1)])
+def test_condition_kernels_match_torch_restatement(ic, ec, gpu_device):
+    """csrc/cond.hip (k_cond_fixed, k_cond_add) against bspline.DeviceBasis.fixed_ctrl /
+    fixed_term -- the reference's ATen op sequence in fp32 (uni_bspline_basis.py:192-301,
+    uni_bspline.py:126-166): every condition output and the reconstruct term, shared and
+    per-row time grids, gripper DoFs left untouched."""
+    from beast_tokenizer_amd import _lib
+    g = [6, 13]
+    x = torch.from_numpy(synth_trajectories(32, 50, 14, seed=7, gripper_indices=g)).to(gpu_device)
+    tok = BEASTBsplineTokenizer(num_dof=14, gripper_zero_order=True, gripper_indices=g, init_cond_order=ic,
+                                end_cond_order=ec, device=str(gpu_device))
+    tok.encode(x)
+    st, b = tok._cond_state, tok._basis
+    t = tok.times.to(gpu_device, torch.float32).reshape(-1)
+    want = b.fixed_ctrl(x[..., tok.joint_indices], t[1] - t[0])
+    names = ("init_pos", "init_vel", "end_pos", "end_vel", "params_init", "params_end")
+    for name, w in zip(names, want):
+        if w is None:
+            assert st[name] is None, name
+        else:
+            np.testing.assert_allclose(st[name].cpu().numpy(), w.cpu().numpy(), rtol=1e-6, atol=1e-7, err_msg=name)
+    jidx = torch.tensor(tok.joint_indices, dtype=torch.int32, device=gpu_device)
+    for times in (t, torch.linspace(0, 1, 30, device=gpu_device).repeat(32, 1) * torch.rand(32, 1, device=gpu_device)):
+        full = b.full_basis_at(times).contiguous()
+        T = full.shape[-2]
+        pos = torch.zeros((32, T, 14), dtype=torch.float32, device=gpu_device)
+        _lib.run("beast_cond_add_f32", pos.data_ptr(), 32, T, 14, jidx.data_ptr(), jidx.numel(), full.data_ptr(),
+                 0 if full.dim() == 2 else T * full.shape[-1], b.n_ctrl, ic, ec, _lib.ptr(st["params_init"]),
+                 _lib.ptr(st["params_end"]), _lib.ptr(st["init_pos"]), _lib.stream_of(gpu_device))
+        ref = b.fixed_term(full, st["params_init"], st["params_end"], st["init_pos"], fit=False)
+        got = pos.cpu().numpy()
+        np.testing.assert_allclose(got[..., tok.joint_indices], ref.cpu().numpy(), rtol=1e-6, atol=1e-6)
+        assert not got[..., g].any()
+
+
 @pytest.mark.parametrize("loop", ["batch"])
 @pytest.mark.parametrize("case", ["traj_k2/2048", "skew/700", "wide3000/2048", "repeat700/300", "runs/2048"])
 def test_bpe_device_loop_matches_hf(case, loop, bpe_golden, gpu_device):

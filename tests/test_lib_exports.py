@@ -65,6 +65,9 @@ def test_abi_version():
                                None, None, None, None)),
     ("beast_encode_list_f32", (None, 3, 4096, 50, 14, 14, 14, None, None, 10, None, None)),
     ("beast_bpe_argmax", (None, 300, 300, None, 0, None)),
+    ("beast_cond_fixed_f32", (None, 4, 50, 700, 14, 1, None, 7, None, None, 4, 13, 1.0, 2, 1, None, None, None,
+                              None, None, None, None)),
+    ("beast_cond_add_f32", (None, 4, 50, 14, None, 7, None, 0, 13, 2, 1, None, None, None, None)),
 ])
 def test_null_pointers_are_rejected_before_any_hip_call(name, args):
     rc = getattr(_lib.load(), name)(*args)
@@ -82,6 +85,16 @@ def test_shape_validation():
                               None)
     assert rc in (_lib.BEAST_E_INVALID, _lib.BEAST_E_UNSUPPORTED)
     rc = lib.beast_quantize_f32(fake, -1, 14, 10, fake, fake, 256, 0, 0, fake, None, None)
+    assert rc == _lib.BEAST_E_INVALID
+    # boundary conditions: orders out of range / both zero, T < 2, a missing init output
+    for ic, ec, T in ((3, 0, 50), (0, 0, 50), (0, -2, 50), (1, 0, 1)):
+        rc = lib.beast_cond_fixed_f32(fake, 4, T, 700, 14, 1, fake, 7, fake, fake, 4, 13, 1.0, ic, ec, fake, fake,
+                                      fake, fake, fake, fake, None)
+        assert rc == _lib.BEAST_E_INVALID, (ic, ec, T)
+    rc = lib.beast_cond_fixed_f32(fake, 4, 50, 700, 14, 1, fake, 7, fake, fake, 4, 13, 1.0, 2, 0, None, fake,
+                                  None, None, fake, None, None)
+    assert rc == _lib.BEAST_E_INVALID
+    rc = lib.beast_cond_add_f32(fake, 4, 50, 5, fake, 7, fake, 0, 13, 1, 1, fake, fake, fake, None)   # D < dj
     assert rc == _lib.BEAST_E_INVALID
 
 
