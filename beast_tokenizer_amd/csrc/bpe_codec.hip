@@ -438,35 +438,32 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
         cd[k] = ck[k] >= 0 && rv[k] != RK_NONE && rv[k] == mv[k];
         if (k < kmax && lane + 64 * k < npos) L.cand[lane + 64 * k] = cd[k];
       }
+      // links only (d) changes, read in this step's round trip: each position's left neighbour
+      // and the symbol after its pair (its right one, nk, is from (a): nxt is unchanged since)
+      int pk[RMP], nnk[RMP];
+#pragma unroll
+      for (int k = 0; k < RMP; ++k) {
+        pk[k] = L.prv[min(lane + 64 * k, last)];
+        nnk[k] = L.nxt[max(nk[k], 0)];
+      }
       wave_sync();
-      // (d) each run's head applies its run (one merge unless a self-pair repeats)
-      int pk[RMP];
+      // (d) each run's head applies its run (one merge unless a self-pair repeats).  The heads'
+      // first merges read everything in one round trip before any write (no head writes what
+      // another head's first merge reads: nxt / cand of its own pair only, prv of the symbol after
+      // it -- read here only as the head's own left neighbour, which marks the same live pair
+      // dirty either way), then the rare self-pair runs one step at a time
+      int cf[RMP];   // cand of the left neighbour (bit 0), of the pair's right symbol (1), of the one after (2)
 #pragma unroll
-      for (int k = 0; k < RMP; ++k) pk[k] = L.prv[min(lane + 64 * k, last)];
-      int pc[RMP];
-#pragma unroll
-      for (int k = 0; k < RMP; ++k) pc[k] = L.cand[max(pk[k], 0)];
-      // the heads' first merges: their reads all issued before any write (no head writes what
-      // another head's first merge reads: nxt / cand of its own pair only, prv of the symbol
-      // after it -- read here only as the head's own left neighbour, which marks the same live
-      // pair dirty either way), then the rare self-pair runs one step at a time
+      for (int k = 0; k < RMP; ++k)
+        cf[k] = (int)L.cand[max(pk[k], 0)] | ((int)L.cand[max(nk[k], 0)] << 1) | ((int)L.cand[max(nnk[k], 0)] << 2);
       bool hd[RMP];
-      int uk[RMP], nnk[RMP], cuk[RMP];
 #pragma unroll
-      for (int k = 0; k < RMP; ++k) {
-        hd[k] = cd[k] && !(pk[k] >= 0 && pc[k]);
-        uk[k] = hd[k] ? L.nxt[lane + 64 * k] : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < RMP; ++k) {
-        nnk[k] = hd[k] ? L.nxt[uk[k]] : -1;
-        cuk[k] = hd[k] ? L.cand[uk[k]] : 0;
-      }
+      for (int k = 0; k < RMP; ++k) hd[k] = cd[k] && !(pk[k] >= 0 && (cf[k] & 1));
 #pragma unroll
       for (int k = 0; k < RMP; ++k) {
         if (!hd[k]) continue;
         const int nid = (int)(rv[k] & 0xFFFFu);
-        const int t = lane + 64 * k, u = uk[k], nn = nnk[k];
+        const int t = lane + 64 * k, u = nk[k], nn = nnk[k];
         L.c[t] = nid;
         L.c[u] = -1;
         L.nxt[t] = (int16_t)nn;
@@ -476,7 +473,7 @@ __device__ __forceinline__ void round_merge(const Map& mm, EncLds& L, int npos, 
       }
 #pragma unroll
       for (int k = 0; k < RMP; ++k) {
-        if (!hd[k] || !cuk[k] || nnk[k] < 0 || !L.cand[nnk[k]]) continue;
+        if (!hd[k] || !(cf[k] & 2) || nnk[k] < 0 || !(cf[k] & 4)) continue;
         const int nid = (int)(rv[k] & 0xFFFFu);
         int t = nnk[k];   // the run of a self-pair goes on
         while (true) {
