@@ -373,6 +373,10 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if st["B"] != B:
             raise RuntimeError(f"Sizes of tensors must match except in dimension 2. Expected size {st['B']} "
                                f"but got size {B} (boundary conditions were fitted on a batch of {st['B']})")
+        sdev = next(v.device for v in (st["init_pos"], st["end_pos"]) if v is not None)
+        if sdev != dev:   # the kernel reads these raw pointers on dev: refuse as ATen's einsum did
+            raise RuntimeError(f"Expected all tensors to be on the same device, but found at least two devices, "
+                               f"{sdev} and {dev}! (boundary conditions were fitted on {sdev})")
         if times is None:
             key = (dev, self._times_version)
             full = self._full_basis.get(key)

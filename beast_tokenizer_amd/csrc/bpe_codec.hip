@@ -301,16 +301,23 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
 // any other entry (rare: regex words self-synchronise within a word) makes the lane re-walk its
 // segment from it -- repeated until no exit changes.  Starts = marked positions at or past
 // their segment's entry, written in order by a wave scan.
+// Invariant: the marks in [ws, se) are exactly the positions of the lane's latest walk, which
+// started at ws and leaves the segment at wex.  The exit passed on, ex, is wex when the entry lies
+// on that walk, or the entry itself when the chain jumps the segment.  A marked entry below ws is
+// a mark of an older walk (e.g. "x!'tion": the walk from "'" marks "t" before the chain is known
+// to enter at "t"), so only a marked entry at or past ws reuses the walk; anything else re-walks.
 __device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, EncLds& L, int n, int lane) {
   const int G = (n + 63) >> 6;
   const int sb = min(lane * G, n), se = min(sb + G, n);
   for (int i = lane; i < n; i += 64) vis[i] = 0;
   wave_sync();
-  int ex = sb;   // exit: the first chain position >= se (n past the end)
+  int ex = sb;    // exit passed to the next lane: the first chain position >= se (n past the end)
+  int ws = sb;    // start of the walk the marks in [ws, se) belong to
+  int wex = sb;   // that walk's exit
   if (sb < se) {
     int p = sb;
     while (p < se) { vis[p] = 1; p = e[p]; }
-    ex = p;
+    wex = ex = p;
   }
   int entry = 0;
   while (true) {
@@ -321,11 +328,14 @@ __device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, EncL
     if (sb < se) {
       if (en >= se) {
         nex = en;                 // the chain jumps this segment
-      } else if (en >= sb && !vis[en]) {
+      } else if (en >= sb && en >= ws && vis[en]) {
+        nex = wex;                // the entry lies on the latest walk
+      } else if (en >= sb) {
         for (int i = en; i < se; ++i) vis[i] = 0;   // re-walk from the true entry
         int p = en;
         while (p < se) { vis[p] = 1; p = e[p]; }
-        nex = p;
+        nex = wex = p;
+        ws = en;
         changed = true;
       }
     } else {

@@ -163,7 +163,7 @@ py::list rows_to_lists(const at::Tensor& ids, const at::Tensor& lens) {
   // every list slot holds a reference to a cached int: instead of one Py_INCREF per slot (a
   // read-modify-write of a refcount that the same few thousand objects keep repeating), count the
   // slots per id first and add each id's count to its refcount once
-  static std::vector<Py_ssize_t> uses(65536, 0);
+  std::vector<Py_ssize_t> uses(65536, 0);   // per call: nothing stale survives a throw
   int32_t hi = -1;
   for (int64_t r = 0; r < R; ++r) {
     const int64_t n = std::min<int64_t>(std::max<int32_t>(L[r], 0), W);
@@ -175,18 +175,31 @@ py::list rows_to_lists(const at::Tensor& ids, const at::Tensor& lens) {
   }
   for (int32_t v = 0; v <= hi; ++v)
     if (uses[v]) { Py_SET_REFCNT(cache[v], Py_REFCNT(cache[v]) + uses[v]); uses[v] = 0; }
+  // on an allocation failure the references counted for slots never filled (row r from slot i on,
+  // and every later row) are handed back before the throw
+  auto fail = [&](int64_t r, int64_t i, PyObject* row, PyObject* out) {
+    for (int64_t rr = r; rr < R; ++rr) {
+      const int64_t n = std::min<int64_t>(std::max<int32_t>(L[rr], 0), W);
+      const int32_t* q = p + rr * W;
+      for (int64_t k = rr == r ? i : 0; k < n; ++k)
+        if (q[k] >= 0 && q[k] < 65536) Py_DECREF(cache[q[k]]);
+    }
+    Py_XDECREF(row);   // drops the slots it holds (a fresh list's empty slots are NULL)
+    Py_XDECREF(out);
+    throw py::error_already_set();
+  };
   PyObject* out = PyList_New(R);
-  if (!out) throw py::error_already_set();   // (the counted references are then leaked, never freed: ints)
+  if (!out) fail(0, 0, nullptr, nullptr);
   for (int64_t r = 0; r < R; ++r) {
     const int64_t n = std::min<int64_t>(std::max<int32_t>(L[r], 0), W);
     PyObject* row = PyList_New(n);
-    if (!row) { Py_DECREF(out); throw py::error_already_set(); }
+    if (!row) fail(r, 0, nullptr, out);
     const int32_t* q = p + r * W;
     for (int64_t i = 0; i < n; ++i) {
       const int32_t v = q[i];
       PyObject* o;
       if (v >= 0 && v < 65536) o = cache[v];   // its reference was counted above
-      else if (!(o = PyLong_FromLong(v))) { Py_DECREF(row); Py_DECREF(out); throw py::error_already_set(); }
+      else if (!(o = PyLong_FromLong(v))) fail(r, i, row, out);
       PyList_SET_ITEM(row, i, o);
     }
     PyList_SET_ITEM(out, r, row);

@@ -71,6 +71,8 @@ FIT_BYTES = T * D * 4 + D * N * 4 * (1 + 4)      # read traj; params written onc
 FIT_FLOPS = 2 * T * N * D                        # per trajectory per direction
 K5_GOLDEN = os.path.join(REPO, "tests", "golden", "k5_bpe.json")
 K5_CHUNK = 8192
+# what this rank computed, returned by main() (tests/test_gpu_bench_dist.py compares the ranks)
+RANK_INFO: dict = {}
 
 
 def parse():
@@ -292,6 +294,7 @@ def fit_bench(dev, args, world, rank):
            "algo_bytes_per_traj": FIT_BYTES, "achieved_GBps": FIT_BYTES * n / el / 1e9 / world,
            "hbm_frac": FIT_BYTES * n / el / world / HBM_PEAK,
            "w_min_checksum": float(ftok.w_min.double().sum()), "w_max_checksum": float(ftok.w_max.double().sum())}
+    RANK_INFO["fit_bounds"] = (ftok.w_min.cpu().tolist(), ftok.w_max.cpu().tolist())
     if world == 1:
         # full-size parity: the bounds are np.quantile (numpy 2.x linear method, the reference's
         # beast_bspline_tokenizer.py:211-214) of the very params the GPU fitted
@@ -390,6 +393,8 @@ def bpe_bench(dev, args, world, rank, reduce):
         del flat, off
     el = times[-1]
     st = res.stats
+    RANK_INFO["bpe_merges"] = [list(m) for m in res.merges]
+    RANK_INFO["bpe_vocab"] = res.vocab
     if world == 1:
         # §8d's byte count needs the pair occurrences every merge rewrote: an untimed rerun of the
         # same loop that counts them (same corpus -> same merges)
@@ -721,8 +726,10 @@ def main():
         if cpu and cpu.get("value"):
             line["gpu_over_cpu"] = value / cpu["value"]
         print(json.dumps(line), flush=True)
+        RANK_INFO["line"] = line
     if world > 1:
         torch.distributed.destroy_process_group()
+    return dict(RANK_INFO, rank=rank, world=world)
 
 
 if __name__ == "__main__":

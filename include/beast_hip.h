@@ -258,10 +258,10 @@ int beast_bpe_apply_argmax(uint32_t* table, int32_t* deltas, int Vt, int vcur, i
                            uint32_t* tlen, uint64_t* ws, int call, void* stream);
 
 /* Device-driven, batched (the default): merges are decided on the GPU, several per pass and
- * exactly HF's sequence -- each pass takes the table's top pairs in HF order while they are
- * symbol-disjoint, the last taken is not a self-pair, no string re-uses an id (only the first
- * may) and no taken row's second-best pair ranks above the next (csrc/bpe_loop.hip, "batched
- * merges", has the proof); stop rules: vocab_size reached, count below min_frequency, log full.
+ * exactly HF's sequence -- each pass takes the table's top pairs in HF order while none chains
+ * onto a taken one (its right symbol a taken left symbol, or its left a taken right), no taken
+ * pair was a self-pair or re-used an id, and no taken row's next key ranks above it
+ * (csrc/bpe_loop.hip, "batched merges", has the proof); stop rules: vocab_size reached, count below min_frequency, log full.
  * Ids of new strings come from a (64-bit string hash, byte length) table of the vocabulary
  * (HF's id reuse); the host replays the log against the real strings.
  * tok_hash / tok_pow: per initial token, h = sum bytes[i] * P^(n-1-i) and P^n (mod 2^64) of its

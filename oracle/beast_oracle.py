@@ -114,13 +114,21 @@ def _clamp_t(x, lo, hi):
     return np.where(hi < r, hi, r).astype(F32)
 
 
+# torch's CPU cast of a NaN float to int64 (``torch.round(nan).to(torch.long)``, beast/utils.py:16):
+# pinned by tests/golden/nonfinite_tokens.npz, which gen_goldens.py wrote with the reference itself
+NAN_TOKEN = np.int64(-(2 ** 63))
+
+
 def continuous_to_discrete(x: np.ndarray, wmin: np.ndarray, wmax: np.ndarray, num_bins: int) -> np.ndarray:
-    """beast/utils.py:4-17 in fp32: sub, div, clamp, mul, round-half-even."""
-    x = x.astype(F32)
-    scale = np.maximum(wmax.astype(F32) - wmin.astype(F32), F32(1e-8)).astype(F32)
-    n = ((x - wmin.astype(F32)) / scale).astype(F32)
-    n = np.clip(n, F32(0), F32(1)).astype(F32)
-    return np.rint((n * F32(num_bins - 1)).astype(F32)).astype(np.int64)
+    """beast/utils.py:4-17 in fp32: sub, div, clamp, mul, round-half-even; NaN -> NAN_TOKEN."""
+    with np.errstate(invalid="ignore"):   # inf - inf, inf / inf: NaN, as in torch
+        x = x.astype(F32)
+        scale = np.maximum(wmax.astype(F32) - wmin.astype(F32), F32(1e-8)).astype(F32)
+        n = ((x - wmin.astype(F32)) / scale).astype(F32)
+        n = np.clip(n, F32(0), F32(1)).astype(F32)
+        r = np.rint((n * F32(num_bins - 1)).astype(F32))
+    nan = np.isnan(r)
+    return np.where(nan, NAN_TOKEN, np.where(nan, 0, r).astype(np.int64))
 
 
 def discrete_to_continuous(tok: np.ndarray, wmin: np.ndarray, wmax: np.ndarray, num_bins: int) -> np.ndarray:

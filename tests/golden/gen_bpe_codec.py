@@ -42,6 +42,38 @@ def case(tok, rows, rng, n_random_decode=32, extra_texts=()):
     return enc, dec
 
 
+FRAGMENTS = ["x!'tion", "a.'s", "?!'ll", "!'t", "''s", ".'re", ",'ve", "-'m", ";'d", "!!'d'm", "'", "''",
+              " 's", " 'll", "'x", "it's", " don't", "  ", " ", "tion", "42", " 7", "été'", "¿'d",
+              "«'»", "#'s'", "..'ll'", "a", "!"]
+
+
+def punct_rows(r, n_rows, lengths):
+    """Rows that string punctuation runs into contractions ("x!'tion", "a.'s", "?!'ll"): the GPT-2
+    regex words then overlap across any fixed split of the row (k_bpe_encode's lane-parallel word
+    chain), at row lengths of one, two and three code points per lane (n <= 64, 128, 192) and more."""
+    rows = []
+    for i in range(n_rows):
+        n = lengths[i % len(lengths)]
+        s = ""
+        while len(s) < n:
+            s += r.choice(FRAGMENTS)
+        rows.append(s[:n])
+    return rows
+
+
+def punct_contractions_case(rng):
+    r = random.Random(17)
+    train = punct_rows(r, 400, [40, 90, 150, 250])
+    tok = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=700, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(256)])
+    tok._tokenizer.train_from_iterator(train, trainer=tr)
+    texts = ["x!'tion", "a.'s", "?!'ll", "x!'tion" * 9, "a.'s" * 16, "?!'ll" * 13] + \
+        punct_rows(r, 120, [7, 33, 63, 64, 65, 100, 127, 128, 129, 170, 192, 193, 260, 400])
+    enc, dec = case(tok, [], rng, extra_texts=texts)
+    return {"model": model_spec(tok), "encode": enc, "decode": dec}
+
+
 def main():
     rng = np.random.default_rng(11)
     hf = json.load(open(os.path.join(OUT, "bpe_hf.json")))
@@ -81,6 +113,8 @@ def main():
             ["".join(r.choice("abcdxyz") for _ in range(r.randrange(1, 30))) for _ in range(120)]
     enc, dec = case(tok, [], rng, extra_texts=texts)
     res["id_reuse"] = {"model": model_spec(tok), "encode": enc, "decode": dec}
+
+    res["punct_contractions"] = punct_contractions_case(rng)
 
     with open(os.path.join(OUT, "bpe_codec.json"), "w") as f:
         json.dump(res, f, separators=(",", ":"))

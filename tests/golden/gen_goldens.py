@@ -292,11 +292,45 @@ def gen_conditions(out):
     print("conditions done")
 
 
+def gen_nonfinite(out):
+    """The reference's quantiser on NaN / +-inf params and on degenerate, inverted and NaN bounds
+    (beast/utils.py:4-17 after the clamp of beast_bspline_tokenizer.py:423-424): what
+    ``torch.round(nan).to(torch.long)`` gives is torch's CPU cast, pinned here instead of numpy's."""
+    res = {}
+    for V in (256, 1024, 4096):
+        g = torch.Generator().manual_seed(V)
+        C = 24
+        lo = -2 * torch.rand(C, generator=g)
+        hi = lo + 0.5 + 2.5 * torch.rand(C, generator=g)
+        hi[3] = lo[3]                     # degenerate range: scale clamps to 1e-8
+        hi[5] = lo[5] - 0.7               # inverted bounds
+        hi[12] = float("nan")             # NaN upper bound
+        lo[17] = float("nan")             # NaN lower bound
+        lo[20], hi[20] = float("-inf"), float("inf")   # infinite bounds
+        x = lo + (hi - lo) * torch.rand(64, C, generator=g)
+        x[0, :] = float("nan")
+        x[1, :] = float("inf")
+        x[2, :] = float("-inf")
+        x[3, ::2] = float("nan")
+        x[4, 1::3] = float("inf")
+        x[5, 2::3] = float("-inf")
+        p = torch.clamp(x, min=lo, max=hi)
+        tok = continuous_to_discrete(p, min_val=lo, max_val=hi, num_bins=V)
+        res[f"v{V}_w_min"], res[f"v{V}_w_max"] = lo.numpy(), hi.numpy()
+        res[f"v{V}_params"], res[f"v{V}_tokens"] = x.numpy(), tok.numpy()
+    np.savez_compressed(os.path.join(out, "nonfinite_tokens.npz"), **res)
+    print("nonfinite done")
+
+
 if __name__ == "__main__":
     out = HERE
     if sys.argv[1:] == ["conditions"]:
         gen_conditions(out)
         sys.exit(0)
+    if sys.argv[1:] == ["nonfinite"]:
+        gen_nonfinite(out)
+        sys.exit(0)
+    gen_nonfinite(out)
     gen_conditions(out)
     gen_quantile(out)
     gen_bspline(out)

@@ -158,3 +158,30 @@ def test_bpe_tokenizer_api_and_errors(gpu_device):
         tok.bpe_to_mp_tokens([[-5] + ids[0]])
     with pytest.raises(ValueError, match="1 or 2 dimensions"):
         tok.bpe_to_mp_tokens(torch.zeros((1, 1, 1), dtype=torch.int64))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_encode_punct_contractions_live_hf(seed, encode_mode, gpu_device):
+    """Punctuation runs into contractions ("x!'tion", "a.'s", "?!'ll"): regex words that overlap
+    any fixed split of the row, which k_bpe_encode's lane-parallel word chain must resolve exactly
+    (round-3 advice: a stale exit gave "t" | "ion" where HF gives "tion").  Live HF on a model
+    trained on such text, rows of 1-7 code points per lane."""
+    import random
+    import sys
+    from pathlib import Path
+    from tokenizers import ByteLevelBPETokenizer
+    from tokenizers.trainers import BpeTrainer
+    sys.path.insert(0, str(Path(__file__).parent / "golden"))
+    from gen_bpe_codec import punct_rows
+    r = random.Random(100 + seed)
+    tok = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=900, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(256)])
+    tok._tokenizer.train_from_iterator(punct_rows(r, 600, [50, 120, 300]), trainer=tr)
+    texts = punct_rows(r, 3000, [5, 31, 64, 65, 96, 128, 129, 150, 192, 193, 256, 320, 448])
+    model = GpuBpeModel(tok, gpu_device)
+    got, status = encode_rows(model, [[ord(c) for c in s] for s in texts], gpu_device)
+    assert not status.any()
+    want = [e.ids for e in tok.encode_batch(texts, add_special_tokens=False)]
+    bad = [i for i in range(len(texts)) if got[i] != want[i]]
+    assert not bad, f"{len(bad)} rows differ, first {texts[bad[0]]!r}"

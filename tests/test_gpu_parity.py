@@ -127,6 +127,20 @@ def test_quantize_bitexact_on_reference_params(name, golden, gpu_device):
     assert np.array_equal(out, g["tokens_llm"])
 
 
+@pytest.mark.parametrize("V", [256, 1024, 4096])
+def test_quantize_nonfinite_matches_reference(V, gpu_device):
+    """k_quantize on NaN / +-inf params and degenerate / inverted / NaN / infinite bounds equals
+    the reference's own tokens (tests/golden/nonfinite_tokens.npz: torch's NaN -> int64 cast)."""
+    g = load_npz("nonfinite_tokens.npz")
+    D, N = 4, 6   # 24 (d n) columns
+    tok = BEASTBsplineTokenizer(num_dof=D, num_basis=N, seq_len=50, vocab_size=V, device=str(gpu_device))
+    tok.load_state_dict({"w_min": g[f"v{V}_w_min"].tolist(), "w_max": g[f"v{V}_w_max"].tolist()})
+    p = torch.from_numpy(g[f"v{V}_params"]).to(gpu_device)
+    out = tok._quantize(p, 0, gpu_device, mode=0).cpu().numpy()
+    want = g[f"v{V}_tokens"].reshape(-1, D, N).transpose(0, 2, 1).reshape(-1, N * D)
+    assert np.array_equal(out, want)
+
+
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_decode_bitexact(name, golden, gpu_device, kernel_mode):
     g = golden[name]

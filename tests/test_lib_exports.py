@@ -198,3 +198,51 @@ def test_stale_fastpath_is_not_loaded(monkeypatch):
         assert bt._fastpath() is None
     finally:
         bt._FAST = saved
+
+
+INTEGRATION = os.path.join(os.path.dirname(HEADER), "..", "INTEGRATION.md")
+
+
+def _integration_blocks(lang):
+    txt = open(INTEGRATION).read()
+    return re.findall(r"```" + lang + r"\n(.*?)```", txt, flags=re.S)
+
+
+def test_integration_ctypes_argtypes_match_header():
+    """INTEGRATION.md's ctypes stubs (§2) bind every entry point with the header's arity, and
+    name nothing the header does not declare (round-3 verdict: the doc had drifted)."""
+    decl = header_decls()
+    seen = 0
+    for block in _integration_blocks("python"):
+        for m in re.finditer(r"lib\.(beast_\w+)\.argtypes\s*=\s*\[(.*?)\]", block, flags=re.S):
+            name, body = m.group(1), m.group(2)
+            assert name in decl, f"INTEGRATION.md binds {name}, which include/beast_hip.h does not declare"
+            n = len([a for a in body.split(",") if a.strip()])
+            assert n == decl[name], f"{name}: INTEGRATION.md lists {n} argtypes, the header {decl[name]}"
+            seen += 1
+        for name in re.findall(r"lib\.(beast_\w+)", block):
+            assert name in decl, f"INTEGRATION.md calls {name}, which include/beast_hip.h does not declare"
+    assert seen >= 8
+    # every beast_* name the prose mentions exists (§3 names SURVEY §8(b)'s sketched communicator
+    # calls only to say the library does not provide them)
+    not_provided = {"beast_comm_init", "beast_comm_destroy", "beast_tokenizer_amd"}   # + the package name
+    for name in set(re.findall(r"`(beast_\w+)(?![\w.])", open(INTEGRATION).read())) - not_provided:
+        if name.endswith("_"):   # a family prefix such as `beast_quantile_*`
+            continue
+        assert name in decl, f"INTEGRATION.md names {name}, not in the header"
+
+
+def test_integration_c_snippet_compiles_against_header(tmp_path):
+    """INTEGRATION.md §3's multi-GPU C snippet compiles against include/beast_hip.h and RCCL's
+    header (hipcc -fsyntax-only): arities, types and the collective's dtype stay in step."""
+    import shutil
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    blocks = _integration_blocks("c")
+    assert blocks, "INTEGRATION.md has no C block"
+    src = tmp_path / "snippet.hip"
+    src.write_text("\n".join(blocks))
+    r = subprocess.run([hipcc, "-fsyntax-only", "-x", "hip", "--offload-arch=gfx950", "-Werror", "-Wno-unused-command-line-argument",
+                        f"-I{os.path.dirname(HEADER)}", str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]

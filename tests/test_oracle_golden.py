@@ -97,6 +97,21 @@ def test_quantiser_edge_cases():
     assert list(O.continuous_to_discrete(v, lo1, hi1, 256)) == [0, 2, 2, 254]
 
 
+@pytest.mark.parametrize("V", [256, 1024, 4096])
+def test_quantiser_nonfinite_matches_reference(V):
+    """NaN / +-inf params, degenerate / inverted / NaN / infinite bounds: the reference's own
+    tokens (tests/golden/nonfinite_tokens.npz, torch's NaN -> int64 cast included), bitwise and
+    without numpy's undefined NaN cast."""
+    import warnings
+    g = load_npz("nonfinite_tokens.npz")
+    lo, hi, x = g[f"v{V}_w_min"], g[f"v{V}_w_max"], g[f"v{V}_params"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        t = O.continuous_to_discrete(O._clamp_t(x, lo, hi), lo, hi, V)
+    assert np.array_equal(t, g[f"v{V}_tokens"])
+    assert (t == O.NAN_TOKEN).any() and (t == V - 1).any() and (t == 0).any()
+
+
 def test_quantile_kat():
     z = load_npz("quantile_kat.npz")
     for k, x in quantile_inputs().items():
