@@ -26,6 +26,7 @@ OPT_GENERIC_KERNELS = 1
 OPT_BLOCK_WAVES = 2
 OPT_MERGE_LDS_MIN = 3
 OPT_BPE_ENCODE_MODE = 5
+OPT_BPE_DEDUP_KEY_BITS = 6
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 
@@ -34,6 +35,7 @@ SIGNATURES = {
     "beast_abi_version": (_i32, []),
     "beast_last_error": (C.c_char_p, []),
     "beast_set_option": (_i32, [_i32, _i32]),
+    "beast_get_option": (_i32, [_i32]),
     "beast_bspline_basis_f32": (_i32, [_vp, _i64, _f32, _f32, _vp, _i32, _i32, _i32, _vp, _vp]),
     "beast_bspline_projection_f64": (_i32, [_vp, _i32, _i32, _f64, _vp, _vp]),
     "beast_encode_f32": (_i32, [_vp, _i64, _i32, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp,
@@ -87,6 +89,10 @@ SIGNATURES = {
     "beast_bpe_encode_lds_bytes": (_sz, [_i32, _i32]),
     "beast_bpe_encode_rows": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
                                      _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "beast_bpe_encode_dedup_table_log2": (_i32, [_i64, _i32]),
+    "beast_bpe_encode_dedup_workspace_bytes": (_sz, [_i64, _i32, _i32, _i32]),
+    "beast_bpe_encode_rows_dedup": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32,
+                                           _i32, _vp, _i32, _vp, _sz, _vp, _i64, _vp, _vp, _vp]),
     "beast_bpe_decode_rows": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
 }
 

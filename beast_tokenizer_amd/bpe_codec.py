@@ -11,6 +11,13 @@ the kernels restate AddedVocabulary's special-token split, the ByteLevel pre-tok
 ``String::from_utf8_lossy`` (tests/test_gpu_parity.py checks them against HF itself and
 against tests/golden/bpe_codec.json).
 
+Encode takes one of two device paths (same ids): by default the batch's distinct words are
+merged once each (``beast_bpe_encode_rows_dedup``: word split + key insert, one merge per
+distinct word, emit); models with special tokens, models whose merges are not rank-monotone
+(a merge combining a token that a later merge also produces, where merging a word's lowest pair
+everywhere at once is not HF's heap order) and rows holding a word of more than 64 byte symbols
+take the per-row kernel (``beast_bpe_encode_rows``), the latter two with HF's heap.
+
 Model features HF supports but BEAST never produces (dropout, subword prefixes/suffixes,
 byte fallback, ``ignore_merges``, normalisers, non-special added tokens, other
 pre-tokenisers) raise ``NotImplementedError``.
@@ -41,6 +48,29 @@ _ENC_ERRORS = {
     5: (NotImplementedError, "BPE input beyond the Basic Multilingual Plane is not supported on the GPU"),
     6: (NotImplementedError, "BPE input row too long for the GPU encoder"),
 }
+ST_FALLBACK = 7   # beast_bpe_encode_rows_dedup: the row needs the per-row kernel
+
+# "auto": the word-dedup path where it applies; "rows": always the per-row kernel (tests, A/B)
+_ENCODE_PATH = {"path": "auto"}
+
+
+def set_encode_path(path: str) -> None:
+    if path not in ("auto", "rows"):
+        raise ValueError(f"unknown encode path {path!r}")
+    _ENCODE_PATH["path"] = path
+
+
+def rank_monotone(merges_abn) -> bool:
+    """True when every merge combines only base symbols or tokens that every merge producing them
+    precedes (all trained models): then a word's lowest-rank pair can be merged at all its
+    occurrences at once, exactly as HF's (rank, pos) heap does one after the other."""
+    eff = {}
+    for r, (a, b, n) in enumerate(merges_abn):   # a pair listed twice keeps its last rank (HF HashMap)
+        eff[(a, b)] = (r, n)
+    made = {}
+    for (a, b), (r, n) in eff.items():
+        made[n] = max(made.get(n, -1), r)
+    return all(made.get(a, -1) < r and made.get(b, -1) < r for (a, b), (r, n) in eff.items())
 
 UNK_MESSAGE = ("BPE sequence contains <unk> tokens. This usually means that the discrete "
                "BEAST tokens went out of the range seen during BPE training. Consider "
@@ -90,6 +120,9 @@ class GpuBpeModel:
                      _lib.stream_of(device))
             mt = None
         self._keep = mt   # the build reads it asynchronously
+        self.monotone = rank_monotone(list(zip(ma, mb, mn)))
+        self._max_id = max(vocab.values()) if vocab else 0   # 0xFFFF marks "no id" in the dedup kernels
+        self._dw_table, self._dw_log2, self._dw_ws = None, 0, None
 
         b2u = bytes_to_unicode()
         self.byte2id = torch.tensor([vocab.get(b2u[b], -1) for b in range(256)], dtype=torch.int32).to(device)
@@ -170,25 +203,75 @@ class GpuBpeModel:
 
     # --------------------------------------------------------------- encode --
     def encode_rows(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,
-                    max_span: Optional[int]):
-        """tok int64 (device), rows tok[row_off[r]:row_off[r+1]] -> (ids [R, W] int32, lens [R], status [R])."""
+                    max_span: Optional[int], resolve: bool = True):
+        """tok int64 (device), rows tok[row_off[r]:row_off[r+1]] -> (ids [R, W] int32, lens [R], status [R]).
+        resolve=False (timing only): the dedup path's ST_FALLBACK rows are left as they are."""
+        R = row_off.numel() - 1
+        if not self._dedup_ok():
+            return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+        out = self._encode_rows_dedup(tok, row_off, max_row, min_token, max_span)
+        if resolve and R and bool((out[2] == ST_FALLBACK).any()):
+            return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+        return out
+
+    def _dedup_ok(self) -> bool:
+        return _ENCODE_PATH["path"] == "auto" and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
+
+    def _encode_rows_kernel(self, tok, row_off, max_row, min_token, max_span):
+        """The per-row kernel (k_bpe_encode): special tokens, fallback rows, non-monotone models
+        (HF's heap, forced for the call)."""
         R = row_off.numel() - 1
         dev = self.device
         cp_bound = 0x10FFFF if max_span is None else max(0, int(max_span))
         max_syms = max_row * _utf8_len(min(cp_bound, 0x10FFFF))
         ids = torch.empty((max(R, 1), max(max_syms, 1)), dtype=torch.int32, device=dev)
         st = torch.empty((2, max(R, 1)), dtype=torch.int32, device=dev)   # lens, status
-        _lib.run("beast_bpe_encode_rows", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+        args = ("beast_bpe_encode_rows", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+                -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
+                self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.spec_cps.data_ptr(),
+                self.spec_len.data_ptr(), self.spec_id.data_ptr(), self.n_spec, self.unk_id, self.fuse_unk,
+                int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(), st[1].data_ptr(),
+                _lib.stream_of(dev))
+        if self.monotone:
+            _lib.run(*args)
+        else:
+            lib = _lib.load()
+            mode = lib.beast_get_option(_lib.OPT_BPE_ENCODE_MODE)
+            lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, mode | 1)
+            try:
+                _lib.run(*args)
+            finally:
+                lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, mode)
+        return ids[:R], st[0, :R], st[1, :R]
+
+    def _encode_rows_dedup(self, tok, row_off, max_row, min_token, max_span):
+        R = row_off.numel() - 1
+        dev = self.device
+        cp_bound = 0x10FFFF if max_span is None else max(0, int(max_span))
+        max_syms = max_row * _utf8_len(min(cp_bound, 0x10FFFF))
+        ids = torch.empty((max(R, 1), max(max_syms, 1)), dtype=torch.int32, device=dev)
+        st = torch.empty((2, max(R, 1)), dtype=torch.int32, device=dev)   # lens, status
+        if R == 0:
+            return ids[:0], st[0, :0], st[1, :0]
+        lib = _lib.load()
+        log2 = int(lib.beast_bpe_encode_dedup_table_log2(R, int(max_row)))
+        if self._dw_table is None or self._dw_log2 < log2:   # zero-filled once; every call leaves it zero
+            self._dw_log2 = log2
+            self._dw_table = torch.zeros(1 << log2, dtype=torch.int64, device=dev)
+        need = int(lib.beast_bpe_encode_dedup_workspace_bytes(R, int(max_row), int(max_syms), self._dw_log2))
+        if self._dw_ws is None or self._dw_ws.numel() < need:
+            self._dw_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _lib.run("beast_bpe_encode_rows_dedup", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
                  -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
-                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.spec_cps.data_ptr(),
-                 self.spec_len.data_ptr(), self.spec_id.data_ptr(), self.n_spec, self.unk_id, self.fuse_unk,
-                 int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(), st[1].data_ptr(),
+                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
+                 int(max_row), int(max_syms), self._dw_table.data_ptr(), self._dw_log2, self._dw_ws.data_ptr(),
+                 self._dw_ws.numel(), ids.data_ptr(), ids.shape[1], st[0].data_ptr(), st[1].data_ptr(),
                  _lib.stream_of(dev))
         return ids[:R], st[0, :R], st[1, :R]
 
     def encode_to_lists(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,
                         max_span: Optional[int]) -> List[List[int]]:
-        ids, lens, status = self.encode_rows(tok, row_off, max_row, min_token, max_span)
+        ids, lens, status = self.encode_rows(tok, row_off, max_row, min_token, max_span, resolve=False)
         R = lens.numel()
         if R == 0:
             return []
@@ -207,6 +290,15 @@ class GpuBpeModel:
         st_h.copy_(status, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         st_np = st_h.numpy()
+        if (st_np == ST_FALLBACK).any():   # a word over 64 byte symbols / a key collision: per-row kernel
+            ids, lens, status = self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+            W = ids.shape[1]
+            ids_h = blk[:R * W].view(R, W)
+            ids_h.copy_(ids, non_blocking=True)
+            lens_h.copy_(lens, non_blocking=True)
+            st_h.copy_(status, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            st_np = st_h.numpy()
         if st_np.any():
             exc, msg = _ENC_ERRORS[int(st_np[np.flatnonzero(st_np)[0]])]
             raise exc(msg)
@@ -222,13 +314,18 @@ class GpuBpeModel:
         """The ids as a device block instead of lists: (ids int64 [R, W] padded with PAD_ID,
         lengths int64 [R]); one small device-to-host copy (the row status, for the reference's
         errors) instead of the whole id block and a list build."""
-        ids, lens, status = self.encode_rows(tok, row_off, max_row, min_token, max_span)
+        ids, lens, status = self.encode_rows(tok, row_off, max_row, min_token, max_span, resolve=False)
         R = lens.numel()
         if R == 0:
             return torch.empty((0, 0), dtype=torch.int64, device=self.device), lens.to(torch.int64)
-        # one copy of the status summary: worst status (first failing row's code) and the widest row
+        # one copy of the status summary: worst status (first failing row's code), the widest row and
+        # whether a row needs the per-row kernel
         first_bad = torch.where(status != 0, torch.arange(R, device=self.device, dtype=torch.int32), R).min()
-        summ = torch.stack([first_bad, lens.max()]).cpu()
+        summ = torch.stack([first_bad, lens.max(), (status == ST_FALLBACK).any().to(torch.int32)]).cpu()
+        if int(summ[2]):
+            ids, lens, status = self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+            first_bad = torch.where(status != 0, torch.arange(R, device=self.device, dtype=torch.int32), R).min()
+            summ = torch.stack([first_bad, lens.max()]).cpu()
         r_bad, w = int(summ[0]), int(summ[1])
         if r_bad < R:
             exc, msg = _ENC_ERRORS[int(status[r_bad])]

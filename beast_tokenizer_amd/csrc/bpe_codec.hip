@@ -306,7 +306,8 @@ __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
 // on that walk, or the entry itself when the chain jumps the segment.  A marked entry below ws is
 // a mark of an older walk (e.g. "x!'tion": the walk from "'" marks "t" before the chain is known
 // to enter at "t"), so only a marked entry at or past ws reuses the walk; anything else re-walks.
-__device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, EncLds& L, int n, int lane) {
+__device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, int32_t* wcp, int32_t* wspec,
+                                            int32_t* nw_out, int n, int lane) {
   const int G = (n + 63) >> 6;
   const int sb = min(lane * G, n), se = min(sb + G, n);
   for (int i = lane; i < n; i += 64) vis[i] = 0;
@@ -352,8 +353,12 @@ __device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, EncL
   int tot;
   int o = wave_excl_scan(cnt, lane, tot);
   for (int i = max(sb, entry); i < se; ++i)
-    if (vis[i]) { L.wcp[o] = i; L.wspec[o] = -1; ++o; }
-  if (lane == 0) { L.wcp[tot] = n; L.misc[0] = tot; }
+    if (vis[i]) {
+      wcp[o] = i;
+      if (wspec) wspec[o] = -1;
+      ++o;
+    }
+  if (lane == 0) { wcp[tot] = n; *nw_out = tot; }
   wave_sync();
 }
 
@@ -579,7 +584,7 @@ __device__ void encode_row(const EncArgs& a, const Map& mm, EncLds& L, int64_t r
 #ifndef BPE_SERIAL_PRETOK
     int32_t* e = L.wcnt;   // scratch until step 4
     for (int i = lane; i < n; i += 64) e[i] = regex_word(L.cps, L.cls, i, n);
-    word_starts(e, L.cand, L, n, lane);
+    word_starts(e, L.cand, L.wcp, L.wspec, L.misc, n, lane);
 #else
     if (lane == 0) {
       int nw = 0, p = 0;
@@ -806,6 +811,396 @@ __global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
     if constexpr (MAP_LDS) encode_row<RMX>(a, lm, L, r, lane, s_b2i, s_lut);
     else encode_row<RMX>(a, a.map, L, r, lane, s_b2i, s_lut);
     wave_sync();
+  }
+}
+
+// ------------------------------------------------------ encode, word dedup --
+// (round 4) HF's BPE merges each pre-tokenised word on its own, so a row's ids are the
+// concatenation of its words' ids, and a word's ids are a function of the word alone (its code
+// points).  A batch of BEAST rows holds few distinct words (K5's codec sample: 302 k words,
+// 77 k distinct, 5.9 byte symbols on average, 47 at most), so the batch is encoded in three
+// launches instead of one wave merging every row in full:
+//   k_dw_words   one wave per row: code points, range checks, classes, regex word starts (as
+//                k_bpe_encode), then per word a 64-bit key of its code points inserted into a
+//                device hash table (CAS); the first inserter of a key records the word (slot,
+//                position, byte symbols) in its workgroup's region -- an LDS list flushed at the
+//                end, so no device-wide counter is contended.  A row holding a word of more than
+//                64 byte symbols is left to k_bpe_encode (ST_FALLBACK).
+//   k_dw_merge   one workgroup per region: every distinct word merged once, in registers --
+//                words of <= 16 byte symbols four to a wave (one 16-lane DPP row each), longer
+//                ones a wave each.  A round probes every adjacent pair's rank in the LDS merge
+//                map, takes the word's lowest (DPP row rotations), merges its occurrences left
+//                to right (a self-pair run takes every other one) and compacts the word with one
+//                ds_permute.  For models whose merges only combine tokens made by earlier merges
+//                (the host checks) this is HF's merge_all; the slots are cleared for the next call.
+//   k_dw_emit    one wave per row: each word's ids copied from its record at the scanned offset,
+//                after checking that the word's code points equal the recorded word's (a 64-bit
+//                key collision makes the row ST_FALLBACK, never a wrong id).
+constexpr int DW_SHORT = 16;       // byte symbols of a short word: one 16-lane DPP row
+constexpr int DW_MID = 64;         // ... of a mid word: one wave; longer -> ST_FALLBACK
+constexpr int ST_FALLBACK = 7;     // the row needs k_bpe_encode
+constexpr int DW_WAVES = 16;       // rows per k_dw_words workgroup (at most)
+constexpr uint32_t SYM_NONE = 0xFFFFu;
+
+struct DwWs {                      // the caller's scratch, carved by dw_layout
+  uint32_t* slot2idx;              // [cap] record of a slot: tier << 31 | record index
+  unsigned long long* occ;         // [R][Lc] slot | cstart << 32 | clen << 48
+  int32_t* nwords;                 // [R]
+  int32_t* cnt;                    // [regions][2] short / mid records of each region
+  uint32_t* rs_slot;               // short records [regions * capS]
+  uint2* rs_meta;                  //   (row, cstart | clen << 16)
+  int32_t* rs_n;                   //   byte symbols, then ids after k_dw_merge
+  uint16_t* rs_sym;                //   [16] byte symbols, then ids
+  uint32_t* rm_slot;               // mid records [regions * capM]
+  uint2* rm_meta;
+  int32_t* rm_n;
+  uint16_t* rm_sym;                //   [64]
+  unsigned long long* table;       // [1 << log2cap] word keys, 0 = empty (the caller's, kept empty)
+  int log2cap, capS, capM, regions, nwv, Lc, S;
+  int key_shift;                   // 64 - BEAST_OPT_BPE_DEDUP_KEY_BITS
+};
+
+__host__ __device__ inline int dw_capm(int Lc) { return Lc / 5 + 1; }   // a mid word spans >= 5 code points
+
+// per-row LDS of k_dw_words
+__host__ __device__ inline size_t dw_row_bytes(int Lc, int S) {
+  return 3 * al16(sizeof(int32_t) * (Lc + 1)) + al16(sizeof(int32_t) * Lc) + al16(sizeof(uint16_t) * S) +
+         2 * al16(Lc) + 16;
+}
+// staging lists of one workgroup of nwv rows
+__host__ __device__ inline size_t dw_stage_bytes(int Lc, int nwv) {
+  return sizeof(uint4) * (size_t)nwv * ((size_t)Lc + dw_capm(Lc));
+}
+
+struct DwRow {
+  int32_t* cps;      // [Lc]
+  int32_t* symoff;   // [Lc + 1]
+  int32_t* wcp;      // [Lc + 1]
+  int32_t* e;        // [Lc]
+  uint16_t* c;       // [S] byte symbols as vocab ids (SYM_NONE: not in the vocab)
+  uint8_t* cls;      // [Lc]
+  uint8_t* vis;      // [Lc]
+  int32_t* misc;     // [4]
+};
+
+__device__ inline DwRow dw_carve(char* p, int Lc, int S) {
+  DwRow R;
+  auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
+  R.cps = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
+  R.symoff = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
+  R.wcp = (int32_t*)take(sizeof(int32_t) * (Lc + 1));
+  R.e = (int32_t*)take(sizeof(int32_t) * Lc);
+  R.c = (uint16_t*)take(sizeof(uint16_t) * S);
+  R.cls = (uint8_t*)take(Lc);
+  R.vis = (uint8_t*)take(Lc);
+  R.misc = (int32_t*)take(16);
+  return R;
+}
+
+__device__ __forceinline__ unsigned long long dw_mix(unsigned long long h) {   // splitmix64 finaliser
+  h ^= h >> 30; h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27; h *= 0x94D049BB133111EBull;
+  return h ^ (h >> 31);
+}
+
+// k_dw_words: rows [blockIdx.x * nwv, +nwv), one per wave; region blockIdx.x
+__global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
+  extern __shared__ __align__(16) char lds_raw[];
+  __shared__ int32_t s_b2i[256];
+  __shared__ uint8_t s_lut[256];
+  __shared__ int s_ns, s_nm;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    s_b2i[i] = a.byte2id[i];
+    s_lut[i] = i < a.lut_n ? a.lut[i] : (uint8_t)CLS_OTHER;
+  }
+  if (threadIdx.x == 0) { s_ns = 0; s_nm = 0; }
+  const int capS = nwv * w.Lc, capM = nwv * dw_capm(w.Lc);
+  uint4* stS = reinterpret_cast<uint4*>(lds_raw);
+  uint4* stM = stS + capS;
+  char* rows = lds_raw + dw_stage_bytes(w.Lc, nwv);
+  const size_t rb = dw_row_bytes(w.Lc, w.S);
+  __syncthreads();
+  DwRow L = dw_carve(rows + (size_t)wave * rb, w.Lc, w.S);
+  const int64_t r = (int64_t)blockIdx.x * nwv + wave;
+  if (r < a.n_rows) {
+    const int64_t r0 = a.row_off[r];
+    const int n = (int)(a.row_off[r + 1] - r0);
+    int st = ST_OK;
+    if (n > a.Lc) st = ST_TOO_LONG;
+    // 1. code points, range checks (reference :181-192 order), classes
+    int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
+    for (int i = lane; st == ST_OK && i < n; i += 64) {
+      const long long v = a.tok[r0 + i] - a.min_tok;
+      below |= v < 0;
+      above |= (a.max_span >= 0 && v > a.max_span);
+      notuni |= v > 0x10FFFF;
+      surr |= (v >= 0xD800 && v <= 0xDFFF);
+      nocls |= v >= a.lut_n;
+      const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
+      L.cps[i] = cp;
+      L.cls[i] = cp < 256 ? s_lut[cp] : (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
+    }
+    if (st == ST_OK) {
+      if (__any(below)) st = ST_BELOW_MIN;
+      else if (__any(above)) st = ST_ABOVE_MAX;
+      else if (__any(notuni)) st = ST_NOT_UNICODE;
+      else if (__any(surr)) st = ST_SURROGATE;
+      else if (__any(nocls)) st = ST_NO_CLASS;
+    }
+    int carry = 0;
+    if (st == ST_OK) {   // UTF-8 symbol offsets
+      for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        int tot;
+        const int len = (i < n) ? utf8_len(L.cps[i]) : 0;
+        const int ex = wave_excl_scan(len, lane, tot);
+        if (i < n) L.symoff[i] = carry + ex;
+        carry += tot;
+      }
+      if (lane == 0) L.symoff[n] = carry;
+      if (carry > w.S) st = ST_TOO_LONG;
+    }
+    wave_sync();
+    int nw = 0;
+    if (st == ST_OK) {
+      // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
+      for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
+      word_starts(L.e, L.vis, L.wcp, nullptr, L.misc, n, lane);
+      for (int i = lane; i < n; i += 64) {
+        const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
+        for (int q = 0; q < len; ++q) L.c[o + q] = (uint16_t)s_b2i[utf8_byte(cp, q)];   // -1 -> SYM_NONE
+      }
+      wave_sync();
+      nw = L.misc[0];
+      bool fall = false;
+      for (int k = lane; k < nw; k += 64) fall |= (L.symoff[L.wcp[k + 1]] - L.symoff[L.wcp[k]]) > DW_MID;
+      if (__any(fall)) st = ST_FALLBACK;
+    }
+    if (st == ST_OK) {
+      const unsigned long long tmask = (1ull << w.log2cap) - 1ull;
+      for (int k = lane; k < nw; k += 64) {
+        const int cs = L.wcp[k], ce = L.wcp[k + 1], bs = L.symoff[cs], blen = L.symoff[ce] - bs;
+        unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce - cs);
+        for (int i = cs; i < ce; ++i) h = (h ^ (unsigned long long)(uint32_t)L.cps[i]) * 0x100000001B3ull;
+        const unsigned long long key = (dw_mix(h) >> w.key_shift) | 1ull;
+        unsigned long long slot = (key * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
+        bool win = false;
+        while (true) {
+          const unsigned long long prev = atomicCAS(&w.table[slot], 0ull, key);
+          if (prev == 0ull) { win = true; break; }
+          if (prev == key) break;
+          slot = (slot + 1) & tmask;
+        }
+        w.occ[r * w.Lc + k] = slot | ((unsigned long long)cs << 32) | ((unsigned long long)(ce - cs) << 48);
+        if (win) {
+          const uint4 rec = make_uint4((uint32_t)slot, (uint32_t)r, (uint32_t)cs | ((uint32_t)(ce - cs) << 16),
+                                       ((uint32_t)wave << 24) | ((uint32_t)blen << 16) | (uint32_t)bs);
+          if (blen <= DW_SHORT) stS[atomicAdd(&s_ns, 1)] = rec;
+          else stM[atomicAdd(&s_nm, 1)] = rec;
+        }
+      }
+    }
+    if (lane == 0) { a.status[r] = st; w.nwords[r] = st == ST_OK ? nw : 0; }
+  }
+  __syncthreads();
+  // flush this region's records (byte symbols from the rows still in LDS)
+  const int ns = s_ns, nm = s_nm;
+  if (threadIdx.x == 0) { w.cnt[2 * blockIdx.x] = ns; w.cnt[2 * blockIdx.x + 1] = nm; }
+  for (int i = threadIdx.x; i < ns + nm; i += blockDim.x) {
+    const bool mid = i >= ns;
+    const uint4 rec = mid ? stM[i - ns] : stS[i];
+    const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
+    const uint16_t* src = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S).c + bs;
+    if (!mid) {
+      const int64_t idx = (int64_t)blockIdx.x * w.capS + i;
+      w.rs_slot[idx] = rec.x;
+      w.rs_meta[idx] = make_uint2(rec.y, rec.z);
+      w.rs_n[idx] = blen;
+      uint16_t* d = w.rs_sym + idx * DW_SHORT;
+      for (int q = 0; q < DW_SHORT; ++q) d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
+      w.slot2idx[rec.x] = (uint32_t)idx;
+    } else {
+      const int64_t idx = (int64_t)blockIdx.x * w.capM + (i - ns);
+      w.rm_slot[idx] = rec.x;
+      w.rm_meta[idx] = make_uint2(rec.y, rec.z);
+      w.rm_n[idx] = blen;
+      uint16_t* d = w.rm_sym + idx * DW_MID;
+      for (int q = 0; q < DW_MID; ++q) d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
+      w.slot2idx[rec.x] = 0x80000000u | (uint32_t)idx;
+    }
+  }
+}
+
+// lane gl of a GW-lane group reads lane gl + 1 (down) / gl - 1 (up) of its group; `fill` past the ends
+template <int GW>
+__device__ __forceinline__ uint32_t grp_down1(uint32_t v, uint32_t fill) {
+  if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x101, 0xF, 0xF, false);
+  else { const uint32_t x = (uint32_t)__shfl_down((int)v, 1); return (threadIdx.x & 63) == 63 ? fill : x; }
+}
+template <int GW>
+__device__ __forceinline__ uint32_t grp_up1(uint32_t v, uint32_t fill) {
+  if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x111, 0xF, 0xF, false);
+  else { const uint32_t x = (uint32_t)__shfl_up((int)v, 1); return (threadIdx.x & 63) == 0 ? fill : x; }
+}
+template <int GW>
+__device__ __forceinline__ uint32_t grp_min(uint32_t v) {   // every lane of the group gets the group's min
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
+  if constexpr (GW == 64) {
+    v = min(v, (uint32_t)__shfl_xor((int)v, 16));
+    v = min(v, (uint32_t)__shfl_xor((int)v, 32));
+  }
+  return v;
+}
+
+// The word's symbols move to the first n lanes of the group, in order (one forward permute).
+template <int GW>
+__device__ __forceinline__ uint32_t grp_compact(uint32_t sym, bool live, int gl, int gbase, int& n) {
+  const unsigned long long bal = __ballot(live);
+  const unsigned long long gm = GW == 64 ? bal : ((bal >> gbase) & ((1ull << GW) - 1ull));
+  const unsigned long long below = gl == 0 ? 0ull : (gm & ((1ull << gl) - 1ull));
+  n = __popcll(gm);
+  const int dst = gbase + (live ? __popcll(below) : GW - 1);   // a dead lane only exists when n < GW
+  const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)sym);
+  return gl < n ? got : SYM_NONE;
+}
+
+// HF Word::merge_all of one word per GW-lane group (see k_dw_merge); sym: the lane's byte symbol
+// (SYM_NONE: no vocab id), blen: the word's byte symbols (0: no word).  Returns the lane's final
+// id (SYM_NONE past the end); n: the word's final length.
+template <int GW, class Map>
+__device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, int blen, int unk_id, int fuse_unk,
+                                                  int& n) {
+  const int lane = threadIdx.x & 63, gl = lane & (GW - 1), gbase = lane - gl;
+  // HF BPE::merge_word's unknown chars: unk_id (consecutive ones fused when fuse_unk), or dropped
+  const bool in = gl < blen;
+  const bool miss = in && raw == SYM_NONE;
+  const bool pmiss = grp_up1<GW>(miss ? 1u : 0u, 0u) != 0u;
+  const bool live = in && !(miss && (unk_id < 0 || (fuse_unk && pmiss)));
+  const uint32_t id = miss ? (uint32_t)unk_id : raw;
+  uint32_t sym = grp_compact<GW>(id, live, gl, gbase, n);
+  const uint32_t mmask = (1u << mm.log2cap) - 1u;
+  for (int round = 0; round < DW_MID; ++round) {   // each round merges >= 1 pair: <= 63 rounds
+    const uint32_t right = grp_down1<GW>(sym, SYM_NONE);
+    const bool has = gl + 1 < n;
+    uint32_t rk = RK_NONE;
+    if (has) {
+      const uint32_t key = (sym << 16) | right;
+      uint32_t h = mm_hash(key, mm.log2cap);
+      uint2 e = mm.kv[h];
+      while (e.x != key && e.x != EMPTY_KEY) {
+        h = (h + 1) & mmask;
+        e = mm.kv[h];
+      }
+      rk = e.x == key ? e.y - 0x10000u : RK_NONE;   // (rank + 1) << 16 | new_id -> rank << 16 | new_id
+    }
+    const uint32_t m = grp_min<GW>(rk);
+    if (!__any(m != RK_NONE)) break;
+    const bool match = has && m != RK_NONE && rk == m;
+    const unsigned long long mb = __ballot(match);
+    const unsigned long long M = GW == 64 ? mb : ((mb >> gbase) & ((1ull << GW) - 1ull));
+    // a run of the same self-pair merges left to right: take a match when the matches right
+    // before it are an even number (HF pops (rank, pos) in position order)
+    const unsigned long long lowm = gl == 0 ? 0ull : ((1ull << gl) - 1ull);
+    const unsigned long long z = ~M & lowm;
+    const int hz = z ? 63 - __clzll(z) : -1;
+    const bool take = match && !((gl - 1 - hz) & 1);
+    const bool dies = grp_up1<GW>(take ? 1u : 0u, 0u) != 0u;
+    if (take) sym = m & 0xFFFFu;
+    sym = grp_compact<GW>(sym, gl < n && !dies, gl, gbase, n);
+  }
+  return sym;
+}
+
+template <bool MAP_LDS>
+__global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
+  extern __shared__ __align__(16) char lds_raw[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  LdsMap lm;
+  if constexpr (MAP_LDS) {
+    const int cap = 1 << a.map.log2cap;
+    uint2* kv = reinterpret_cast<uint2*>(lds_raw);
+    const uint4* g = reinterpret_cast<const uint4*>(a.map.kv);
+    for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) reinterpret_cast<uint4*>(kv)[i] = g[i];
+    lm.kv = kv; lm.rank2new = nullptr; lm.log2cap = a.map.log2cap;
+  }
+  const int ns = w.cnt[2 * blockIdx.x], nm = w.cnt[2 * blockIdx.x + 1];
+  if constexpr (MAP_LDS) __syncthreads();
+  const int tasks = nm + (ns + 3) / 4;   // the mid words first: their rounds are the longest chains
+  for (int t = wave; t < tasks; t += nwv) {
+    if (t < nm) {
+      const int64_t idx = (int64_t)blockIdx.x * w.capM + t;
+      uint16_t* sp = w.rm_sym + idx * DW_MID;
+      const int blen = w.rm_n[idx];
+      const uint32_t raw = lane < blen ? sp[lane] : SYM_NONE;
+      int n;
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, blen, a.unk_id, a.fuse_unk, n)
+                                 : dw_merge_word<DW_MID>(a.map, raw, blen, a.unk_id, a.fuse_unk, n);
+      if (lane < n) sp[lane] = (uint16_t)v;
+      if (lane == 0) { w.rm_n[idx] = n; w.table[w.rm_slot[idx]] = 0ull; }
+    } else {
+      const int k = 4 * (t - nm) + (lane >> 4), gl = lane & 15;
+      const bool valid = k < ns;
+      const int64_t idx = (int64_t)blockIdx.x * w.capS + (valid ? k : 0);
+      uint16_t* sp = w.rs_sym + idx * DW_SHORT;
+      const int blen = valid ? w.rs_n[idx] : 0;
+      const uint32_t raw = gl < blen ? sp[gl] : SYM_NONE;
+      int n;
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n)
+                                 : dw_merge_word<DW_SHORT>(a.map, raw, blen, a.unk_id, a.fuse_unk, n);
+      if (valid && gl < n) sp[gl] = (uint16_t)v;
+      if (valid && gl == 0) { w.rs_n[idx] = n; w.table[w.rs_slot[idx]] = 0ull; }
+    }
+  }
+}
+
+// k_dw_emit: one wave per row
+__global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
+    if (a.status[r] != ST_OK) {
+      if (lane == 0) a.out_len[r] = 0;
+      continue;
+    }
+    const int nw = w.nwords[r];
+    const long long* tr = a.tok + a.row_off[r];
+    int32_t* out = a.out_ids + r * a.out_stride;
+    int carry = 0;
+    bool bad = false;
+    for (int base = 0; base < nw; base += 64) {
+      const int k = base + lane;
+      int n = 0;
+      const uint16_t* src = nullptr;
+      if (k < nw) {
+        const unsigned long long o = w.occ[r * w.Lc + k];
+        const uint32_t slot = (uint32_t)o;
+        const int cs = (int)((o >> 32) & 0xFFFF), cl = (int)(o >> 48);
+        const uint32_t rec = w.slot2idx[slot];
+        const bool mid = rec >> 31;
+        const int64_t li = rec & 0x7FFFFFFFu;
+        const uint2 meta = mid ? w.rm_meta[li] : w.rs_meta[li];
+        n = mid ? w.rm_n[li] : w.rs_n[li];
+        src = mid ? w.rm_sym + li * DW_MID : w.rs_sym + li * DW_SHORT;
+        const int wcs = (int)(meta.y & 0xFFFF), wcl = (int)(meta.y >> 16);
+        if ((int64_t)meta.x != r || wcs != cs) {   // another occurrence recorded the word: same code points?
+          if (wcl != cl) bad = true;
+          const long long* tw = a.tok + a.row_off[meta.x] + wcs;
+          for (int i = 0; i < cl && !bad; ++i) bad = tw[i] != tr[cs + i];
+        }
+      }
+      int tot;
+      const int off = carry + wave_excl_scan(n, lane, tot);
+      for (int i = 0; i < n; ++i) out[off + i] = (int32_t)src[i];
+      carry += tot;
+    }
+    const bool coll = __any(bad);
+    if (lane == 0) {
+      a.out_len[r] = coll ? 0 : carry;
+      if (coll) a.status[r] = ST_FALLBACK;
+    }
   }
 }
 
@@ -1122,6 +1517,111 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
   BEAST_LAUNCHED("k_bpe_encode");
   return BEAST_OK;
 }
+
+
+// ------------------------------------------------------- word dedup, host --
+static int dw_nwv(int Lc, int S) {   // rows per k_dw_words workgroup: as many as the LDS holds, <= 16
+  const size_t per = dw_row_bytes(Lc, S) + dw_stage_bytes(Lc, 1);
+  const size_t room = LDS_BUDGET - STATIC_LDS;
+  return (int)std::min<size_t>((size_t)DW_WAVES, room / per);
+}
+
+static size_t dw_carve_host(DwWs& w, char* base, int64_t R, int Lc, int S, int log2cap) {
+  w.nwv = dw_nwv(Lc, S);
+  const int nwv = w.nwv > 0 ? w.nwv : 1;
+  w.Lc = Lc; w.S = S; w.log2cap = log2cap;
+  w.regions = (int)((R + nwv - 1) / nwv);
+  w.capS = nwv * Lc;
+  w.capM = nwv * dw_capm(Lc);
+  size_t o = 0;
+  auto take = [&](size_t bytes) { char* r = base ? base + o : nullptr; o += al16(bytes); return r; };
+  const size_t nS = (size_t)w.regions * w.capS, nM = (size_t)w.regions * w.capM;
+  w.slot2idx = (uint32_t*)take(sizeof(uint32_t) << log2cap);
+  w.occ = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)R * Lc);
+  w.nwords = (int32_t*)take(sizeof(int32_t) * (size_t)R);
+  w.cnt = (int32_t*)take(sizeof(int32_t) * 2 * (size_t)w.regions);
+  w.rs_slot = (uint32_t*)take(sizeof(uint32_t) * nS);
+  w.rs_meta = (uint2*)take(sizeof(uint2) * nS);
+  w.rs_n = (int32_t*)take(sizeof(int32_t) * nS);
+  w.rs_sym = (uint16_t*)take(sizeof(uint16_t) * DW_SHORT * nS);
+  w.rm_slot = (uint32_t*)take(sizeof(uint32_t) * nM);
+  w.rm_meta = (uint2*)take(sizeof(uint2) * nM);
+  w.rm_n = (int32_t*)take(sizeof(int32_t) * nM);
+  w.rm_sym = (uint16_t*)take(sizeof(uint16_t) * DW_MID * nM);
+  return o;
+}
+
+
+extern "C" int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps) {
+  const int64_t words = std::max<int64_t>(1, n_rows) * std::max(1, max_row_cps);
+  return std::max(10, log2_ceil(2 * words));
+}
+
+extern "C" size_t beast_bpe_encode_dedup_workspace_bytes(int64_t n_rows, int max_row_cps, int max_row_syms,
+                                                        int table_log2) {
+  if (n_rows < 0 || max_row_cps < 0 || max_row_syms < 0 || table_log2 < 1 || table_log2 > 31) return 0;
+  DwWs w;
+  return dw_carve_host(w, nullptr, n_rows, max_row_cps, max_row_syms, table_log2);
+}
+
+extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int64_t n_rows,
+                                           int64_t min_tok, int64_t max_span, const uint8_t* cls_lut, int64_t lut_n,
+                                           const int32_t* byte2id, const void* map, int n_merges, int unk_id,
+                                           int fuse_unk, int max_row_cps, int max_row_syms, uint64_t* table,
+                                           int table_log2, void* ws, size_t ws_bytes, int32_t* out_ids,
+                                           int64_t out_stride, int32_t* out_len, int32_t* status, void* stream) {
+  BEAST_REQUIRE(n_rows >= 0, "n_rows must be >= 0");
+  if (n_rows == 0) return BEAST_OK;
+  BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && map && table && ws && out_ids && out_len && status,
+                "null pointer argument");
+  BEAST_REQUIRE(lut_n > 0 && lut_n <= 65536, "class LUT size %lld out of range", (long long)lut_n);
+  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
+  BEAST_REQUIRE(max_row_cps >= 0 && max_row_cps < 32768, "max_row_cps %d out of range", max_row_cps);
+  BEAST_REQUIRE(max_row_syms >= 0 && max_row_syms <= 16384, "max_row_syms %d out of range", max_row_syms);
+  BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
+  BEAST_REQUIRE(table_log2 >= beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps) && table_log2 <= 31,
+                "table_log2 %d below beast_bpe_encode_dedup_table_log2 (%d)", table_log2,
+                beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps));
+  BEAST_REQUIRE_CODE(dw_nwv(max_row_cps, max_row_syms) > 0, BEAST_E_UNSUPPORTED,
+                     "rows of %d code points exceed k_dw_words' LDS budget", max_row_cps);
+  DwWs w;
+  const size_t need = dw_carve_host(w, static_cast<char*>(ws), n_rows, max_row_cps, max_row_syms, table_log2);
+  BEAST_REQUIRE_CODE(ws_bytes >= need, BEAST_E_WORKSPACE, "dedup workspace too small: %zu < %zu", ws_bytes, need);
+  w.table = reinterpret_cast<unsigned long long*>(table);
+  w.key_shift = 64 - beast::g_bpe_dedup_key_bits;
+  EncArgs a{};
+  a.tok = reinterpret_cast<const long long*>(tok);
+  a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
+  a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
+  a.map = map_view(map, n_merges);
+  a.n_merges = n_merges;
+  a.unk_id = unk_id; a.fuse_unk = fuse_unk;
+  a.Lc = max_row_cps; a.S = max_row_syms;
+  a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
+  hipStream_t s = beast::as_stream(stream);
+  const size_t lds1 = dw_stage_bytes(w.Lc, w.nwv) + (size_t)w.nwv * dw_row_bytes(w.Lc, w.S);
+  if (lds1 > 65536)
+    BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_words),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1),
+              "hipFuncSetAttribute(k_dw_words)");
+  hipLaunchKernelGGL(k_dw_words, dim3(w.regions), dim3(64 * w.nwv), lds1, s, a, w);
+  BEAST_LAUNCHED("k_dw_words");
+  const size_t map_lds = a.map.log2cap <= LDS_MAP_MAX_LOG2 ? al16(sizeof(uint2) << a.map.log2cap) : 0;
+  if (map_lds > 0) {
+    if (map_lds > 65536)
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_merge<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds),
+                "hipFuncSetAttribute(k_dw_merge)");
+    hipLaunchKernelGGL(k_dw_merge<true>, dim3(w.regions), dim3(64 * DW_WAVES), map_lds, s, a, w);
+  } else {
+    hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions), dim3(64 * DW_WAVES), 0, s, a, w);
+  }
+  BEAST_LAUNCHED("k_dw_merge");
+  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), 0, s, a, w);
+  BEAST_LAUNCHED("k_dw_emit");
+  return BEAST_OK;
+}
+
 
 extern "C" int beast_bpe_decode_rows(const int32_t* ids, const int64_t* row_off, int64_t n_rows,
                                      const int32_t* tok_off, const uint8_t* tok_bytes, const uint8_t* tok_skip,

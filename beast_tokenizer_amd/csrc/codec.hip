@@ -1480,6 +1480,21 @@ extern "C" int beast_set_option(int option, int value) {
     beast::g_bpe_encode_mode = value;
     return BEAST_OK;
   }
+  if (option == BEAST_OPT_BPE_DEDUP_KEY_BITS) {
+    BEAST_REQUIRE(value >= 2 && value <= 64, "BEAST_OPT_BPE_DEDUP_KEY_BITS: %d is not 2..64", value);
+    beast::g_bpe_dedup_key_bits = value;
+    return BEAST_OK;
+  }
   BEAST_REQUIRE(false, "unknown option %d", option);
+  return BEAST_E_INVALID;
+}
+
+extern "C" int beast_get_option(int option) {
+  if (option == BEAST_OPT_GENERIC_KERNELS) return g_generic_only ? 1 : 0;
+  if (option == BEAST_OPT_BLOCK_WAVES) return g_block_waves;
+  if (option == BEAST_OPT_MERGE_LDS_MIN) return (int)beast::g_merge_lds_min;
+  if (option == BEAST_OPT_BPE_ENCODE_MODE) return beast::g_bpe_encode_mode;
+  if (option == BEAST_OPT_BPE_DEDUP_KEY_BITS) return beast::g_bpe_dedup_key_bits;
+  beast::set_error("unknown option %d", option);
   return BEAST_E_INVALID;
 }

@@ -17,6 +17,8 @@ void set_error(const char* fmt, ...);
 extern int64_t g_merge_lds_min;
 // BEAST_OPT_BPE_ENCODE_MODE: bit 0 = heap merge, bit 1 = one workgroup per 4 rows
 extern int g_bpe_encode_mode;
+// BEAST_OPT_BPE_DEDUP_KEY_BITS: width of the dedup encode's word keys (tests force collisions)
+extern int g_bpe_dedup_key_bits;
 int hip_fail(hipError_t e, const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -8,6 +8,7 @@ namespace beast {
 static thread_local char g_err[512] = "";
 int64_t g_merge_lds_min = 4096;   // measured at K5: 65,536 -> 4,096 cut the merge loop 62.6 -> 58.8 ms
 int g_bpe_encode_mode = 0;
+int g_bpe_dedup_key_bits = 64;
 
 void set_error(const char* fmt, ...) {
   va_list ap;

@@ -15,11 +15,13 @@ on the stream the kernels run on; ``value`` / ``ms_per_step`` come from the medi
 (one 20-step window is ~0.3 ms of wall clock: start-up jitter would dominate a single one).
 
 Extra objects in that line:
-  roofline      dominant kernel: algorithmic bytes / its average launch duration
-                (HIP events on the kernel's stream around back-to-back launches)
-  mfma          the fit kernel's MFMA utilisation: issued MFMA flops per launch from the
-                rocprofv3 SQ_INSTS_MFMA pass (profiles/pmc_mfma.json) over the live launch
-                duration, against the f32 MFMA peak
+  roofline      dominant kernel: algorithmic bytes / its average launch duration -- rocprofv3's
+                average in this very command, from the same-tree profile summary
+                (profiles/r04/profile_summary.json, used only when its library fingerprint is this
+                tree's), with `traffic` its PMC HBM bytes per launch; the HIP-event durations of
+                this run are kept beside them (`events`)
+  mfma          the fit kernel's MFMA utilisation: issued MFMA flops per launch from the same
+                profile's SQ_INSTS_MFMA pass over the same launch duration, against the f32 MFMA peak
   cpu_baseline  the oracle's restatement of the reference op sequence (oracle/
                 beast_oracle.py, bitwise equal to the reference in the build
                 container) timed on this host's cores on the SAME B=4096 batch the GPU
@@ -70,6 +72,7 @@ REC_BYTES = N * D * 8 + T * D * 4                # read tokens, write positions
 FIT_BYTES = T * D * 4 + D * N * 4 * (1 + 4)      # read traj; params written once, read/written per radix pass
 FIT_FLOPS = 2 * T * N * D                        # per trajectory per direction
 K5_GOLDEN = os.path.join(REPO, "tests", "golden", "k5_bpe.json")
+PROFILE = os.path.join(REPO, "profiles", "r04", "profile_summary.json")
 K5_CHUNK = 8192
 # what this rank computed, returned by main() (tests/test_gpu_bench_dist.py compares the ranks)
 RANK_INFO: dict = {}
@@ -97,12 +100,10 @@ def parse():
     ap.add_argument("--bpe-sample", type=int, default=20000, help="sequences of the same-sample GPU/HF comparison")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--dump-k5", default=None, help="write the K5 corpus (uint8 bins, npz) and exit")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM bytes from rocprofv3 --pmc (tools/gpu_pmc.sh)")
-    ap.add_argument("--bpe-counters", default=os.path.join(REPO, "profiles", "r03", "bpe_loop_counters.json"),
-                    help="per-pass HBM bytes of the BPE merge loop (tools/make_bpe_counters.py)")
-    ap.add_argument("--pmc-mfma", default=os.path.join(REPO, "profiles", "pmc_mfma.json"),
-                    help="per-launch MFMA instruction counts from rocprofv3 --pmc SQ_INSTS_MFMA")
+    ap.add_argument("--profile", default=PROFILE,
+                    help="same-tree profile summary (tools/make_profile_summary.py): rocprofv3 kernel averages of "
+                         "this command and PMC bytes / MFMA counts per launch; used only when its library "
+                         "fingerprint equals this tree's")
     return ap.parse_args()
 
 
@@ -139,6 +140,52 @@ def kernel_time_us(launch, stream: torch.cuda.Stream, reps: int = 100, rounds: i
             stream.synchronize()
             per.append(s.elapsed_time(e) * 1e3 / reps)
     return float(np.median(per))
+
+
+def load_profile(path: str):
+    """The same-tree profile summary, or (None, reason).  Same tree = the library fingerprint
+    (beast_tokenizer_amd/_build.py: every source, header and flag of libbeast_hip.so) recorded
+    with the profile equals the running tree's, so no fraction comes from other kernels."""
+    if not path or not os.path.exists(path):
+        return None, f"{os.path.relpath(path, REPO) if path else path} missing"
+    from beast_tokenizer_amd import _build
+    with open(path) as f:
+        prof = json.load(f)
+    fp = _build._fingerprint()
+    if prof.get("lib_fingerprint") != fp:
+        return None, f"{os.path.relpath(path, REPO)} was measured on another tree (fingerprint " \
+                     f"{str(prof.get('lib_fingerprint'))[:12]} != {fp[:12]})"
+    return prof, None
+
+
+def codec_roofline(prof, note, t_enc: float, t_rec: float, B: int) -> dict:
+    """Dominant codec kernel at the bench's batch: algorithmic bytes per launch over its average
+    launch duration.  With a same-tree profile the duration is rocprofv3's average for the kernel
+    in the driver's own command (profiles/rNN/profile_summary.json, from its kernel_stats.csv) and
+    `traffic` its PMC HBM bytes per launch; the HIP-event durations of this run stay beside them."""
+    algo = {"k_encode_pipe": ENC_BYTES * B, "k_reconstruct": REC_BYTES * B}
+    ev = {"k_encode_pipe": t_enc, "k_reconstruct": t_rec}
+    kern = (prof or {}).get("kernels", {})
+    if prof and B == 4096 and all(k in kern for k in algo):
+        us = {k: kern[k]["avg_ns"] / 1e3 for k in algo}
+        src = f"rocprofv3 kernel average, {prof.get('stats_csv')} (tree {str(prof.get('git_head_measured'))[:10]})"
+    else:
+        us, src = ev, "HIP events around back-to-back launches on the kernel's stream" + \
+            (f" (no same-tree profile: {note})" if note else "")
+    k = max(us, key=us.get)
+    achieved = algo[k] / (us[k] * 1e-6)
+    kev = max(ev, key=ev.get)
+    pmc = (prof or {}).get("pmc", {}).get(k) if prof else None
+    return {"bound": "hbm", "kernel": k, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK, "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+            "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same tree)",
+            "algo_bytes_per_launch": algo[k], "avg_launch_us": us[k], "duration_source": src,
+            "profile": os.path.relpath(PROFILE, REPO) if prof else None,
+            "profile_git_head": prof.get("git_head_measured") if prof else None,
+            "lib_fingerprint": prof.get("lib_fingerprint") if prof else None,
+            "rocprof_us": {kk: us[kk] for kk in algo} if prof else None,
+            "events": {"k_encode_pipe_us": t_enc, "k_reconstruct_us": t_rec, "kernel": kev,
+                       "frac": algo[kev] / (ev[kev] * 1e-6) / HBM_PEAK}}
 
 
 def max_over_ranks(v: float, world: int, dev) -> float:
@@ -193,30 +240,24 @@ def large_batch_roofline(tok, dev, stream, B: int):
     return out
 
 
-def mfma_utilisation(path: str, times_us: dict) -> dict:
+def mfma_utilisation(prof, note, times_us: dict) -> dict:
     """MFMA utilisation of the fit GEMM (north_star; reference GEMM mp/uni_bspline.py:564-586):
-    issued MFMA flops per launch (rocprofv3 --pmc SQ_INSTS_MFMA, each v_mfma_f32_16x16x4_f32 =
-    16*16*4*2 flops) and the algorithmic 2*T*N*D flops per trajectory, both over the live
-    launch duration, against the dense f32 MFMA peak."""
-    if not os.path.exists(path):
-        return {"error": f"{os.path.relpath(path, REPO)} missing"}
-    with open(path) as f:
-        pmc = json.load(f)
-    out = {"peak_tflops": F32_MFMA_PEAK / 1e12, "source": os.path.relpath(path, REPO),
-           "flops_per_mfma": pmc.get("flops_per_mfma", 2048)}
-    for key, rec in pmc.get("launches", {}).items():
-        us = times_us.get(key)
-        if us is None:
-            continue
-        B = rec["batch"]
-        issued = rec["mfma_insts_per_launch"] * out["flops_per_mfma"]
-        algo = FIT_FLOPS * B
-        out[key] = {"kernel": rec["kernel"], "batch": B, "avg_launch_us": us,
-                    "issued_flops_per_launch": issued, "algorithmic_flops_per_launch": algo,
-                    "issued_tflops": issued / (us * 1e-6) / 1e12, "util_issued": issued / (us * 1e-6) / F32_MFMA_PEAK,
-                    "util_algorithmic": algo / (us * 1e-6) / F32_MFMA_PEAK,
-                    "mfma_busy_cycles_per_launch": rec.get("mfma_busy_cycles_per_launch")}
-    return out
+    issued MFMA flops per launch (same-tree rocprofv3 --pmc SQ_INSTS_MFMA of k_encode_pipe at
+    B = 4,096, each v_mfma_f32_16x16x4_f32 = 16*16*4*2 flops) and the algorithmic 2*T*N*D flops per
+    trajectory, both over the launch duration the roofline uses, against the dense f32 MFMA peak."""
+    pm = (prof or {}).get("pmc", {}).get("k_encode_pipe", {})
+    if not pm.get("mfma_insts_per_launch"):
+        return {"error": f"no same-tree SQ_INSTS_MFMA pass ({note or 'profile lacks it'})"}
+    us = times_us["encode_4096"]
+    issued = pm["mfma_insts_per_launch"] * 2048
+    algo = FIT_FLOPS * 4096
+    return {"peak_tflops": F32_MFMA_PEAK / 1e12, "source": os.path.relpath(PROFILE, REPO), "flops_per_mfma": 2048,
+            "encode_4096": {"kernel": "k_encode_pipe", "batch": 4096, "avg_launch_us": us,
+                            "issued_flops_per_launch": issued, "algorithmic_flops_per_launch": algo,
+                            "issued_tflops": issued / (us * 1e-6) / 1e12,
+                            "util_issued": issued / (us * 1e-6) / F32_MFMA_PEAK,
+                            "util_algorithmic": algo / (us * 1e-6) / F32_MFMA_PEAK,
+                            "mfma_busy_cycles_per_launch": pm.get("mfma_busy_cycles_per_launch")}}
 
 
 def cpu_baseline(x_np: np.ndarray, gpu_tokens: np.ndarray, tok_bounds, seconds: float):
@@ -376,7 +417,7 @@ def bpe_bytes(stats: dict) -> dict:
             "symbols_start": int(S0), "symbols_end": int(S0 - int(np.sum(apps))), "distinct_words": int(W)}
 
 
-def bpe_bench(dev, args, world, rank, reduce):
+def bpe_bench(dev, args, world, rank, reduce, prof=None, prof_note=None):
     from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
     golden = k5_golden()
     allrows = k5_corpus(dev, args.bpe_seqs, rank, world, golden)
@@ -410,28 +451,33 @@ def bpe_bench(dev, args, world, rank, reduce):
            "us_per_merge": st["merge_loop_s"] / max(st["n_merges"], 1) * 1e6, "loop": st.get("loop"),
            "words": st["n_words"], "symbols": st["n_syms"], "distinct_words": st.get("n_distinct"),
            "corpus_sha256": sha}
-    rb = bpe_bytes(st)
-    if "algo_bytes" in rb:
-        rb.update({"achieved_GBps": rb["algo_bytes"] / el / 1e9, "peak_GBps": HBM_PEAK / 1e9,
-                   "frac": rb["algo_bytes"] / el / HBM_PEAK, "bound": "hbm",
-                   "note": "§8d counts a full scan of the live symbols per merge; the kernels visit only "
-                           "candidate words, so this is an effective rate, not bytes moved"})
-    # measured beside it: the HBM bytes the loop's two kernels move per pass (rocprofv3 FETCH_SIZE +
-    # WRITE_SIZE of k_merge_batch and k_apply_batch at K5, profiles/r03/bpe_loop_counters.json)
-    # times the passes this run took, over the live loop time
-    if os.path.exists(args.bpe_counters) and st.get("passes"):
-        with open(args.bpe_counters) as f:
-            cnt = json.load(f)
-        pp = cnt.get("per_pass", {})
-        if pp.get("bytes"):
-            moved = pp["bytes"] * st["passes"]
-            rb["counters"] = {"source": os.path.relpath(args.bpe_counters, REPO), "bytes_per_pass": pp["bytes"],
-                              "passes": st["passes"], "traffic": moved,
-                              "achieved_GBps": moved / st["merge_loop_s"] / 1e9,
-                              "frac": moved / st["merge_loop_s"] / HBM_PEAK,
-                              "in_kernel_GBps": pp.get("hbm_GBps_in_kernels"),
-                              "note": "counter bytes over the whole loop (launch gaps and the decision chain "
-                                      "included); in_kernel_GBps is over the two kernels' own time"}
+    # roofline of the merge loop: the HBM bytes its two kernels move per launch (same-tree rocprofv3
+    # --pmc FETCH_SIZE + WRITE_SIZE of k_merge_batch and k_apply_batch at K5) times the passes this run
+    # took, over the loop's wall time; §8d's notional count (a full scan of the live symbols per
+    # merge, which the kernels never do) is kept beside it
+    notional = bpe_bytes(st)
+    if "algo_bytes" in notional:
+        notional.update({"achieved_GBps": notional["algo_bytes"] / el / 1e9,
+                         "frac": notional["algo_bytes"] / el / HBM_PEAK,
+                         "note": "§8d counts a full scan of the live symbols per merge; the kernels visit only "
+                                 "candidate words, so this is an effective rate, not bytes moved"})
+    pm = (prof or {}).get("pmc", {})
+    if prof and "k_merge_batch" in pm and "k_apply_batch" in pm and st.get("passes"):
+        per_pass = pm["k_merge_batch"]["hbm_bytes_per_launch"] + pm["k_apply_batch"]["hbm_bytes_per_launch"]
+        moved = per_pass * st["passes"]
+        kern = prof.get("kernels", {})
+        k_us = sum(kern[k]["avg_ns"] / 1e3 for k in ("k_merge_batch", "k_apply_batch") if k in kern)
+        rb = {"bound": "hbm", "achieved_GBps": moved / st["merge_loop_s"] / 1e9, "peak_GBps": HBM_PEAK / 1e9,
+              "frac": moved / st["merge_loop_s"] / HBM_PEAK, "traffic": moved, "bytes_per_pass": per_pass,
+              "passes": st["passes"], "loop_s": st["merge_loop_s"],
+              "in_kernel_GBps": per_pass / k_us / 1e3 if k_us else None,
+              "source": os.path.relpath(PROFILE, REPO),
+              "note": "PMC bytes per pass x passes over the loop's wall time (launch gaps and the decision "
+                      "chain included); in_kernel_GBps over the two kernels' rocprof averages"}
+    else:
+        rb = {"bound": "hbm", "frac": None, "traffic": None,
+              "error": f"no same-tree BPE loop counters ({prof_note or 'profile lacks them'})"}
+    rb["notional"] = notional
     out["roofline"] = rb
     if golden is not None and golden.get("merges") is not None and args.bpe_seqs == golden["trajectories"] \
             and args.bpe_vocab == golden["vocab_size"]:
@@ -550,10 +596,25 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     out = {}
     enc = {}
 
-    def launch_enc():
-        enc["r"] = model.encode_rows(flat, off, width, lo, span)
+    from beast_tokenizer_amd.bpe_codec import set_encode_path
+
+    def launch_enc():   # resolve=False: no host sync inside the timed launches (status checked below)
+        enc["r"] = model.encode_rows(flat, off, width, lo, span, resolve=False)
     t_enc = kernel_time_us(launch_enc, stream, reps=20, rounds=3)
+    path = "dedup" if model._dedup_ok() else "rows"
+    st_enc = enc["r"][2]
+    n_fallback = int((st_enc == 7).sum())
+    set_encode_path("rows")                      # the per-row kernel beside it (same ids)
+    try:
+        t_enc_rows = kernel_time_us(launch_enc, stream, reps=20, rounds=3)
+        rows_ref = enc["r"]
+    finally:
+        set_encode_path("auto")
+    enc["r"] = model.encode_rows(flat, off, width, lo, span)
     ids, lens, _ = enc["r"]
+    live = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]
+    assert torch.equal(lens, rows_ref[1]) and torch.equal(ids[live], rows_ref[0][:, :ids.shape[1]][live]), \
+        "dedup encode != per-row encode"
     lens_np = lens.cpu().numpy()
     n_ids = int(lens_np.sum())
     mask = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]
@@ -582,8 +643,9 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     torch.cuda.synchronize()
     t_api_tens = (time.perf_counter() - t0) / 10
     assert blk[1].tolist() == [len(r) for r in lists]
-    out.update({"rows": R, "ids_per_row": n_ids / R,
+    out.update({"rows": R, "ids_per_row": n_ids / R, "encode_path": path, "encode_fallback_rows": n_fallback,
                 "encode_kernel_us": t_enc, "encode_rows_per_s_kernel": R / (t_enc * 1e-6),
+                "encode_row_kernel_us": t_enc_rows,
                 "decode_kernel_us": t_dec, "decode_rows_per_s_kernel": R / (t_dec * 1e-6),
                 "encode_api_rows_per_s": R / t_api_enc, "encode_api_tensors_rows_per_s": R / t_api_tens,
                 "encode_kernel_GBps": (R * width * 8 + n_ids * 4) / (t_enc * 1e-6) / 1e9,
@@ -669,29 +731,18 @@ def main():
     value = B * world * args.steps / el
     gpu_tokens = tok.encode(x)[0].cpu().numpy()
 
-    # ---- dominant-kernel roofline, measured live on the kernel's stream
+    # ---- dominant-kernel roofline: the same-tree rocprofv3 average when the profile matches this
+    #      tree, HIP events measured live on the kernel's stream beside it
+    prof, prof_note = load_profile(args.profile)
     launch_enc, launch_rec = launchers(tok, dev, stream, x, B)
     t_enc = kernel_time_us(launch_enc, stream)
     t_rec = kernel_time_us(launch_rec, stream)
-    if t_enc >= t_rec:
-        kname, tk, kbytes = "k_encode", t_enc, ENC_BYTES * B
-    else:
-        kname, tk, kbytes = "k_reconstruct", t_rec, REC_BYTES * B
-    achieved = kbytes / (tk * 1e-6)
-    traffic = None
-    if os.path.exists(args.pmc):
-        with open(args.pmc) as f:
-            pmc = json.load(f)
-        traffic = pmc.get(kname, {}).get("hbm_bytes_per_launch")
-    roof = {"bound": "hbm", "kernel": kname, "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK, "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
-            "algo_bytes_per_launch": kbytes,
-            "avg_launch_us": tk, "k_encode_us": t_enc, "k_reconstruct_us": t_rec}
-    times_us = {"encode_4096": t_enc}
+    roof = codec_roofline(prof, prof_note, t_enc, t_rec, B)
+    times_us = {"encode_4096": (roof["rocprof_us"] or {}).get("k_encode_pipe", t_enc)}
     if not args.no_large:
         roof["large_batch"] = lb = large_batch_roofline(tok, dev, stream, args.large_batch)
-        times_us[f"encode_{args.large_batch}"] = lb["k_encode_us"]
-    mfma = mfma_utilisation(args.pmc_mfma, times_us)
+        lb["duration_source"] = "HIP events (rocprof's average for these instantiations mixes fit_parameters' launches)"
+    mfma = mfma_utilisation(prof, prof_note, times_us)
 
     fitb = None
     if not args.no_fit:
@@ -699,7 +750,7 @@ def main():
 
     bpe = None
     if not args.no_bpe:
-        bpe = bpe_bench(dev, args, world, rank, reduce)
+        bpe = bpe_bench(dev, args, world, rank, reduce, prof, prof_note)
 
     cpu, parity = None, None
     if rank == 0 and not args.no_cpu:

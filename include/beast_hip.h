@@ -53,12 +53,17 @@ const char* beast_last_error(void);
  * BEAST_OPT_BPE_ENCODE_MODE = m (tests, measurements): beast_bpe_encode_rows' per-word merge by
  * rounds (0, the default) or by HF's min-heap (1); m + 2 also launches one workgroup per 4 rows
  * instead of only the resident ones.  Results are identical.
+ * BEAST_OPT_BPE_DEDUP_KEY_BITS = k (tests): beast_bpe_encode_rows_dedup keeps only k bits of its
+ * 64-bit word keys, so different words collide; the collisions are detected (ST_FALLBACK rows).
  * Options are process-wide and not synchronised: set them before launching, not concurrently. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
 #define BEAST_OPT_MERGE_LDS_MIN 3
 #define BEAST_OPT_BPE_ENCODE_MODE 5
+#define BEAST_OPT_BPE_DEDUP_KEY_BITS 6
 int beast_set_option(int option, int value);
+/* the option's current value (BEAST_E_INVALID for an unknown option) */
+int beast_get_option(int option);
 
 /* ---------------------------------------------------------------- H1/H2 ---
  * Replaces UniBSplineBasis.basis (MP_lite_PyTorch/mp_pytorch/basis_gn/
@@ -351,6 +356,24 @@ int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_
                           const int32_t* spec_id, int n_spec, int unk_id, int fuse_unk, int max_row_cps,
                           int max_row_syms, int32_t* out_ids, int64_t out_stride, int32_t* out_len,
                           int32_t* status, void* stream);
+/* The same encode, each distinct word of the batch merged once (round 4; bit-exact with
+ * beast_bpe_encode_rows for models whose merges only combine tokens made by earlier merges --
+ * every trained model; the caller checks and uses beast_bpe_encode_rows otherwise, or when the
+ * model has special tokens).  Three launches: word split + key insert, one merge per distinct
+ * word, emit.  status as above plus 7 (ST_FALLBACK): the row holds a word of more than 64 byte
+ * symbols, or a 64-bit word-key collision was detected; the caller re-encodes such rows with
+ * beast_bpe_encode_rows.  table: 2^table_log2 uint64 word keys, table_log2 >=
+ * beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps), zero-filled before its first use; every
+ * call leaves it zero again (reuse it across calls, not across concurrent streams).  ws: scratch
+ * of beast_bpe_encode_dedup_workspace_bytes bytes (no initialisation). */
+int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps);
+size_t beast_bpe_encode_dedup_workspace_bytes(int64_t n_rows, int max_row_cps, int max_row_syms, int table_log2);
+int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
+                                int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
+                                const void* map, int n_merges, int unk_id, int fuse_unk, int max_row_cps,
+                                int max_row_syms, uint64_t* table, int table_log2, void* ws, size_t ws_bytes,
+                                int32_t* out_ids, int64_t out_stride, int32_t* out_len, int32_t* status,
+                                void* stream);
 /* Decode rows ids[row_off[r] .. row_off[r+1]).  tok_off[n_vocab+1] / tok_bytes: each id's
  * ByteLevel-decoded bytes; tok_skip[id] = 1 for special tokens (skip_special_tokens) and
  * unassigned ids.  out[r][0 .. min(count, L)) = code point + min_tok; out_count[r] = code

@@ -51,12 +51,19 @@ def decode_rows(model, id_rows, dev, L):
     return [out[i, :counts[i]].tolist() for i in range(len(seqs))], counts, status.cpu().numpy()
 
 
-@pytest.fixture(params=[0, 1, 3], ids=["rounds", "heap", "heap_wide_grid"])
+@pytest.fixture(params=[("auto", 0), ("rows", 0), ("rows", 1), ("rows", 3)],
+                ids=["dedup", "rounds", "heap", "heap_wide_grid"])
 def encode_mode(request):
-    """k_bpe_encode's per-word merge (rounds by default, HF's heap) and its grid: same ids."""
+    """The word-dedup encode (the default: k_dw_words / k_dw_merge / k_dw_emit, falling back to
+    k_bpe_encode where it must) and k_bpe_encode itself with its per-word merge by rounds or by
+    HF's heap, and its grid: same ids."""
     from beast_tokenizer_amd import _lib
-    _lib.run("beast_set_option", _lib.OPT_BPE_ENCODE_MODE, request.param)
+    from beast_tokenizer_amd.bpe_codec import set_encode_path
+    path, mode = request.param
+    set_encode_path(path)
+    _lib.run("beast_set_option", _lib.OPT_BPE_ENCODE_MODE, mode)
     yield request.param
+    set_encode_path("auto")
     _lib.run("beast_set_option", _lib.OPT_BPE_ENCODE_MODE, 0)
 
 
@@ -185,3 +192,84 @@ def test_encode_punct_contractions_live_hf(seed, encode_mode, gpu_device):
     want = [e.ids for e in tok.encode_batch(texts, add_special_tokens=False)]
     bad = [i for i in range(len(texts)) if got[i] != want[i]]
     assert not bad, f"{len(bad)} rows differ, first {texts[bad[0]]!r}"
+
+
+def _trained_model(span, rows, width, vocab, seed, gpu_device):
+    from tokenizers import ByteLevelBPETokenizer
+    from tokenizers.trainers import BpeTrainer
+    rng = np.random.default_rng(seed)
+    centre = rng.integers(0, span + 1, size=(rows, 1))
+    train = np.clip(centre + np.round(rng.normal(0, span / 12, size=(rows, width))), 0, span).astype(np.int64)
+    tok = ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=vocab, min_frequency=2, show_progress=False, special_tokens=[],
+                    initial_alphabet=[chr(i) for i in range(span + 1)], max_token_length=10000)
+    tok._tokenizer.train_from_iterator(["".join(map(chr, r)) for r in train], trainer=tr)
+    return tok, GpuBpeModel(tok, gpu_device), rng, centre
+
+
+def test_dedup_fallback_rows_for_long_words(gpu_device):
+    """Rows holding a word of more than 64 byte symbols come back ST_FALLBACK from the dedup path
+    (resolve=False) and are re-encoded by k_bpe_encode (resolve=True): HF's ids either way."""
+    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK
+    tok, model, rng, _ = _trained_model(255, 800, 120, 1200, 5, gpu_device)
+    assert model.monotone and model.n_spec == 0
+    rows = [rng.integers(0, 256, size=120) for _ in range(300)]
+    rows[7] = np.full(120, ord("a"))                      # one 120-letter word
+    rows[100] = np.concatenate([np.full(40, 0xE9), [0x20], rows[100][:50]])   # "é" x 40: 80 byte symbols
+    seqs = [np.asarray(r, dtype=np.int64) for r in rows]
+    flat, off, width = rows_from_sequences(seqs, gpu_device)
+    _, _, st = model.encode_rows(flat, off, width, 0, None, resolve=False)
+    st = st.cpu().numpy()
+    assert st[7] == ST_FALLBACK and st[100] == ST_FALLBACK and (st[np.r_[0:7, 8:100, 101:300]] == 0).all()
+    got, status = encode_rows(model, rows, gpu_device)
+    assert not status.any()
+    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in rows], add_special_tokens=False)]
+    assert got == want
+    assert model.encode_to_lists(flat, off, width, 0, None) == want
+
+
+@pytest.mark.parametrize("bits", [3, 8, 20])
+def test_dedup_key_collisions_are_detected(bits, gpu_device):
+    """With only `bits` bits of the 64-bit word keys, different words share keys: every such row
+    is caught by the content check (ST_FALLBACK, never a wrong id) and re-encoded per row."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK
+    tok, model, rng, centre = _trained_model(255, 1500, 140, 2048, 9, gpu_device)
+    test = np.clip(centre[:1000] + np.round(rng.normal(0, 255 / 8, size=(1000, 140))), 0, 255).astype(np.int64)
+    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
+    flat, off, width = rows_from_sequences(list(test), gpu_device)
+    st0 = model.encode_rows(flat, off, width, 0, 255, resolve=False)[2].cpu().numpy()   # long-word rows only
+    _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, bits)
+    try:
+        ids, lens, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
+        ids, lens, st = ids.cpu().numpy(), lens.cpu().numpy(), st.cpu().numpy()
+        ok = st == 0
+        assert (st[~ok] == ST_FALLBACK).all() and (st[st0 == ST_FALLBACK] == ST_FALLBACK).all()
+        if bits <= 8:
+            assert (~ok).sum() > (st0 != 0).sum() + 100          # many rows hit a collision
+        for i in np.flatnonzero(ok):          # the rows that passed the check are HF's
+            assert ids[i, :lens[i]].tolist() == want[i]
+        got, status = encode_rows(model, list(test), gpu_device)
+        assert not status.any() and got == want
+    finally:
+        _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, 64)
+    # the table is left empty: a normal call right after falls back on the long-word rows only
+    _, _, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
+    assert np.array_equal(st.cpu().numpy(), st0)
+
+
+def test_dedup_non_monotone_model_uses_heap(gpu_device):
+    """A hand-written model whose merges are not rank-monotone ("aa" + "a" ranked before "a" + "a")
+    takes k_bpe_encode with HF's heap: HF's ids, where merging a word's lowest pair everywhere at
+    once would not be."""
+    from tokenizers import ByteLevelBPETokenizer
+    vocab = {c: i for i, c in enumerate("abcx")}
+    for t in ("aa", "aaa", "ab", "aab"):
+        vocab[t] = len(vocab)
+    tok = ByteLevelBPETokenizer(vocab=vocab, merges=[("aa", "a"), ("a", "a"), ("aa", "b"), ("a", "b")])
+    model = GpuBpeModel(tok, gpu_device)
+    assert not model.monotone
+    texts = ["aaaa", "aaaaa", "aab", "aaab", "xaaaax", "abab", "aaaaaaab"]
+    got, status = encode_rows(model, [[ord(c) for c in s] for s in texts], gpu_device)
+    assert not status.any()
+    assert got == [e.ids for e in tok.encode_batch(texts, add_special_tokens=False)]

@@ -259,3 +259,13 @@ def test_rows_to_lists_matches_numpy():
     assert all(type(v) is int for row in got for v in row)
     with pytest.raises(ValueError):
         fp.rows_to_lists(torch.from_numpy(ids.astype(np.int64)), torch.from_numpy(lens))
+
+
+def test_rank_monotone_check():
+    """bpe_codec.rank_monotone decides whether the word-dedup encode (lowest pair merged everywhere
+    at once) is HF's heap order for a model."""
+    from beast_tokenizer_amd.bpe_codec import rank_monotone
+    assert rank_monotone([(0, 1, 5), (5, 2, 6), (1, 2, 7)])
+    assert not rank_monotone([(5, 0, 6), (0, 0, 5)])                    # (aa, a) before (a, a)
+    assert not rank_monotone([(0, 1, 5), (5, 0, 6), (2, 3, 5)])         # id 5 also made after its use
+    assert rank_monotone([(0, 1, 5), (0, 1, 5), (5, 0, 6)])
