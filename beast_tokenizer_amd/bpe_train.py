@@ -149,16 +149,22 @@ class GpuBpeOps:
         """Distinct words of >= 2 symbols x their counts (HF trains on word counts)."""
         n = words["n_words"]
         dev, s = self.device, self.stream
-        ws = torch.empty(_lib.load().beast_bpe_dedup_workspace_bytes(n), dtype=torch.uint8, device=dev)
+        nbytes = _lib.load().beast_bpe_dedup_workspace_bytes(n)   # a table for n / 4 distinct words
         m = max(n, 1)
         ow = torch.empty(m, dtype=torch.int32, device=dev)
         ol = torch.empty(m, dtype=torch.int32, device=dev)
         oc = torch.empty(m, dtype=torch.int32, device=dev)
         on = torch.empty(1, dtype=torch.int64, device=dev)
-        _lib.run("beast_bpe_dedup_words", words["sym"].data_ptr(), words["wstart"].data_ptr(), words["wlen"].data_ptr(),
-                 n, ws.data_ptr(), ws.numel(), ow.data_ptr(), ol.data_ptr(), oc.data_ptr(), on.data_ptr(), s)
-        nu = self._read_i64(on, 1)[0]
-        del ws
+        while True:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            _lib.run("beast_bpe_dedup_words", words["sym"].data_ptr(), words["wstart"].data_ptr(),
+                     words["wlen"].data_ptr(), n, ws.data_ptr(), ws.numel(), ow.data_ptr(), ol.data_ptr(),
+                     oc.data_ptr(), on.data_ptr(), s)
+            nu = self._read_i64(on, 1)[0]
+            del ws
+            if nu >= 0:
+                break
+            nbytes *= 4   # more distinct words than the table holds: a 4x larger one
         return self._repack(words, words["sym"], ow, ol, oc, nu, words["n_syms"])
 
     def _repack(self, words, sym, ow, ol, oc, nu: int, cap: int):

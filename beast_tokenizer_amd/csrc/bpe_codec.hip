@@ -26,11 +26,16 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "pretok.h"
 
 namespace {
 
 constexpr uint32_t EMPTY_KEY = 0xFFFFFFFFu;
-[[maybe_unused]] constexpr int CLS_OTHER = 0, CLS_LETTER = 1, CLS_NUMBER = 2, CLS_WS = 3;
+using beast_pt::CLS_OTHER;
+using beast_pt::regex_word;
+using beast_pt::wave_excl_scan;
+using beast_pt::wave_sync;
+using beast_pt::word_starts;
 constexpr int WAVES = 4;            // rows in flight per workgroup (decode)
 constexpr int ENC_MAX_WAVES = 16;   // encode: as many rows per workgroup as the LDS holds, up to 16
 constexpr int BLOCK = 64 * WAVES;
@@ -60,12 +65,6 @@ __device__ unsigned long long g_bpe_rs[BPE_RS][12];
 #else
 #define BPE_STAMP(k) do { } while (0)
 #endif
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -254,113 +253,6 @@ struct EncArgs {
   int32_t* out_len;
   int32_t* status;
 };
-
-// GPT-2 regex from code point i of [.., n): returns the end of the word.
-//   's|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+
-__device__ __forceinline__ int regex_word(const int32_t* cps, const uint8_t* cls, int i, int n) {
-  const int c = cps[i];
-  if (c == '\'' && i + 1 < n) {
-    const int c1 = cps[i + 1];
-    if (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd') return i + 2;
-    if (i + 2 < n) {
-      const int c2 = cps[i + 2];
-      if ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l')) return i + 3;
-    }
-  }
-  int k = cls[i], st = i;
-  if (c == ' ' && i + 1 < n && cls[i + 1] != CLS_WS) { k = cls[i + 1]; st = i + 1; }
-  int j;
-  if (k != CLS_WS) {
-    j = st + 1;
-    while (j < n && cls[j] == k) ++j;
-  } else {
-    j = i + 1;
-    while (j < n && cls[j] == CLS_WS) ++j;
-    if (j < n && j - i >= 2) --j;  // \s+(?!\S): the last blank starts the next word
-  }
-  return j;
-}
-
-__device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
-  int x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  total = __shfl(x, 63);
-  return x - v;
-}
-
-// 2. (see encode_row) the word starts of a row from e[i], the end of the regex word that would
-// start at code point i: the chain 0 -> e[0] -> e[e[0]] -> ... < n.  Lane-parallel instead of one
-// lane following ~n / 2 dependent links: lane s walks the chain from the start of its segment
-// [s G, s G + G) (G = ceil(n / 64)), marking what it visits (vis, one byte per code point), and
-// records where it leaves the segment.  The true chain enters segment s where it left segment
-// s - 1; a marked entry means lane s's walk already is the true chain from there (the chain is a
-// function of the position), an entry past the segment means the segment holds no start, and
-// any other entry (rare: regex words self-synchronise within a word) makes the lane re-walk its
-// segment from it -- repeated until no exit changes.  Starts = marked positions at or past
-// their segment's entry, written in order by a wave scan.
-// Invariant: the marks in [ws, se) are exactly the positions of the lane's latest walk, which
-// started at ws and leaves the segment at wex.  The exit passed on, ex, is wex when the entry lies
-// on that walk, or the entry itself when the chain jumps the segment.  A marked entry below ws is
-// a mark of an older walk (e.g. "x!'tion": the walk from "'" marks "t" before the chain is known
-// to enter at "t"), so only a marked entry at or past ws reuses the walk; anything else re-walks.
-__device__ __forceinline__ void word_starts(const int32_t* e, uint8_t* vis, int32_t* wcp, int32_t* wspec,
-                                            int32_t* nw_out, int n, int lane) {
-  const int G = (n + 63) >> 6;
-  const int sb = min(lane * G, n), se = min(sb + G, n);
-  for (int i = lane; i < n; i += 64) vis[i] = 0;
-  wave_sync();
-  int ex = sb;    // exit passed to the next lane: the first chain position >= se (n past the end)
-  int ws = sb;    // start of the walk the marks in [ws, se) belong to
-  int wex = sb;   // that walk's exit
-  if (sb < se) {
-    int p = sb;
-    while (p < se) { vis[p] = 1; p = e[p]; }
-    wex = ex = p;
-  }
-  int entry = 0;
-  while (true) {
-    const int prev = __shfl_up(ex, 1);
-    const int en = lane == 0 ? 0 : prev;
-    int nex = ex;
-    bool changed = false;
-    if (sb < se) {
-      if (en >= se) {
-        nex = en;                 // the chain jumps this segment
-      } else if (en >= sb && en >= ws && vis[en]) {
-        nex = wex;                // the entry lies on the latest walk
-      } else if (en >= sb) {
-        for (int i = en; i < se; ++i) vis[i] = 0;   // re-walk from the true entry
-        int p = en;
-        while (p < se) { vis[p] = 1; p = e[p]; }
-        nex = wex = p;
-        ws = en;
-        changed = true;
-      }
-    } else {
-      nex = en > sb ? en : sb;   // empty segment (past n): pass the exit on
-    }
-    changed |= nex != ex || en != entry;
-    ex = nex;
-    entry = en;
-    if (!__any(changed)) break;
-  }
-  wave_sync();
-  int cnt = 0;
-  for (int i = max(sb, entry); i < se; ++i) cnt += vis[i];
-  int tot;
-  int o = wave_excl_scan(cnt, lane, tot);
-  for (int i = max(sb, entry); i < se; ++i)
-    if (vis[i]) {
-      wcp[o] = i;
-      if (wspec) wspec[o] = -1;
-      ++o;
-    }
-  if (lane == 0) { wcp[tot] = n; *nw_out = tot; }
-  wave_sync();
-}
 
 // 4b. (see encode_row) the round merge of a row of <= 64 * RMP byte symbols
 template <int RMP, class Map>
@@ -923,7 +815,11 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
   __syncthreads();
   DwRow L = dw_carve(rows + (size_t)wave * rb, w.Lc, w.S);
   const int64_t r = (int64_t)blockIdx.x * nwv + wave;
+#ifdef BPE_STAMPS
+  if (lane == 0 && r < BPE_RS) g_bpe_rs[r][10] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (r < a.n_rows) {
+    BPE_STAMP(0);
     const int64_t r0 = a.row_off[r];
     const int n = (int)(a.row_off[r + 1] - r0);
     int st = ST_OK;
@@ -948,6 +844,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
       else if (__any(surr)) st = ST_SURROGATE;
       else if (__any(nocls)) st = ST_NO_CLASS;
     }
+    BPE_STAMP(1);
     int carry = 0;
     if (st == ST_OK) {   // UTF-8 symbol offsets
       for (int base = 0; base < n; base += 64) {
@@ -962,11 +859,13 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
       if (carry > w.S) st = ST_TOO_LONG;
     }
     wave_sync();
+    BPE_STAMP(2);
     int nw = 0;
     if (st == ST_OK) {
       // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
       for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
       word_starts(L.e, L.vis, L.wcp, nullptr, L.misc, n, lane);
+      BPE_STAMP(3);
       for (int i = lane; i < n; i += 64) {
         const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
         for (int q = 0; q < len; ++q) L.c[o + q] = (uint16_t)s_b2i[utf8_byte(cp, q)];   // -1 -> SYM_NONE
@@ -977,6 +876,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
       for (int k = lane; k < nw; k += 64) fall |= (L.symoff[L.wcp[k + 1]] - L.symoff[L.wcp[k]]) > DW_MID;
       if (__any(fall)) st = ST_FALLBACK;
     }
+    BPE_STAMP(4);
     if (st == ST_OK) {
       const unsigned long long tmask = (1ull << w.log2cap) - 1ull;
       for (int k = lane; k < nw; k += 64) {
@@ -1001,7 +901,11 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
         }
       }
     }
+    BPE_STAMP(5);
     if (lane == 0) { a.status[r] = st; w.nwords[r] = st == ST_OK ? nw : 0; }
+#ifdef BPE_STAMPS
+    if (lane == 0 && r < BPE_RS) g_bpe_rs[r][9] = (unsigned long long)nw;
+#endif
   }
   __syncthreads();
   // flush this region's records (byte symbols from the rows still in LDS)
@@ -1030,6 +934,10 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
       w.slot2idx[rec.x] = 0x80000000u | (uint32_t)idx;
     }
   }
+#ifdef BPE_STAMPS
+  __syncthreads();
+  if (r < a.n_rows) BPE_STAMP(6);
+#endif
 }
 
 // lane gl of a GW-lane group reads lane gl + 1 (down) / gl - 1 (up) of its group; `fill` past the ends

@@ -18,6 +18,7 @@
 
 #include "bpe_common.h"
 #include "common.h"
+#include "pretok.h"
 
 namespace {
 
@@ -161,18 +162,19 @@ __device__ void pretok_serial(const long long* __restrict__ tok, const int64_t* 
 // stride (every load instruction touches 64 cache lines), branches on its own word
 // structure, and scatters 2-byte stores the same way.  Here the lanes load the row coalesced
 // into LDS, classify it, evaluate the regex from every position at once (end of the word
-// that would start there), scan the UTF-8 lengths, and lane 0 only follows the word chain
-// 0 -> end[0] -> ...; the emission is lane-parallel over words and code points, so the
+// that would start there), scan the UTF-8 lengths, and walk the word chain 0 -> end[0] -> ...
+// together (csrc/pretok.h word_starts); the emission is lane-parallel over words and code points, so the
 // stores of a wave land in one contiguous stretch.  Rows longer than PT_LC code points (or
 // with code points outside [0, 2^31)) take pretok_serial on lane 0.
 constexpr int PT_LC = 512;
 constexpr int PT_WAVES = 4;
 struct PtLds {
   int32_t cp[PT_LC];
-  int16_t nxt[PT_LC];       // end of the word starting at i
+  int32_t e[PT_LC];         // end of the word starting at i
+  int32_t wcp[PT_LC + 1];   // first code point of word w
   int16_t so[PT_LC + 1];    // byte-symbol offset of code point i
-  int16_t wcp[PT_LC + 1];   // first code point of word w
   uint8_t cls[PT_LC];
+  uint8_t vis[PT_LC];       // word_starts' marks
   int32_t nw;
 };
 
@@ -224,44 +226,11 @@ __global__ __launch_bounds__(64 * PT_WAVES) void k_pretok_wave(
     }
     if (lane == 0) L.so[n] = (int16_t)carry;
     pt_wave_sync();
-    // 2. the end of the word that starts at every position (pretok_serial's rules)
-    for (int i = lane; i < n; i += 64) {
-      const int c = L.cp[i];
-      int j = 0;
-      if (c == '\'' && i + 1 < n) {
-        const int c1 = L.cp[i + 1];
-        if (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd') j = i + 2;
-        else if (i + 2 < n) {
-          const int c2 = L.cp[i + 2];
-          if ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l')) j = i + 3;
-        }
-      }
-      if (j == 0) {
-        int k = L.cls[i], st = i;
-        if (c == ' ' && i + 1 < n && L.cls[i + 1] != CLS_WS) { k = L.cls[i + 1]; st = i + 1; }
-        if (k != CLS_WS) {
-          j = st + 1;
-          while (j < n && L.cls[j] == k) ++j;
-        } else {
-          j = i + 1;
-          while (j < n && L.cls[j] == CLS_WS) ++j;
-          if (j < n && j - i >= 2) --j;   // \s+(?!\S): leave the last blank for the next word
-        }
-      }
-      L.nxt[i] = (int16_t)j;
-    }
+    // 2. the end of the word that starts at every position (pretok_serial's rules), 3. the word
+    //    chain 0 -> e[0] -> ... walked lane-parallel (csrc/pretok.h; round 3 walked it on lane 0)
+    for (int i = lane; i < n; i += 64) L.e[i] = beast_pt::regex_word(L.cp, L.cls, i, n);
     pt_wave_sync();
-    // 3. lane 0 follows the chain
-    if (lane == 0) {
-      int nw = 0, p = 0;
-      while (p < n) {
-        L.wcp[nw++] = (int16_t)p;
-        p = L.nxt[p];
-      }
-      L.wcp[nw] = (int16_t)n;
-      L.nw = nw;
-    }
-    pt_wave_sync();
+    beast_pt::word_starts(L.e, L.vis, L.wcp, nullptr, &L.nw, n, lane);
     const int nw = L.nw;
     if (!EMIT) {
       if (lane == 0) {
@@ -440,15 +409,23 @@ struct DedupWs {
   uint32_t* cnt;              // [cap]
   uint32_t* rep;              // [n] distinct -> representative word
   uint32_t* slot;             // [n] distinct -> table slot
-  unsigned long long* nu;     // distinct count
+  unsigned long long* nu;     // distinct count; nu[1]: overflow flag
   uint64_t cap;
 };
 
+// Table of the distinct words (keys + counts, 12 B a slot).  Round 4: sized for a quarter of the
+// word occurrences, not twice them -- corpora of trajectories repeat their words (K5: 13 % distinct),
+// and 2^24 slots (201 MB) stay in the 256 MB MALL where 2^27 (1.6 GB, round 3) made every probe an
+// HBM round trip and took a 1.6 GB memset.  A table that fills up is detected (a probe run past
+// DEDUP_MAX_PROBE slots sets the overflow flag, *out_n = -1) and the caller retries with a larger
+// workspace: the capacity is the largest power of two the workspace holds.
+constexpr int DEDUP_MAX_PROBE = 1024;
 __host__ __device__ inline uint64_t dedup_cap(int64_t n) {
   uint64_t c = 1024;
-  while (c < (uint64_t)n * 2) c <<= 1;
+  while (c < (uint64_t)n / 4) c <<= 1;
   return c;
 }
+__host__ __device__ inline size_t dedup_fixed_bytes(int64_t n) { return (size_t)(n > 0 ? n : 1) * 8 + 64; }
 
 // One thread per word.  The table slot of the word's content is found as before; then the
 // atomics that serialised at the memory side are aggregated.  New distinct words go to an LDS
@@ -504,7 +481,12 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict
         const uint64_t h = word_hash(s, L);
         const unsigned long long mine = ((h >> 32) << 32) | (unsigned long long)(uint32_t)(w + 1);
         k = h & mask;
-        while (true) {
+        for (int probe = 0;; ++probe) {
+          if (probe == DEDUP_MAX_PROBE) {   // table too full: the caller retries with a larger one
+            ws.nu[1] = 1ull;
+            have = false;
+            break;
+          }
           unsigned long long v = ws.keys[k];
           if (v == 0ull) {
             v = atomicCAS(&ws.keys[k], 0ull, mine);
@@ -561,8 +543,8 @@ __global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ wlen, DedupWs ws,
                                                       uint32_t* __restrict__ ow, uint32_t* __restrict__ ol,
                                                       uint32_t* __restrict__ oc, int64_t* __restrict__ out_n) {
-  const int64_t nu = (int64_t)*ws.nu;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *out_n = nu;
+  const int64_t nu = ws.nu[1] ? 0 : (int64_t)ws.nu[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out_n = ws.nu[1] ? -1 : nu;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nu; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t r = ws.rep[i];
     ow[i] = wstart[r];
@@ -570,6 +552,7 @@ __global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict
     oc[i] = ws.cnt[ws.slot[i]];
   }
 }
+
 
 // keep the words that can still merge (>= 2 symbols); one atomic per wave
 __global__ __launch_bounds__(256) void k_compact_words(const uint32_t* __restrict__ wstart,
@@ -799,10 +782,8 @@ extern "C" int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* ws
 }
 
 extern "C" size_t beast_bpe_dedup_workspace_bytes(int64_t n_words) {
-  const uint64_t cap = dedup_cap(n_words > 0 ? n_words : 1);
-  return (size_t)(cap * 12 + (uint64_t)(n_words > 0 ? n_words : 1) * 8 + 64);
+  return (size_t)(dedup_cap(n_words > 0 ? n_words : 1) * 12) + dedup_fixed_bytes(n_words);
 }
-
 extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
                                      int64_t n_words, void* workspace, size_t ws_bytes, uint32_t* out_wstart,
                                      uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_n, void* stream) {
@@ -814,7 +795,8 @@ extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart
   hipStream_t s = beast::as_stream(stream);
   const int64_t n = n_words > 0 ? n_words : 1;
   DedupWs ws;
-  ws.cap = dedup_cap(n);
+  ws.cap = 1024;   // the largest power of two the workspace holds
+  while ((ws.cap * 2) * 12 + dedup_fixed_bytes(n_words) <= ws_bytes) ws.cap *= 2;
   char* p = static_cast<char*>(workspace);
   ws.keys = reinterpret_cast<unsigned long long*>(p);  p += ws.cap * 8;
   ws.cnt = reinterpret_cast<uint32_t*>(p);              p += ws.cap * 4;
@@ -822,7 +804,7 @@ extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart
   ws.slot = reinterpret_cast<uint32_t*>(p);             p += n * 4;
   ws.nu = reinterpret_cast<unsigned long long*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
   BEAST_HIP(hipMemsetAsync(workspace, 0, ws.cap * 12, s), "dedup memset");
-  BEAST_HIP(hipMemsetAsync(ws.nu, 0, 8, s), "dedup memset");
+  BEAST_HIP(hipMemsetAsync(ws.nu, 0, 16, s), "dedup memset");
   if (n_words > 0) {
     hipLaunchKernelGGL(k_dedup_insert, dim3(grid_for(n_words, 256, 16384)), dim3(256), 0, s, sym, wstart, wlen,
                        n_words, ws);

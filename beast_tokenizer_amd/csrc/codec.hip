@@ -117,6 +117,11 @@ __device__ __forceinline__ void st16(void* p, u32x4_t v) {
   }
 }
 template <int SP>
+__device__ __forceinline__ void st4(float* p, float v) {
+  if constexpr (SP == 2) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else *p = v;
+}
+template <int SP>
 __device__ __forceinline__ void st16(void* p, float4 v) {
   st16<SP>(p, u32x4_t{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)});
 }
@@ -1049,10 +1054,22 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
                                                           0, 0);
         // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
         if (ok) {
+#ifdef BEAST_REC_DIRECT
+          // (measurement variant) every lane stores its accumulators straight to HBM
+          float* gp = a.pos_out + (b0 + j) * (int64_t)Tout * ndo + min(max(dst[d], 0), ndo - 1);
+#pragma unroll
+          for (int i = 0; i < RT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int t = i * 16 + lk * 4 + r;
+              if (t < Tout && (a.phases & 4)) st4<(S::W == 7) ? LAT_SP : 0>(gp + t * ndo, acc[i][r]);
+            }
+#else
 #pragma unroll
           for (int i = 0; i < RT; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) oc[(i * 16 + r) * ndo] = acc[i][r];
+#endif
         }
       } else {
         const float* Ph = phi + (kind * RTR + lr) * Np4 + lk * KS;
@@ -1080,9 +1097,17 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
       }
     }
     if (tile == blockIdx.x) STAMP(1, 5);
+#ifdef BEAST_REC_DIRECT
+    if constexpr (RT > 0) {
+      if (tile + gridDim.x < a.ntiles) __syncthreads();   // the next tile's DMA overwrites the tokens
+    } else {
+#endif
     __syncthreads();
     if (tile == blockIdx.x) STAMP(1, 6);
     if (a.phases & 4) rec_store<S>(a, a.pos_out + b0 * (int64_t)Tout * ndo, ob, nb, RTR);
+#ifdef BEAST_REC_DIRECT
+    }
+#endif
     if (tile == blockIdx.x) STAMP(1, 7);
   }
 #ifdef BEAST_STAMPS

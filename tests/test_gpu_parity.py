@@ -571,6 +571,38 @@ def test_bpe_pretok_ragged_rows_match_oracle(gpu_device):
     assert ws[0] == 0 and np.all(ws[1: w["n_words"]] == (ws + wl)[: w["n_words"] - 1])
 
 
+def test_bpe_dedup_table_overflow_retries(gpu_device):
+    """Round 4 sizes the dedup table for a quarter of the word occurrences.  A corpus whose words
+    are nearly all distinct overflows it: the kernel flags it (*out_n = -1) and GpuBpeOps.dedup
+    retries with a 4x table -- the distinct words x counts stay a Counter's."""
+    from collections import Counter
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, fixed_rows_to_device
+    from beast_tokenizer_amd.pretok import class_lut
+    rng = np.random.default_rng(12)
+    # rows of distinct 3-letter words separated by a space: almost every occurrence is new
+    letters = np.r_[65:91, 97:123]
+    R, W = 4000, 12
+    arr = np.full((R, W * 4), 32, dtype=np.int64)
+    for k in range(3):
+        arr[:, k::4] = letters[rng.integers(0, len(letters), size=(R, W))]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr).to(gpu_device))
+    present = np.zeros(128, dtype=bool)
+    present[np.unique(arr)] = True
+    _, _, byte2id = build_alphabet(present, [chr(i) for i in range(128)], [])
+    ops = GpuBpeOps(gpu_device)
+    w = ops.pretokenize(flat, off, 0, class_lut(128), byte2id)
+
+    def words_of(d):
+        sym = d["sym"].cpu().numpy().view(np.uint16)
+        ws, wl = d["wstart"].cpu().numpy(), d["wlen"].cpu().numpy()
+        return [tuple(sym[a:a + n]) for a, n in zip(ws[: d["n_words"]], wl[: d["n_words"]])]
+    want = Counter(x for x in words_of(w) if len(x) >= 2)
+    assert len(want) > w["n_words"] // 4          # more distinct words than the first table holds
+    u = ops.dedup(w)
+    got = dict(zip(words_of(u), u["wcount"].cpu().numpy()[: u["n_words"]].tolist()))
+    assert got == dict(want)
+
+
 def test_bpe_dedup_and_compact_match_counter(gpu_device):
     """Distinct words x counts equal a Counter over the pre-tokenised words (>= 2 symbols);
     compaction keeps exactly the words that can still merge."""

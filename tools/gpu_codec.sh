@@ -12,7 +12,7 @@ python - <<'PY'
 import json
 l = json.loads(open("gpurun_out/bench_codec.json").read().strip().splitlines()[-1])
 r = l["roofline"]
-print("value %.1fM  ms/step %.4f  enc %.2f us  rec %.2f us  large enc %.1f rec %.1f" % (l["value"] / 1e6, l["ms_per_step"], r["k_encode_us"], r["k_reconstruct_us"], r["large_batch"]["k_encode_us"], r["large_batch"]["k_reconstruct_us"]))
+print("value %.1fM  ms/step %.4f  enc %.2f us  rec %.2f us  large enc %.1f rec %.1f" % (l["value"] / 1e6, l["ms_per_step"], r["events"]["k_encode_pipe_us"], r["events"]["k_reconstruct_us"], r["large_batch"]["k_encode_us"], r["large_batch"]["k_reconstruct_us"]))
 d = json.load(open("gpurun_out/stamps_codec.json"))
 for B, res in d.items():
     for k, v in res.items():
