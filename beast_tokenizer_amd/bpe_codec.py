@@ -254,19 +254,23 @@ class GpuBpeModel:
         if R == 0:
             return ids[:0], st[0, :0], st[1, :0]
         lib = _lib.load()
-        log2 = int(lib.beast_bpe_encode_dedup_table_log2(R, int(max_row)))
+        # record indices are 24-bit: chunks of rows whose code-point bound stays below 2^24
+        chunk = max(1, min(R, ((1 << 24) - 1) // max(1, int(max_row))))
+        log2 = int(lib.beast_bpe_encode_dedup_table_log2(chunk, int(max_row)))
         if self._dw_table is None or self._dw_log2 < log2:   # zero-filled once; every call leaves it zero
             self._dw_log2 = log2
             self._dw_table = torch.zeros(1 << log2, dtype=torch.int64, device=dev)
-        need = int(lib.beast_bpe_encode_dedup_workspace_bytes(R, int(max_row), int(max_syms), self._dw_log2))
+        need = int(lib.beast_bpe_encode_dedup_workspace_bytes(chunk, int(max_row), int(max_syms), self._dw_log2))
         if self._dw_ws is None or self._dw_ws.numel() < need:
             self._dw_ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        _lib.run("beast_bpe_encode_rows_dedup", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
-                 -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
-                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
-                 int(max_row), int(max_syms), self._dw_table.data_ptr(), self._dw_log2, self._dw_ws.data_ptr(),
-                 self._dw_ws.numel(), ids.data_ptr(), ids.shape[1], st[0].data_ptr(), st[1].data_ptr(),
-                 _lib.stream_of(dev))
+        for a in range(0, R, chunk):
+            n = min(chunk, R - a)
+            _lib.run("beast_bpe_encode_rows_dedup", tok.data_ptr(), row_off[a:].data_ptr(), n, int(min_token),
+                     -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
+                     self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
+                     int(max_row), int(max_syms), self._dw_table.data_ptr(), self._dw_log2, self._dw_ws.data_ptr(),
+                     self._dw_ws.numel(), ids[a].data_ptr(), ids.shape[1], st[0, a:].data_ptr(),
+                     st[1, a:].data_ptr(), _lib.stream_of(dev))
         return ids[:R], st[0, :R], st[1, :R]
 
     def encode_to_lists(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,

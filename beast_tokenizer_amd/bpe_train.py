@@ -382,6 +382,30 @@ class GpuBpeOps:
         return [tuple(int(v) for v in r) for r in log], n >= max_merges
 
 
+def replay_log(id2str: List[str], str2id: Dict[str, int], log) -> Optional[List[Tuple[str, str]]]:
+    """Replay the device loop's merge log [(a, b, nid, reused)] against the real strings (id2str /
+    str2id extended in place): an id the device re-used must be the string's, a new one the next
+    id.  None at the first entry that disagrees (a 64-bit string-hash collision on the device).
+    The C++ host fast path does it when built (csrc/fastpath.cpp replay_merge_log)."""
+    arr = np.asarray(log, dtype=np.int32).reshape(-1, 4)
+    from .beast_bspline_tokenizer import _fastpath
+    fp = _fastpath()
+    if fp is not None and hasattr(fp, "replay_merge_log"):
+        return fp.replay_merge_log(id2str, str2id, torch.from_numpy(np.ascontiguousarray(arr)))
+    merges: List[Tuple[str, str]] = []
+    for a, b, nid, reused in arr.tolist():
+        new_tok = id2str[a] + id2str[b]
+        have = str2id.get(new_tok)
+        if (have is not None) != bool(reused) or (have is not None and have != nid) or \
+                (have is None and nid != len(id2str)):
+            return None
+        if have is None:
+            str2id[new_tok] = nid
+            id2str.append(new_tok)
+        merges.append((id2str[a], id2str[b]))
+    return merges
+
+
 def build_alphabet(present: np.ndarray, initial_alphabet: Sequence[str], special_tokens: Sequence[str]):
     """HF BpeTrainer: special tokens first, then compute_alphabet sorted by code point."""
     b2u = bytes_to_unicode()
@@ -477,17 +501,11 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
         # merges decided on the GPU; the host replays the log against the real strings
         log, full = ops.loop_run(words, table, Vt, id2str, vocab_size, min_frequency, max_len,
                                  reduce=loop_reduce if sharded else None, count_applications=count_applications)
-        for a, b, nid, reused in log:
-            new_tok = id2str[a] + id2str[b]
-            have = str2id.get(new_tok)
-            if (have is not None) != bool(reused) or (have is not None and have != nid) or \
-                    (have is None and nid != len(id2str)):
-                full = True     # a 64-bit string-hash collision: redo on the host-driven loop
-                break
-            if have is None:
-                str2id[new_tok] = nid
-                id2str.append(new_tok)
-            merges.append((id2str[a], id2str[b]))
+        replayed = replay_log(id2str, str2id, log)
+        if replayed is None:
+            full = True     # a 64-bit string-hash collision: redo on the host-driven loop
+        else:
+            merges = replayed
         if full:
             return train_bpe(tokens, seq_off, vocab_size, min_frequency=min_frequency, special_tokens=special_tokens,
                              max_token_length=max_token_length, initial_alphabet=initial_alphabet, ops=None,

@@ -734,19 +734,20 @@ constexpr int ST_FALLBACK = 7;     // the row needs k_bpe_encode
 constexpr int DW_WAVES = 16;       // rows per k_dw_words workgroup (at most)
 constexpr uint32_t SYM_NONE = 0xFFFFu;
 
-struct DwWs {                      // the caller's scratch, carved by dw_layout
-  uint32_t* slot2idx;              // [cap] record of a slot: tier << 31 | record index
+struct DwWs {                      // the caller's scratch, carved by dw_carve_host
+  uint32_t* slot2idx;              // [cap] record of a slot: k_dw_words: tier << 31 | index;
+                                   //   k_dw_merge: tier << 31 | ids << 24 | index (ids <= 64)
   unsigned long long* occ;         // [R][Lc] slot | cstart << 32 | clen << 48
   int32_t* nwords;                 // [R]
   int32_t* cnt;                    // [regions][2] short / mid records of each region
   uint32_t* rs_slot;               // short records [regions * capS]
-  uint2* rs_meta;                  //   (row, cstart | clen << 16)
-  int32_t* rs_n;                   //   byte symbols, then ids after k_dw_merge
+  int32_t* rs_n;                   //   byte symbols (<= 16)
   uint16_t* rs_sym;                //   [16] byte symbols, then ids
+  int32_t* rs_cps;                 //   [16] code points (-1 past the word: k_dw_emit's content check)
   uint32_t* rm_slot;               // mid records [regions * capM]
-  uint2* rm_meta;
   int32_t* rm_n;
   uint16_t* rm_sym;                //   [64]
+  int32_t* rm_cps;                 //   [64]
   unsigned long long* table;       // [1 << log2cap] word keys, 0 = empty (the caller's, kept empty)
   int log2cap, capS, capM, regions, nwv, Lc, S;
   int key_shift;                   // 64 - BEAST_OPT_BPE_DEDUP_KEY_BITS
@@ -826,8 +827,8 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
     if (n > a.Lc) st = ST_TOO_LONG;
     // 1. code points, range checks (reference :181-192 order), classes
     int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
-    for (int i = lane; st == ST_OK && i < n; i += 64) {
-      const long long v = a.tok[r0 + i] - a.min_tok;
+    auto code_point = [&](int i, long long t) {
+      const long long v = t - a.min_tok;
       below |= v < 0;
       above |= (a.max_span >= 0 && v > a.max_span);
       notuni |= v > 0x10FFFF;
@@ -836,6 +837,16 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
       const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
       L.cps[i] = cp;
       L.cls[i] = cp < 256 ? s_lut[cp] : (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
+    };
+    if (st == ST_OK) {   // the first 256 code points' loads all in flight together
+      constexpr int PF = 4;
+      long long tv[PF];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) tv[k] = lane + 64 * k < n ? a.tok[r0 + lane + 64 * k] : 0;
+#pragma unroll
+      for (int k = 0; k < PF; ++k)
+        if (lane + 64 * k < n) code_point(lane + 64 * k, tv[k]);
+      for (int i = lane + 64 * PF; i < n; i += 64) code_point(i, a.tok[r0 + i]);
     }
     if (st == ST_OK) {
       if (__any(below)) st = ST_BELOW_MIN;
@@ -885,10 +896,16 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
         for (int i = cs; i < ce; ++i) h = (h ^ (unsigned long long)(uint32_t)L.cps[i]) * 0x100000001B3ull;
         const unsigned long long key = (dw_mix(h) >> w.key_shift) | 1ull;
         unsigned long long slot = (key * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
+        // a plain (L2-served) read first: the common words occur thousands of times in a batch and
+        // a CAS on one address serialises at the memory side (round 4: 98 us of a 132 us launch
+        // when every occurrence CASed); a stale empty read only costs one CAS that returns the key
         bool win = false;
         while (true) {
-          const unsigned long long prev = atomicCAS(&w.table[slot], 0ull, key);
-          if (prev == 0ull) { win = true; break; }
+          unsigned long long prev = __hip_atomic_load(&w.table[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (prev == 0ull) {
+            prev = atomicCAS(&w.table[slot], 0ull, key);
+            if (prev == 0ull) { win = true; break; }
+          }
           if (prev == key) break;
           slot = (slot + 1) & tmask;
         }
@@ -915,24 +932,21 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
     const bool mid = i >= ns;
     const uint4 rec = mid ? stM[i - ns] : stS[i];
     const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
-    const uint16_t* src = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S).c + bs;
-    if (!mid) {
-      const int64_t idx = (int64_t)blockIdx.x * w.capS + i;
-      w.rs_slot[idx] = rec.x;
-      w.rs_meta[idx] = make_uint2(rec.y, rec.z);
-      w.rs_n[idx] = blen;
-      uint16_t* d = w.rs_sym + idx * DW_SHORT;
-      for (int q = 0; q < DW_SHORT; ++q) d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
-      w.slot2idx[rec.x] = (uint32_t)idx;
-    } else {
-      const int64_t idx = (int64_t)blockIdx.x * w.capM + (i - ns);
-      w.rm_slot[idx] = rec.x;
-      w.rm_meta[idx] = make_uint2(rec.y, rec.z);
-      w.rm_n[idx] = blen;
-      uint16_t* d = w.rm_sym + idx * DW_MID;
-      for (int q = 0; q < DW_MID; ++q) d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
-      w.slot2idx[rec.x] = 0x80000000u | (uint32_t)idx;
+    const int cs = rec.z & 0xFFFF, cl = rec.z >> 16;
+    const DwRow Rw = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S);
+    const uint16_t* src = Rw.c + bs;
+    const int32_t* cps = Rw.cps + cs;
+    const int cap = mid ? DW_MID : DW_SHORT;
+    const int64_t idx = mid ? (int64_t)blockIdx.x * w.capM + (i - ns) : (int64_t)blockIdx.x * w.capS + i;
+    uint16_t* d = (mid ? w.rm_sym : w.rs_sym) + idx * cap;
+    int32_t* dc = (mid ? w.rm_cps : w.rs_cps) + idx * cap;
+    (mid ? w.rm_slot : w.rs_slot)[idx] = rec.x;
+    (mid ? w.rm_n : w.rs_n)[idx] = blen;
+    for (int q = 0; q < cap; ++q) {
+      d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
+      dc[q] = q < cl ? cps[q] : -1;
     }
+    w.slot2idx[rec.x] = (mid ? 0x80000000u : 0u) | (uint32_t)idx;
   }
 #ifdef BPE_STAMPS
   __syncthreads();
@@ -1038,70 +1052,98 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
   const int ns = w.cnt[2 * blockIdx.x], nm = w.cnt[2 * blockIdx.x + 1];
   if constexpr (MAP_LDS) __syncthreads();
   const int tasks = nm + (ns + 3) / 4;   // the mid words first: their rounds are the longest chains
-  for (int t = wave; t < tasks; t += nwv) {
+  // a task's inputs (its words' byte symbols and lengths) are loaded one task ahead, without a
+  // dependence between them: entries past a region's count are never used
+  struct Task { int blen; uint32_t raw; };
+  auto load = [&](int t) -> Task {
+    Task k{0, SYM_NONE};
+    if (t >= tasks) return k;
     if (t < nm) {
       const int64_t idx = (int64_t)blockIdx.x * w.capM + t;
-      uint16_t* sp = w.rm_sym + idx * DW_MID;
-      const int blen = w.rm_n[idx];
-      const uint32_t raw = lane < blen ? sp[lane] : SYM_NONE;
-      int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, blen, a.unk_id, a.fuse_unk, n)
-                                 : dw_merge_word<DW_MID>(a.map, raw, blen, a.unk_id, a.fuse_unk, n);
-      if (lane < n) sp[lane] = (uint16_t)v;
-      if (lane == 0) { w.rm_n[idx] = n; w.table[w.rm_slot[idx]] = 0ull; }
+      k.blen = w.rm_n[idx];
+      k.raw = w.rm_sym[idx * DW_MID + lane];
     } else {
-      const int k = 4 * (t - nm) + (lane >> 4), gl = lane & 15;
-      const bool valid = k < ns;
-      const int64_t idx = (int64_t)blockIdx.x * w.capS + (valid ? k : 0);
-      uint16_t* sp = w.rs_sym + idx * DW_SHORT;
-      const int blen = valid ? w.rs_n[idx] : 0;
-      const uint32_t raw = gl < blen ? sp[gl] : SYM_NONE;
-      int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n)
-                                 : dw_merge_word<DW_SHORT>(a.map, raw, blen, a.unk_id, a.fuse_unk, n);
-      if (valid && gl < n) sp[gl] = (uint16_t)v;
-      if (valid && gl == 0) { w.rs_n[idx] = n; w.table[w.rs_slot[idx]] = 0ull; }
+      const int kk = 4 * (t - nm) + (lane >> 4);
+      const int64_t idx = (int64_t)blockIdx.x * w.capS + (kk < ns ? kk : 0);
+      k.blen = kk < ns ? w.rs_n[idx] : 0;
+      k.raw = w.rs_sym[idx * DW_SHORT + (lane & 15)];
     }
+    return k;
+  };
+  Task cur = load(wave);
+  for (int t = wave; t < tasks; t += nwv) {
+    const Task nxt = load(t + nwv);
+    if (t < nm) {
+      const int64_t idx = (int64_t)blockIdx.x * w.capM + t;
+      const uint32_t raw = lane < cur.blen ? cur.raw : SYM_NONE;
+      int n;
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n)
+                                 : dw_merge_word<DW_MID>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n);
+      if (lane < n) w.rm_sym[idx * DW_MID + lane] = (uint16_t)v;
+      if (lane == 0) {
+        const uint32_t slot = w.rm_slot[idx];
+        w.slot2idx[slot] = 0x80000000u | ((uint32_t)n << 24) | (uint32_t)idx;
+        w.table[slot] = 0ull;
+      }
+    } else {
+      const int kk = 4 * (t - nm) + (lane >> 4), gl = lane & 15;
+      const bool valid = kk < ns;
+      const int64_t idx = (int64_t)blockIdx.x * w.capS + (valid ? kk : 0);
+      const uint32_t raw = gl < cur.blen ? cur.raw : SYM_NONE;
+      int n;
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n)
+                                 : dw_merge_word<DW_SHORT>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n);
+      if (valid && gl < n) w.rs_sym[idx * DW_SHORT + gl] = (uint16_t)v;
+      if (valid && gl == 0) {
+        const uint32_t slot = w.rs_slot[idx];
+        w.slot2idx[slot] = ((uint32_t)n << 24) | (uint32_t)idx;
+        w.table[slot] = 0ull;
+      }
+    }
+    cur = nxt;
   }
 }
 
-// k_dw_emit: one wave per row
+// k_dw_emit: one wave per row.  Three dependent round trips: the row's code points and its word
+// occurrences (together), the slots' records (ids count + index), the records' ids and code points.
 __global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
+  extern __shared__ __align__(16) char lds_raw[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int32_t* cp = reinterpret_cast<int32_t*>(lds_raw) + (size_t)wave * w.Lc;   // the row's code points
   for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
     if (a.status[r] != ST_OK) {
       if (lane == 0) a.out_len[r] = 0;
       continue;
     }
     const int nw = w.nwords[r];
-    const long long* tr = a.tok + a.row_off[r];
+    const int64_t r0 = a.row_off[r];
+    const int n = (int)(a.row_off[r + 1] - r0);
+    for (int i = lane; i < n; i += 64) cp[i] = (int32_t)(a.tok[r0 + i] - a.min_tok);
+    wave_sync();
     int32_t* out = a.out_ids + r * a.out_stride;
     int carry = 0;
     bool bad = false;
     for (int base = 0; base < nw; base += 64) {
       const int k = base + lane;
-      int n = 0;
-      const uint16_t* src = nullptr;
+      int cnt = 0, cs = 0, cl = 0;
+      const uint16_t* ids = nullptr;
+      const int32_t* wcp = nullptr;
       if (k < nw) {
         const unsigned long long o = w.occ[r * w.Lc + k];
-        const uint32_t slot = (uint32_t)o;
-        const int cs = (int)((o >> 32) & 0xFFFF), cl = (int)(o >> 48);
-        const uint32_t rec = w.slot2idx[slot];
+        cs = (int)((o >> 32) & 0xFFFF);
+        cl = (int)(o >> 48);
+        const uint32_t rec = w.slot2idx[(uint32_t)o];
         const bool mid = rec >> 31;
-        const int64_t li = rec & 0x7FFFFFFFu;
-        const uint2 meta = mid ? w.rm_meta[li] : w.rs_meta[li];
-        n = mid ? w.rm_n[li] : w.rs_n[li];
-        src = mid ? w.rm_sym + li * DW_MID : w.rs_sym + li * DW_SHORT;
-        const int wcs = (int)(meta.y & 0xFFFF), wcl = (int)(meta.y >> 16);
-        if ((int64_t)meta.x != r || wcs != cs) {   // another occurrence recorded the word: same code points?
-          if (wcl != cl) bad = true;
-          const long long* tw = a.tok + a.row_off[meta.x] + wcs;
-          for (int i = 0; i < cl && !bad; ++i) bad = tw[i] != tr[cs + i];
-        }
+        const int64_t li = rec & 0xFFFFFFu;
+        cnt = (int)((rec >> 24) & 0x7F);
+        ids = mid ? w.rm_sym + li * DW_MID : w.rs_sym + li * DW_SHORT;
+        wcp = mid ? w.rm_cps + li * DW_MID : w.rs_cps + li * DW_SHORT;
+        if (cl > (mid ? DW_MID : DW_SHORT) || (cl < (mid ? DW_MID : DW_SHORT) && wcp[cl] != -1)) bad = true;
+        for (int i = 0; i < cl && i < DW_MID; ++i) bad |= wcp[i] != cp[cs + i];   // the recorded word's code points
       }
       int tot;
-      const int off = carry + wave_excl_scan(n, lane, tot);
-      for (int i = 0; i < n; ++i) out[off + i] = (int32_t)src[i];
+      const int off = carry + wave_excl_scan(cnt, lane, tot);
+      for (int i = 0; i < cnt; ++i) out[off + i] = (int32_t)ids[i];
       carry += tot;
     }
     const bool coll = __any(bad);
@@ -1109,6 +1151,7 @@ __global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
       a.out_len[r] = coll ? 0 : carry;
       if (coll) a.status[r] = ST_FALLBACK;
     }
+    wave_sync();   // cp is reused by the wave's next row
   }
 }
 
@@ -1449,13 +1492,13 @@ static size_t dw_carve_host(DwWs& w, char* base, int64_t R, int Lc, int S, int l
   w.nwords = (int32_t*)take(sizeof(int32_t) * (size_t)R);
   w.cnt = (int32_t*)take(sizeof(int32_t) * 2 * (size_t)w.regions);
   w.rs_slot = (uint32_t*)take(sizeof(uint32_t) * nS);
-  w.rs_meta = (uint2*)take(sizeof(uint2) * nS);
   w.rs_n = (int32_t*)take(sizeof(int32_t) * nS);
   w.rs_sym = (uint16_t*)take(sizeof(uint16_t) * DW_SHORT * nS);
+  w.rs_cps = (int32_t*)take(sizeof(int32_t) * DW_SHORT * nS);
   w.rm_slot = (uint32_t*)take(sizeof(uint32_t) * nM);
-  w.rm_meta = (uint2*)take(sizeof(uint2) * nM);
   w.rm_n = (int32_t*)take(sizeof(int32_t) * nM);
   w.rm_sym = (uint16_t*)take(sizeof(uint16_t) * DW_MID * nM);
+  w.rm_cps = (int32_t*)take(sizeof(int32_t) * DW_MID * nM);
   return o;
 }
 
@@ -1490,6 +1533,8 @@ extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* ro
   BEAST_REQUIRE(table_log2 >= beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps) && table_log2 <= 31,
                 "table_log2 %d below beast_bpe_encode_dedup_table_log2 (%d)", table_log2,
                 beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps));
+  BEAST_REQUIRE_CODE(n_rows * (int64_t)std::max(1, max_row_cps) < (int64_t(1) << 24), BEAST_E_UNSUPPORTED,
+                     "n_rows x max_row_cps must stay below 2^24 (record indices); encode in chunks");
   BEAST_REQUIRE_CODE(dw_nwv(max_row_cps, max_row_syms) > 0, BEAST_E_UNSUPPORTED,
                      "rows of %d code points exceed k_dw_words' LDS budget", max_row_cps);
   DwWs w;
@@ -1525,7 +1570,8 @@ extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* ro
     hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions), dim3(64 * DW_WAVES), 0, s, a, w);
   }
   BEAST_LAUNCHED("k_dw_merge");
-  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), 0, s, a, w);
+  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), sizeof(int32_t) * WAVES * (size_t)std::max(1, w.Lc),
+                     s, a, w);
   BEAST_LAUNCHED("k_dw_emit");
   return BEAST_OK;
 }

@@ -192,22 +192,33 @@ __global__ __launch_bounds__(64 * PT_WAVES) void k_pretok_wave(
     const uint16_t* __restrict__ byte2id, uint16_t* __restrict__ sym, uint32_t* __restrict__ wstart,
     uint32_t* __restrict__ wlen) {
   __shared__ PtLds lds[PT_WAVES];
+  __shared__ uint8_t s_lut[256];   // classes of code points < 256 (every BEAST bin of a 256 vocab)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lut[i] = i < lut_n ? lut[i] : (uint8_t)CLS_OTHER;
+  __syncthreads();
   PtLds& L = lds[wv];
+  constexpr int PF = PT_LC / 64;
   for (int64_t sidx = (int64_t)blockIdx.x * PT_WAVES + wv; sidx < n_seq; sidx += (int64_t)gridDim.x * PT_WAVES) {
     const int64_t r0 = seq_off[sidx], n64 = seq_off[sidx + 1] - r0;
     bool serial = n64 > PT_LC;
     const int n = serial ? 0 : (int)n64;
-    // 1. code points and classes (coalesced), then the UTF-8 symbol offsets
+    // 1. code points and classes, then the UTF-8 symbol offsets.  Every load of the row is issued
+    //    before the first is used (round 3 waited for each 64-code-point chunk, then for its class
+    //    from the global LUT: two dependent round trips per chunk)
+    long long tv[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) tv[k] = (lane + 64 * k < n) ? tok[r0 + lane + 64 * k] : 0;
     int carry = 0;
-    for (int base = 0; base < n; base += 64) {
-      const int i = base + lane;
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      if (64 * k >= n) break;
+      const int i = 64 * k + lane;
       int len = 0;
       if (i < n) {
-        const long long c = tok[r0 + i] - mn;
+        const long long c = tv[k] - mn;
         serial |= (c < 0) | (c > 0x7FFFFFFFLL);
         L.cp[i] = (int32_t)c;
-        L.cls[i] = (c >= 0 && c < lut_n) ? lut[c] : (uint8_t)CLS_OTHER;
+        L.cls[i] = (c >= 0 && c < 256) ? s_lut[c] : (c >= 0 && c < lut_n) ? lut[c] : (uint8_t)CLS_OTHER;
         len = utf8_len(c);
       }
       int x = len;

@@ -308,6 +308,52 @@ PyMethodDef g_fast_defs[] = {
 
 }  // namespace
 
+
+// The BPE trainer's log replay (bpe_train.train_bpe): for each logged merge (a, b, nid, reused) of
+// the device loop, the new token's string id2str[a] + id2str[b] against the vocabulary -- an id the
+// device re-used must be the string's, a new one must be the next id -- then the merge as a pair of
+// strings.  id2str (list) and str2id (dict) are extended in place.  Returns the merges, or None at
+// the first entry that disagrees (a 64-bit string-hash collision on the device: the caller reruns
+// on the host-driven loop).  The same checks as the Python loop, ~10x faster (1,724 merges: the
+// Python loop took ~2 ms of the K5 merge loop's wall time).
+py::object replay_merge_log(py::list id2str, py::dict str2id, const at::Tensor& log) {
+  if (log.is_cuda() || log.scalar_type() != at::kInt || log.dim() != 2 || (log.numel() && log.size(1) != 4) ||
+      !log.is_contiguous())
+    throw std::invalid_argument("replay_merge_log: host int32 log [n, 4] expected");
+  const int64_t n = log.numel() ? log.size(0) : 0;
+  const int32_t* L = log.data_ptr<int32_t>();
+  PyObject* ids = id2str.ptr();
+  PyObject* s2i = str2id.ptr();
+  PyObject* merges = PyList_New(n);
+  if (!merges) throw py::error_already_set();
+  for (int64_t k = 0; k < n; ++k) {
+    const int32_t a = L[4 * k], b = L[4 * k + 1], nid = L[4 * k + 2], reused = L[4 * k + 3];
+    const Py_ssize_t nt = PyList_GET_SIZE(ids);
+    if (a < 0 || b < 0 || a >= nt || b >= nt) { Py_DECREF(merges); return py::none(); }
+    PyObject* sa = PyList_GET_ITEM(ids, a);   // borrowed
+    PyObject* sb = PyList_GET_ITEM(ids, b);
+    PyObject* tok = PyUnicode_Concat(sa, sb);
+    if (!tok) { Py_DECREF(merges); throw py::error_already_set(); }
+    PyObject* have = PyDict_GetItemWithError(s2i, tok);   // borrowed
+    if (!have && PyErr_Occurred()) { Py_DECREF(tok); Py_DECREF(merges); throw py::error_already_set(); }
+    const bool ok = have ? (reused && PyLong_AsLong(have) == nid) : (!reused && nid == nt);
+    if (!ok) { Py_DECREF(tok); Py_DECREF(merges); return py::none(); }
+    if (!have) {
+      PyObject* id = PyLong_FromLong(nid);
+      if (!id || PyDict_SetItem(s2i, tok, id) < 0 || PyList_Append(ids, tok) < 0) {
+        Py_XDECREF(id); Py_DECREF(tok); Py_DECREF(merges);
+        throw py::error_already_set();
+      }
+      Py_DECREF(id);
+    }
+    Py_DECREF(tok);
+    PyObject* pair = PyTuple_Pack(2, sa, sb);
+    if (!pair) { Py_DECREF(merges); throw py::error_already_set(); }
+    PyList_SET_ITEM(merges, k, pair);
+  }
+  return py::reinterpret_steal<py::list>(merges);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "host fast path of the BEAST encode / reconstruct calls (see csrc/fastpath.cpp)";
   py::class_<Plan>(m, "Plan")
@@ -325,4 +371,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.add_object(def.ml_name, py::reinterpret_steal<py::object>(f));
   }
   m.def("rows_to_lists", &rows_to_lists, py::arg("ids"), py::arg("lens"));
+  m.def("replay_merge_log", &replay_merge_log, py::arg("id2str"), py::arg("str2id"), py::arg("log"));
 }

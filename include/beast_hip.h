@@ -365,7 +365,8 @@ int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_
  * beast_bpe_encode_rows.  table: 2^table_log2 uint64 word keys, table_log2 >=
  * beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps), zero-filled before its first use; every
  * call leaves it zero again (reuse it across calls, not across concurrent streams).  ws: scratch
- * of beast_bpe_encode_dedup_workspace_bytes bytes (no initialisation). */
+ * of beast_bpe_encode_dedup_workspace_bytes bytes (no initialisation).  n_rows * max_row_cps < 2^24 (larger
+ * batches: call per chunk of rows). */
 int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps);
 size_t beast_bpe_encode_dedup_workspace_bytes(int64_t n_rows, int max_row_cps, int max_row_syms, int table_log2);
 int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,

@@ -269,3 +269,50 @@ def test_rank_monotone_check():
     assert not rank_monotone([(5, 0, 6), (0, 0, 5)])                    # (aa, a) before (a, a)
     assert not rank_monotone([(0, 1, 5), (5, 0, 6), (2, 3, 5)])         # id 5 also made after its use
     assert rank_monotone([(0, 1, 5), (0, 1, 5), (5, 0, 6)])
+
+
+def test_replay_merge_log_cpp_matches_python():
+    """The trainer's log replay (bpe_train.replay_log): the C++ fast path (csrc/fastpath.cpp
+    replay_merge_log) and the Python loop give the same merges and vocabulary, and both refuse a
+    log whose ids disagree with the strings (a device string-hash collision)."""
+    import numpy as np
+    from beast_tokenizer_amd import bpe_train
+    from beast_tokenizer_amd.beast_bspline_tokenizer import _fastpath
+    base = [chr(c) for c in range(97, 103)] + ["Ā", "ÿ"]          # a..f + two 2-byte chars
+
+    def fresh():
+        ids = list(base)
+        return ids, {s: i for i, s in enumerate(ids)}
+    n0 = len(base)
+    # new tokens ab, abc, Āÿ, dd, dddd, then a merge whose string exists: "a" + "b" re-uses "ab"
+    good = [(0, 1, n0, 0), (n0, 2, n0 + 1, 0), (6, 7, n0 + 2, 0), (3, 3, n0 + 3, 0),
+            (n0 + 3, n0 + 3, n0 + 4, 0), (0, 1, n0, 1)]
+    fp = _fastpath()
+    if fp is None:
+        pytest.skip("host fast path not built (python -m beast_tokenizer_amd._build)")
+    results = []
+    for use_cpp in (True, False):
+        ids, s2i = fresh()
+        if use_cpp:
+            m = fp.replay_merge_log(ids, s2i, torch.tensor(good, dtype=torch.int32))
+        else:
+            import beast_tokenizer_amd.beast_bspline_tokenizer as bt
+            saved, bt._FAST = bt._FAST, False
+            try:
+                m = bpe_train.replay_log(ids, s2i, good)
+            finally:
+                bt._FAST = saved
+        results.append((m, ids, dict(s2i)))
+        assert m[0] == ("a", "b") and ids[n0] == "ab" and ids[n0 + 1] == "abc" and ids[n0 + 2] == "Āÿ"
+        assert m[-1] == ("a", "b") and len(ids) == n0 + 5
+        for bad in ([(0, 1, n0 + 1, 0)], [(0, 1, n0, 1)], [(0, 1, n0, 0), (0, 1, n0 + 1, 0)]):
+            i2, s2 = fresh()
+            if use_cpp:
+                assert fp.replay_merge_log(i2, s2, torch.tensor(bad, dtype=torch.int32)) is None
+            else:
+                saved, bt._FAST = bt._FAST, False
+                try:
+                    assert bpe_train.replay_log(i2, s2, bad) is None
+                finally:
+                    bt._FAST = saved
+    assert results[0] == results[1]
