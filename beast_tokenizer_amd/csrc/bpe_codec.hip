@@ -890,31 +890,48 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
     BPE_STAMP(4);
     if (st == ST_OK) {
       const unsigned long long tmask = (1ull << w.log2cap) - 1ull;
-      for (int k = lane; k < nw; k += 64) {
-        const int cs = L.wcp[k], ce = L.wcp[k + 1], bs = L.symoff[cs], blen = L.symoff[ce] - bs;
-        unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce - cs);
-        for (int i = cs; i < ce; ++i) h = (h ^ (unsigned long long)(uint32_t)L.cps[i]) * 0x100000001B3ull;
-        const unsigned long long key = (dw_mix(h) >> w.key_shift) | 1ull;
-        unsigned long long slot = (key * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
-        // a plain (L2-served) read first: the common words occur thousands of times in a batch and
-        // a CAS on one address serialises at the memory side (round 4: 98 us of a 132 us launch
-        // when every occurrence CASed); a stale empty read only costs one CAS that returns the key
-        bool win = false;
-        while (true) {
-          unsigned long long prev = __hip_atomic_load(&w.table[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (prev == 0ull) {
-            prev = atomicCAS(&w.table[slot], 0ull, key);
-            if (prev == 0ull) { win = true; break; }
-          }
-          if (prev == key) break;
-          slot = (slot + 1) & tmask;
+      // two words per lane per step, their first table reads in flight together
+      for (int k0 = lane; k0 < nw; k0 += 128) {
+        int kk[2], cs[2], ce[2], bs[2], blen[2];
+        unsigned long long key[2], slot[2], prev[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          kk[u] = k0 + 64 * u;
+          const bool ok = kk[u] < nw;
+          cs[u] = ok ? L.wcp[kk[u]] : 0;
+          ce[u] = ok ? L.wcp[kk[u] + 1] : 0;
+          bs[u] = L.symoff[cs[u]];
+          blen[u] = L.symoff[ce[u]] - bs[u];
+          unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce[u] - cs[u]);
+          for (int i = cs[u]; i < ce[u]; ++i) h = (h ^ (unsigned long long)(uint32_t)L.cps[i]) * 0x100000001B3ull;
+          key[u] = (dw_mix(h) >> w.key_shift) | 1ull;
+          slot[u] = (key[u] * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
+          // a plain (L2-served) read first: the common words occur thousands of times in a batch and
+          // a CAS on one address serialises at the memory side (round 4: 98 us of a 132 us launch
+          // when every occurrence CASed); a stale empty read only costs one CAS that returns the key
+          prev[u] = ok ? __hip_atomic_load(&w.table[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
         }
-        w.occ[r * w.Lc + k] = slot | ((unsigned long long)cs << 32) | ((unsigned long long)(ce - cs) << 48);
-        if (win) {
-          const uint4 rec = make_uint4((uint32_t)slot, (uint32_t)r, (uint32_t)cs | ((uint32_t)(ce - cs) << 16),
-                                       ((uint32_t)wave << 24) | ((uint32_t)blen << 16) | (uint32_t)bs);
-          if (blen <= DW_SHORT) stS[atomicAdd(&s_ns, 1)] = rec;
-          else stM[atomicAdd(&s_nm, 1)] = rec;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (kk[u] >= nw) continue;
+          bool win = false;
+          unsigned long long pv = prev[u], sl = slot[u];
+          while (true) {
+            if (pv == 0ull) {
+              pv = atomicCAS(&w.table[sl], 0ull, key[u]);
+              if (pv == 0ull) { win = true; break; }
+            }
+            if (pv == key[u]) break;
+            sl = (sl + 1) & tmask;
+            pv = __hip_atomic_load(&w.table[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          w.occ[r * w.Lc + kk[u]] = sl | ((unsigned long long)cs[u] << 32) | ((unsigned long long)(ce[u] - cs[u]) << 48);
+          if (win) {
+            const uint4 rec = make_uint4((uint32_t)sl, (uint32_t)r, (uint32_t)cs[u] | ((uint32_t)(ce[u] - cs[u]) << 16),
+                                         ((uint32_t)wave << 24) | ((uint32_t)blen[u] << 16) | (uint32_t)bs[u]);
+            if (blen[u] <= DW_SHORT) stS[atomicAdd(&s_ns, 1)] = rec;
+            else stM[atomicAdd(&s_nm, 1)] = rec;
+          }
         }
       }
     }
@@ -928,25 +945,36 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
   // flush this region's records (byte symbols from the rows still in LDS)
   const int ns = s_ns, nm = s_nm;
   if (threadIdx.x == 0) { w.cnt[2 * blockIdx.x] = ns; w.cnt[2 * blockIdx.x + 1] = nm; }
-  for (int i = threadIdx.x; i < ns + nm; i += blockDim.x) {
-    const bool mid = i >= ns;
-    const uint4 rec = mid ? stM[i - ns] : stS[i];
+  // 16 lanes per short record and 64 per mid one (one lane per symbol / code point): coalesced
+  // stores instead of one thread writing a record's 32 scattered elements
+  const int lq = threadIdx.x & 15;
+  for (int i = threadIdx.x >> 4; i < ns; i += blockDim.x >> 4) {
+    const uint4 rec = stS[i];
     const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
     const int cs = rec.z & 0xFFFF, cl = rec.z >> 16;
     const DwRow Rw = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S);
-    const uint16_t* src = Rw.c + bs;
-    const int32_t* cps = Rw.cps + cs;
-    const int cap = mid ? DW_MID : DW_SHORT;
-    const int64_t idx = mid ? (int64_t)blockIdx.x * w.capM + (i - ns) : (int64_t)blockIdx.x * w.capS + i;
-    uint16_t* d = (mid ? w.rm_sym : w.rs_sym) + idx * cap;
-    int32_t* dc = (mid ? w.rm_cps : w.rs_cps) + idx * cap;
-    (mid ? w.rm_slot : w.rs_slot)[idx] = rec.x;
-    (mid ? w.rm_n : w.rs_n)[idx] = blen;
-    for (int q = 0; q < cap; ++q) {
-      d[q] = q < blen ? src[q] : (uint16_t)SYM_NONE;
-      dc[q] = q < cl ? cps[q] : -1;
+    const int64_t idx = (int64_t)blockIdx.x * w.capS + i;
+    w.rs_sym[idx * DW_SHORT + lq] = lq < blen ? Rw.c[bs + lq] : (uint16_t)SYM_NONE;
+    w.rs_cps[idx * DW_SHORT + lq] = lq < cl ? Rw.cps[cs + lq] : -1;
+    if (lq == 0) {
+      w.rs_slot[idx] = rec.x;
+      w.rs_n[idx] = blen;
+      w.slot2idx[rec.x] = (uint32_t)idx;
     }
-    w.slot2idx[rec.x] = (mid ? 0x80000000u : 0u) | (uint32_t)idx;
+  }
+  for (int i = wave; i < nm; i += nwv) {
+    const uint4 rec = stM[i];
+    const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
+    const int cs = rec.z & 0xFFFF, cl = rec.z >> 16;
+    const DwRow Rw = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S);
+    const int64_t idx = (int64_t)blockIdx.x * w.capM + i;
+    w.rm_sym[idx * DW_MID + lane] = lane < blen ? Rw.c[bs + lane] : (uint16_t)SYM_NONE;
+    w.rm_cps[idx * DW_MID + lane] = lane < cl ? Rw.cps[cs + lane] : -1;
+    if (lane == 0) {
+      w.rm_slot[idx] = rec.x;
+      w.rm_n[idx] = blen;
+      w.slot2idx[rec.x] = 0x80000000u | (uint32_t)idx;
+    }
   }
 #ifdef BPE_STAMPS
   __syncthreads();
@@ -1105,11 +1133,20 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
 }
 
 // k_dw_emit: one wave per row.  Three dependent round trips: the row's code points and its word
-// occurrences (together), the slots' records (ids count + index), the records' ids and code points.
+// occurrences (together), the slots' records (ids count + index), the records' ids and code points
+// (wide loads of the whole record, compared and copied from registers: a per-element loop would
+// make the lane with the longest word a chain of dependent loads).
+__device__ __forceinline__ uint32_t u16_of(const uint4& a, const uint4& b, int q) {
+  const uint4& v = q < 8 ? a : b;
+  const int e = q & 7;
+  const uint32_t wd = (e >> 1) == 0 ? v.x : (e >> 1) == 1 ? v.y : (e >> 1) == 2 ? v.z : v.w;
+  return (e & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+}
+
 __global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
   extern __shared__ __align__(16) char lds_raw[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t* cp = reinterpret_cast<int32_t*>(lds_raw) + (size_t)wave * w.Lc;   // the row's code points
+  int32_t* cp = reinterpret_cast<int32_t*>(lds_raw) + (size_t)wave * (w.Lc + DW_MID);   // the row's code points
   for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
     if (a.status[r] != ST_OK) {
       if (lane == 0) a.out_len[r] = 0;
@@ -1118,32 +1155,62 @@ __global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
     const int nw = w.nwords[r];
     const int64_t r0 = a.row_off[r];
     const int n = (int)(a.row_off[r + 1] - r0);
-    for (int i = lane; i < n; i += 64) cp[i] = (int32_t)(a.tok[r0 + i] - a.min_tok);
+    for (int i = lane; i < n + DW_MID; i += 64) cp[i] = i < n ? (int32_t)(a.tok[r0 + i] - a.min_tok) : -1;
     wave_sync();
     int32_t* out = a.out_ids + r * a.out_stride;
     int carry = 0;
     bool bad = false;
     for (int base = 0; base < nw; base += 64) {
       const int k = base + lane;
-      int cnt = 0, cs = 0, cl = 0;
-      const uint16_t* ids = nullptr;
-      const int32_t* wcp = nullptr;
+      int cnt = 0;
+      uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0;
+      const uint16_t* mid_ids = nullptr;
       if (k < nw) {
         const unsigned long long o = w.occ[r * w.Lc + k];
-        cs = (int)((o >> 32) & 0xFFFF);
-        cl = (int)(o >> 48);
+        const int cs = (int)((o >> 32) & 0xFFFF), cl = (int)(o >> 48);
         const uint32_t rec = w.slot2idx[(uint32_t)o];
-        const bool mid = rec >> 31;
         const int64_t li = rec & 0xFFFFFFu;
         cnt = (int)((rec >> 24) & 0x7F);
-        ids = mid ? w.rm_sym + li * DW_MID : w.rs_sym + li * DW_SHORT;
-        wcp = mid ? w.rm_cps + li * DW_MID : w.rs_cps + li * DW_SHORT;
-        if (cl > (mid ? DW_MID : DW_SHORT) || (cl < (mid ? DW_MID : DW_SHORT) && wcp[cl] != -1)) bad = true;
-        for (int i = 0; i < cl && i < DW_MID; ++i) bad |= wcp[i] != cp[cs + i];   // the recorded word's code points
+        if (!(rec >> 31)) {   // short record: 16 ids (32 B) and 16 code points (64 B), -1 past the word
+          const uint4* ip = reinterpret_cast<const uint4*>(w.rs_sym + li * DW_SHORT);
+          const int4* cq = reinterpret_cast<const int4*>(w.rs_cps + li * DW_SHORT);
+          i0 = ip[0];
+          i1 = ip[1];
+          const int4 c0 = cq[0], c1 = cq[1], c2 = cq[2], c3 = cq[3];
+          const int rc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
+                              c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
+          bad |= cl > DW_SHORT;
+#pragma unroll
+          for (int q = 0; q < DW_SHORT; ++q) bad |= rc[q] != (q < cl ? cp[cs + q] : -1);
+        } else {              // mid record (rare): 64 code points, four wide loads at a time
+          mid_ids = w.rm_sym + li * DW_MID;
+          const int4* cq = reinterpret_cast<const int4*>(w.rm_cps + li * DW_MID);
+#pragma unroll 1
+          for (int q0 = 0; q0 < DW_MID; q0 += 16) {
+            int4 c4[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) c4[t] = cq[q0 / 4 + t];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int rc[4] = {c4[t].x, c4[t].y, c4[t].z, c4[t].w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int q = q0 + 4 * t + e;
+                bad |= rc[e] != (q < cl ? cp[cs + q] : -1);
+              }
+            }
+          }
+        }
       }
       int tot;
       const int off = carry + wave_excl_scan(cnt, lane, tot);
-      for (int i = 0; i < cnt; ++i) out[off + i] = (int32_t)ids[i];
+      if (mid_ids == nullptr) {
+#pragma unroll
+        for (int q = 0; q < DW_SHORT; ++q)
+          if (q < cnt) out[off + q] = (int32_t)u16_of(i0, i1, q);
+      } else {
+        for (int q = 0; q < cnt; ++q) out[off + q] = (int32_t)mid_ids[q];
+      }
       carry += tot;
     }
     const bool coll = __any(bad);
@@ -1570,7 +1637,7 @@ extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* ro
     hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions), dim3(64 * DW_WAVES), 0, s, a, w);
   }
   BEAST_LAUNCHED("k_dw_merge");
-  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), sizeof(int32_t) * WAVES * (size_t)std::max(1, w.Lc),
+  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), sizeof(int32_t) * WAVES * (size_t)(w.Lc + DW_MID),
                      s, a, w);
   BEAST_LAUNCHED("k_dw_emit");
   return BEAST_OK;
