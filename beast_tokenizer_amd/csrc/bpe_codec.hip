@@ -62,6 +62,9 @@ __device__ unsigned long long g_bpe_rs[BPE_RS][12];
   do {                                                                                        \
     if (lane == 0 && r < BPE_RS) g_bpe_rs[r][k] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
+// k_dw_merge waves (workgroup * 16 + wave < 16384): start after staging, end, tasks, merge rounds
+constexpr int BPE_MS = 16384;
+__device__ unsigned long long g_bpe_ms[BPE_MS][4];
 #else
 #define BPE_STAMP(k) do { } while (0)
 #endif
@@ -732,6 +735,7 @@ constexpr int DW_SHORT = 16;       // byte symbols of a short word: one 16-lane 
 constexpr int DW_MID = 64;         // ... of a mid word: one wave; longer -> ST_FALLBACK
 constexpr int ST_FALLBACK = 7;     // the row needs k_bpe_encode
 constexpr int DW_WAVES = 16;       // rows per k_dw_words workgroup (at most)
+constexpr int DW_MSPLIT = 4;       // k_dw_merge workgroups per region
 constexpr uint32_t SYM_NONE = 0xFFFFu;
 
 struct DwWs {                      // the caller's scratch, carved by dw_carve_host
@@ -751,6 +755,7 @@ struct DwWs {                      // the caller's scratch, carved by dw_carve_h
   unsigned long long* table;       // [1 << log2cap] word keys, 0 = empty (the caller's, kept empty)
   int log2cap, capS, capM, regions, nwv, Lc, S;
   int key_shift;                   // 64 - BEAST_OPT_BPE_DEDUP_KEY_BITS
+  int ltab_log2;                   // k_dw_words' workgroup table: 1 << ltab_log2 > nwv * Lc words
 };
 
 __host__ __device__ inline int dw_capm(int Lc) { return Lc / 5 + 1; }   // a mid word spans >= 5 code points
@@ -764,6 +769,14 @@ __host__ __device__ inline size_t dw_row_bytes(int Lc, int S) {
 __host__ __device__ inline size_t dw_stage_bytes(int Lc, int nwv) {
   return sizeof(uint4) * (size_t)nwv * ((size_t)Lc + dw_capm(Lc));
 }
+
+// the workgroup's word table (32-bit key, device slot): more slots than the rows can hold words
+__host__ __device__ inline int dw_ltab_log2(int Lc, int nwv) {
+  int l = 4;
+  while ((1ll << l) <= (long long)nwv * Lc) ++l;
+  return l;
+}
+__host__ __device__ inline size_t dw_ltab_bytes(int Lc, int nwv) { return (size_t)8 << dw_ltab_log2(Lc, nwv); }
 
 struct DwRow {
   int32_t* cps;      // [Lc]
@@ -796,6 +809,16 @@ __device__ __forceinline__ unsigned long long dw_mix(unsigned long long h) {   /
   return h ^ (h >> 31);
 }
 
+// a word's 64-bit key: FNV-1a over its code points, splitmix64-finalised, truncated (tests), odd
+__device__ __forceinline__ unsigned long long dw_word_key(const int32_t* cps, int cs, int ce, int key_shift) {
+  unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce - cs);
+  for (int i = cs; i < ce; ++i) h = (h ^ (unsigned long long)(uint32_t)cps[i]) * 0x100000001B3ull;
+  return (dw_mix(h) >> key_shift) | 1ull;
+}
+__device__ __forceinline__ uint32_t dw_lkey(unsigned long long key) {   // nonzero; keeps truncated keys' bits
+  return (uint32_t)(key ^ (key >> 32)) | 1u;
+}
+
 // k_dw_words: rows [blockIdx.x * nwv, +nwv), one per wave; region blockIdx.x
 __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
   extern __shared__ __align__(16) char lds_raw[];
@@ -813,17 +836,21 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
   uint4* stM = stS + capS;
   char* rows = lds_raw + dw_stage_bytes(w.Lc, nwv);
   const size_t rb = dw_row_bytes(w.Lc, w.S);
+  const int lcap = 1 << w.ltab_log2;
+  uint32_t* lkey = reinterpret_cast<uint32_t*>(rows + (size_t)nwv * rb);
+  uint32_t* lval = lkey + lcap;
+  for (int i = threadIdx.x; i < lcap; i += blockDim.x) lkey[i] = 0u;
   __syncthreads();
   DwRow L = dw_carve(rows + (size_t)wave * rb, w.Lc, w.S);
   const int64_t r = (int64_t)blockIdx.x * nwv + wave;
 #ifdef BPE_STAMPS
   if (lane == 0 && r < BPE_RS) g_bpe_rs[r][10] = __builtin_amdgcn_s_memrealtime();
 #endif
+  int st = ST_OK, nw = 0;
   if (r < a.n_rows) {
     BPE_STAMP(0);
     const int64_t r0 = a.row_off[r];
     const int n = (int)(a.row_off[r + 1] - r0);
-    int st = ST_OK;
     if (n > a.Lc) st = ST_TOO_LONG;
     // 1. code points, range checks (reference :181-192 order), classes
     int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
@@ -871,7 +898,6 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
     }
     wave_sync();
     BPE_STAMP(2);
-    int nw = 0;
     if (st == ST_OK) {
       // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
       for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
@@ -889,31 +915,46 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
     }
     BPE_STAMP(4);
     if (st == ST_OK) {
+      // (a) the workgroup's table: one representative occurrence per distinct word of the
+      // workgroup's rows goes on to the device table.  (A 32-bit table key that two words share
+      // only merges their lookups: k_dw_emit's content check sends such rows to ST_FALLBACK.)
+      const uint32_t lmask = (uint32_t)lcap - 1u;
+      for (int k = lane; k < nw; k += 64) {
+        const uint32_t lk = dw_lkey(dw_word_key(L.cps, L.wcp[k], L.wcp[k + 1], w.key_shift));
+        uint32_t ls = (lk * 0x9E3779B1u) >> (32 - w.ltab_log2);
+        bool rep = false;
+        while (true) {
+          const uint32_t pv = atomicCAS(&lkey[ls], 0u, lk);
+          if (pv == 0u) { rep = true; break; }
+          if (pv == lk) break;
+          ls = (ls + 1) & lmask;
+        }
+        L.e[k] = (int32_t)(ls | (rep ? 0x80000000u : 0u));
+      }
+      wave_sync();
+      // (b) representatives: the device table, two words per lane per step with their first
+      // reads in flight together.  A plain (L2-served) read first: a CAS on one address
+      // serialises at the memory side; a stale empty read only costs one CAS that returns the key
       const unsigned long long tmask = (1ull << w.log2cap) - 1ull;
-      // two words per lane per step, their first table reads in flight together
       for (int k0 = lane; k0 < nw; k0 += 128) {
-        int kk[2], cs[2], ce[2], bs[2], blen[2];
+        int kk[2], cs[2], ce[2], bs[2], blen[2], le[2];
         unsigned long long key[2], slot[2], prev[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           kk[u] = k0 + 64 * u;
-          const bool ok = kk[u] < nw;
+          le[u] = kk[u] < nw ? L.e[kk[u]] : 0;
+          const bool ok = le[u] < 0;   // a representative
           cs[u] = ok ? L.wcp[kk[u]] : 0;
           ce[u] = ok ? L.wcp[kk[u] + 1] : 0;
           bs[u] = L.symoff[cs[u]];
           blen[u] = L.symoff[ce[u]] - bs[u];
-          unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce[u] - cs[u]);
-          for (int i = cs[u]; i < ce[u]; ++i) h = (h ^ (unsigned long long)(uint32_t)L.cps[i]) * 0x100000001B3ull;
-          key[u] = (dw_mix(h) >> w.key_shift) | 1ull;
+          key[u] = dw_word_key(L.cps, cs[u], ce[u], w.key_shift);
           slot[u] = (key[u] * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
-          // a plain (L2-served) read first: the common words occur thousands of times in a batch and
-          // a CAS on one address serialises at the memory side (round 4: 98 us of a 132 us launch
-          // when every occurrence CASed); a stale empty read only costs one CAS that returns the key
           prev[u] = ok ? __hip_atomic_load(&w.table[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          if (kk[u] >= nw) continue;
+          if (le[u] >= 0) continue;
           bool win = false;
           unsigned long long pv = prev[u], sl = slot[u];
           while (true) {
@@ -925,7 +966,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
             sl = (sl + 1) & tmask;
             pv = __hip_atomic_load(&w.table[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
-          w.occ[r * w.Lc + kk[u]] = sl | ((unsigned long long)cs[u] << 32) | ((unsigned long long)(ce[u] - cs[u]) << 48);
+          lval[le[u] & 0x7FFFFFFF] = (uint32_t)sl;
           if (win) {
             const uint4 rec = make_uint4((uint32_t)sl, (uint32_t)r, (uint32_t)cs[u] | ((uint32_t)(ce[u] - cs[u]) << 16),
                                          ((uint32_t)wave << 24) | ((uint32_t)blen[u] << 16) | (uint32_t)bs[u]);
@@ -933,6 +974,17 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
             else stM[atomicAdd(&s_nm, 1)] = rec;
           }
         }
+      }
+    }
+  }
+  __syncthreads();   // every representative's device slot is in lval
+  if (r < a.n_rows) {
+    if (st == ST_OK) {
+      // (c) every occurrence: its word's device slot from the workgroup table
+      for (int k = lane; k < nw; k += 64) {
+        const int cs = L.wcp[k], ce = L.wcp[k + 1];
+        const uint32_t sl = lval[L.e[k] & 0x7FFFFFFF];
+        w.occ[r * w.Lc + k] = sl | ((unsigned long long)cs << 32) | ((unsigned long long)(ce - cs) << 48);
       }
     }
     BPE_STAMP(5);
@@ -1023,7 +1075,7 @@ __device__ __forceinline__ uint32_t grp_compact(uint32_t sym, bool live, int gl,
 // id (SYM_NONE past the end); n: the word's final length.
 template <int GW, class Map>
 __device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, int blen, int unk_id, int fuse_unk,
-                                                  int& n) {
+                                                  int& n, int& rounds) {
   const int lane = threadIdx.x & 63, gl = lane & (GW - 1), gbase = lane - gl;
   // HF BPE::merge_word's unknown chars: unk_id (consecutive ones fused when fuse_unk), or dropped
   const bool in = gl < blen;
@@ -1038,17 +1090,24 @@ __device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, i
     const bool has = gl + 1 < n;
     uint32_t rk = RK_NONE;
     if (has) {
+      // four probe slots read together (one LDS round trip for almost every chain: the map is
+      // <= half full, and most pairs are misses, whose linear-probe chains average two slots)
       const uint32_t key = (sym << 16) | right;
       uint32_t h = mm_hash(key, mm.log2cap);
-      uint2 e = mm.kv[h];
-      while (e.x != key && e.x != EMPTY_KEY) {
-        h = (h + 1) & mmask;
-        e = mm.kv[h];
+      for (bool done = false; !done; h = (h + 4) & mmask) {
+        uint2 e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) e[q] = mm.kv[(h + q) & mmask];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!done && e[q].x == key) rk = e[q].y - 0x10000u;   // (rank + 1) << 16 | new_id -> rank << 16 | new_id
+          done |= e[q].x == key || e[q].x == EMPTY_KEY;
+        }
       }
-      rk = e.x == key ? e.y - 0x10000u : RK_NONE;   // (rank + 1) << 16 | new_id -> rank << 16 | new_id
     }
     const uint32_t m = grp_min<GW>(rk);
     if (!__any(m != RK_NONE)) break;
+    ++rounds;
     const bool match = has && m != RK_NONE && rk == m;
     const unsigned long long mb = __ballot(match);
     const unsigned long long M = GW == 64 ? mb : ((mb >> gbase) & ((1ull << GW) - 1ull));
@@ -1077,9 +1136,12 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
     for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) reinterpret_cast<uint4*>(kv)[i] = g[i];
     lm.kv = kv; lm.rank2new = nullptr; lm.log2cap = a.map.log2cap;
   }
-  const int ns = w.cnt[2 * blockIdx.x], nm = w.cnt[2 * blockIdx.x + 1];
+  const int reg = blockIdx.x / DW_MSPLIT, part = blockIdx.x % DW_MSPLIT;
+  const int ns = w.cnt[2 * reg], nm = w.cnt[2 * reg + 1];
   if constexpr (MAP_LDS) __syncthreads();
   const int tasks = nm + (ns + 3) / 4;   // the mid words first: their rounds are the longest chains
+  // DW_MSPLIT workgroups share a region (task t to workgroup t / nwv % DW_MSPLIT): a region's
+  // merges are chains of dependent LDS round trips, so the CU wants more than its 16 waves
   // a task's inputs (its words' byte symbols and lengths) are loaded one task ahead, without a
   // dependence between them: entries past a region's count are never used
   struct Task { int blen; uint32_t raw; };
@@ -1087,26 +1149,32 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
     Task k{0, SYM_NONE};
     if (t >= tasks) return k;
     if (t < nm) {
-      const int64_t idx = (int64_t)blockIdx.x * w.capM + t;
+      const int64_t idx = (int64_t)reg * w.capM + t;
       k.blen = w.rm_n[idx];
       k.raw = w.rm_sym[idx * DW_MID + lane];
     } else {
       const int kk = 4 * (t - nm) + (lane >> 4);
-      const int64_t idx = (int64_t)blockIdx.x * w.capS + (kk < ns ? kk : 0);
+      const int64_t idx = (int64_t)reg * w.capS + (kk < ns ? kk : 0);
       k.blen = kk < ns ? w.rs_n[idx] : 0;
       k.raw = w.rs_sym[idx * DW_SHORT + (lane & 15)];
     }
     return k;
   };
-  Task cur = load(wave);
-  for (int t = wave; t < tasks; t += nwv) {
-    const Task nxt = load(t + nwv);
+  const int t0 = part * nwv + wave, tstep = DW_MSPLIT * nwv;
+  int nrounds = 0, ntasks = 0;
+#ifdef BPE_STAMPS
+  const int msi = blockIdx.x * nwv + wave;
+  if (lane == 0 && msi < BPE_MS) g_bpe_ms[msi][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  Task cur = load(t0);
+  for (int t = t0; t < tasks; t += tstep) {
+    const Task nxt = load(t + tstep);
     if (t < nm) {
-      const int64_t idx = (int64_t)blockIdx.x * w.capM + t;
+      const int64_t idx = (int64_t)reg * w.capM + t;
       const uint32_t raw = lane < cur.blen ? cur.raw : SYM_NONE;
       int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n)
-                                 : dw_merge_word<DW_MID>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n);
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds)
+                                 : dw_merge_word<DW_MID>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (lane < n) w.rm_sym[idx * DW_MID + lane] = (uint16_t)v;
       if (lane == 0) {
         const uint32_t slot = w.rm_slot[idx];
@@ -1116,11 +1184,11 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
     } else {
       const int kk = 4 * (t - nm) + (lane >> 4), gl = lane & 15;
       const bool valid = kk < ns;
-      const int64_t idx = (int64_t)blockIdx.x * w.capS + (valid ? kk : 0);
+      const int64_t idx = (int64_t)reg * w.capS + (valid ? kk : 0);
       const uint32_t raw = gl < cur.blen ? cur.raw : SYM_NONE;
       int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n)
-                                 : dw_merge_word<DW_SHORT>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n);
+      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds)
+                                 : dw_merge_word<DW_SHORT>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (valid && gl < n) w.rs_sym[idx * DW_SHORT + gl] = (uint16_t)v;
       if (valid && gl == 0) {
         const uint32_t slot = w.rs_slot[idx];
@@ -1129,7 +1197,17 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
       }
     }
     cur = nxt;
+    ++ntasks;
   }
+#ifdef BPE_STAMPS
+  if (lane == 0 && msi < BPE_MS) {
+    g_bpe_ms[msi][1] = __builtin_amdgcn_s_memrealtime();
+    g_bpe_ms[msi][2] = (unsigned long long)ntasks;
+    g_bpe_ms[msi][3] = (unsigned long long)nrounds;
+  }
+#else
+  (void)nrounds; (void)ntasks;
+#endif
 }
 
 // k_dw_emit: one wave per row.  Three dependent round trips: the row's code points and its word
@@ -1427,6 +1505,9 @@ int grid_for(int64_t n_rows, int per_cu = 4) {
 extern "C" int beast_debug_bpe_stamps(unsigned long long* host) {   // [4096][12]
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_rs), sizeof(g_bpe_rs)) == hipSuccess ? 0 : -2;
 }
+extern "C" int beast_debug_bpe_merge_stamps(unsigned long long* host) {   // [16384][4]
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_ms), sizeof(g_bpe_ms)) == hipSuccess ? 0 : -2;
+}
 #endif
 
 extern "C" int beast_bpe_mergemap_log2cap(int n_merges) {
@@ -1538,16 +1619,21 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
 
 
 // ------------------------------------------------------- word dedup, host --
+static size_t dw_words_lds(int Lc, int S, int nwv) {
+  return dw_stage_bytes(Lc, nwv) + (size_t)nwv * dw_row_bytes(Lc, S) + dw_ltab_bytes(Lc, nwv);
+}
 static int dw_nwv(int Lc, int S) {   // rows per k_dw_words workgroup: as many as the LDS holds, <= 16
-  const size_t per = dw_row_bytes(Lc, S) + dw_stage_bytes(Lc, 1);
   const size_t room = LDS_BUDGET - STATIC_LDS;
-  return (int)std::min<size_t>((size_t)DW_WAVES, room / per);
+  for (int nv = DW_WAVES; nv > 0; --nv)
+    if (dw_words_lds(Lc, S, nv) <= room) return nv;
+  return 0;
 }
 
 static size_t dw_carve_host(DwWs& w, char* base, int64_t R, int Lc, int S, int log2cap) {
   w.nwv = dw_nwv(Lc, S);
   const int nwv = w.nwv > 0 ? w.nwv : 1;
   w.Lc = Lc; w.S = S; w.log2cap = log2cap;
+  w.ltab_log2 = dw_ltab_log2(Lc, nwv);
   w.regions = (int)((R + nwv - 1) / nwv);
   w.capS = nwv * Lc;
   w.capM = nwv * dw_capm(Lc);
@@ -1619,7 +1705,7 @@ extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* ro
   a.Lc = max_row_cps; a.S = max_row_syms;
   a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
   hipStream_t s = beast::as_stream(stream);
-  const size_t lds1 = dw_stage_bytes(w.Lc, w.nwv) + (size_t)w.nwv * dw_row_bytes(w.Lc, w.S);
+  const size_t lds1 = dw_words_lds(w.Lc, w.S, w.nwv);
   if (lds1 > 65536)
     BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_words),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1),
@@ -1632,9 +1718,9 @@ extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* ro
       BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_merge<true>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds),
                 "hipFuncSetAttribute(k_dw_merge)");
-    hipLaunchKernelGGL(k_dw_merge<true>, dim3(w.regions), dim3(64 * DW_WAVES), map_lds, s, a, w);
+    hipLaunchKernelGGL(k_dw_merge<true>, dim3(w.regions * DW_MSPLIT), dim3(64 * DW_WAVES), map_lds, s, a, w);
   } else {
-    hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions), dim3(64 * DW_WAVES), 0, s, a, w);
+    hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions * DW_MSPLIT), dim3(64 * DW_WAVES), 0, s, a, w);
   }
   BEAST_LAUNCHED("k_dw_merge");
   hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), sizeof(int32_t) * WAVES * (size_t)(w.Lc + DW_MID),

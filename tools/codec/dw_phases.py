@@ -53,6 +53,20 @@ def main():
            "row_start_us_p50_max": [float(x) for x in us(np.percentile(st[:, 0] - t00, [50, 100]))],
            "row_end_us_p50_max": [float(x) for x in us(np.percentile(st[:, 6] - t00, [50, 100]))],
            "words_p50_max": [float(np.median(st[:, 9])), int(st[:, 9].max())]}
+    mb = (C.c_ulonglong * (16384 * 4))()
+    fm = lib.beast_debug_bpe_merge_stamps
+    fm.argtypes = [C.c_void_p]
+    assert fm(mb) == 0
+    ms = np.frombuffer(mb, dtype=np.uint64).reshape(16384, 4).astype(np.int64)
+    ms = ms[ms[:, 0] > 0]
+    m0 = ms[:, 0].min()
+    dur = ms[:, 1] - ms[:, 0]
+    out["k_dw_merge_waves"] = {"waves": int(len(ms)), "start_us_p50_max": [float(x) for x in us(np.percentile(ms[:, 0] - m0, [50, 100]))],
+                               "end_us_p50_max": [float(x) for x in us(np.percentile(ms[:, 1] - m0, [50, 100]))],
+                               "dur_us_p50_p90_p99_max": q(dur),
+                               "tasks_p50_max": [float(np.median(ms[:, 2])), int(ms[:, 2].max())],
+                               "rounds_p50_p90_max": [float(x) for x in np.percentile(ms[:, 3], [50, 90, 100])],
+                               "us_per_round": float(np.sum(dur) / 100.0 / max(1, np.sum(ms[:, 3])))}
     print(json.dumps(out, indent=1))
 
 
