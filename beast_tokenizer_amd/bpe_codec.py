@@ -50,12 +50,13 @@ _ENC_ERRORS = {
 }
 ST_FALLBACK = 7   # beast_bpe_encode_rows_dedup: the row needs the per-row kernel
 
-# "auto": the word-dedup path where it applies; "rows": always the per-row kernel (tests, A/B)
+# "auto": the by-words encode (k_bpe_words) where it applies; "rows": always the per-row kernel;
+# "dedup3": the three-launch device-table form (A/B only)
 _ENCODE_PATH = {"path": "auto"}
 
 
 def set_encode_path(path: str) -> None:
-    if path not in ("auto", "rows"):
+    if path not in ("auto", "rows", "dedup3"):
         raise ValueError(f"unknown encode path {path!r}")
     _ENCODE_PATH["path"] = path
 
@@ -215,7 +216,7 @@ class GpuBpeModel:
         return out
 
     def _dedup_ok(self) -> bool:
-        return _ENCODE_PATH["path"] == "auto" and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
+        return _ENCODE_PATH["path"] in ("auto", "dedup3") and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
 
     def _encode_rows_kernel(self, tok, row_off, max_row, min_token, max_span):
         """The per-row kernel (k_bpe_encode): special tokens, fallback rows, non-monotone models
@@ -254,6 +255,13 @@ class GpuBpeModel:
         if R == 0:
             return ids[:0], st[0, :0], st[1, :0]
         lib = _lib.load()
+        if _ENCODE_PATH["path"] == "auto":
+            _lib.run("beast_bpe_encode_rows_words", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+                     -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
+                     self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
+                     int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(),
+                     st[1].data_ptr(), _lib.stream_of(dev))
+            return ids[:R], st[0, :R], st[1, :R]
         # record indices are 24-bit: chunks of rows whose code-point bound stays below 2^24
         chunk = max(1, min(R, ((1 << 24) - 1) // max(1, int(max_row))))
         log2 = int(lib.beast_bpe_encode_dedup_table_log2(chunk, int(max_row)))

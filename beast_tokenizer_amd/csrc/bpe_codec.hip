@@ -819,6 +819,79 @@ __device__ __forceinline__ uint32_t dw_lkey(unsigned long long key) {   // nonze
   return (uint32_t)(key ^ (key >> 32)) | 1u;
 }
 
+// One row's pre-tokenisation into its LDS image (one wave): code points, the reference's range
+// checks in its order (:181-192), classes, UTF-8 symbol offsets, the regex word starts (as
+// k_bpe_encode, no special tokens), byte symbols as vocab ids; a word of more than 64 byte
+// symbols makes the row ST_FALLBACK.  st / nw: the row's status and word count.
+__device__ __forceinline__ void dw_pretok_row(const EncArgs& a, const DwRow& L, int64_t r, int lane,
+                                              const int32_t* s_b2i, const uint8_t* s_lut, int S, int& st, int& nw) {
+  BPE_STAMP(0);
+  const int64_t r0 = a.row_off[r];
+  const int n = (int)(a.row_off[r + 1] - r0);
+  if (n > a.Lc) st = ST_TOO_LONG;
+  // 1. code points, range checks (reference :181-192 order), classes
+  int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
+  auto code_point = [&](int i, long long t) {
+    const long long v = t - a.min_tok;
+    below |= v < 0;
+    above |= (a.max_span >= 0 && v > a.max_span);
+    notuni |= v > 0x10FFFF;
+    surr |= (v >= 0xD800 && v <= 0xDFFF);
+    nocls |= v >= a.lut_n;
+    const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
+    L.cps[i] = cp;
+    L.cls[i] = cp < 256 ? s_lut[cp] : (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
+  };
+  if (st == ST_OK) {   // the first 256 code points' loads all in flight together
+    constexpr int PF = 4;
+    long long tv[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) tv[k] = lane + 64 * k < n ? a.tok[r0 + lane + 64 * k] : 0;
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+      if (lane + 64 * k < n) code_point(lane + 64 * k, tv[k]);
+    for (int i = lane + 64 * PF; i < n; i += 64) code_point(i, a.tok[r0 + i]);
+  }
+  if (st == ST_OK) {
+    if (__any(below)) st = ST_BELOW_MIN;
+    else if (__any(above)) st = ST_ABOVE_MAX;
+    else if (__any(notuni)) st = ST_NOT_UNICODE;
+    else if (__any(surr)) st = ST_SURROGATE;
+    else if (__any(nocls)) st = ST_NO_CLASS;
+  }
+  BPE_STAMP(1);
+  int carry = 0;
+  if (st == ST_OK) {   // UTF-8 symbol offsets
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      int tot;
+      const int len = (i < n) ? utf8_len(L.cps[i]) : 0;
+      const int ex = wave_excl_scan(len, lane, tot);
+      if (i < n) L.symoff[i] = carry + ex;
+      carry += tot;
+    }
+    if (lane == 0) L.symoff[n] = carry;
+    if (carry > S) st = ST_TOO_LONG;
+  }
+  wave_sync();
+  BPE_STAMP(2);
+  if (st == ST_OK) {
+    // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
+    for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
+    word_starts(L.e, L.vis, L.wcp, nullptr, L.misc, n, lane);
+    BPE_STAMP(3);
+    for (int i = lane; i < n; i += 64) {
+      const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
+      for (int q = 0; q < len; ++q) L.c[o + q] = (uint16_t)s_b2i[utf8_byte(cp, q)];   // -1 -> SYM_NONE
+    }
+    wave_sync();
+    nw = L.misc[0];
+    bool fall = false;
+    for (int k = lane; k < nw; k += 64) fall |= (L.symoff[L.wcp[k + 1]] - L.symoff[L.wcp[k]]) > DW_MID;
+    if (__any(fall)) st = ST_FALLBACK;
+  }
+}
+
 // k_dw_words: rows [blockIdx.x * nwv, +nwv), one per wave; region blockIdx.x
 __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
   extern __shared__ __align__(16) char lds_raw[];
@@ -848,71 +921,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
 #endif
   int st = ST_OK, nw = 0;
   if (r < a.n_rows) {
-    BPE_STAMP(0);
-    const int64_t r0 = a.row_off[r];
-    const int n = (int)(a.row_off[r + 1] - r0);
-    if (n > a.Lc) st = ST_TOO_LONG;
-    // 1. code points, range checks (reference :181-192 order), classes
-    int below = 0, above = 0, notuni = 0, surr = 0, nocls = 0;
-    auto code_point = [&](int i, long long t) {
-      const long long v = t - a.min_tok;
-      below |= v < 0;
-      above |= (a.max_span >= 0 && v > a.max_span);
-      notuni |= v > 0x10FFFF;
-      surr |= (v >= 0xD800 && v <= 0xDFFF);
-      nocls |= v >= a.lut_n;
-      const int cp = (int)((v < 0 || v > 0x10FFFF) ? 0 : v);
-      L.cps[i] = cp;
-      L.cls[i] = cp < 256 ? s_lut[cp] : (cp < a.lut_n) ? a.lut[cp] : CLS_OTHER;
-    };
-    if (st == ST_OK) {   // the first 256 code points' loads all in flight together
-      constexpr int PF = 4;
-      long long tv[PF];
-#pragma unroll
-      for (int k = 0; k < PF; ++k) tv[k] = lane + 64 * k < n ? a.tok[r0 + lane + 64 * k] : 0;
-#pragma unroll
-      for (int k = 0; k < PF; ++k)
-        if (lane + 64 * k < n) code_point(lane + 64 * k, tv[k]);
-      for (int i = lane + 64 * PF; i < n; i += 64) code_point(i, a.tok[r0 + i]);
-    }
-    if (st == ST_OK) {
-      if (__any(below)) st = ST_BELOW_MIN;
-      else if (__any(above)) st = ST_ABOVE_MAX;
-      else if (__any(notuni)) st = ST_NOT_UNICODE;
-      else if (__any(surr)) st = ST_SURROGATE;
-      else if (__any(nocls)) st = ST_NO_CLASS;
-    }
-    BPE_STAMP(1);
-    int carry = 0;
-    if (st == ST_OK) {   // UTF-8 symbol offsets
-      for (int base = 0; base < n; base += 64) {
-        const int i = base + lane;
-        int tot;
-        const int len = (i < n) ? utf8_len(L.cps[i]) : 0;
-        const int ex = wave_excl_scan(len, lane, tot);
-        if (i < n) L.symoff[i] = carry + ex;
-        carry += tot;
-      }
-      if (lane == 0) L.symoff[n] = carry;
-      if (carry > w.S) st = ST_TOO_LONG;
-    }
-    wave_sync();
-    BPE_STAMP(2);
-    if (st == ST_OK) {
-      // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
-      for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
-      word_starts(L.e, L.vis, L.wcp, nullptr, L.misc, n, lane);
-      BPE_STAMP(3);
-      for (int i = lane; i < n; i += 64) {
-        const int cp = L.cps[i], len = utf8_len(cp), o = L.symoff[i];
-        for (int q = 0; q < len; ++q) L.c[o + q] = (uint16_t)s_b2i[utf8_byte(cp, q)];   // -1 -> SYM_NONE
-      }
-      wave_sync();
-      nw = L.misc[0];
-      bool fall = false;
-      for (int k = lane; k < nw; k += 64) fall |= (L.symoff[L.wcp[k + 1]] - L.symoff[L.wcp[k]]) > DW_MID;
-      if (__any(fall)) st = ST_FALLBACK;
-    }
+    dw_pretok_row(a, L, r, lane, s_b2i, s_lut, w.S, st, nw);
     BPE_STAMP(4);
     if (st == ST_OK) {
       // (a) the workgroup's table: one representative occurrence per distinct word of the
@@ -1300,6 +1309,193 @@ __global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
   }
 }
 
+// ------------------------------------------------------- encode by words, one launch --
+// k_bpe_words: a workgroup takes nwv rows (one wave each) through the whole encode in LDS:
+//   1. pre-tokenisation of each row (dw_pretok_row);
+//   2. exact dedup of the workgroup's words: a table keyed by a 32-bit hash of the word's code
+//      points, each entry (hash, first occurrence); a hash match is confirmed by comparing the
+//      code points with the entry's occurrence, so equal hashes of different words only lengthen
+//      the probe;
+//   3. the distinct words counting-sorted by byte-symbol length, longest first, so the four
+//      words of a 16-lane task have similar round counts;
+//   4. every distinct word merged once (dw_merge_word), its ids written over its own byte
+//      symbols in the row image, its id count beside it;
+//   5. each row's ids gathered from its words' first occurrences.
+// Nothing but the bins and the ids touches HBM (and the merge map when it is too large for LDS).
+__device__ __forceinline__ uint32_t bw_hash(const int32_t* cps, int cs, int ce) {   // FNV-1a + murmur3 fmix
+  uint32_t h = 0x811C9DC5u ^ (uint32_t)(ce - cs);
+  for (int i = cs; i < ce; ++i) h = (h ^ (uint32_t)cps[i]) * 0x01000193u;
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
+__host__ __device__ inline size_t bw_lds_bytes(int Lc, int S, int nwv, int map_log2 /* < 0: map in HBM */) {
+  size_t b = map_log2 >= 0 ? al16(sizeof(uint2) << map_log2) : 0;
+  b += dw_ltab_bytes(Lc, nwv);
+  b += 2 * al16(sizeof(uint32_t) * (size_t)nwv * Lc);
+  return b + (size_t)nwv * dw_row_bytes(Lc, S);
+}
+
+template <bool MAP_LDS>
+__global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab_log2, int hash_shift) {
+  extern __shared__ __align__(16) char lds_raw[];
+  __shared__ int32_t s_b2i[256];
+  __shared__ uint8_t s_lut[256];
+  __shared__ int s_nd;
+  __shared__ int s_hist[DW_MID + 1];   // distinct words per byte-symbol length, then sort cursors
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  char* p = lds_raw;
+  LdsMap lm;
+  if constexpr (MAP_LDS) {
+    const int cap = 1 << a.map.log2cap;
+    uint4* kv = reinterpret_cast<uint4*>(p);
+    const uint4* g = reinterpret_cast<const uint4*>(a.map.kv);
+    for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) kv[i] = g[i];
+    lm.kv = reinterpret_cast<const uint2*>(p); lm.rank2new = nullptr; lm.log2cap = a.map.log2cap;
+    p += al16(sizeof(uint2) << a.map.log2cap);
+  }
+  const int lcap = 1 << ltab_log2;
+  unsigned long long* ltab = reinterpret_cast<unsigned long long*>(p);
+  p += sizeof(unsigned long long) * (size_t)lcap;
+  const int capw = nwv * a.Lc;
+  uint32_t* dl = reinterpret_cast<uint32_t*>(p);   // distinct words: wave << 22 | word << 7 | byte symbols
+  p += al16(sizeof(uint32_t) * (size_t)capw);
+  uint32_t* ds = reinterpret_cast<uint32_t*>(p);   // ... sorted, longest first
+  p += al16(sizeof(uint32_t) * (size_t)capw);
+  char* rows = p;
+  const size_t rb = dw_row_bytes(a.Lc, a.S);
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    s_b2i[i] = a.byte2id[i];
+    s_lut[i] = i < a.lut_n ? a.lut[i] : (uint8_t)CLS_OTHER;
+  }
+  for (int i = threadIdx.x; i < lcap; i += blockDim.x) ltab[i] = 0ull;
+  if (threadIdx.x <= DW_MID) s_hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_nd = 0;
+  __syncthreads();
+  const DwRow L = dw_carve(rows + (size_t)wave * rb, a.Lc, a.S);
+  const int64_t r = (int64_t)blockIdx.x * nwv + wave;
+#ifdef BPE_STAMPS
+  if (lane == 0 && r < BPE_RS) g_bpe_rs[r][10] = __builtin_amdgcn_s_memrealtime();
+#endif
+  int st = ST_OK, nw = 0;
+  if (r < a.n_rows) dw_pretok_row(a, L, r, lane, s_b2i, s_lut, a.S, st, nw);
+  __syncthreads();   // every row's code points, word starts and symbols are readable workgroup-wide
+  if (r < a.n_rows) BPE_STAMP(4);
+  // 2. exact dedup; L.e[k] = the word's first occurrence (wave << 16 | word)
+  if (r < a.n_rows && st == ST_OK) {
+    const uint32_t lmask = (uint32_t)lcap - 1u;
+    for (int k = lane; k < nw; k += 64) {
+      const int cs = L.wcp[k], ce = L.wcp[k + 1], len = ce - cs;
+      const uint32_t hk = (bw_hash(L.cps, cs, ce) >> hash_shift) | 1u;
+      const uint32_t me = ((uint32_t)wave << 16) | (uint32_t)k;
+      const unsigned long long mine = ((unsigned long long)hk << 32) | me;
+      uint32_t ls = (hk * 0x9E3779B1u) >> (32 - ltab_log2), rep = me;
+      while (true) {
+        unsigned long long e = ltab[ls];
+        if (e == 0ull) {
+          e = atomicCAS(&ltab[ls], 0ull, mine);
+          if (e == 0ull) break;
+        }
+        if ((uint32_t)(e >> 32) == hk) {
+          const uint32_t o = (uint32_t)e;
+          const DwRow Ro = dw_carve(rows + (size_t)(o >> 16) * rb, a.Lc, a.S);
+          const int ocs = Ro.wcp[o & 0xFFFF];
+          bool same = Ro.wcp[(o & 0xFFFF) + 1] - ocs == len;
+          for (int i = 0; same && i < len; ++i) same = Ro.cps[ocs + i] == L.cps[cs + i];
+          if (same) { rep = o; break; }
+        }
+        ls = (ls + 1) & lmask;
+      }
+      L.e[k] = (int32_t)rep;
+      if (rep == me) {
+        const int blen = L.symoff[ce] - L.symoff[cs];   // 1..64 (longer words made the row ST_FALLBACK)
+        dl[atomicAdd(&s_nd, 1)] = ((uint32_t)wave << 22) | ((uint32_t)k << 7) | (uint32_t)blen;
+        atomicAdd(&s_hist[blen], 1);
+      }
+    }
+  }
+  __syncthreads();
+  // 3. counting sort, longest first: lane l holds length 64 - l
+  if (wave == 0) {
+    int tot;
+    const int ex = wave_excl_scan(s_hist[DW_MID - lane], lane, tot);
+    s_hist[DW_MID - lane] = ex;
+  }
+  __syncthreads();
+  const int nd = s_nd;
+  for (int i = threadIdx.x; i < nd; i += blockDim.x) {
+    const uint32_t v = dl[i];
+    ds[atomicAdd(&s_hist[v & 127u], 1)] = v;
+  }
+  __syncthreads();
+  if (r < a.n_rows) BPE_STAMP(5);
+  // 4. merges: a mid word (17..64 byte symbols) per wave, short ones four to a wave
+  const int nmid = s_hist[DW_SHORT + 1];   // the cursor of length 17 has passed every longer word
+  const int tasks = nmid + (nd - nmid + 3) / 4;
+  int nrounds = 0;
+  for (int t = wave; t < tasks; t += nwv) {
+    if (t < nmid) {
+      const uint32_t v = ds[t];
+      const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
+      const int k = (v >> 7) & 0x7FFF, blen = v & 127u;
+      const int bs = Rw.symoff[Rw.wcp[k]];
+      const uint32_t raw = lane < blen ? (uint32_t)Rw.c[bs + lane] : SYM_NONE;
+      int n;
+      const uint32_t id = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
+                                  : dw_merge_word<DW_MID>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      if (lane < n) Rw.c[bs + lane] = (uint16_t)id;
+      if (lane == 0) Rw.vis[k] = (uint8_t)n;
+    } else {
+      const int j = nmid + 4 * (t - nmid) + (lane >> 4), gl = lane & 15;
+      const bool valid = j < nd;
+      const uint32_t v = valid ? ds[j] : 0u;
+      const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
+      const int k = (v >> 7) & 0x7FFF, blen = valid ? (int)(v & 127u) : 0;
+      const int bs = valid ? Rw.symoff[Rw.wcp[k]] : 0;
+      const uint32_t raw = gl < blen ? (uint32_t)Rw.c[bs + gl] : SYM_NONE;
+      int n;
+      const uint32_t id = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
+                                  : dw_merge_word<DW_SHORT>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
+      if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
+    }
+  }
+  __syncthreads();
+  if (r < a.n_rows) BPE_STAMP(6);
+  // 5. the row's ids from its words' first occurrences
+  if (r < a.n_rows) {
+    if (st != ST_OK) {
+      if (lane == 0) { a.out_len[r] = 0; a.status[r] = st; }
+    } else {
+      int32_t* out = a.out_ids + r * a.out_stride;
+      int carry = 0;
+      for (int base = 0; base < nw; base += 64) {
+        const int k = base + lane;
+        int cnt = 0;
+        const uint16_t* src = nullptr;
+        if (k < nw) {
+          const uint32_t o = (uint32_t)L.e[k];
+          const DwRow Ro = dw_carve(rows + (size_t)(o >> 16) * rb, a.Lc, a.S);
+          const int ko = o & 0xFFFF;
+          cnt = Ro.vis[ko];
+          src = Ro.c + Ro.symoff[Ro.wcp[ko]];
+        }
+        int tot;
+        const int off = carry + wave_excl_scan(cnt, lane, tot);
+        for (int q = 0; q < cnt; ++q) out[off + q] = (int32_t)src[q];
+        carry += tot;
+      }
+      if (lane == 0) { a.out_len[r] = carry; a.status[r] = ST_OK; }
+    }
+#ifdef BPE_STAMPS
+    if (lane == 0 && r < BPE_RS) { g_bpe_rs[r][7] = __builtin_amdgcn_s_memrealtime(); g_bpe_rs[r][8] = nd; g_bpe_rs[r][9] = nw; }
+    if (lane == 0 && r < BPE_RS) g_bpe_rs[r][11] = (unsigned long long)nrounds;
+#endif
+  }
+  (void)nrounds;
+}
+
 // ---------------------------------------------------------------- decode --
 struct DecArgs {
   const int32_t* ids;
@@ -1655,6 +1851,57 @@ static size_t dw_carve_host(DwWs& w, char* base, int64_t R, int Lc, int S, int l
   return o;
 }
 
+
+extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows,
+                                           int64_t min_tok, int64_t max_span, const uint8_t* cls_lut, int64_t lut_n,
+                                           const int32_t* byte2id, const void* map, int n_merges, int unk_id,
+                                           int fuse_unk, int max_row_cps, int max_row_syms, int32_t* out_ids,
+                                           int64_t out_stride, int32_t* out_len, int32_t* status, void* stream) {
+  BEAST_REQUIRE(n_rows >= 0, "n_rows must be >= 0");
+  if (n_rows == 0) return BEAST_OK;
+  BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && map && out_ids && out_len && status, "null pointer argument");
+  BEAST_REQUIRE(lut_n > 0 && lut_n <= 65536, "class LUT size %lld out of range", (long long)lut_n);
+  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
+  BEAST_REQUIRE(max_row_cps >= 0 && max_row_cps < 32768, "max_row_cps %d out of range", max_row_cps);
+  BEAST_REQUIRE(max_row_syms >= 0 && max_row_syms <= 16384, "max_row_syms %d out of range", max_row_syms);
+  BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
+  EncArgs a{};
+  a.tok = reinterpret_cast<const long long*>(tok);
+  a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
+  a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
+  a.map = map_view(map, n_merges);
+  a.n_merges = n_merges;
+  a.unk_id = unk_id; a.fuse_unk = fuse_unk;
+  a.Lc = max_row_cps; a.S = max_row_syms;
+  a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
+  // as many rows per workgroup as the LDS holds (<= 16), the merge map staged when it fits beside them
+  const size_t room = LDS_BUDGET - STATIC_LDS;
+  int map_log2 = a.map.log2cap <= LDS_MAP_MAX_LOG2 ? a.map.log2cap : -1, nwv = 0;
+  for (int pass = 0; pass < 2 && nwv == 0; ++pass) {
+    for (int nv = DW_WAVES; nv > 0 && nwv == 0; --nv)
+      if (bw_lds_bytes(a.Lc, a.S, nv, map_log2) <= room) nwv = nv;
+    if (nwv == 0) map_log2 = -1;
+  }
+  BEAST_REQUIRE_CODE(nwv > 0, BEAST_E_UNSUPPORTED, "rows of %d code points exceed k_bpe_words' LDS budget", max_row_cps);
+  const int ltab_log2 = dw_ltab_log2(a.Lc, nwv);
+  const int hash_shift = 32 - std::min(32, std::max(1, beast::g_bpe_dedup_key_bits));
+  const size_t lds = bw_lds_bytes(a.Lc, a.S, nwv, map_log2);
+  hipStream_t s = beast::as_stream(stream);
+  const dim3 grid((unsigned)((n_rows + nwv - 1) / nwv)), block(64 * nwv);
+  if (map_log2 >= 0) {
+    if (lds > 65536)
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bpe_words<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute(k_bpe_words)");
+    hipLaunchKernelGGL(k_bpe_words<true>, grid, block, lds, s, a, ltab_log2, hash_shift);
+  } else {
+    if (lds > 65536)
+      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bpe_words<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute(k_bpe_words)");
+    hipLaunchKernelGGL(k_bpe_words<false>, grid, block, lds, s, a, ltab_log2, hash_shift);
+  }
+  BEAST_LAUNCHED("k_bpe_words");
+  return BEAST_OK;
+}
 
 extern "C" int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps) {
   const int64_t words = std::max<int64_t>(1, n_rows) * std::max(1, max_row_cps);

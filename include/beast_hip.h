@@ -375,6 +375,15 @@ int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int6
                                 int max_row_syms, uint64_t* table, int table_log2, void* ws, size_t ws_bytes,
                                 int32_t* out_ids, int64_t out_stride, int32_t* out_len, int32_t* status,
                                 void* stream);
+/* The same encode in one launch, no workspace: each workgroup pre-tokenises its rows (up to 16),
+ * merges every distinct word among them once (exact dedup by code points in LDS) and gathers
+ * each row's ids.  Same model condition and statuses as beast_bpe_encode_rows_dedup; 7
+ * (ST_FALLBACK) only for a word of more than 64 byte symbols. */
+int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
+                                int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
+                                const void* map, int n_merges, int unk_id, int fuse_unk, int max_row_cps,
+                                int max_row_syms, int32_t* out_ids, int64_t out_stride, int32_t* out_len,
+                                int32_t* status, void* stream);
 /* Decode rows ids[row_off[r] .. row_off[r+1]).  tok_off[n_vocab+1] / tok_bytes: each id's
  * ByteLevel-decoded bytes; tok_skip[id] = 1 for special tokens (skip_special_tokens) and
  * unassigned ids.  out[r][0 .. min(count, L)) = code point + min_tok; out_count[r] = code

@@ -51,8 +51,8 @@ def decode_rows(model, id_rows, dev, L):
     return [out[i, :counts[i]].tolist() for i in range(len(seqs))], counts, status.cpu().numpy()
 
 
-@pytest.fixture(params=[("auto", 0), ("rows", 0), ("rows", 1), ("rows", 3)],
-                ids=["dedup", "rounds", "heap", "heap_wide_grid"])
+@pytest.fixture(params=[("auto", 0), ("dedup3", 0), ("rows", 0), ("rows", 1), ("rows", 3)],
+                ids=["words", "dedup3", "rounds", "heap", "heap_wide_grid"])
 def encode_mode(request):
     """The word-dedup encode (the default: k_dw_words / k_dw_merge / k_dw_emit, falling back to
     k_bpe_encode where it must) and k_bpe_encode itself with its per-word merge by rounds or by
@@ -229,33 +229,60 @@ def test_dedup_fallback_rows_for_long_words(gpu_device):
 
 
 @pytest.mark.parametrize("bits", [3, 8, 20])
-def test_dedup_key_collisions_are_detected(bits, gpu_device):
-    """With only `bits` bits of the 64-bit word keys, different words share keys: every such row
-    is caught by the content check (ST_FALLBACK, never a wrong id) and re-encoded per row."""
+def test_words_hash_collisions_are_exact(bits, gpu_device):
+    """k_bpe_words with only `bits` bits of its 32-bit word hashes: different words share hashes
+    and the code-point compare behind every hash match keeps them apart -- the same statuses (the
+    long-word rows only) and HF's ids on every other row, with no re-encode."""
     from beast_tokenizer_amd import _lib
-    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK
     tok, model, rng, centre = _trained_model(255, 1500, 140, 2048, 9, gpu_device)
     test = np.clip(centre[:1000] + np.round(rng.normal(0, 255 / 8, size=(1000, 140))), 0, 255).astype(np.int64)
     want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
     flat, off, width = rows_from_sequences(list(test), gpu_device)
-    st0 = model.encode_rows(flat, off, width, 0, 255, resolve=False)[2].cpu().numpy()   # long-word rows only
+    st0 = model.encode_rows(flat, off, width, 0, 255, resolve=False)[2].cpu().numpy()
     _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, bits)
     try:
         ids, lens, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
         ids, lens, st = ids.cpu().numpy(), lens.cpu().numpy(), st.cpu().numpy()
-        ok = st == 0
-        assert (st[~ok] == ST_FALLBACK).all() and (st[st0 == ST_FALLBACK] == ST_FALLBACK).all()
-        if bits <= 8:
-            assert (~ok).sum() > (st0 != 0).sum() + 100          # many rows hit a collision
-        for i in np.flatnonzero(ok):          # the rows that passed the check are HF's
-            assert ids[i, :lens[i]].tolist() == want[i]
-        got, status = encode_rows(model, list(test), gpu_device)
-        assert not status.any() and got == want
     finally:
         _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, 64)
-    # the table is left empty: a normal call right after falls back on the long-word rows only
-    _, _, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
-    assert np.array_equal(st.cpu().numpy(), st0)
+    assert np.array_equal(st, st0)
+    for i in np.flatnonzero(st == 0):
+        assert ids[i, :lens[i]].tolist() == want[i]
+
+
+@pytest.mark.parametrize("bits", [3, 8, 20])
+def test_dedup_key_collisions_are_detected(bits, gpu_device):
+    """The three-launch form with only `bits` bits of the 64-bit word keys: different words share
+    keys, every such row is caught by the content check (ST_FALLBACK, never a wrong id) and
+    re-encoded per row."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK, set_encode_path
+    tok, model, rng, centre = _trained_model(255, 1500, 140, 2048, 9, gpu_device)
+    test = np.clip(centre[:1000] + np.round(rng.normal(0, 255 / 8, size=(1000, 140))), 0, 255).astype(np.int64)
+    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
+    flat, off, width = rows_from_sequences(list(test), gpu_device)
+    set_encode_path("dedup3")
+    try:
+        st0 = model.encode_rows(flat, off, width, 0, 255, resolve=False)[2].cpu().numpy()   # long-word rows only
+        _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, bits)
+        try:
+            ids, lens, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
+            ids, lens, st = ids.cpu().numpy(), lens.cpu().numpy(), st.cpu().numpy()
+            ok = st == 0
+            assert (st[~ok] == ST_FALLBACK).all() and (st[st0 == ST_FALLBACK] == ST_FALLBACK).all()
+            if bits <= 8:
+                assert (~ok).sum() > (st0 != 0).sum() + 100          # many rows hit a collision
+            for i in np.flatnonzero(ok):          # the rows that passed the check are HF's
+                assert ids[i, :lens[i]].tolist() == want[i]
+            got, status = encode_rows(model, list(test), gpu_device)
+            assert not status.any() and got == want
+        finally:
+            _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, 64)
+        # the table is left empty: a normal call right after falls back on the long-word rows only
+        _, _, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
+        assert np.array_equal(st.cpu().numpy(), st0)
+    finally:
+        set_encode_path("auto")
 
 
 def test_dedup_non_monotone_model_uses_heap(gpu_device):
