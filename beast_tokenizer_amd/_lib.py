@@ -89,12 +89,8 @@ SIGNATURES = {
     "beast_bpe_encode_lds_bytes": (_sz, [_i32, _i32]),
     "beast_bpe_encode_rows": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
                                      _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
-    "beast_bpe_encode_dedup_table_log2": (_i32, [_i64, _i32]),
-    "beast_bpe_encode_dedup_workspace_bytes": (_sz, [_i64, _i32, _i32, _i32]),
     "beast_bpe_encode_rows_words": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32,
                                            _i32, _vp, _i64, _vp, _vp, _vp]),
-    "beast_bpe_encode_rows_dedup": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32,
-                                           _i32, _vp, _i32, _vp, _sz, _vp, _i64, _vp, _vp, _vp]),
     "beast_bpe_decode_rows": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _i64, _i32, _vp, _vp, _vp, _vp]),
 }
 

@@ -11,9 +11,9 @@ the kernels restate AddedVocabulary's special-token split, the ByteLevel pre-tok
 ``String::from_utf8_lossy`` (tests/test_gpu_parity.py checks them against HF itself and
 against tests/golden/bpe_codec.json).
 
-Encode takes one of two device paths (same ids): by default the batch's distinct words are
-merged once each (``beast_bpe_encode_rows_dedup``: word split + key insert, one merge per
-distinct word, emit); models with special tokens, models whose merges are not rank-monotone
+Encode takes one of two device paths (same ids): by default each workgroup's distinct words are
+merged once each (``beast_bpe_encode_rows_words``, one launch: pre-tokenise, exact dedup in LDS,
+one merge per distinct word, gather); models with special tokens, models whose merges are not rank-monotone
 (a merge combining a token that a later merge also produces, where merging a word's lowest pair
 everywhere at once is not HF's heap order) and rows holding a word of more than 64 byte symbols
 take the per-row kernel (``beast_bpe_encode_rows``), the latter two with HF's heap.
@@ -48,15 +48,14 @@ _ENC_ERRORS = {
     5: (NotImplementedError, "BPE input beyond the Basic Multilingual Plane is not supported on the GPU"),
     6: (NotImplementedError, "BPE input row too long for the GPU encoder"),
 }
-ST_FALLBACK = 7   # beast_bpe_encode_rows_dedup: the row needs the per-row kernel
+ST_FALLBACK = 7   # beast_bpe_encode_rows_words: the row needs the per-row kernel
 
-# "auto": the by-words encode (k_bpe_words) where it applies; "rows": always the per-row kernel;
-# "dedup3": the three-launch device-table form (A/B only)
+# "auto": the by-words encode (k_bpe_words) where it applies; "rows": always the per-row kernel (tests, A/B)
 _ENCODE_PATH = {"path": "auto"}
 
 
 def set_encode_path(path: str) -> None:
-    if path not in ("auto", "rows", "dedup3"):
+    if path not in ("auto", "rows"):
         raise ValueError(f"unknown encode path {path!r}")
     _ENCODE_PATH["path"] = path
 
@@ -122,8 +121,7 @@ class GpuBpeModel:
             mt = None
         self._keep = mt   # the build reads it asynchronously
         self.monotone = rank_monotone(list(zip(ma, mb, mn)))
-        self._max_id = max(vocab.values()) if vocab else 0   # 0xFFFF marks "no id" in the dedup kernels
-        self._dw_table, self._dw_log2, self._dw_ws = None, 0, None
+        self._max_id = max(vocab.values()) if vocab else 0   # 0xFFFF marks "no id" in k_bpe_words
 
         b2u = bytes_to_unicode()
         self.byte2id = torch.tensor([vocab.get(b2u[b], -1) for b in range(256)], dtype=torch.int32).to(device)
@@ -206,17 +204,20 @@ class GpuBpeModel:
     def encode_rows(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,
                     max_span: Optional[int], resolve: bool = True):
         """tok int64 (device), rows tok[row_off[r]:row_off[r+1]] -> (ids [R, W] int32, lens [R], status [R]).
-        resolve=False (timing only): the dedup path's ST_FALLBACK rows are left as they are."""
+        resolve=False (timing only): the by-words path's ST_FALLBACK rows are left as they are."""
         R = row_off.numel() - 1
-        if not self._dedup_ok():
+        if not self._words_ok():
             return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
-        out = self._encode_rows_dedup(tok, row_off, max_row, min_token, max_span)
+        try:
+            out = self._encode_rows_words(tok, row_off, max_row, min_token, max_span)
+        except NotImplementedError:   # rows too long for k_bpe_words' LDS image: the per-row kernel
+            return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
         if resolve and R and bool((out[2] == ST_FALLBACK).any()):
             return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
         return out
 
-    def _dedup_ok(self) -> bool:
-        return _ENCODE_PATH["path"] in ("auto", "dedup3") and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
+    def _words_ok(self) -> bool:
+        return _ENCODE_PATH["path"] == "auto" and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
 
     def _encode_rows_kernel(self, tok, row_off, max_row, min_token, max_span):
         """The per-row kernel (k_bpe_encode): special tokens, fallback rows, non-monotone models
@@ -245,7 +246,7 @@ class GpuBpeModel:
                 lib.beast_set_option(_lib.OPT_BPE_ENCODE_MODE, mode)
         return ids[:R], st[0, :R], st[1, :R]
 
-    def _encode_rows_dedup(self, tok, row_off, max_row, min_token, max_span):
+    def _encode_rows_words(self, tok, row_off, max_row, min_token, max_span):
         R = row_off.numel() - 1
         dev = self.device
         cp_bound = 0x10FFFF if max_span is None else max(0, int(max_span))
@@ -254,31 +255,11 @@ class GpuBpeModel:
         st = torch.empty((2, max(R, 1)), dtype=torch.int32, device=dev)   # lens, status
         if R == 0:
             return ids[:0], st[0, :0], st[1, :0]
-        lib = _lib.load()
-        if _ENCODE_PATH["path"] == "auto":
-            _lib.run("beast_bpe_encode_rows_words", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
-                     -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
-                     self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
-                     int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(),
-                     st[1].data_ptr(), _lib.stream_of(dev))
-            return ids[:R], st[0, :R], st[1, :R]
-        # record indices are 24-bit: chunks of rows whose code-point bound stays below 2^24
-        chunk = max(1, min(R, ((1 << 24) - 1) // max(1, int(max_row))))
-        log2 = int(lib.beast_bpe_encode_dedup_table_log2(chunk, int(max_row)))
-        if self._dw_table is None or self._dw_log2 < log2:   # zero-filled once; every call leaves it zero
-            self._dw_log2 = log2
-            self._dw_table = torch.zeros(1 << log2, dtype=torch.int64, device=dev)
-        need = int(lib.beast_bpe_encode_dedup_workspace_bytes(chunk, int(max_row), int(max_syms), self._dw_log2))
-        if self._dw_ws is None or self._dw_ws.numel() < need:
-            self._dw_ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        for a in range(0, R, chunk):
-            n = min(chunk, R - a)
-            _lib.run("beast_bpe_encode_rows_dedup", tok.data_ptr(), row_off[a:].data_ptr(), n, int(min_token),
-                     -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
-                     self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
-                     int(max_row), int(max_syms), self._dw_table.data_ptr(), self._dw_log2, self._dw_ws.data_ptr(),
-                     self._dw_ws.numel(), ids[a].data_ptr(), ids.shape[1], st[0, a:].data_ptr(),
-                     st[1, a:].data_ptr(), _lib.stream_of(dev))
+        _lib.run("beast_bpe_encode_rows_words", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+                 -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
+                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
+                 int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(),
+                 st[1].data_ptr(), _lib.stream_of(dev))
         return ids[:R], st[0, :R], st[1, :R]
 
     def encode_to_lists(self, tok: torch.Tensor, row_off: torch.Tensor, max_row: int, min_token: int,

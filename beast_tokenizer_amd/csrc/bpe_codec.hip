@@ -62,9 +62,6 @@ __device__ unsigned long long g_bpe_rs[BPE_RS][12];
   do {                                                                                        \
     if (lane == 0 && r < BPE_RS) g_bpe_rs[r][k] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
-// k_dw_merge waves (workgroup * 16 + wave < 16384): start after staging, end, tasks, merge rounds
-constexpr int BPE_MS = 16384;
-__device__ unsigned long long g_bpe_ms[BPE_MS][4];
 #else
 #define BPE_STAMP(k) do { } while (0)
 #endif
@@ -709,68 +706,25 @@ __global__ __launch_bounds__(64 * ENC_MAX_WAVES) void k_bpe_encode(EncArgs a) {
   }
 }
 
-// ------------------------------------------------------ encode, word dedup --
+// ------------------------------------------------------ encode, by words --
 // (round 4) HF's BPE merges each pre-tokenised word on its own, so a row's ids are the
 // concatenation of its words' ids, and a word's ids are a function of the word alone (its code
 // points).  A batch of BEAST rows holds few distinct words (K5's codec sample: 302 k words,
-// 77 k distinct, 5.9 byte symbols on average, 47 at most), so the batch is encoded in three
-// launches instead of one wave merging every row in full:
-//   k_dw_words   one wave per row: code points, range checks, classes, regex word starts (as
-//                k_bpe_encode), then per word a 64-bit key of its code points inserted into a
-//                device hash table (CAS); the first inserter of a key records the word (slot,
-//                position, byte symbols) in its workgroup's region -- an LDS list flushed at the
-//                end, so no device-wide counter is contended.  A row holding a word of more than
-//                64 byte symbols is left to k_bpe_encode (ST_FALLBACK).
-//   k_dw_merge   one workgroup per region: every distinct word merged once, in registers --
-//                words of <= 16 byte symbols four to a wave (one 16-lane DPP row each), longer
-//                ones a wave each.  A round probes every adjacent pair's rank in the LDS merge
-//                map, takes the word's lowest (DPP row rotations), merges its occurrences left
-//                to right (a self-pair run takes every other one) and compacts the word with one
-//                ds_permute.  For models whose merges only combine tokens made by earlier merges
-//                (the host checks) this is HF's merge_all; the slots are cleared for the next call.
-//   k_dw_emit    one wave per row: each word's ids copied from its record at the scanned offset,
-//                after checking that the word's code points equal the recorded word's (a 64-bit
-//                key collision makes the row ST_FALLBACK, never a wrong id).
-constexpr int DW_SHORT = 16;       // byte symbols of a short word: one 16-lane DPP row
+// 77 k distinct, 5.9 byte symbols on average, 47 at most), so k_bpe_words (below) merges each
+// distinct word of a workgroup's rows once instead of every word of every row.
+constexpr int DW_TINY = 8;         // byte symbols of a tiny word: half a DPP row
+constexpr int DW_SHORT = 16;       // ... of a short word: one 16-lane DPP row
 constexpr int DW_MID = 64;         // ... of a mid word: one wave; longer -> ST_FALLBACK
 constexpr int ST_FALLBACK = 7;     // the row needs k_bpe_encode
-constexpr int DW_WAVES = 16;       // rows per k_dw_words workgroup (at most)
-constexpr int DW_MSPLIT = 4;       // k_dw_merge workgroups per region
+constexpr int DW_WAVES = 16;       // rows per k_bpe_words workgroup (at most)
 constexpr uint32_t SYM_NONE = 0xFFFFu;
 
-struct DwWs {                      // the caller's scratch, carved by dw_carve_host
-  uint32_t* slot2idx;              // [cap] record of a slot: k_dw_words: tier << 31 | index;
-                                   //   k_dw_merge: tier << 31 | ids << 24 | index (ids <= 64)
-  unsigned long long* occ;         // [R][Lc] slot | cstart << 32 | clen << 48
-  int32_t* nwords;                 // [R]
-  int32_t* cnt;                    // [regions][2] short / mid records of each region
-  uint32_t* rs_slot;               // short records [regions * capS]
-  int32_t* rs_n;                   //   byte symbols (<= 16)
-  uint16_t* rs_sym;                //   [16] byte symbols, then ids
-  int32_t* rs_cps;                 //   [16] code points (-1 past the word: k_dw_emit's content check)
-  uint32_t* rm_slot;               // mid records [regions * capM]
-  int32_t* rm_n;
-  uint16_t* rm_sym;                //   [64]
-  int32_t* rm_cps;                 //   [64]
-  unsigned long long* table;       // [1 << log2cap] word keys, 0 = empty (the caller's, kept empty)
-  int log2cap, capS, capM, regions, nwv, Lc, S;
-  int key_shift;                   // 64 - BEAST_OPT_BPE_DEDUP_KEY_BITS
-  int ltab_log2;                   // k_dw_words' workgroup table: 1 << ltab_log2 > nwv * Lc words
-};
-
-__host__ __device__ inline int dw_capm(int Lc) { return Lc / 5 + 1; }   // a mid word spans >= 5 code points
-
-// per-row LDS of k_dw_words
+// per-row LDS of k_bpe_words
 __host__ __device__ inline size_t dw_row_bytes(int Lc, int S) {
   return 3 * al16(sizeof(int32_t) * (Lc + 1)) + al16(sizeof(int32_t) * Lc) + al16(sizeof(uint16_t) * S) +
          2 * al16(Lc) + 16;
 }
-// staging lists of one workgroup of nwv rows
-__host__ __device__ inline size_t dw_stage_bytes(int Lc, int nwv) {
-  return sizeof(uint4) * (size_t)nwv * ((size_t)Lc + dw_capm(Lc));
-}
-
-// the workgroup's word table (32-bit key, device slot): more slots than the rows can hold words
+// the workgroup's word table (32-bit hash, first occurrence): more slots than the rows can hold words
 __host__ __device__ inline int dw_ltab_log2(int Lc, int nwv) {
   int l = 4;
   while ((1ll << l) <= (long long)nwv * Lc) ++l;
@@ -801,22 +755,6 @@ __device__ inline DwRow dw_carve(char* p, int Lc, int S) {
   R.vis = (uint8_t*)take(Lc);
   R.misc = (int32_t*)take(16);
   return R;
-}
-
-__device__ __forceinline__ unsigned long long dw_mix(unsigned long long h) {   // splitmix64 finaliser
-  h ^= h >> 30; h *= 0xBF58476D1CE4E5B9ull;
-  h ^= h >> 27; h *= 0x94D049BB133111EBull;
-  return h ^ (h >> 31);
-}
-
-// a word's 64-bit key: FNV-1a over its code points, splitmix64-finalised, truncated (tests), odd
-__device__ __forceinline__ unsigned long long dw_word_key(const int32_t* cps, int cs, int ce, int key_shift) {
-  unsigned long long h = 0xCBF29CE484222325ull ^ (unsigned long long)(ce - cs);
-  for (int i = cs; i < ce; ++i) h = (h ^ (unsigned long long)(uint32_t)cps[i]) * 0x100000001B3ull;
-  return (dw_mix(h) >> key_shift) | 1ull;
-}
-__device__ __forceinline__ uint32_t dw_lkey(unsigned long long key) {   // nonzero; keeps truncated keys' bits
-  return (uint32_t)(key ^ (key >> 32)) | 1u;
 }
 
 // One row's pre-tokenisation into its LDS image (one wave): code points, the reference's range
@@ -877,7 +815,7 @@ __device__ __forceinline__ void dw_pretok_row(const EncArgs& a, const DwRow& L, 
   BPE_STAMP(2);
   if (st == ST_OK) {
     // 2. word starts (as k_bpe_encode, no special tokens); 3. byte symbols as vocab ids
-    for (int i = lane; i < n; i += 64) L.e[i] = regex_word(L.cps, L.cls, i, n);
+    beast_pt::regex_ends(L.cps, L.cls, L.wcp, L.e, n, lane);   // wcp: scratch until word_starts
     word_starts(L.e, L.vis, L.wcp, nullptr, L.misc, n, lane);
     BPE_STAMP(3);
     for (int i = lane; i < n; i += 64) {
@@ -892,170 +830,32 @@ __device__ __forceinline__ void dw_pretok_row(const EncArgs& a, const DwRow& L, 
   }
 }
 
-// k_dw_words: rows [blockIdx.x * nwv, +nwv), one per wave; region blockIdx.x
-__global__ __launch_bounds__(64 * DW_WAVES) void k_dw_words(EncArgs a, DwWs w) {
-  extern __shared__ __align__(16) char lds_raw[];
-  __shared__ int32_t s_b2i[256];
-  __shared__ uint8_t s_lut[256];
-  __shared__ int s_ns, s_nm;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    s_b2i[i] = a.byte2id[i];
-    s_lut[i] = i < a.lut_n ? a.lut[i] : (uint8_t)CLS_OTHER;
-  }
-  if (threadIdx.x == 0) { s_ns = 0; s_nm = 0; }
-  const int capS = nwv * w.Lc, capM = nwv * dw_capm(w.Lc);
-  uint4* stS = reinterpret_cast<uint4*>(lds_raw);
-  uint4* stM = stS + capS;
-  char* rows = lds_raw + dw_stage_bytes(w.Lc, nwv);
-  const size_t rb = dw_row_bytes(w.Lc, w.S);
-  const int lcap = 1 << w.ltab_log2;
-  uint32_t* lkey = reinterpret_cast<uint32_t*>(rows + (size_t)nwv * rb);
-  uint32_t* lval = lkey + lcap;
-  for (int i = threadIdx.x; i < lcap; i += blockDim.x) lkey[i] = 0u;
-  __syncthreads();
-  DwRow L = dw_carve(rows + (size_t)wave * rb, w.Lc, w.S);
-  const int64_t r = (int64_t)blockIdx.x * nwv + wave;
-#ifdef BPE_STAMPS
-  if (lane == 0 && r < BPE_RS) g_bpe_rs[r][10] = __builtin_amdgcn_s_memrealtime();
-#endif
-  int st = ST_OK, nw = 0;
-  if (r < a.n_rows) {
-    dw_pretok_row(a, L, r, lane, s_b2i, s_lut, w.S, st, nw);
-    BPE_STAMP(4);
-    if (st == ST_OK) {
-      // (a) the workgroup's table: one representative occurrence per distinct word of the
-      // workgroup's rows goes on to the device table.  (A 32-bit table key that two words share
-      // only merges their lookups: k_dw_emit's content check sends such rows to ST_FALLBACK.)
-      const uint32_t lmask = (uint32_t)lcap - 1u;
-      for (int k = lane; k < nw; k += 64) {
-        const uint32_t lk = dw_lkey(dw_word_key(L.cps, L.wcp[k], L.wcp[k + 1], w.key_shift));
-        uint32_t ls = (lk * 0x9E3779B1u) >> (32 - w.ltab_log2);
-        bool rep = false;
-        while (true) {
-          const uint32_t pv = atomicCAS(&lkey[ls], 0u, lk);
-          if (pv == 0u) { rep = true; break; }
-          if (pv == lk) break;
-          ls = (ls + 1) & lmask;
-        }
-        L.e[k] = (int32_t)(ls | (rep ? 0x80000000u : 0u));
-      }
-      wave_sync();
-      // (b) representatives: the device table, two words per lane per step with their first
-      // reads in flight together.  A plain (L2-served) read first: a CAS on one address
-      // serialises at the memory side; a stale empty read only costs one CAS that returns the key
-      const unsigned long long tmask = (1ull << w.log2cap) - 1ull;
-      for (int k0 = lane; k0 < nw; k0 += 128) {
-        int kk[2], cs[2], ce[2], bs[2], blen[2], le[2];
-        unsigned long long key[2], slot[2], prev[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          kk[u] = k0 + 64 * u;
-          le[u] = kk[u] < nw ? L.e[kk[u]] : 0;
-          const bool ok = le[u] < 0;   // a representative
-          cs[u] = ok ? L.wcp[kk[u]] : 0;
-          ce[u] = ok ? L.wcp[kk[u] + 1] : 0;
-          bs[u] = L.symoff[cs[u]];
-          blen[u] = L.symoff[ce[u]] - bs[u];
-          key[u] = dw_word_key(L.cps, cs[u], ce[u], w.key_shift);
-          slot[u] = (key[u] * 0x9E3779B97F4A7C15ull) >> (64 - w.log2cap);
-          prev[u] = ok ? __hip_atomic_load(&w.table[slot[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          if (le[u] >= 0) continue;
-          bool win = false;
-          unsigned long long pv = prev[u], sl = slot[u];
-          while (true) {
-            if (pv == 0ull) {
-              pv = atomicCAS(&w.table[sl], 0ull, key[u]);
-              if (pv == 0ull) { win = true; break; }
-            }
-            if (pv == key[u]) break;
-            sl = (sl + 1) & tmask;
-            pv = __hip_atomic_load(&w.table[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          lval[le[u] & 0x7FFFFFFF] = (uint32_t)sl;
-          if (win) {
-            const uint4 rec = make_uint4((uint32_t)sl, (uint32_t)r, (uint32_t)cs[u] | ((uint32_t)(ce[u] - cs[u]) << 16),
-                                         ((uint32_t)wave << 24) | ((uint32_t)blen[u] << 16) | (uint32_t)bs[u]);
-            if (blen[u] <= DW_SHORT) stS[atomicAdd(&s_ns, 1)] = rec;
-            else stM[atomicAdd(&s_nm, 1)] = rec;
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();   // every representative's device slot is in lval
-  if (r < a.n_rows) {
-    if (st == ST_OK) {
-      // (c) every occurrence: its word's device slot from the workgroup table
-      for (int k = lane; k < nw; k += 64) {
-        const int cs = L.wcp[k], ce = L.wcp[k + 1];
-        const uint32_t sl = lval[L.e[k] & 0x7FFFFFFF];
-        w.occ[r * w.Lc + k] = sl | ((unsigned long long)cs << 32) | ((unsigned long long)(ce - cs) << 48);
-      }
-    }
-    BPE_STAMP(5);
-    if (lane == 0) { a.status[r] = st; w.nwords[r] = st == ST_OK ? nw : 0; }
-#ifdef BPE_STAMPS
-    if (lane == 0 && r < BPE_RS) g_bpe_rs[r][9] = (unsigned long long)nw;
-#endif
-  }
-  __syncthreads();
-  // flush this region's records (byte symbols from the rows still in LDS)
-  const int ns = s_ns, nm = s_nm;
-  if (threadIdx.x == 0) { w.cnt[2 * blockIdx.x] = ns; w.cnt[2 * blockIdx.x + 1] = nm; }
-  // 16 lanes per short record and 64 per mid one (one lane per symbol / code point): coalesced
-  // stores instead of one thread writing a record's 32 scattered elements
-  const int lq = threadIdx.x & 15;
-  for (int i = threadIdx.x >> 4; i < ns; i += blockDim.x >> 4) {
-    const uint4 rec = stS[i];
-    const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
-    const int cs = rec.z & 0xFFFF, cl = rec.z >> 16;
-    const DwRow Rw = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S);
-    const int64_t idx = (int64_t)blockIdx.x * w.capS + i;
-    w.rs_sym[idx * DW_SHORT + lq] = lq < blen ? Rw.c[bs + lq] : (uint16_t)SYM_NONE;
-    w.rs_cps[idx * DW_SHORT + lq] = lq < cl ? Rw.cps[cs + lq] : -1;
-    if (lq == 0) {
-      w.rs_slot[idx] = rec.x;
-      w.rs_n[idx] = blen;
-      w.slot2idx[rec.x] = (uint32_t)idx;
-    }
-  }
-  for (int i = wave; i < nm; i += nwv) {
-    const uint4 rec = stM[i];
-    const int bs = rec.w & 0xFFFF, blen = (rec.w >> 16) & 0xFF, wv = rec.w >> 24;
-    const int cs = rec.z & 0xFFFF, cl = rec.z >> 16;
-    const DwRow Rw = dw_carve(rows + (size_t)wv * rb, w.Lc, w.S);
-    const int64_t idx = (int64_t)blockIdx.x * w.capM + i;
-    w.rm_sym[idx * DW_MID + lane] = lane < blen ? Rw.c[bs + lane] : (uint16_t)SYM_NONE;
-    w.rm_cps[idx * DW_MID + lane] = lane < cl ? Rw.cps[cs + lane] : -1;
-    if (lane == 0) {
-      w.rm_slot[idx] = rec.x;
-      w.rm_n[idx] = blen;
-      w.slot2idx[rec.x] = 0x80000000u | (uint32_t)idx;
-    }
-  }
-#ifdef BPE_STAMPS
-  __syncthreads();
-  if (r < a.n_rows) BPE_STAMP(6);
-#endif
-}
-
 // lane gl of a GW-lane group reads lane gl + 1 (down) / gl - 1 (up) of its group; `fill` past the ends
 template <int GW>
 __device__ __forceinline__ uint32_t grp_down1(uint32_t v, uint32_t fill) {
+  if constexpr (GW == 8) {   // row_shl:1, and the last lane of each half-row takes the fill
+    const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x101, 0xF, 0xF, false);
+    return (threadIdx.x & 7) == 7 ? fill : x;
+  }
   if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x101, 0xF, 0xF, false);
   else { const uint32_t x = (uint32_t)__shfl_down((int)v, 1); return (threadIdx.x & 63) == 63 ? fill : x; }
 }
 template <int GW>
 __device__ __forceinline__ uint32_t grp_up1(uint32_t v, uint32_t fill) {
+  if constexpr (GW == 8) {   // row_shr:1, and the first lane of each half-row takes the fill
+    const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x111, 0xF, 0xF, false);
+    return (threadIdx.x & 7) == 0 ? fill : x;
+  }
   if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x111, 0xF, 0xF, false);
   else { const uint32_t x = (uint32_t)__shfl_up((int)v, 1); return (threadIdx.x & 63) == 0 ? fill : x; }
 }
 template <int GW>
 __device__ __forceinline__ uint32_t grp_min(uint32_t v) {   // every lane of the group gets the group's min
+  if constexpr (GW == 8) {   // half-row mirror (lane i with 7 - i), then the quad's xor 2 and xor 1
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  }
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
@@ -1079,7 +879,12 @@ __device__ __forceinline__ uint32_t grp_compact(uint32_t sym, bool live, int gl,
   return gl < n ? got : SYM_NONE;
 }
 
-// HF Word::merge_all of one word per GW-lane group (see k_dw_merge); sym: the lane's byte symbol
+// HF Word::merge_all of one word per GW-lane group: words of <= 16 byte symbols four to a wave
+// (one 16-lane DPP row each), longer ones a wave each.  A round probes every adjacent pair's rank
+// in the merge map, takes the word's lowest (DPP row rotations), merges its occurrences left to
+// right (a self-pair run takes every other one) and compacts the word with one ds_permute.  For
+// models whose merges only combine tokens made by earlier merges (the host checks) this is HF's
+// merge_all.  raw: the lane's byte symbol
 // (SYM_NONE: no vocab id), blen: the word's byte symbols (0: no word).  Returns the lane's final
 // id (SYM_NONE past the end); n: the word's final length.
 template <int GW, class Map>
@@ -1131,182 +936,6 @@ __device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, i
     sym = grp_compact<GW>(sym, gl < n && !dies, gl, gbase, n);
   }
   return sym;
-}
-
-template <bool MAP_LDS>
-__global__ __launch_bounds__(64 * DW_WAVES) void k_dw_merge(EncArgs a, DwWs w) {
-  extern __shared__ __align__(16) char lds_raw[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  LdsMap lm;
-  if constexpr (MAP_LDS) {
-    const int cap = 1 << a.map.log2cap;
-    uint2* kv = reinterpret_cast<uint2*>(lds_raw);
-    const uint4* g = reinterpret_cast<const uint4*>(a.map.kv);
-    for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) reinterpret_cast<uint4*>(kv)[i] = g[i];
-    lm.kv = kv; lm.rank2new = nullptr; lm.log2cap = a.map.log2cap;
-  }
-  const int reg = blockIdx.x / DW_MSPLIT, part = blockIdx.x % DW_MSPLIT;
-  const int ns = w.cnt[2 * reg], nm = w.cnt[2 * reg + 1];
-  if constexpr (MAP_LDS) __syncthreads();
-  const int tasks = nm + (ns + 3) / 4;   // the mid words first: their rounds are the longest chains
-  // DW_MSPLIT workgroups share a region (task t to workgroup t / nwv % DW_MSPLIT): a region's
-  // merges are chains of dependent LDS round trips, so the CU wants more than its 16 waves
-  // a task's inputs (its words' byte symbols and lengths) are loaded one task ahead, without a
-  // dependence between them: entries past a region's count are never used
-  struct Task { int blen; uint32_t raw; };
-  auto load = [&](int t) -> Task {
-    Task k{0, SYM_NONE};
-    if (t >= tasks) return k;
-    if (t < nm) {
-      const int64_t idx = (int64_t)reg * w.capM + t;
-      k.blen = w.rm_n[idx];
-      k.raw = w.rm_sym[idx * DW_MID + lane];
-    } else {
-      const int kk = 4 * (t - nm) + (lane >> 4);
-      const int64_t idx = (int64_t)reg * w.capS + (kk < ns ? kk : 0);
-      k.blen = kk < ns ? w.rs_n[idx] : 0;
-      k.raw = w.rs_sym[idx * DW_SHORT + (lane & 15)];
-    }
-    return k;
-  };
-  const int t0 = part * nwv + wave, tstep = DW_MSPLIT * nwv;
-  int nrounds = 0, ntasks = 0;
-#ifdef BPE_STAMPS
-  const int msi = blockIdx.x * nwv + wave;
-  if (lane == 0 && msi < BPE_MS) g_bpe_ms[msi][0] = __builtin_amdgcn_s_memrealtime();
-#endif
-  Task cur = load(t0);
-  for (int t = t0; t < tasks; t += tstep) {
-    const Task nxt = load(t + tstep);
-    if (t < nm) {
-      const int64_t idx = (int64_t)reg * w.capM + t;
-      const uint32_t raw = lane < cur.blen ? cur.raw : SYM_NONE;
-      int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds)
-                                 : dw_merge_word<DW_MID>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds);
-      if (lane < n) w.rm_sym[idx * DW_MID + lane] = (uint16_t)v;
-      if (lane == 0) {
-        const uint32_t slot = w.rm_slot[idx];
-        w.slot2idx[slot] = 0x80000000u | ((uint32_t)n << 24) | (uint32_t)idx;
-        w.table[slot] = 0ull;
-      }
-    } else {
-      const int kk = 4 * (t - nm) + (lane >> 4), gl = lane & 15;
-      const bool valid = kk < ns;
-      const int64_t idx = (int64_t)reg * w.capS + (valid ? kk : 0);
-      const uint32_t raw = gl < cur.blen ? cur.raw : SYM_NONE;
-      int n;
-      const uint32_t v = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds)
-                                 : dw_merge_word<DW_SHORT>(a.map, raw, cur.blen, a.unk_id, a.fuse_unk, n, nrounds);
-      if (valid && gl < n) w.rs_sym[idx * DW_SHORT + gl] = (uint16_t)v;
-      if (valid && gl == 0) {
-        const uint32_t slot = w.rs_slot[idx];
-        w.slot2idx[slot] = ((uint32_t)n << 24) | (uint32_t)idx;
-        w.table[slot] = 0ull;
-      }
-    }
-    cur = nxt;
-    ++ntasks;
-  }
-#ifdef BPE_STAMPS
-  if (lane == 0 && msi < BPE_MS) {
-    g_bpe_ms[msi][1] = __builtin_amdgcn_s_memrealtime();
-    g_bpe_ms[msi][2] = (unsigned long long)ntasks;
-    g_bpe_ms[msi][3] = (unsigned long long)nrounds;
-  }
-#else
-  (void)nrounds; (void)ntasks;
-#endif
-}
-
-// k_dw_emit: one wave per row.  Three dependent round trips: the row's code points and its word
-// occurrences (together), the slots' records (ids count + index), the records' ids and code points
-// (wide loads of the whole record, compared and copied from registers: a per-element loop would
-// make the lane with the longest word a chain of dependent loads).
-__device__ __forceinline__ uint32_t u16_of(const uint4& a, const uint4& b, int q) {
-  const uint4& v = q < 8 ? a : b;
-  const int e = q & 7;
-  const uint32_t wd = (e >> 1) == 0 ? v.x : (e >> 1) == 1 ? v.y : (e >> 1) == 2 ? v.z : v.w;
-  return (e & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-}
-
-__global__ __launch_bounds__(BLOCK) void k_dw_emit(EncArgs a, DwWs w) {
-  extern __shared__ __align__(16) char lds_raw[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int32_t* cp = reinterpret_cast<int32_t*>(lds_raw) + (size_t)wave * (w.Lc + DW_MID);   // the row's code points
-  for (int64_t r = (int64_t)blockIdx.x * WAVES + wave; r < a.n_rows; r += (int64_t)gridDim.x * WAVES) {
-    if (a.status[r] != ST_OK) {
-      if (lane == 0) a.out_len[r] = 0;
-      continue;
-    }
-    const int nw = w.nwords[r];
-    const int64_t r0 = a.row_off[r];
-    const int n = (int)(a.row_off[r + 1] - r0);
-    for (int i = lane; i < n + DW_MID; i += 64) cp[i] = i < n ? (int32_t)(a.tok[r0 + i] - a.min_tok) : -1;
-    wave_sync();
-    int32_t* out = a.out_ids + r * a.out_stride;
-    int carry = 0;
-    bool bad = false;
-    for (int base = 0; base < nw; base += 64) {
-      const int k = base + lane;
-      int cnt = 0;
-      uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0;
-      const uint16_t* mid_ids = nullptr;
-      if (k < nw) {
-        const unsigned long long o = w.occ[r * w.Lc + k];
-        const int cs = (int)((o >> 32) & 0xFFFF), cl = (int)(o >> 48);
-        const uint32_t rec = w.slot2idx[(uint32_t)o];
-        const int64_t li = rec & 0xFFFFFFu;
-        cnt = (int)((rec >> 24) & 0x7F);
-        if (!(rec >> 31)) {   // short record: 16 ids (32 B) and 16 code points (64 B), -1 past the word
-          const uint4* ip = reinterpret_cast<const uint4*>(w.rs_sym + li * DW_SHORT);
-          const int4* cq = reinterpret_cast<const int4*>(w.rs_cps + li * DW_SHORT);
-          i0 = ip[0];
-          i1 = ip[1];
-          const int4 c0 = cq[0], c1 = cq[1], c2 = cq[2], c3 = cq[3];
-          const int rc[16] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w,
-                              c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w};
-          bad |= cl > DW_SHORT;
-#pragma unroll
-          for (int q = 0; q < DW_SHORT; ++q) bad |= rc[q] != (q < cl ? cp[cs + q] : -1);
-        } else {              // mid record (rare): 64 code points, four wide loads at a time
-          mid_ids = w.rm_sym + li * DW_MID;
-          const int4* cq = reinterpret_cast<const int4*>(w.rm_cps + li * DW_MID);
-#pragma unroll 1
-          for (int q0 = 0; q0 < DW_MID; q0 += 16) {
-            int4 c4[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) c4[t] = cq[q0 / 4 + t];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int rc[4] = {c4[t].x, c4[t].y, c4[t].z, c4[t].w};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int q = q0 + 4 * t + e;
-                bad |= rc[e] != (q < cl ? cp[cs + q] : -1);
-              }
-            }
-          }
-        }
-      }
-      int tot;
-      const int off = carry + wave_excl_scan(cnt, lane, tot);
-      if (mid_ids == nullptr) {
-#pragma unroll
-        for (int q = 0; q < DW_SHORT; ++q)
-          if (q < cnt) out[off + q] = (int32_t)u16_of(i0, i1, q);
-      } else {
-        for (int q = 0; q < cnt; ++q) out[off + q] = (int32_t)mid_ids[q];
-      }
-      carry += tot;
-    }
-    const bool coll = __any(bad);
-    if (lane == 0) {
-      a.out_len[r] = coll ? 0 : carry;
-      if (coll) a.status[r] = ST_FALLBACK;
-    }
-    wave_sync();   // cp is reused by the wave's next row
-  }
 }
 
 // ------------------------------------------------------- encode by words, one launch --
@@ -1430,9 +1059,12 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
   }
   __syncthreads();
   if (r < a.n_rows) BPE_STAMP(5);
-  // 4. merges: a mid word (17..64 byte symbols) per wave, short ones four to a wave
+  // 4. merges: a mid word (17..64 byte symbols) per wave, words of 9..16 four to a wave (16-lane
+  // rows), words of <= 8 eight to a wave (half rows)
   const int nmid = s_hist[DW_SHORT + 1];   // the cursor of length 17 has passed every longer word
-  const int tasks = nmid + (nd - nmid + 3) / 4;
+  const int n9 = s_hist[DW_TINY + 1];      // ... of length 9: every word of 9 or more
+  const int t16 = nmid + (n9 - nmid + 3) / 4;
+  const int tasks = t16 + (nd - n9 + 7) / 8;
   int nrounds = 0;
   for (int t = wave; t < tasks; t += nwv) {
     if (t < nmid) {
@@ -1446,9 +1078,9 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
                                   : dw_merge_word<DW_MID>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (lane < n) Rw.c[bs + lane] = (uint16_t)id;
       if (lane == 0) Rw.vis[k] = (uint8_t)n;
-    } else {
+    } else if (t < t16) {
       const int j = nmid + 4 * (t - nmid) + (lane >> 4), gl = lane & 15;
-      const bool valid = j < nd;
+      const bool valid = j < n9;
       const uint32_t v = valid ? ds[j] : 0u;
       const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
       const int k = (v >> 7) & 0x7FFF, blen = valid ? (int)(v & 127u) : 0;
@@ -1457,6 +1089,19 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
       int n;
       const uint32_t id = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
                                   : dw_merge_word<DW_SHORT>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
+      if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
+    } else {
+      const int j = n9 + 8 * (t - t16) + (lane >> 3), gl = lane & 7;
+      const bool valid = j < nd;
+      const uint32_t v = valid ? ds[j] : 0u;
+      const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
+      const int k = (v >> 7) & 0x7FFF, blen = valid ? (int)(v & 127u) : 0;
+      const int bs = valid ? Rw.symoff[Rw.wcp[k]] : 0;
+      const uint32_t raw = gl < blen ? (uint32_t)Rw.c[bs + gl] : SYM_NONE;
+      int n;
+      const uint32_t id = MAP_LDS ? dw_merge_word<DW_TINY>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
+                                  : dw_merge_word<DW_TINY>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
       if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
     }
@@ -1701,9 +1346,6 @@ int grid_for(int64_t n_rows, int per_cu = 4) {
 extern "C" int beast_debug_bpe_stamps(unsigned long long* host) {   // [4096][12]
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_rs), sizeof(g_bpe_rs)) == hipSuccess ? 0 : -2;
 }
-extern "C" int beast_debug_bpe_merge_stamps(unsigned long long* host) {   // [16384][4]
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_ms), sizeof(g_bpe_ms)) == hipSuccess ? 0 : -2;
-}
 #endif
 
 extern "C" int beast_bpe_mergemap_log2cap(int n_merges) {
@@ -1814,44 +1456,6 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
 }
 
 
-// ------------------------------------------------------- word dedup, host --
-static size_t dw_words_lds(int Lc, int S, int nwv) {
-  return dw_stage_bytes(Lc, nwv) + (size_t)nwv * dw_row_bytes(Lc, S) + dw_ltab_bytes(Lc, nwv);
-}
-static int dw_nwv(int Lc, int S) {   // rows per k_dw_words workgroup: as many as the LDS holds, <= 16
-  const size_t room = LDS_BUDGET - STATIC_LDS;
-  for (int nv = DW_WAVES; nv > 0; --nv)
-    if (dw_words_lds(Lc, S, nv) <= room) return nv;
-  return 0;
-}
-
-static size_t dw_carve_host(DwWs& w, char* base, int64_t R, int Lc, int S, int log2cap) {
-  w.nwv = dw_nwv(Lc, S);
-  const int nwv = w.nwv > 0 ? w.nwv : 1;
-  w.Lc = Lc; w.S = S; w.log2cap = log2cap;
-  w.ltab_log2 = dw_ltab_log2(Lc, nwv);
-  w.regions = (int)((R + nwv - 1) / nwv);
-  w.capS = nwv * Lc;
-  w.capM = nwv * dw_capm(Lc);
-  size_t o = 0;
-  auto take = [&](size_t bytes) { char* r = base ? base + o : nullptr; o += al16(bytes); return r; };
-  const size_t nS = (size_t)w.regions * w.capS, nM = (size_t)w.regions * w.capM;
-  w.slot2idx = (uint32_t*)take(sizeof(uint32_t) << log2cap);
-  w.occ = (unsigned long long*)take(sizeof(unsigned long long) * (size_t)R * Lc);
-  w.nwords = (int32_t*)take(sizeof(int32_t) * (size_t)R);
-  w.cnt = (int32_t*)take(sizeof(int32_t) * 2 * (size_t)w.regions);
-  w.rs_slot = (uint32_t*)take(sizeof(uint32_t) * nS);
-  w.rs_n = (int32_t*)take(sizeof(int32_t) * nS);
-  w.rs_sym = (uint16_t*)take(sizeof(uint16_t) * DW_SHORT * nS);
-  w.rs_cps = (int32_t*)take(sizeof(int32_t) * DW_SHORT * nS);
-  w.rm_slot = (uint32_t*)take(sizeof(uint32_t) * nM);
-  w.rm_n = (int32_t*)take(sizeof(int32_t) * nM);
-  w.rm_sym = (uint16_t*)take(sizeof(uint16_t) * DW_MID * nM);
-  w.rm_cps = (int32_t*)take(sizeof(int32_t) * DW_MID * nM);
-  return o;
-}
-
-
 extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows,
                                            int64_t min_tok, int64_t max_span, const uint8_t* cls_lut, int64_t lut_n,
                                            const int32_t* byte2id, const void* map, int n_merges, int unk_id,
@@ -1902,80 +1506,6 @@ extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* ro
   BEAST_LAUNCHED("k_bpe_words");
   return BEAST_OK;
 }
-
-extern "C" int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps) {
-  const int64_t words = std::max<int64_t>(1, n_rows) * std::max(1, max_row_cps);
-  return std::max(10, log2_ceil(2 * words));
-}
-
-extern "C" size_t beast_bpe_encode_dedup_workspace_bytes(int64_t n_rows, int max_row_cps, int max_row_syms,
-                                                        int table_log2) {
-  if (n_rows < 0 || max_row_cps < 0 || max_row_syms < 0 || table_log2 < 1 || table_log2 > 31) return 0;
-  DwWs w;
-  return dw_carve_host(w, nullptr, n_rows, max_row_cps, max_row_syms, table_log2);
-}
-
-extern "C" int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int64_t n_rows,
-                                           int64_t min_tok, int64_t max_span, const uint8_t* cls_lut, int64_t lut_n,
-                                           const int32_t* byte2id, const void* map, int n_merges, int unk_id,
-                                           int fuse_unk, int max_row_cps, int max_row_syms, uint64_t* table,
-                                           int table_log2, void* ws, size_t ws_bytes, int32_t* out_ids,
-                                           int64_t out_stride, int32_t* out_len, int32_t* status, void* stream) {
-  BEAST_REQUIRE(n_rows >= 0, "n_rows must be >= 0");
-  if (n_rows == 0) return BEAST_OK;
-  BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && map && table && ws && out_ids && out_len && status,
-                "null pointer argument");
-  BEAST_REQUIRE(lut_n > 0 && lut_n <= 65536, "class LUT size %lld out of range", (long long)lut_n);
-  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
-  BEAST_REQUIRE(max_row_cps >= 0 && max_row_cps < 32768, "max_row_cps %d out of range", max_row_cps);
-  BEAST_REQUIRE(max_row_syms >= 0 && max_row_syms <= 16384, "max_row_syms %d out of range", max_row_syms);
-  BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
-  BEAST_REQUIRE(table_log2 >= beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps) && table_log2 <= 31,
-                "table_log2 %d below beast_bpe_encode_dedup_table_log2 (%d)", table_log2,
-                beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps));
-  BEAST_REQUIRE_CODE(n_rows * (int64_t)std::max(1, max_row_cps) < (int64_t(1) << 24), BEAST_E_UNSUPPORTED,
-                     "n_rows x max_row_cps must stay below 2^24 (record indices); encode in chunks");
-  BEAST_REQUIRE_CODE(dw_nwv(max_row_cps, max_row_syms) > 0, BEAST_E_UNSUPPORTED,
-                     "rows of %d code points exceed k_dw_words' LDS budget", max_row_cps);
-  DwWs w;
-  const size_t need = dw_carve_host(w, static_cast<char*>(ws), n_rows, max_row_cps, max_row_syms, table_log2);
-  BEAST_REQUIRE_CODE(ws_bytes >= need, BEAST_E_WORKSPACE, "dedup workspace too small: %zu < %zu", ws_bytes, need);
-  w.table = reinterpret_cast<unsigned long long*>(table);
-  w.key_shift = 64 - beast::g_bpe_dedup_key_bits;
-  EncArgs a{};
-  a.tok = reinterpret_cast<const long long*>(tok);
-  a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
-  a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
-  a.map = map_view(map, n_merges);
-  a.n_merges = n_merges;
-  a.unk_id = unk_id; a.fuse_unk = fuse_unk;
-  a.Lc = max_row_cps; a.S = max_row_syms;
-  a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
-  hipStream_t s = beast::as_stream(stream);
-  const size_t lds1 = dw_words_lds(w.Lc, w.S, w.nwv);
-  if (lds1 > 65536)
-    BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_words),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1),
-              "hipFuncSetAttribute(k_dw_words)");
-  hipLaunchKernelGGL(k_dw_words, dim3(w.regions), dim3(64 * w.nwv), lds1, s, a, w);
-  BEAST_LAUNCHED("k_dw_words");
-  const size_t map_lds = a.map.log2cap <= LDS_MAP_MAX_LOG2 ? al16(sizeof(uint2) << a.map.log2cap) : 0;
-  if (map_lds > 0) {
-    if (map_lds > 65536)
-      BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_merge<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds),
-                "hipFuncSetAttribute(k_dw_merge)");
-    hipLaunchKernelGGL(k_dw_merge<true>, dim3(w.regions * DW_MSPLIT), dim3(64 * DW_WAVES), map_lds, s, a, w);
-  } else {
-    hipLaunchKernelGGL(k_dw_merge<false>, dim3(w.regions * DW_MSPLIT), dim3(64 * DW_WAVES), 0, s, a, w);
-  }
-  BEAST_LAUNCHED("k_dw_merge");
-  hipLaunchKernelGGL(k_dw_emit, dim3(grid_for(n_rows, 8)), dim3(BLOCK), sizeof(int32_t) * WAVES * (size_t)(w.Lc + DW_MID),
-                     s, a, w);
-  BEAST_LAUNCHED("k_dw_emit");
-  return BEAST_OK;
-}
-
 
 extern "C" int beast_bpe_decode_rows(const int32_t* ids, const int64_t* row_off, int64_t n_rows,
                                      const int32_t* tok_off, const uint8_t* tok_bytes, const uint8_t* tok_skip,

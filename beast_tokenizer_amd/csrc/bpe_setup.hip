@@ -221,13 +221,10 @@ __global__ __launch_bounds__(64 * PT_WAVES) void k_pretok_wave(
         L.cls[i] = (c >= 0 && c < 256) ? s_lut[c] : (c >= 0 && c < lut_n) ? lut[c] : (uint8_t)CLS_OTHER;
         len = utf8_len(c);
       }
-      int x = len;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-      }
-      if (i < n) L.so[i] = (int16_t)(carry + x - len);
-      carry += __shfl(x, 63);
+      int tot;
+      const int ex = beast_pt::wave_excl_scan(len, lane, tot);
+      if (i < n) L.so[i] = (int16_t)(carry + ex);
+      carry += tot;
     }
     if (__any(serial)) {   // wave-uniform
       if (lane == 0)
@@ -239,8 +236,7 @@ __global__ __launch_bounds__(64 * PT_WAVES) void k_pretok_wave(
     pt_wave_sync();
     // 2. the end of the word that starts at every position (pretok_serial's rules), 3. the word
     //    chain 0 -> e[0] -> ... walked lane-parallel (csrc/pretok.h; round 3 walked it on lane 0)
-    for (int i = lane; i < n; i += 64) L.e[i] = beast_pt::regex_word(L.cp, L.cls, i, n);
-    pt_wave_sync();
+    beast_pt::regex_ends(L.cp, L.cls, L.wcp, L.e, n, lane);   // wcp: scratch until word_starts
     beast_pt::word_starts(L.e, L.vis, L.wcp, nullptr, &L.nw, n, lane);
     const int nw = L.nw;
     if (!EMIT) {

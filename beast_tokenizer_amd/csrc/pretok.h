@@ -43,14 +43,59 @@ __device__ __forceinline__ int regex_word(const int32_t* cps, const uint8_t* cls
   return j;
 }
 
+// Exclusive prefix sum over the wave (all 64 lanes active) by DPP: row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast:15 / row_bcast:31 carry the rows' totals -- no LDS round trip (a
+// __shfl_up ladder is six ds_bpermute round trips).
 __device__ __forceinline__ int wave_excl_scan(int v, int lane, int& total) {
   int x = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  total = __shfl(x, 63);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+  total = __builtin_amdgcn_readlane(x, 63);
+  (void)lane;
   return x - v;
+}
+
+// e[i] = regex_word(cps, cls, i, n) for every i, without the per-position class-run loops: the
+// end of each class run comes from one ballot per 64 positions (run[p] = one past the last
+// position of p's run; scratch [n]), so every lane's regex end is a few independent reads.
+__device__ __forceinline__ void regex_ends(const int32_t* cps, const uint8_t* cls, int32_t* run, int32_t* e, int n,
+                                           int lane) {
+  int carry = n;   // one past the first run end in the chunks after the current one
+  for (int base = (n - 1) & ~63; base >= 0; base -= 64) {
+    const int p = base + lane;
+    const bool in = p < n;
+    const int c0 = in ? (int)cls[p] : -1;
+    const int c1 = p + 1 < n ? (int)cls[p + 1] : -2;
+    const unsigned long long m = __ballot(in && c0 != c1);   // p ends its run
+    const unsigned long long rest = m >> lane;
+    if (in) run[p] = rest ? p + __builtin_ctzll(rest) + 1 : carry;
+    if (m) carry = base + __builtin_ctzll(m) + 1;
+  }
+  wave_sync();
+  for (int i = lane; i < n; i += 64) {
+    const int c = cps[i];
+    const int c1 = i + 1 < n ? cps[i + 1] : -1, c2 = i + 2 < n ? cps[i + 2] : -1;
+    const int k0 = cls[i], k1 = i + 1 < n ? (int)cls[i + 1] : CLS_WS;
+    int j;
+    if (c == '\'' && (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd')) {
+      j = i + 2;
+    } else if (c == '\'' && ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l'))) {
+      j = i + 3;
+    } else if (c == ' ' && i + 1 < n && k1 != CLS_WS) {
+      j = run[i + 1];                      // " ?" + the run of the next code point's class
+    } else if (k0 != CLS_WS) {
+      j = run[i];
+    } else {
+      j = run[i];                          // \s+, giving back the last blank before a non-blank
+      if (j < n && j - i >= 2) --j;
+    }
+    e[i] = j;
+  }
+  wave_sync();
 }
 
 // The word starts of a row from e[i], the end of the regex word that would

@@ -583,7 +583,7 @@ def hf_bpe_same_sample(rows: torch.Tensor, vocab: int):
 def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     """Per-row BPE inference with the trained model: the reference's
     _discrete_to_bpe / _bpe_to_discrete loops (beast_bspline_bpe_tokenizer.py:175-247) as one
-    k_bpe_encode / k_bpe_decode launch per batch.  Kernel rows/s from HIP events over
+    k_bpe_words (the per-row k_bpe_encode timed beside it) / k_bpe_decode launch per batch.  Kernel rows/s from HIP events over
     back-to-back launches on the kernel's stream; API rows/s include the host list build."""
     from beast_tokenizer_amd.beast_bpe_trainer import tokenizer_from_result
     from beast_tokenizer_amd.bpe_codec import GpuBpeModel, rows_from_tensor
@@ -601,7 +601,7 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     def launch_enc():   # resolve=False: no host sync inside the timed launches (status checked below)
         enc["r"] = model.encode_rows(flat, off, width, lo, span, resolve=False)
     t_enc = kernel_time_us(launch_enc, stream, reps=20, rounds=3)
-    path = "dedup" if model._dedup_ok() else "rows"
+    path = "words" if model._words_ok() else "rows"
     st_enc = enc["r"][2]
     n_fallback = int((st_enc == 7).sum())
     set_encode_path("rows")                      # the per-row kernel beside it (same ids)
@@ -614,7 +614,7 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
     ids, lens, _ = enc["r"]
     live = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]
     assert torch.equal(lens, rows_ref[1]) and torch.equal(ids[live], rows_ref[0][:, :ids.shape[1]][live]), \
-        "dedup encode != per-row encode"
+        "by-words encode != per-row encode"
     lens_np = lens.cpu().numpy()
     n_ids = int(lens_np.sum())
     mask = torch.arange(ids.shape[1], device=dev)[None, :] < lens[:, None]

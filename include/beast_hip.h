@@ -53,8 +53,9 @@ const char* beast_last_error(void);
  * BEAST_OPT_BPE_ENCODE_MODE = m (tests, measurements): beast_bpe_encode_rows' per-word merge by
  * rounds (0, the default) or by HF's min-heap (1); m + 2 also launches one workgroup per 4 rows
  * instead of only the resident ones.  Results are identical.
- * BEAST_OPT_BPE_DEDUP_KEY_BITS = k (tests): beast_bpe_encode_rows_dedup keeps only k bits of its
- * 64-bit word keys, so different words collide; the collisions are detected (ST_FALLBACK rows).
+ * BEAST_OPT_BPE_DEDUP_KEY_BITS = k (tests): beast_bpe_encode_rows_words keeps only k bits of its
+ * 32-bit word hashes, so different words share hashes; the code-point compare behind every hash
+ * match keeps them apart (same ids).
  * Options are process-wide and not synchronised: set them before launching, not concurrently. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
@@ -356,29 +357,13 @@ int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_
                           const int32_t* spec_id, int n_spec, int unk_id, int fuse_unk, int max_row_cps,
                           int max_row_syms, int32_t* out_ids, int64_t out_stride, int32_t* out_len,
                           int32_t* status, void* stream);
-/* The same encode, each distinct word of the batch merged once (round 4; bit-exact with
- * beast_bpe_encode_rows for models whose merges only combine tokens made by earlier merges --
- * every trained model; the caller checks and uses beast_bpe_encode_rows otherwise, or when the
- * model has special tokens).  Three launches: word split + key insert, one merge per distinct
- * word, emit.  status as above plus 7 (ST_FALLBACK): the row holds a word of more than 64 byte
- * symbols, or a 64-bit word-key collision was detected; the caller re-encodes such rows with
- * beast_bpe_encode_rows.  table: 2^table_log2 uint64 word keys, table_log2 >=
- * beast_bpe_encode_dedup_table_log2(n_rows, max_row_cps), zero-filled before its first use; every
- * call leaves it zero again (reuse it across calls, not across concurrent streams).  ws: scratch
- * of beast_bpe_encode_dedup_workspace_bytes bytes (no initialisation).  n_rows * max_row_cps < 2^24 (larger
- * batches: call per chunk of rows). */
-int beast_bpe_encode_dedup_table_log2(int64_t n_rows, int max_row_cps);
-size_t beast_bpe_encode_dedup_workspace_bytes(int64_t n_rows, int max_row_cps, int max_row_syms, int table_log2);
-int beast_bpe_encode_rows_dedup(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
-                                int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
-                                const void* map, int n_merges, int unk_id, int fuse_unk, int max_row_cps,
-                                int max_row_syms, uint64_t* table, int table_log2, void* ws, size_t ws_bytes,
-                                int32_t* out_ids, int64_t out_stride, int32_t* out_len, int32_t* status,
-                                void* stream);
-/* The same encode in one launch, no workspace: each workgroup pre-tokenises its rows (up to 16),
- * merges every distinct word among them once (exact dedup by code points in LDS) and gathers
- * each row's ids.  Same model condition and statuses as beast_bpe_encode_rows_dedup; 7
- * (ST_FALLBACK) only for a word of more than 64 byte symbols. */
+/* The same encode by words (round 4), one launch, no workspace: each workgroup pre-tokenises
+ * its rows (up to 16), merges every distinct word among them once (exact dedup by code points in
+ * LDS) and gathers each row's ids.  Bit-exact with beast_bpe_encode_rows for models whose merges
+ * only combine tokens made by earlier merges -- every trained model; the caller checks and uses
+ * beast_bpe_encode_rows otherwise, or when the model has special tokens.  status as above plus
+ * 7 (ST_FALLBACK): the row holds a word of more than 64 byte symbols; the caller re-encodes such
+ * rows with beast_bpe_encode_rows. */
 int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
                                 int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
                                 const void* map, int n_merges, int unk_id, int fuse_unk, int max_row_cps,

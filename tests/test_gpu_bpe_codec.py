@@ -51,11 +51,11 @@ def decode_rows(model, id_rows, dev, L):
     return [out[i, :counts[i]].tolist() for i in range(len(seqs))], counts, status.cpu().numpy()
 
 
-@pytest.fixture(params=[("auto", 0), ("dedup3", 0), ("rows", 0), ("rows", 1), ("rows", 3)],
-                ids=["words", "dedup3", "rounds", "heap", "heap_wide_grid"])
+@pytest.fixture(params=[("auto", 0), ("rows", 0), ("rows", 1), ("rows", 3)],
+                ids=["words", "rounds", "heap", "heap_wide_grid"])
 def encode_mode(request):
-    """The word-dedup encode (the default: k_dw_words / k_dw_merge / k_dw_emit, falling back to
-    k_bpe_encode where it must) and k_bpe_encode itself with its per-word merge by rounds or by
+    """The by-words encode (the default: k_bpe_words, falling back to k_bpe_encode where it
+    must) and k_bpe_encode itself with its per-word merge by rounds or by
     HF's heap, and its grid: same ids."""
     from beast_tokenizer_amd import _lib
     from beast_tokenizer_amd.bpe_codec import set_encode_path
@@ -207,8 +207,8 @@ def _trained_model(span, rows, width, vocab, seed, gpu_device):
     return tok, GpuBpeModel(tok, gpu_device), rng, centre
 
 
-def test_dedup_fallback_rows_for_long_words(gpu_device):
-    """Rows holding a word of more than 64 byte symbols come back ST_FALLBACK from the dedup path
+def test_words_fallback_rows_for_long_words(gpu_device):
+    """Rows holding a word of more than 64 byte symbols come back ST_FALLBACK from k_bpe_words
     (resolve=False) and are re-encoded by k_bpe_encode (resolve=True): HF's ids either way."""
     from beast_tokenizer_amd.bpe_codec import ST_FALLBACK
     tok, model, rng, _ = _trained_model(255, 800, 120, 1200, 5, gpu_device)
@@ -250,42 +250,7 @@ def test_words_hash_collisions_are_exact(bits, gpu_device):
         assert ids[i, :lens[i]].tolist() == want[i]
 
 
-@pytest.mark.parametrize("bits", [3, 8, 20])
-def test_dedup_key_collisions_are_detected(bits, gpu_device):
-    """The three-launch form with only `bits` bits of the 64-bit word keys: different words share
-    keys, every such row is caught by the content check (ST_FALLBACK, never a wrong id) and
-    re-encoded per row."""
-    from beast_tokenizer_amd import _lib
-    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK, set_encode_path
-    tok, model, rng, centre = _trained_model(255, 1500, 140, 2048, 9, gpu_device)
-    test = np.clip(centre[:1000] + np.round(rng.normal(0, 255 / 8, size=(1000, 140))), 0, 255).astype(np.int64)
-    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
-    flat, off, width = rows_from_sequences(list(test), gpu_device)
-    set_encode_path("dedup3")
-    try:
-        st0 = model.encode_rows(flat, off, width, 0, 255, resolve=False)[2].cpu().numpy()   # long-word rows only
-        _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, bits)
-        try:
-            ids, lens, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
-            ids, lens, st = ids.cpu().numpy(), lens.cpu().numpy(), st.cpu().numpy()
-            ok = st == 0
-            assert (st[~ok] == ST_FALLBACK).all() and (st[st0 == ST_FALLBACK] == ST_FALLBACK).all()
-            if bits <= 8:
-                assert (~ok).sum() > (st0 != 0).sum() + 100          # many rows hit a collision
-            for i in np.flatnonzero(ok):          # the rows that passed the check are HF's
-                assert ids[i, :lens[i]].tolist() == want[i]
-            got, status = encode_rows(model, list(test), gpu_device)
-            assert not status.any() and got == want
-        finally:
-            _lib.run("beast_set_option", _lib.OPT_BPE_DEDUP_KEY_BITS, 64)
-        # the table is left empty: a normal call right after falls back on the long-word rows only
-        _, _, st = model.encode_rows(flat, off, width, 0, 255, resolve=False)
-        assert np.array_equal(st.cpu().numpy(), st0)
-    finally:
-        set_encode_path("auto")
-
-
-def test_dedup_non_monotone_model_uses_heap(gpu_device):
+def test_words_non_monotone_model_uses_heap(gpu_device):
     """A hand-written model whose merges are not rank-monotone ("aa" + "a" ranked before "a" + "a")
     takes k_bpe_encode with HF's heap: HF's ids, where merging a word's lowest pair everywhere at
     once would not be."""

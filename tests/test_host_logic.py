@@ -262,7 +262,7 @@ def test_rows_to_lists_matches_numpy():
 
 
 def test_rank_monotone_check():
-    """bpe_codec.rank_monotone decides whether the word-dedup encode (lowest pair merged everywhere
+    """bpe_codec.rank_monotone decides whether the by-words encode (lowest pair merged everywhere
     at once) is HF's heap order for a model."""
     from beast_tokenizer_amd.bpe_codec import rank_monotone
     assert rank_monotone([(0, 1, 5), (5, 2, 6), (1, 2, 7)])

@@ -1,5 +1,5 @@
-"""Encode A/B on the bench's codec workload (tools only): k_bpe_words (one launch), the
-three-launch device-table form and the per-row kernel -- same ids, event time per call.
+"""Encode A/B on the bench's codec workload (tools only): k_bpe_words and the per-row kernel --
+same ids, event time per call (each path twice, interleaved).
     python tools/codec/words_ab.py [N]
 """
 import json
@@ -17,7 +17,7 @@ def main():
     n_launch = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     dev, model, args = setup()
     out, ref = {}, None
-    for path in ("rows", "auto", "dedup3", "auto"):
+    for path in ("rows", "auto", "rows", "auto"):
         set_encode_path(path)
         ids, lens, st = model.encode_rows(*args, resolve=False)
         torch.cuda.synchronize()

@@ -42,9 +42,7 @@ KERNELS = {
     "k_merge_batch": lambda n: "k_merge_batch(" in n,
     "k_apply_batch": lambda n: "k_apply_batch<" in n,
     "k_bpe_encode": lambda n: "k_bpe_encode<" in n,
-    "k_dw_words": lambda n: "k_dw_words(" in n,
-    "k_dw_merge": lambda n: "k_dw_merge<" in n,
-    "k_dw_emit": lambda n: "k_dw_emit(" in n,
+    "k_bpe_words": lambda n: "k_bpe_words<" in n,
     "k_bpe_decode": lambda n: "k_bpe_decode(" in n,
 }
 
