@@ -561,9 +561,8 @@ __device__ __forceinline__ void bar_only() {
 // OPS wave-instructions of 16-byte LDS-DMA from each of the PIPE_MW DMA waves: slot
 // i = op * PIPE_MT + tid of the destination <- source float4 min(first + i, last).
 template <int OPS>
-__device__ __forceinline__ void dma16_fixed(void* lds, const float4* src, int64_t first, int64_t last,
-                                            int tid = threadIdx.x) {
-  const int wb = tid & ~63;
+__device__ __forceinline__ void dma16_fixed(void* lds, const float4* src, int64_t first, int64_t last) {
+  const int tid = threadIdx.x, wb = tid & ~63;
 #pragma unroll
   for (int op = 0; op < OPS; ++op)
     __builtin_amdgcn_global_load_lds(src + min(first + op * PIPE_MT + tid, last),
@@ -730,24 +729,11 @@ __global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(const float* __rest
       dma4<PIPE_MT>(whi, a.w_max, PS::DN);
     }
     dma4<PIPE_MT>(lcol, a.dof_src, PS::D);
-#ifndef BEAST_PIPE_YB_STORE_WAVES
     dma16_fixed<PS::Y_OPS>(YB, src, min(last, (b0 + PIPE_SUB) * tile16), min(last, (b0 + 2 * PIPE_SUB) * tile16 - 1));
     STAMP(0, 1);
     wait_vm_lgkm<PS::Y_OPS>();   // A and the constants have landed (B's DMA is the newest)
-#else
-    STAMP(0, 1);
-    wait_vm_lgkm<0>();           // A and the constants have landed
-#endif
     STAMP(0, 2);
   }
-#ifdef BEAST_PIPE_YB_STORE_WAVES
-  else {   // the store waves fetch sub-tile B: the fit waves' first wait covers A only
-    const float4* src = reinterpret_cast<const float4*>(traj);
-    const int64_t last = B * tile16 - 1;
-    dma16_fixed<PS::Y_OPS>(YB, src, min(last, (b0 + PIPE_SUB) * tile16), min(last, (b0 + 2 * PIPE_SUB) * tile16 - 1),
-                           tid - PIPE_MT);
-  }
-#endif
   bar_only();
   if (mw) {
     pipe_fit<S>(g, m, P, YA, lcol, pbA, nbA, wave, lane);
