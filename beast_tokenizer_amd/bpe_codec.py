@@ -24,6 +24,7 @@ pre-tokenisers) raise ``NotImplementedError``.
 """
 from __future__ import annotations
 
+import ctypes
 import itertools
 import json
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -120,6 +121,15 @@ class GpuBpeModel:
                      _lib.stream_of(device))
             mt = None
         self._keep = mt   # the build reads it asynchronously
+        # k_bpe_words' merge map: a bucketed cuckoo table built on the host (one LDS round trip a lookup)
+        wm_bytes = int(lib.beast_bpe_wordmap_bytes(self.n_merges))
+        wm_host = np.zeros(wm_bytes // 4, dtype=np.uint32)
+        arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in (ma, mb, mn)]
+        lb = ctypes.c_int(0)
+        _lib.run("beast_bpe_wordmap_build_host", *[x.ctypes.data if self.n_merges else None for x in arrs],
+                 self.n_merges, wm_host.ctypes.data, wm_bytes, ctypes.byref(lb))
+        self.wordmap_log2b = lb.value
+        self.wordmap = torch.from_numpy(wm_host[:4 << lb.value].view(np.int32).copy()).to(device)
         self.monotone = rank_monotone(list(zip(ma, mb, mn)))
         self._max_id = max(vocab.values()) if vocab else 0   # 0xFFFF marks "no id" in k_bpe_words
 
@@ -257,7 +267,7 @@ class GpuBpeModel:
             return ids[:0], st[0, :0], st[1, :0]
         _lib.run("beast_bpe_encode_rows_words", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
                  -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
-                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.unk_id, self.fuse_unk,
+                 self.byte2id.data_ptr(), self.wordmap.data_ptr(), self.wordmap_log2b, self.unk_id, self.fuse_unk,
                  int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(),
                  st[1].data_ptr(), _lib.stream_of(dev))
         return ids[:R], st[0, :R], st[1, :R]

@@ -81,6 +81,20 @@ __device__ __forceinline__ uint32_t mm_hash(uint32_t key, int log2cap) {
   return (key * 0x9E3779B1u) >> (32 - log2cap);
 }
 
+// k_bpe_words' merge map: two-choice bucketed cuckoo hashing, 1 << log2b buckets of two (key,
+// value) slots (16 bytes), every key in one of its two buckets -- a lookup is exactly two 16-byte
+// reads, one LDS round trip, where a linear-probe chain is a loop whose longest lane sets the
+// wave's pace.  Built on the host (beast_bpe_wordmap_build_host); same key / value encoding as
+// the merge map above.
+struct WordMap {
+  const uint4* b;
+  int log2b;
+};
+__host__ __device__ __forceinline__ uint32_t wm_h1(uint32_t key, int log2b) { return (key * 0x9E3779B1u) >> (32 - log2b); }
+__host__ __device__ __forceinline__ uint32_t wm_h2(uint32_t key, int log2b) {
+  return ((key ^ 0x5BD1E995u) * 0x85EBCA77u) >> (32 - log2b);
+}
+
 __global__ void k_mergemap_clear(uint2* __restrict__ kv, int cap) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < cap) kv[i] = make_uint2(EMPTY_KEY, 0u);
@@ -887,8 +901,8 @@ __device__ __forceinline__ uint32_t grp_compact(uint32_t sym, bool live, int gl,
 // merge_all.  raw: the lane's byte symbol
 // (SYM_NONE: no vocab id), blen: the word's byte symbols (0: no word).  Returns the lane's final
 // id (SYM_NONE past the end); n: the word's final length.
-template <int GW, class Map>
-__device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, int blen, int unk_id, int fuse_unk,
+template <int GW>
+__device__ __forceinline__ uint32_t dw_merge_word(const WordMap& mm, uint32_t raw, int blen, int unk_id, int fuse_unk,
                                                   int& n, int& rounds) {
   const int lane = threadIdx.x & 63, gl = lane & (GW - 1), gbase = lane - gl;
   // HF BPE::merge_word's unknown chars: unk_id (consecutive ones fused when fuse_unk), or dropped
@@ -898,31 +912,24 @@ __device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, i
   const bool live = in && !(miss && (unk_id < 0 || (fuse_unk && pmiss)));
   const uint32_t id = miss ? (uint32_t)unk_id : raw;
   uint32_t sym = grp_compact<GW>(id, live, gl, gbase, n);
-  const uint32_t mmask = (1u << mm.log2cap) - 1u;
   for (int round = 0; round < DW_MID; ++round) {   // each round merges >= 1 pair: <= 63 rounds
     const uint32_t right = grp_down1<GW>(sym, SYM_NONE);
     const bool has = gl + 1 < n;
     uint32_t rk = RK_NONE;
     if (has) {
-      // four probe slots read together (one LDS round trip for almost every chain: the map is
-      // <= half full, and most pairs are misses, whose linear-probe chains average two slots)
       const uint32_t key = (sym << 16) | right;
-      uint32_t h = mm_hash(key, mm.log2cap);
-      for (bool done = false; !done; h = (h + 4) & mmask) {
-        uint2 e[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) e[q] = mm.kv[(h + q) & mmask];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (!done && e[q].x == key) rk = e[q].y - 0x10000u;   // (rank + 1) << 16 | new_id -> rank << 16 | new_id
-          done |= e[q].x == key || e[q].x == EMPTY_KEY;
-        }
-      }
+      const uint4 b1 = mm.b[wm_h1(key, mm.log2b)], b2 = mm.b[wm_h2(key, mm.log2b)];
+      const uint32_t v = b1.x == key ? b1.y : b1.z == key ? b1.w : b2.x == key ? b2.y : b2.z == key ? b2.w : 0u;
+      rk = v ? v - 0x10000u : RK_NONE;   // (rank + 1) << 16 | new_id -> rank << 16 | new_id
     }
     const uint32_t m = grp_min<GW>(rk);
     if (!__any(m != RK_NONE)) break;
     ++rounds;
     const bool match = has && m != RK_NONE && rk == m;
+#ifdef BEAST_WORDS_SELFPAIR_FAST
+    bool take = match;
+    if (__any(match && grp_up1<GW>(match ? 1u : 0u, 0u) != 0u)) {
+#endif
     const unsigned long long mb = __ballot(match);
     const unsigned long long M = GW == 64 ? mb : ((mb >> gbase) & ((1ull << GW) - 1ull));
     // a run of the same self-pair merges left to right: take a match when the matches right
@@ -930,7 +937,12 @@ __device__ __forceinline__ uint32_t dw_merge_word(const Map& mm, uint32_t raw, i
     const unsigned long long lowm = gl == 0 ? 0ull : ((1ull << gl) - 1ull);
     const unsigned long long z = ~M & lowm;
     const int hz = z ? 63 - __clzll(z) : -1;
+#ifdef BEAST_WORDS_SELFPAIR_FAST
+    take = match && !((gl - 1 - hz) & 1);
+    }
+#else
     const bool take = match && !((gl - 1 - hz) & 1);
+#endif
     const bool dies = grp_up1<GW>(take ? 1u : 0u, 0u) != 0u;
     if (take) sym = m & 0xFFFFu;
     sym = grp_compact<GW>(sym, gl < n && !dies, gl, gbase, n);
@@ -959,15 +971,15 @@ __device__ __forceinline__ uint32_t bw_hash(const int32_t* cps, int cs, int ce) 
   return h ^ (h >> 16);
 }
 
-__host__ __device__ inline size_t bw_lds_bytes(int Lc, int S, int nwv, int map_log2 /* < 0: map in HBM */) {
-  size_t b = map_log2 >= 0 ? al16(sizeof(uint2) << map_log2) : 0;
+__host__ __device__ inline size_t bw_lds_bytes(int Lc, int S, int nwv, int wm_log2b /* < 0: map in HBM */) {
+  size_t b = wm_log2b >= 0 ? sizeof(uint4) << wm_log2b : 0;
   b += dw_ltab_bytes(Lc, nwv);
   b += 2 * al16(sizeof(uint32_t) * (size_t)nwv * Lc);
   return b + (size_t)nwv * dw_row_bytes(Lc, S);
 }
 
 template <bool MAP_LDS>
-__global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab_log2, int hash_shift) {
+__global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap wm, int ltab_log2, int hash_shift) {
   extern __shared__ __align__(16) char lds_raw[];
   __shared__ int32_t s_b2i[256];
   __shared__ uint8_t s_lut[256];
@@ -975,14 +987,12 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
   __shared__ int s_hist[DW_MID + 1];   // distinct words per byte-symbol length, then sort cursors
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   char* p = lds_raw;
-  LdsMap lm;
+  WordMap lm = wm;
   if constexpr (MAP_LDS) {
-    const int cap = 1 << a.map.log2cap;
     uint4* kv = reinterpret_cast<uint4*>(p);
-    const uint4* g = reinterpret_cast<const uint4*>(a.map.kv);
-    for (int i = threadIdx.x; i < cap / 2; i += blockDim.x) kv[i] = g[i];
-    lm.kv = reinterpret_cast<const uint2*>(p); lm.rank2new = nullptr; lm.log2cap = a.map.log2cap;
-    p += al16(sizeof(uint2) << a.map.log2cap);
+    for (int i = threadIdx.x; i < (1 << wm.log2b); i += blockDim.x) kv[i] = wm.b[i];
+    lm.b = kv;
+    p += sizeof(uint4) << wm.log2b;
   }
   const int lcap = 1 << ltab_log2;
   unsigned long long* ltab = reinterpret_cast<unsigned long long*>(p);
@@ -1074,8 +1084,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
       const int bs = Rw.symoff[Rw.wcp[k]];
       const uint32_t raw = lane < blen ? (uint32_t)Rw.c[bs + lane] : SYM_NONE;
       int n;
-      const uint32_t id = MAP_LDS ? dw_merge_word<DW_MID>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
-                                  : dw_merge_word<DW_MID>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      const uint32_t id = dw_merge_word<DW_MID>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (lane < n) Rw.c[bs + lane] = (uint16_t)id;
       if (lane == 0) Rw.vis[k] = (uint8_t)n;
     } else if (t < t16) {
@@ -1087,8 +1096,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
       const int bs = valid ? Rw.symoff[Rw.wcp[k]] : 0;
       const uint32_t raw = gl < blen ? (uint32_t)Rw.c[bs + gl] : SYM_NONE;
       int n;
-      const uint32_t id = MAP_LDS ? dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
-                                  : dw_merge_word<DW_SHORT>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      const uint32_t id = dw_merge_word<DW_SHORT>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
       if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
     } else {
@@ -1100,8 +1108,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, int ltab
       const int bs = valid ? Rw.symoff[Rw.wcp[k]] : 0;
       const uint32_t raw = gl < blen ? (uint32_t)Rw.c[bs + gl] : SYM_NONE;
       int n;
-      const uint32_t id = MAP_LDS ? dw_merge_word<DW_TINY>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds)
-                                  : dw_merge_word<DW_TINY>(a.map, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
+      const uint32_t id = dw_merge_word<DW_TINY>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
       if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
       if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
     }
@@ -1456,16 +1463,72 @@ extern "C" int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off,
 }
 
 
+// ---- k_bpe_words' merge map (host build) ----
+extern "C" int beast_bpe_wordmap_log2buckets(int n_merges) {   // buckets >= merges: at most half the slots used
+  return std::max(4, log2_ceil(std::max(1, n_merges)));
+}
+extern "C" size_t beast_bpe_wordmap_bytes(int n_merges) {   // room for one doubling if an insertion fails
+  return sizeof(uint32_t) * 4 * ((size_t)2 << beast_bpe_wordmap_log2buckets(n_merges));
+}
+static bool wordmap_try(const int32_t* ma, const int32_t* mb, const int32_t* mn, int n, uint32_t* t, int lb) {
+  const size_t nb = (size_t)1 << lb;
+  for (size_t i = 0; i < 4 * nb; i += 2) { t[i] = EMPTY_KEY; t[i + 1] = 0u; }
+  auto slot_of = [&](uint32_t key) -> uint32_t* {   // the key's slot, if present
+    for (uint32_t bk : {wm_h1(key, lb), wm_h2(key, lb)})
+      for (int q = 0; q < 2; ++q)
+        if (t[4 * bk + 2 * q] == key) return &t[4 * bk + 2 * q];
+    return nullptr;
+  };
+  uint32_t rng = 0x2545F491u;
+  for (int i = 0; i < n; ++i) {
+    uint32_t key = ((uint32_t)ma[i] << 16) | (uint32_t)mb[i];
+    uint32_t val = ((uint32_t)(i + 1) << 16) | (uint32_t)mn[i];
+    if (uint32_t* e = slot_of(key)) { e[1] = val; continue; }   // a pair listed twice keeps its last rank
+    uint32_t bk = wm_h1(key, lb);
+    bool placed = false;
+    for (int kick = 0; kick < 512 && !placed; ++kick) {
+      for (uint32_t c : {wm_h1(key, lb), wm_h2(key, lb)})
+        for (int q = 0; q < 2 && !placed; ++q)
+          if (t[4 * c + 2 * q] == EMPTY_KEY) { t[4 * c + 2 * q] = key; t[4 * c + 2 * q + 1] = val; placed = true; }
+      if (placed) break;
+      // evict a pseudo-random slot of the bucket not just left, carry its key on
+      rng ^= rng << 13; rng ^= rng >> 17; rng ^= rng << 5;
+      bk = (bk == wm_h1(key, lb)) ? wm_h2(key, lb) : wm_h1(key, lb);
+      const int q = rng & 1;
+      std::swap(key, t[4 * bk + 2 * q]);
+      std::swap(val, t[4 * bk + 2 * q + 1]);
+    }
+    if (!placed) return false;
+  }
+  return true;
+}
+extern "C" int beast_bpe_wordmap_build_host(const int32_t* merge_a, const int32_t* merge_b, const int32_t* merge_new,
+                                            int n_merges, void* host_out, size_t bytes, int* log2b_out) {
+  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
+  BEAST_REQUIRE(host_out && log2b_out && (n_merges == 0 || (merge_a && merge_b && merge_new)), "null pointer argument");
+  BEAST_REQUIRE_CODE(bytes >= beast_bpe_wordmap_bytes(n_merges), BEAST_E_WORKSPACE, "word map buffer %zu < %zu", bytes,
+                     beast_bpe_wordmap_bytes(n_merges));
+  uint32_t* t = static_cast<uint32_t*>(host_out);
+  const int lb0 = beast_bpe_wordmap_log2buckets(n_merges);
+  for (int lb = lb0; lb <= lb0 + 1; ++lb)
+    if (wordmap_try(merge_a, merge_b, merge_new, n_merges, t, lb)) {
+      *log2b_out = lb;
+      return BEAST_OK;
+    }
+  BEAST_REQUIRE_CODE(false, BEAST_E_UNSUPPORTED, "word map: cuckoo insertion failed");
+  return BEAST_E_UNSUPPORTED;
+}
+
 extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows,
                                            int64_t min_tok, int64_t max_span, const uint8_t* cls_lut, int64_t lut_n,
-                                           const int32_t* byte2id, const void* map, int n_merges, int unk_id,
+                                           const int32_t* byte2id, const void* wordmap, int wordmap_log2b, int unk_id,
                                            int fuse_unk, int max_row_cps, int max_row_syms, int32_t* out_ids,
                                            int64_t out_stride, int32_t* out_len, int32_t* status, void* stream) {
   BEAST_REQUIRE(n_rows >= 0, "n_rows must be >= 0");
   if (n_rows == 0) return BEAST_OK;
-  BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && map && out_ids && out_len && status, "null pointer argument");
+  BEAST_REQUIRE(tok && row_off && cls_lut && byte2id && wordmap && out_ids && out_len && status, "null pointer argument");
   BEAST_REQUIRE(lut_n > 0 && lut_n <= 65536, "class LUT size %lld out of range", (long long)lut_n);
-  BEAST_REQUIRE(n_merges >= 0 && n_merges < 65536, "n_merges out of range (0..65535): %d", n_merges);
+  BEAST_REQUIRE(wordmap_log2b >= 4 && wordmap_log2b <= 20, "wordmap_log2b %d out of range (4..20)", wordmap_log2b);
   BEAST_REQUIRE(max_row_cps >= 0 && max_row_cps < 32768, "max_row_cps %d out of range", max_row_cps);
   BEAST_REQUIRE(max_row_syms >= 0 && max_row_syms <= 16384, "max_row_syms %d out of range", max_row_syms);
   BEAST_REQUIRE(out_stride >= max_row_syms, "out_stride %lld < max_row_syms %d", (long long)out_stride, max_row_syms);
@@ -1473,14 +1536,13 @@ extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* ro
   a.tok = reinterpret_cast<const long long*>(tok);
   a.row_off = row_off; a.n_rows = n_rows; a.min_tok = min_tok; a.max_span = max_span;
   a.lut = cls_lut; a.lut_n = (int)lut_n; a.byte2id = byte2id;
-  a.map = map_view(map, n_merges);
-  a.n_merges = n_merges;
   a.unk_id = unk_id; a.fuse_unk = fuse_unk;
   a.Lc = max_row_cps; a.S = max_row_syms;
   a.out_ids = out_ids; a.out_stride = out_stride; a.out_len = out_len; a.status = status;
+  const WordMap wm{static_cast<const uint4*>(wordmap), wordmap_log2b};
   // as many rows per workgroup as the LDS holds (<= 16), the merge map staged when it fits beside them
   const size_t room = LDS_BUDGET - STATIC_LDS;
-  int map_log2 = a.map.log2cap <= LDS_MAP_MAX_LOG2 ? a.map.log2cap : -1, nwv = 0;
+  int map_log2 = wordmap_log2b <= 13 ? wordmap_log2b : -1, nwv = 0;
   for (int pass = 0; pass < 2 && nwv == 0; ++pass) {
     for (int nv = DW_WAVES; nv > 0 && nwv == 0; --nv)
       if (bw_lds_bytes(a.Lc, a.S, nv, map_log2) <= room) nwv = nv;
@@ -1496,12 +1558,12 @@ extern "C" int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* ro
     if (lds > 65536)
       BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bpe_words<true>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute(k_bpe_words)");
-    hipLaunchKernelGGL(k_bpe_words<true>, grid, block, lds, s, a, ltab_log2, hash_shift);
+    hipLaunchKernelGGL(k_bpe_words<true>, grid, block, lds, s, a, wm, ltab_log2, hash_shift);
   } else {
     if (lds > 65536)
       BEAST_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bpe_words<false>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute(k_bpe_words)");
-    hipLaunchKernelGGL(k_bpe_words<false>, grid, block, lds, s, a, ltab_log2, hash_shift);
+    hipLaunchKernelGGL(k_bpe_words<false>, grid, block, lds, s, a, wm, ltab_log2, hash_shift);
   }
   BEAST_LAUNCHED("k_bpe_words");
   return BEAST_OK;

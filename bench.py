@@ -650,6 +650,11 @@ def bpe_codec_bench(res, rows: torch.Tensor, dev, args):
                 "encode_api_rows_per_s": R / t_api_enc, "encode_api_tensors_rows_per_s": R / t_api_tens,
                 "encode_kernel_GBps": (R * width * 8 + n_ids * 4) / (t_enc * 1e-6) / 1e9,
                 "decode_kernel_GBps": (n_ids * 4 + R * width * 8) / (t_dec * 1e-6) / 1e9})
+    kern = (RANK_INFO.get("profile") or {}).get("kernels", {})
+    if "k_bpe_words" in kern and R == 4096:   # the same-tree profile of this command
+        out["encode_rocprof_us"] = kern["k_bpe_words"]["avg_ns"] / 1e3
+    if "k_bpe_decode" in kern and R == 4096:
+        out["decode_rocprof_us"] = kern["k_bpe_decode"]["avg_ns"] / 1e3
     if not args.no_cpu:
         host = rows.cpu().numpy() - lo
         n = min(R, 2048)
@@ -734,6 +739,7 @@ def main():
     # ---- dominant-kernel roofline: the same-tree rocprofv3 average when the profile matches this
     #      tree, HIP events measured live on the kernel's stream beside it
     prof, prof_note = load_profile(args.profile)
+    RANK_INFO["profile"] = prof
     launch_enc, launch_rec = launchers(tok, dev, stream, x, B)
     t_enc = kernel_time_us(launch_enc, stream)
     t_rec = kernel_time_us(launch_rec, stream)

@@ -363,10 +363,19 @@ int beast_bpe_encode_rows(const int64_t* tok, const int64_t* row_off, int64_t n_
  * only combine tokens made by earlier merges -- every trained model; the caller checks and uses
  * beast_bpe_encode_rows otherwise, or when the model has special tokens.  status as above plus
  * 7 (ST_FALLBACK): the row holds a word of more than 64 byte symbols; the caller re-encodes such
- * rows with beast_bpe_encode_rows. */
+ * rows with beast_bpe_encode_rows.
+ * wordmap: the merges as a two-choice bucketed cuckoo table of 1 << wordmap_log2b buckets,
+ * built on the host by beast_bpe_wordmap_build_host into a buffer of beast_bpe_wordmap_bytes
+ * (HOST pointers; it returns the bucket count's log2) and copied to the device (its first
+ * 16 << log2b bytes). */
+int beast_bpe_wordmap_log2buckets(int n_merges);
+size_t beast_bpe_wordmap_bytes(int n_merges);
+int beast_bpe_wordmap_build_host(const int32_t* host_merge_a, const int32_t* host_merge_b,
+                                 const int32_t* host_merge_new, int n_merges, void* host_out, size_t bytes,
+                                 int* host_log2b_out);
 int beast_bpe_encode_rows_words(const int64_t* tok, const int64_t* row_off, int64_t n_rows, int64_t min_tok,
                                 int64_t max_span, const uint8_t* cls_lut, int64_t lut_n, const int32_t* byte2id,
-                                const void* map, int n_merges, int unk_id, int fuse_unk, int max_row_cps,
+                                const void* wordmap, int wordmap_log2b, int unk_id, int fuse_unk, int max_row_cps,
                                 int max_row_syms, int32_t* out_ids, int64_t out_stride, int32_t* out_len,
                                 int32_t* status, void* stream);
 /* Decode rows ids[row_off[r] .. row_off[r+1]).  tok_off[n_vocab+1] / tok_bytes: each id's

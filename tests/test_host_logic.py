@@ -316,3 +316,51 @@ def test_replay_merge_log_cpp_matches_python():
                 finally:
                     bt._FAST = saved
     assert results[0] == results[1]
+
+
+@pytest.mark.parametrize("n", [0, 1, 17, 1792, 5000])
+def test_wordmap_build_host(n):
+    """k_bpe_words' merge map (beast_bpe_wordmap_build_host, host code): every merge pair sits in
+    one of its two buckets with (last rank + 1) << 16 | new id, absent pairs in neither; the
+    buckets follow the kernel's hashes (wm_h1 / wm_h2, restated here)."""
+    import ctypes
+    from beast_tokenizer_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(n)
+    ma = rng.integers(0, 2048, n).astype(np.int32)
+    mb = rng.integers(0, 2048, n).astype(np.int32)
+    if n > 10:
+        ma[5], mb[5] = ma[3], mb[3]               # a pair listed twice keeps its last rank
+    mn = (256 + np.arange(n)).astype(np.int32)
+    nbytes = int(lib.beast_bpe_wordmap_bytes(n))
+    t = np.zeros(nbytes // 4, dtype=np.uint32)
+    lb = ctypes.c_int(0)
+    _lib.run("beast_bpe_wordmap_build_host", ma.ctypes.data if n else None, mb.ctypes.data if n else None,
+             mn.ctypes.data if n else None, n, t.ctypes.data, nbytes, ctypes.byref(lb))
+    lb = lb.value
+    assert lb >= 4 and (16 << lb) <= nbytes
+    M = 0xFFFFFFFF
+
+    def h1(k):
+        return ((k * 0x9E3779B1) & M) >> (32 - lb)
+
+    def h2(k):
+        return (((k ^ 0x5BD1E995) * 0x85EBCA77) & M) >> (32 - lb)
+
+    def find(k):
+        for bk in (h1(k), h2(k)):
+            for q in range(2):
+                if t[4 * bk + 2 * q] == k:
+                    return int(t[4 * bk + 2 * q + 1])
+        return 0
+
+    want = {}
+    for i in range(n):
+        want[(int(ma[i]) << 16) | int(mb[i])] = ((i + 1) << 16) | int(mn[i])
+    for k, v in want.items():
+        assert find(k) == v
+    used = sum(int(t[4 * b + 2 * q] != M) for b in range(1 << lb) for q in range(2))
+    assert used == len(want)
+    for k in rng.integers(0, 2048 << 16, 200):
+        if int(k) not in want:
+            assert find(int(k)) == 0
