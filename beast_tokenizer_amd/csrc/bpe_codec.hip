@@ -926,10 +926,6 @@ __device__ __forceinline__ uint32_t dw_merge_word(const WordMap& mm, uint32_t ra
     if (!__any(m != RK_NONE)) break;
     ++rounds;
     const bool match = has && m != RK_NONE && rk == m;
-#ifdef BEAST_WORDS_SELFPAIR_FAST
-    bool take = match;
-    if (__any(match && grp_up1<GW>(match ? 1u : 0u, 0u) != 0u)) {
-#endif
     const unsigned long long mb = __ballot(match);
     const unsigned long long M = GW == 64 ? mb : ((mb >> gbase) & ((1ull << GW) - 1ull));
     // a run of the same self-pair merges left to right: take a match when the matches right
@@ -937,12 +933,7 @@ __device__ __forceinline__ uint32_t dw_merge_word(const WordMap& mm, uint32_t ra
     const unsigned long long lowm = gl == 0 ? 0ull : ((1ull << gl) - 1ull);
     const unsigned long long z = ~M & lowm;
     const int hz = z ? 63 - __clzll(z) : -1;
-#ifdef BEAST_WORDS_SELFPAIR_FAST
-    take = match && !((gl - 1 - hz) & 1);
-    }
-#else
     const bool take = match && !((gl - 1 - hz) & 1);
-#endif
     const bool dies = grp_up1<GW>(take ? 1u : 0u, 0u) != 0u;
     if (take) sym = m & 0xFFFFu;
     sym = grp_compact<GW>(sym, gl < n && !dies, gl, gbase, n);
@@ -983,7 +974,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   extern __shared__ __align__(16) char lds_raw[];
   __shared__ int32_t s_b2i[256];
   __shared__ uint8_t s_lut[256];
-  __shared__ int s_nd;
+  __shared__ int s_nd, s_next;
   __shared__ int s_hist[DW_MID + 1];   // distinct words per byte-symbol length, then sort cursors
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   char* p = lds_raw;
@@ -1010,7 +1001,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   }
   for (int i = threadIdx.x; i < lcap; i += blockDim.x) ltab[i] = 0ull;
   if (threadIdx.x <= DW_MID) s_hist[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_nd = 0;
+  if (threadIdx.x == 0) { s_nd = 0; s_next = nwv; }
   __syncthreads();
   const DwRow L = dw_carve(rows + (size_t)wave * rb, a.Lc, a.S);
   const int64_t r = (int64_t)blockIdx.x * nwv + wave;
@@ -1076,7 +1067,10 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   const int t16 = nmid + (n9 - nmid + 3) / 4;
   const int tasks = t16 + (nd - n9 + 7) / 8;
   int nrounds = 0;
-  for (int t = wave; t < tasks; t += nwv) {
+  // tasks longest first, each wave taking the next one when it is done (an LDS counter): the
+  // workgroup waits for its slowest wave at the barrier below (29.8 vs 33.0 us with tasks dealt
+  // round-robin, profiles/r04/ab/encode_words_variants_r04d.txt)
+  for (int t = wave; t < tasks;) {
     if (t < nmid) {
       const uint32_t v = ds[t];
       const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
@@ -1112,6 +1106,9 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
       if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
       if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
     }
+    int nt = 0;
+    if (lane == 0) nt = atomicAdd(&s_next, 1);
+    t = __builtin_amdgcn_readfirstlane(nt);
   }
   __syncthreads();
   if (r < a.n_rows) BPE_STAMP(6);
