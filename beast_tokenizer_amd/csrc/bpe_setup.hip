@@ -443,8 +443,17 @@ __host__ __device__ inline size_t dedup_fixed_bytes(int64_t n) { return (size_t)
 // (DEDUP_LDS entries, linear probing; a full probe falls back to the global atomic) and flushed
 // once per workgroup -- the common words occur millions of times.
 constexpr int DEDUP_LDS = 4096;
-constexpr int DEDUP_NEW = 1024;   // LDS new-word list; flushed when a pass could overflow it
-__global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+#ifndef DEDUP_NEW
+#define DEDUP_NEW 1024            // LDS new-word list; flushed when a pass could overflow it
+#endif
+#ifndef DEDUP_T
+// threads per workgroup: the LDS tables (41 KB) cap a CU at three workgroups, so 512 threads hold
+// twice the waves of 256 for this chain of dependent loads (K5: 2.14 vs 2.83 ms per call;
+// symbols loaded as aligned 16-byte blocks instead, 3.38 / 3.95 ms:
+// profiles/r04/ab/bpe_dedup_ab_r04.txt)
+#define DEDUP_T 512
+#endif
+__global__ __launch_bounds__(DEDUP_T) void k_dedup_insert(const uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                       const uint32_t* __restrict__ wlen, int64_t nw, DedupWs ws) {
   __shared__ uint32_t lkey[DEDUP_LDS];   // slot + 1, 0 = empty
   __shared__ uint32_t lcnt[DEDUP_LDS];
@@ -538,7 +547,7 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint16_t* __restrict
       if (!done) atomicAdd(&ws.cnt[k], 1u);
     }
     __syncthreads();
-    if (ncnt > (uint32_t)(DEDUP_NEW - 256)) flush_new();   // the next pass adds <= 256
+    if (ncnt > (uint32_t)(DEDUP_NEW - DEDUP_T)) flush_new();   // the next pass adds <= DEDUP_T
   }
   flush_new();
   __syncthreads();
@@ -813,7 +822,8 @@ extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart
   BEAST_HIP(hipMemsetAsync(workspace, 0, ws.cap * 12, s), "dedup memset");
   BEAST_HIP(hipMemsetAsync(ws.nu, 0, 16, s), "dedup memset");
   if (n_words > 0) {
-    hipLaunchKernelGGL(k_dedup_insert, dim3(grid_for(n_words, 256, 16384)), dim3(256), 0, s, sym, wstart, wlen,
+    hipLaunchKernelGGL(k_dedup_insert, dim3(grid_for(n_words, DEDUP_T, 16384 * 256 / DEDUP_T)), dim3(DEDUP_T), 0, s,
+                       sym, wstart, wlen,
                        n_words, ws);
     BEAST_LAUNCHED("k_dedup_insert");
   }
