@@ -12,7 +12,7 @@ i=0
 while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $group --kernel-trace --output-format csv -d "$OUT/p$i" -o run \
+  timeout -s KILL 240 rocprofv3 --kernel-include-regex "k_merge_batch|k_apply_batch" --pmc $group --kernel-trace --output-format csv -d "$OUT/p$i" -o run \
     -- python3 "$R/tools/bpe_profile.py" 1 > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done <<GROUPS
 ${PMC_GROUPS:-SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_LDS

@@ -22,5 +22,7 @@ PMC_GROUPS=$'FETCH_SIZE\nWRITE_SIZE\nSQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_I
   bash "$R/tools/gpu_pmc.sh" "prof_$TAG/codec_pmc" 4096 50
 rc=$?; echo "codec pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
 PMC_GROUPS=$'FETCH_SIZE\nWRITE_SIZE' bash "$R/tools/bpe_pmc.sh" "prof_$TAG/bpe_pmc"
-rc=$?; echo "bpe pmc rc=$rc"
+rc=$?; echo "bpe pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd "$R" && bash tools/codec/bpe_encode_pmc.sh
+rc=$?; echo "encode pmc rc=$rc"
 exit $rc
