@@ -106,7 +106,9 @@ def _fingerprint() -> str:
     says nothing there), and a library built from other sources must never be reused."""
     import hashlib
     h = hashlib.sha256()
-    h.update(" ".join(CXXFLAGS).encode())
+    # the include flags name absolute paths: hash them relative to the repository, so a snapshot
+    # of the same tree elsewhere (the GPU box's scratch copy) has the same fingerprint
+    h.update(" ".join(f.replace(REPO, "<repo>") for f in CXXFLAGS).encode())
     h.update(repr(sorted(FILE_FLAGS.items())).encode())
     for p in _sources() + sorted(_deps()) + [__file__]:
         h.update(os.path.relpath(p, REPO).encode())
