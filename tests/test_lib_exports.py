@@ -246,3 +246,21 @@ def test_integration_c_snippet_compiles_against_header(tmp_path):
     r = subprocess.run([hipcc, "-fsyntax-only", "-x", "hip", "--offload-arch=gfx950", "-Werror", "-Wno-unused-command-line-argument",
                         f"-I{os.path.dirname(HEADER)}", str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_library_fingerprint_is_path_independent(tmp_path):
+    """bench.py uses profiles/rNN/profile_summary.json only when its library fingerprint equals the
+    running tree's; the GPU box runs a copy of the tree under another path, so the fingerprint must
+    not depend on where the tree lies (round 4: the absolute -I paths in the flags made it)."""
+    import importlib.util
+    import shutil
+    from beast_tokenizer_amd import _build
+    pkg = tmp_path / "elsewhere" / "beast_tokenizer_amd"
+    shutil.copytree(_build.CSRC, pkg / "csrc", ignore=shutil.ignore_patterns("build", "*.o"))
+    shutil.copytree(_build.INCLUDE, tmp_path / "elsewhere" / "include")
+    shutil.copy(_build.__file__, pkg / "_build.py")
+    spec = importlib.util.spec_from_file_location("_build_copy", pkg / "_build.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.REPO != _build.REPO
+    assert mod._fingerprint() == _build._fingerprint()
