@@ -89,6 +89,8 @@ SIGNATURES = {
     "beast_bpe_encode_lds_bytes": (_sz, [_i32, _i32]),
     "beast_bpe_encode_rows": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _i32,
                                      _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
+    "beast_bpe_train": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _sz, _vp,
+                               _i32, _vp, _vp, _i32, _vp, _vp]),
     "beast_bpe_wordmap_log2buckets": (_i32, [_i32]),
     "beast_bpe_wordmap_bytes": (_sz, [_i32]),
     "beast_bpe_wordmap_build_host": (_i32, [_vp, _vp, _vp, _i32, _vp, _sz, _vp]),

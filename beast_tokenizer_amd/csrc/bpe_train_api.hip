@@ -1,0 +1,367 @@
+// beast_bpe_train: the whole byte-level BPE training in one C-ABI call (host code over the
+// library's own entry points) -- what FIGBPE.fit_from_sequences does through HF
+// (beast/beast_bpe_trainer.py:61-74, :76-98: BpeTrainer(vocab_size, min_frequency,
+// special_tokens, initial_alphabet = chr(0 .. max - min), max_token_length) on the strings
+// "".join(map(chr, seq - min))).  The same steps as beast_tokenizer_amd/bpe_train.py:train_bpe
+// on one GPU: min / max, the code points present, the alphabet (special tokens, then byte-level
+// chars by code point), pre-tokenisation (count, scan, emit), distinct words x counts, the
+// length-ordered repack + word signatures, the pair table, then the device-driven batched
+// merge loop with two chunks of passes in flight, and the host replay of its merge log against
+// the real strings.  Single device, Vt <= 4,096 (the batched loop); a 64-bit string-hash
+// collision or a full merge log comes back BEAST_E_UNSUPPORTED (the Python driver then reruns
+// on its host-driven loop).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+// GPT-2 bytes_to_unicode: bytes 33-126, 161-172, 174-255 map to themselves, the other 68 to
+// U+0100 + k in ascending byte order
+void bytes_to_unicode(uint32_t (&b2u)[256]) {
+  int k = 0;
+  for (int b = 0; b < 256; ++b) {
+    const bool keep = (b >= 33 && b <= 126) || (b >= 161 && b <= 172) || (b >= 174 && b <= 255);
+    b2u[b] = keep ? (uint32_t)b : (uint32_t)(256 + k++);
+  }
+}
+
+void append_utf8(std::string& s, uint32_t cp) {
+  if (cp < 0x80) {
+    s += (char)cp;
+  } else if (cp < 0x800) {
+    s += (char)(0xC0 | (cp >> 6));
+    s += (char)(0x80 | (cp & 63));
+  } else if (cp < 0x10000) {
+    s += (char)(0xE0 | (cp >> 12));
+    s += (char)(0x80 | ((cp >> 6) & 63));
+    s += (char)(0x80 | (cp & 63));
+  } else {
+    s += (char)(0xF0 | (cp >> 18));
+    s += (char)(0x80 | ((cp >> 12) & 63));
+    s += (char)(0x80 | ((cp >> 6) & 63));
+    s += (char)(0x80 | (cp & 63));
+  }
+}
+
+size_t utf8_chars(const std::string& s) {   // HF counts token lengths in characters
+  size_t n = 0;
+  for (unsigned char c : s) n += (c & 0xC0) != 0x80;
+  return n;
+}
+
+// device allocations released on every return path
+struct DevMem {
+  std::vector<void*> ptrs;
+  ~DevMem() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <class T>
+  T* get(size_t count) {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    return static_cast<T*>(p);
+  }
+};
+
+struct HostPinned {
+  void* p = nullptr;
+  ~HostPinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+constexpr uint64_t LOOP_P = 0x9E3779B97F4A7C15ull;   // bpe_train.py GpuBpeOps.LOOP_P
+constexpr int ST_ACTIVE = 0, ST_VCUR = 1, ST_NMERGES = 2;
+constexpr int KMAX = 8, CHUNK = 64;
+
+}  // namespace
+
+#define TRY(call)                  \
+  do {                             \
+    const int rc_ = (call);        \
+    if (rc_ != BEAST_OK) return rc_; \
+  } while (0)
+#define ALLOC(var, T, n)                                                         \
+  T* var = mem.get<T>(n);                                                        \
+  BEAST_REQUIRE_CODE(var != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of %zu x %zu bytes failed", \
+                     (size_t)(n), sizeof(T))
+
+extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                               int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                               const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                               int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
+                               int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
+                               int max_merges_out, int* out_n_merges, void* stream) {
+  BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
+                    out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
+                "beast_bpe_train: null pointer argument");
+  BEAST_REQUIRE(n_seq >= 1 && vocab_size >= 1 && n_special >= 0, "beast_bpe_train: bad sizes");
+  hipStream_t s = beast::as_stream(stream);
+  DevMem mem;
+  int64_t n_tok = 0;
+  BEAST_HIP(hipMemcpyAsync(&n_tok, seq_off + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "seq_off read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  BEAST_REQUIRE(n_tok > 0, "No non-empty sequences provided for BPE training.");   // reference :84-85
+  BEAST_REQUIRE(tokens != nullptr, "beast_bpe_train: null pointer argument");
+
+  // ---- min / max (reference :86-87), the code points present
+  ALLOC(mm, int64_t, 2);
+  TRY(beast_i64_minmax(tokens, n_tok, mm, stream));
+  int64_t mmh[2];
+  BEAST_HIP(hipMemcpyAsync(mmh, mm, sizeof(mmh), hipMemcpyDeviceToHost, s), "minmax read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  const int64_t mn = mmh[0], mx = mmh[1], K = mx - mn;
+  BEAST_REQUIRE_CODE(K < 0xD800, BEAST_E_UNSUPPORTED,
+                     "BPE alphabet reaches the UTF-16 surrogate range (max - min token >= 55296)");
+  BEAST_REQUIRE(lut_n >= K + 1, "beast_bpe_train: class LUT covers %lld code points, the corpus needs %lld",
+                (long long)lut_n, (long long)(K + 1));
+  const int64_t n_cp = K + 1;
+  ALLOC(pr, uint8_t, n_cp);
+  TRY(beast_bpe_cp_presence(tokens, n_tok, mn, pr, n_cp, stream));
+  std::vector<uint8_t> present(n_cp);
+  BEAST_HIP(hipMemcpyAsync(present.data(), pr, n_cp, hipMemcpyDeviceToHost, s), "presence read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+
+  // ---- alphabet (HF BpeTrainer: special tokens, then compute_alphabet by code point)
+  uint32_t b2u[256];
+  bytes_to_unicode(b2u);
+  bool seen[256] = {};
+  for (int64_t cp = 0; cp < n_cp; ++cp)
+    if (present[cp]) {
+      std::string u;
+      append_utf8(u, (uint32_t)cp);
+      for (unsigned char c : u) seen[c] = true;
+    }
+  std::vector<uint32_t> chars;
+  for (int b = 0; b < 256; ++b)
+    if (seen[b]) chars.push_back(b2u[b]);
+  for (int64_t cp = 0; cp < n_cp; ++cp) chars.push_back((uint32_t)cp);   // initial_alphabet = chr(0 .. K)
+  std::sort(chars.begin(), chars.end());
+  chars.erase(std::unique(chars.begin(), chars.end()), chars.end());
+  std::vector<std::string> id2str;
+  std::unordered_map<std::string, int> str2id;
+  for (int i = 0; i < n_special; ++i) {
+    const std::string t(special_tokens[i]);
+    if (!str2id.count(t)) {
+      str2id.emplace(t, (int)id2str.size());
+      id2str.push_back(t);
+    }
+  }
+  for (uint32_t c : chars) {
+    std::string u;
+    append_utf8(u, c);
+    if (!str2id.count(u)) {
+      str2id.emplace(u, (int)id2str.size());
+      id2str.push_back(u);
+    }
+  }
+  uint16_t byte2id[256];
+  for (int b = 0; b < 256; ++b) {
+    std::string u;
+    append_utf8(u, b2u[b]);
+    byte2id[b] = seen[b] ? (uint16_t)str2id.at(u) : (uint16_t)0xFFFF;
+  }
+  const int n_base = (int)id2str.size();
+  const int Vt = std::max(vocab_size, n_base);
+  BEAST_REQUIRE_CODE(Vt <= 4096, BEAST_E_UNSUPPORTED,
+                     "beast_bpe_train: Vt %d > 4096 (the batched device loop); use the Python driver", Vt);
+  BEAST_REQUIRE_CODE(max_vocab >= Vt && max_merges_out >= std::max(vocab_size - n_base, 0), BEAST_E_WORKSPACE,
+                     "beast_bpe_train: output capacity (vocab %d, merges %d) below the vocabulary size %d", max_vocab,
+                     max_merges_out, Vt);
+
+  // ---- pre-tokenisation: words per sequence, offsets, then the byte symbols
+  ALLOC(wps, int64_t, n_seq);
+  ALLOC(sps, int64_t, n_seq);
+  TRY(beast_bpe_pretok_count(tokens, seq_off, n_seq, mn, cls_lut, lut_n, wps, sps, stream));
+  ALLOC(scan_ws, uint8_t, beast_scan_workspace_bytes(n_seq));
+  ALLOC(woff, int64_t, n_seq + 1);
+  ALLOC(soff, int64_t, n_seq + 1);
+  TRY(beast_exclusive_scan_i64(wps, woff, n_seq, scan_ws, stream));
+  TRY(beast_exclusive_scan_i64(sps, soff, n_seq, scan_ws, stream));
+  int64_t nw = 0, ns = 0;
+  BEAST_HIP(hipMemcpyAsync(&nw, woff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "word count read");
+  BEAST_HIP(hipMemcpyAsync(&ns, soff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "symbol count read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  BEAST_REQUIRE_CODE(ns < (int64_t(1) << 32), BEAST_E_UNSUPPORTED,
+                     "BPE corpus has >= 2^32 byte symbols on one GPU; shard it over more ranks");
+  ALLOC(b2i_d, uint16_t, 256);
+  BEAST_HIP(hipMemcpyAsync(b2i_d, byte2id, sizeof(byte2id), hipMemcpyHostToDevice, s), "byte2id upload");
+  ALLOC(sym, uint16_t, ns);
+  ALLOC(wstart, uint32_t, nw);
+  ALLOC(wlen, uint32_t, nw);
+  TRY(beast_bpe_pretok_emit(tokens, seq_off, n_seq, mn, cls_lut, lut_n, woff, soff, b2i_d, sym, wstart, wlen, stream));
+
+  // ---- distinct words x counts (the table grows 4x while it overflows), repack, signatures
+  ALLOC(ow, uint32_t, nw);
+  ALLOC(ol, uint32_t, nw);
+  ALLOC(oc, uint32_t, nw);
+  ALLOC(on, int64_t, 1);
+  int64_t nu = -1;
+  for (size_t nbytes = beast_bpe_dedup_workspace_bytes(nw); nu < 0; nbytes *= 4) {
+    void* dws = nullptr;
+    BEAST_HIP(hipMalloc(&dws, nbytes), "dedup workspace");
+    const int rc = beast_bpe_dedup_words(sym, wstart, wlen, nw, dws, nbytes, ow, ol, oc, on, stream);
+    if (rc == BEAST_OK) {
+      const hipError_t e1 = hipMemcpyAsync(&nu, on, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+      const hipError_t e2 = hipStreamSynchronize(s);
+      (void)hipFree(dws);
+      BEAST_HIP(e1, "distinct count read");
+      BEAST_HIP(e2, "stream sync");
+    } else {
+      (void)hipFree(dws);
+      return rc;
+    }
+  }
+  ALLOC(rp_ws, uint8_t, beast_bpe_repack_workspace_bytes(nu));
+  ALLOC(sym2, uint16_t, ns + 3 * nu);   // spans rounded up to 4
+  ALLOC(w2, uint32_t, nu);
+  ALLOC(l2, uint32_t, nu);
+  ALLOC(c2, uint32_t, nu);
+  TRY(beast_bpe_repack_words(sym, ow, ol, oc, nu, rp_ws, beast_bpe_repack_workspace_bytes(nu), sym2, w2, l2, c2, on,
+                             stream));
+  ALLOC(sig, uint64_t, nu);
+  TRY(beast_bpe_word_signatures(sym2, w2, l2, nu, sig, stream));
+
+  // ---- the pair table and the loop state
+  ALLOC(table, uint32_t, (size_t)Vt * Vt);
+  BEAST_HIP(hipMemsetAsync(table, 0, sizeof(uint32_t) * (size_t)Vt * Vt, s), "pair table memset");
+  TRY(beast_bpe_count_pairs(sym2, w2, l2, c2, nu, table, Vt, n_base, stream));
+  std::vector<uint64_t> hp(2 * (size_t)n_base);   // [0, n): string hash, [n, 2n): P^bytes
+  std::vector<uint32_t> tlen(Vt, 0u);
+  int max_tlen = 0;
+  for (int i = 0; i < n_base; ++i) {
+    uint64_t h = 0, pw = 1;
+    for (unsigned char c : id2str[i]) {
+      h = h * LOOP_P + c;
+      pw *= LOOP_P;
+    }
+    hp[i] = h;
+    hp[n_base + i] = pw;
+    tlen[i] = (uint32_t)utf8_chars(id2str[i]);
+    max_tlen = std::max(max_tlen, (int)tlen[i]);
+  }
+  ALLOC(hp_d, uint64_t, hp.size());
+  ALLOC(tlen_d, uint32_t, Vt);
+  BEAST_HIP(hipMemcpyAsync(hp_d, hp.data(), sizeof(uint64_t) * hp.size(), hipMemcpyHostToDevice, s), "hash upload");
+  BEAST_HIP(hipMemcpyAsync(tlen_d, tlen.data(), sizeof(uint32_t) * Vt, hipMemcpyHostToDevice, s), "tlen upload");
+  const int max_merges = 4 * std::max(vocab_size - n_base, 0) + 1024;
+  const size_t lws_bytes = beast_bpe_loop_workspace_bytes(Vt, max_merges);
+  ALLOC(lws, uint8_t, lws_bytes);
+  TRY(beast_bpe_loop_init(lws, lws_bytes, Vt, max_merges, n_base, vocab_size, min_frequency, hp_d, hp_d + n_base,
+                          tlen_d, max_tlen, stream));
+  const void* st_p = nullptr;
+  const void* log_p = nullptr;
+  TRY(beast_bpe_loop_state(lws, Vt, max_merges, &st_p, &log_p));
+  const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
+  ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
+  BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
+  const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
+  ALLOC(bws, uint8_t, bw_bytes);
+  const int max_len = max_token_length > 0 ? max_token_length : 0x7FFFFFFF;
+  auto run = [&](int steps, int flags) {
+    return beast_bpe_loop_batch(lws, Vt, max_merges, steps, KMAX, flags, sym2, w2, l2, c2, nu, tlen_d, max_len, sig,
+                                table, argws, bws, bw_bytes, vocab_size, nullptr, nullptr, stream);
+  };
+
+  // ---- the loop: two chunks of passes in flight, the host reads the state the older one left
+  HostPinned stage;
+  BEAST_HIP(hipHostMalloc(&stage.p, 2 * 64, hipHostMallocDefault), "pinned state");
+  int32_t* st_host = static_cast<int32_t*>(stage.p);
+  struct Inflight { hipEvent_t ev; int slot; int passes; };
+  std::vector<Inflight> inflight;
+  auto release = [&]() {
+    for (auto& f : inflight) (void)hipEventDestroy(f.ev);
+    inflight.clear();
+  };
+  auto launch = [&](int steps, int flags) -> int {
+    if (int rc = run(steps, flags)) return rc;
+    const int slot = inflight.empty() ? 0 : 1 - inflight.back().slot;
+    if (hipMemcpyAsync(st_host + 16 * slot, st_p, 64, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return beast::hip_fail(hipGetLastError(), "loop state copy");
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return beast::hip_fail(hipGetLastError(), "event");
+    (void)hipEventRecord(ev, s);
+    inflight.push_back({ev, slot, steps});
+    return BEAST_OK;
+  };
+  int vcur = n_base, rc = BEAST_OK;
+  rc = launch(std::max(1, std::min(CHUNK, (vocab_size - vcur + KMAX - 1) / KMAX)), 1 /* BATCH_INIT */);
+  while (rc == BEAST_OK) {
+    int queued = 0;
+    for (auto& f : inflight) queued += f.passes;
+    const int left = vocab_size - vcur - 4 * queued;
+    if (left > 0 && (rc = launch(std::min(CHUNK, (left + KMAX - 1) / KMAX), 0)) != BEAST_OK) break;
+    Inflight f = inflight.front();
+    inflight.erase(inflight.begin());
+    const hipError_t e = hipEventSynchronize(f.ev);
+    (void)hipEventDestroy(f.ev);
+    if (e != hipSuccess) { rc = beast::hip_fail(e, "loop event"); break; }
+    const int32_t* h = st_host + 16 * f.slot;
+    const int active = h[ST_ACTIVE];
+    vcur = h[ST_VCUR];
+    if (!active || vcur >= vocab_size) break;
+    if (inflight.empty() && (rc = launch(1, 0)) != BEAST_OK) break;
+  }
+  release();
+  if (rc != BEAST_OK) return rc;
+  int32_t state[16];
+  BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  const int n_log = state[ST_NMERGES];
+  BEAST_REQUIRE_CODE(n_log < max_merges, BEAST_E_UNSUPPORTED,
+                     "beast_bpe_train: merge log full; use the Python driver's host-driven loop");
+  std::vector<int32_t> log(4 * (size_t)std::max(n_log, 1));
+  if (n_log > 0) {
+    BEAST_HIP(hipMemcpyAsync(log.data(), log_p, sizeof(int32_t) * 4 * n_log, hipMemcpyDeviceToHost, s), "log read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  }
+
+  // ---- replay the log against the real strings (bpe_train.py replay_log)
+  int n_merges = 0;
+  for (int i = 0; i < n_log; ++i) {
+    const int a = log[4 * i], b = log[4 * i + 1], nid = log[4 * i + 2], reused = log[4 * i + 3];
+    BEAST_REQUIRE_CODE(a >= 0 && b >= 0 && a < (int)id2str.size() && b < (int)id2str.size(), BEAST_E_UNSUPPORTED,
+                       "beast_bpe_train: merge log entry %d out of range", i);
+    const std::string t = id2str[a] + id2str[b];
+    auto it = str2id.find(t);
+    const bool have = it != str2id.end();
+    BEAST_REQUIRE_CODE(have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size()),
+                       BEAST_E_UNSUPPORTED,
+                       "beast_bpe_train: 64-bit string-hash collision at merge %d; use the Python driver", i);
+    if (!have) {
+      str2id.emplace(t, nid);
+      id2str.push_back(t);
+    }
+    BEAST_REQUIRE_CODE(n_merges < max_merges_out, BEAST_E_WORKSPACE, "beast_bpe_train: merge capacity %d too small",
+                       max_merges_out);
+    out_merges[2 * n_merges] = a;
+    out_merges[2 * n_merges + 1] = b;
+    ++n_merges;
+  }
+
+  // ---- outputs: the vocabulary's strings in id order, the merges, the token range
+  BEAST_REQUIRE_CODE((int)id2str.size() <= max_vocab, BEAST_E_WORKSPACE, "beast_bpe_train: vocab capacity %d < %zu",
+                     max_vocab, id2str.size());
+  size_t off = 0;
+  for (size_t i = 0; i < id2str.size(); ++i) {
+    out_vocab_off[i] = (int64_t)off;
+    BEAST_REQUIRE_CODE(off + id2str[i].size() <= vocab_bytes_cap, BEAST_E_WORKSPACE,
+                       "beast_bpe_train: vocab byte capacity %zu too small", vocab_bytes_cap);
+    std::memcpy(out_vocab_bytes + off, id2str[i].data(), id2str[i].size());
+    off += id2str[i].size();
+  }
+  out_vocab_off[id2str.size()] = (int64_t)off;
+  *out_n_vocab = (int)id2str.size();
+  *out_n_merges = n_merges;
+  *out_min_token = mn;
+  *out_max_token = mx;
+  return BEAST_OK;
+}

@@ -300,6 +300,28 @@ int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_
                          uint32_t* tlen, int max_token_length, uint64_t* sig, uint32_t* table, uint64_t* argws,
                          void* batch_ws, size_t batch_ws_bytes, int vocab_size, int32_t* deltas, uint32_t* apps,
                          void* stream);
+/* One-call training (round 4; SURVEY.md §8b's beast_bpe_train): FIGBPE.fit_from_sequences
+ * (beast/beast_bpe_trainer.py:76-98 -> :61-74, HF BpeTrainer(vocab_size, min_frequency,
+ * special_tokens, initial_alphabet = chr(0 .. max - min), max_token_length).train_from_iterator
+ * over the strings "".join(map(chr, seq - min))) on one GPU, the steps above in order: min /
+ * max, presence, alphabet (special tokens, then byte-level chars and the initial alphabet by
+ * code point), pretok count / scan / emit, dedup, repack, signatures, pair table, the batched
+ * loop, the host replay of its log.  tokens / seq_off [n_seq + 1] / cls_lut [lut_n >= max - min
+ * + 1] (beast_tokenizer_amd/pretok.py class_lut) are DEVICE pointers; special_tokens n_special
+ * NUL-terminated UTF-8 strings (host).  Outputs (HOST): the token range, the vocabulary as UTF-8
+ * strings in id order (out_vocab_bytes[out_vocab_off[i] .. out_vocab_off[i+1])), the merges as
+ * id pairs out_merges[2m], [2m+1] (merge m's token is their concatenation, the next new id
+ * unless the string already had one).  Capacities: max_vocab >= max(vocab_size, alphabet),
+ * max_merges_out >= vocab_size - alphabet.  Synchronises the stream.  BEAST_E_UNSUPPORTED for
+ * Vt > 4096, a full merge log or a 64-bit string-hash collision (the Python driver,
+ * bpe_train.train_bpe, reruns those on its host-driven loop); one GPU (the multi-rank forms
+ * are the Python driver's, over torch.distributed). */
+int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                    int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                    const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                    int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap, int64_t* out_vocab_off,
+                    int max_vocab, int* out_n_vocab, int32_t* out_merges, int max_merges_out, int* out_n_merges,
+                    void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

@@ -1,0 +1,65 @@
+"""The one-call training C-ABI (``beast_bpe_train``, csrc/bpe_train_api.hip) against HF: the
+golden HF BpeTrainer vocabularies / merges of tests/golden/bpe_hf.json on their corpora, live HF
+with special tokens, max_token_length and min_frequency, and the Python driver on the same GPU."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_json, load_npz
+from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe, train_bpe_capi
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["rand256/700", "skew/2048", "runs/700", "traj_k3/700", "repeat700/2048",
+                                  "rand256/2048"])
+def test_capi_train_matches_hf_golden(case, gpu_device):
+    ref = load_json("bpe_hf.json").get(case)
+    if ref is None:
+        pytest.skip(f"no golden {case}")
+    cname, vs = case.split("/")
+    arr = load_npz("bpe_corpora.npz")[cname]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    res = train_bpe_capi(flat, off, int(vs))
+    assert (res.min_token, res.max_token) == (ref["min_token"], ref["max_token"])
+    assert res.vocab == ref["vocab"]
+    assert [list(m) for m in res.merges] == ref["merges"]
+    py = train_bpe(flat, off, int(vs))
+    assert py.vocab == res.vocab and py.merges == res.merges
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("special,max_len,min_freq", [
+    ((), 10000, 2), (("<pad>", "<eos>"), 10000, 2), ((), 3, 2), ((), 10000, 5), (("<s>",), 2, 3)])
+def test_capi_train_options_match_live_hf(special, max_len, min_freq, gpu_device):
+    tokenizers = pytest.importorskip("tokenizers")
+    from tokenizers.trainers import BpeTrainer
+    rng = np.random.default_rng(len(special) * 100 + max_len + min_freq)
+    base = rng.integers(0, 300, size=7)
+    arr = base[rng.integers(0, 7, size=(40, 30))]
+    arr[::5] = rng.integers(0, 300, size=(8, 30))
+    lo, hi = int(arr.min()), int(arr.max())
+    bpe = tokenizers.ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=1200, min_frequency=min_freq, show_progress=False, special_tokens=list(special),
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=max_len)
+    bpe._tokenizer.train_from_iterator(["".join(map(chr, r - lo)) for r in arr], trainer=tr)
+    m = json.loads(bpe._tokenizer.to_str())["model"]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    res = train_bpe_capi(flat, off, 1200, min_frequency=min_freq, special_tokens=special, max_token_length=max_len)
+    assert res.vocab == m["vocab"]
+    assert [list(x) for x in res.merges] == [list(x) for x in m["merges"]]
+
+
+@pytest.mark.gpu
+def test_capi_train_rejects_empty_and_wide(gpu_device):
+    from beast_tokenizer_amd import _lib
+    flat = torch.zeros(0, dtype=torch.int64, device=gpu_device)
+    off = torch.zeros(2, dtype=torch.int64, device=gpu_device)
+    with pytest.raises(ValueError, match="No non-empty sequences"):
+        train_bpe_capi(flat, off, 300)
+    arr = np.arange(0, 6000, dtype=np.int64).reshape(60, 100)   # alphabet > 4096: the Python driver's loop
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr).to(gpu_device))
+    with pytest.raises(NotImplementedError, match="4096"):
+        train_bpe_capi(flat, off, 6500)
+    assert _lib.load() is not None
