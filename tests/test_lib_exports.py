@@ -264,3 +264,20 @@ def test_library_fingerprint_is_path_independent(tmp_path):
     spec.loader.exec_module(mod)
     assert mod.REPO != _build.REPO
     assert mod._fingerprint() == _build._fingerprint()
+
+
+def test_docs_name_existing_tests():
+    """Every test_* name DESIGN.md / INTEGRATION.md cite is a test function or module in tests/."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tests = os.path.join(root, "tests")
+    src = ""
+    for f in os.listdir(tests):
+        if f.endswith(".py"):
+            with open(os.path.join(tests, f)) as fh:
+                src += fh.read()
+    modules = {f[:-3] for f in os.listdir(tests) if f.endswith(".py")}
+    for doc in ("DESIGN.md", "INTEGRATION.md"):
+        with open(os.path.join(root, doc)) as fh:
+            names = set(re.findall(r"\btest_[a-z0-9_]+", fh.read()))
+        missing = [n for n in sorted(names) if n not in modules and not re.search(rf"def {n}\b", src)]
+        assert not missing, f"{doc} cites tests that do not exist: {missing}"
