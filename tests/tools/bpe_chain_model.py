@@ -7,7 +7,7 @@ the same words -- with the round-3 rule, and with a chained candidate taken when
 so far has been applied, its exact count still beats the next untaken old key and every new pair
 the batch created (their counts are the merges' own deltas) -- checks both against the host-driven
 loop (HF's sequence), and prints the pass counts.
-    python tools/bpe_chain_model.py [n_sequences] [vocab]
+    python tests/tools/bpe_chain_model.py [n_sequences] [vocab]
 """
 import os
 import sys
@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REPO = os.path.dirname(HERE)
+REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from cpu_ops import NumpyBpeOps  # noqa: E402

@@ -2,15 +2,15 @@
 a K5-like corpus (the oracle's encode of N synthetic trajectories, seed 7, with the golden bounds),
 HF's ByteLevel pre-tokeniser, and HF's own BPE model built from the first k merges of
 tests/golden/k5_bpe.json.  Asks whether dropping fully merged words from the merge loop's
-signature scan could pay.      python tools/bpe_live_words.py [N]
+signature scan could pay.      python tests/tools/bpe_live_words.py [N]
 """
 import sys, json, numpy as np, time
 import os
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle import beast_oracle as O
 from beast_tokenizer_amd.synthetic import synth_trajectories
 from tokenizers import pre_tokenizers, Tokenizer, models
-g = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'tests', 'golden', 'k5_bpe.json')))
+g = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), 'tests', 'golden', 'k5_bpe.json')))
 TAU = 2 * np.pi
 times = O.times_grid(TAU, 50)
 pj = O.basis(times, TAU, 4, 10)

@@ -2,14 +2,14 @@
 timed against the reference itself (mp_pytorch + beast.utils through tests/golden/gen_goldens.py's
 RefGlue) on the same B=4,096 batch, same threads, in this container (the reference does not
 travel to the GPU box).  Writes profiles/r02/cpu_port_vs_reference.json.
-    python tools/cpu_port_vs_reference.py [threads]"""
+    python tests/tools/cpu_port_vs_reference.py [threads]"""
 import json
 import os
 import sys
 import time
 
 sys.dont_write_bytecode = True
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
 
