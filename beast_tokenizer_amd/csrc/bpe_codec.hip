@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
     s_lut[i] = i < a.lut_n ? a.lut[i] : (uint8_t)CLS_OTHER;
   }
   for (int i = threadIdx.x; i < lcap; i += blockDim.x) ltab[i] = 0ull;
-  if (threadIdx.x <= DW_MID) s_hist[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i <= DW_MID; i += blockDim.x) s_hist[i] = 0;   // 65 bins: one wave is 64 threads
   if (threadIdx.x == 0) { s_nd = 0; s_next = nwv; }
   __syncthreads();
   const DwRow L = dw_carve(rows + (size_t)wave * rb, a.Lc, a.S);
@@ -1062,8 +1062,10 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   if (r < a.n_rows) BPE_STAMP(5);
   // 4. merges: a mid word (17..64 byte symbols) per wave, words of 9..16 four to a wave (16-lane
   // rows), words of <= 8 eight to a wave (half rows)
-  const int nmid = s_hist[DW_SHORT + 1];   // the cursor of length 17 has passed every longer word
-  const int n9 = s_hist[DW_TINY + 1];      // ... of length 9: every word of 9 or more
+  // the cursor of length 17 has passed every longer word, that of length 9 every word of 9 or
+  // more (clamped: the task count bounds the loop below, so it never exceeds the word count)
+  const int nmid = min(max(s_hist[DW_SHORT + 1], 0), nd);
+  const int n9 = min(max(s_hist[DW_TINY + 1], nmid), nd);
   const int t16 = nmid + (n9 - nmid + 3) / 4;
   const int tasks = t16 + (nd - n9 + 7) / 8;
   int nrounds = 0;

@@ -265,3 +265,23 @@ def test_words_non_monotone_model_uses_heap(gpu_device):
     got, status = encode_rows(model, [[ord(c) for c in s] for s in texts], gpu_device)
     assert not status.any()
     assert got == [e.ids for e in tok.encode_batch(texts, add_special_tokens=False)]
+
+
+@pytest.mark.parametrize("width", [1500, 3500])
+def test_words_long_rows_match_hf(width, gpu_device):
+    """Long rows change k_bpe_words' launch: fewer rows per workgroup as the row image grows, and
+    past ~3,300 code points the merge map no longer fits beside one row, so the lookups read the
+    cuckoo map from HBM (k_bpe_words<false>).  HF's ids either way."""
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_codec import ST_FALLBACK
+    tok, model, rng, centre = _trained_model(255, 600, 140, 1500, 11, gpu_device)
+    test = np.clip(centre[:24] + np.round(rng.normal(0, 255 / 12, size=(24, width))), 0, 255).astype(np.int64)
+    flat, off, w = rows_from_sequences(list(test), gpu_device)
+    ids, lens, st = model.encode_rows(flat, off, w, 0, 255, resolve=False)
+    st = st.cpu().numpy()
+    want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in test], add_special_tokens=False)]
+    ids, lens = ids.cpu().numpy(), lens.cpu().numpy()
+    assert ((st == 0) | (st == ST_FALLBACK)).all() and (st == 0).sum() >= 12
+    for i in np.flatnonzero(st == 0):
+        assert ids[i, :lens[i]].tolist() == want[i]
+    assert _lib.load() is not None
