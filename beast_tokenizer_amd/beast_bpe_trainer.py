@@ -72,7 +72,12 @@ class FIGBPE:
         max_token_length: int = 10000,
         device: Optional[Union[str, torch.device]] = None,
         process_group=None,
+        replicate: bool = True,
     ) -> None:
+        """``process_group`` / ``replicate`` (extensions): train on the union of
+        the ranks' corpora; ``replicate`` all-gathers the distinct words once and runs the
+        merge loop on every rank, ``replicate=False`` keeps each rank's words and all-reduces
+        the pair-count changes every pass."""
         self.vocab_size = vocab_size
         self.min_frequency = min_frequency
         self.special_tokens = list(special_tokens or [])
@@ -80,6 +85,7 @@ class FIGBPE:
         self.max_token_length = max_token_length
         self.device = torch.device(device) if device is not None else None
         self.process_group = process_group
+        self.replicate = replicate
 
         self.tokenizer: Optional[ByteLevelBPETokenizer] = None
         self.min_token: Optional[int] = None
@@ -97,7 +103,7 @@ class FIGBPE:
     def _train(self, tokens: torch.Tensor, seq_off: torch.Tensor, alphabet=None) -> FIGBPEState:
         res = train_bpe(tokens, seq_off, self.vocab_size, min_frequency=self.min_frequency,
                         special_tokens=self.special_tokens, max_token_length=self.max_token_length,
-                        initial_alphabet=alphabet, reduce=self._reducer())
+                        initial_alphabet=alphabet, reduce=self._reducer(), replicate=self.replicate)
         self.last_result = res
         tokenizer = tokenizer_from_result(res, self.special_tokens)
         self.tokenizer = tokenizer
@@ -117,7 +123,8 @@ class FIGBPE:
         # the strings are already shifted code points: min_token is 0 by construction
         res = train_bpe(tokens, off, self.vocab_size, min_frequency=self.min_frequency,
                         special_tokens=self.special_tokens, max_token_length=self.max_token_length,
-                        initial_alphabet=list(alphabet), reduce=self._reducer(), mn_mx=(0, hi))
+                        initial_alphabet=list(alphabet), reduce=self._reducer(), mn_mx=(0, hi),
+                        replicate=self.replicate)
         self.last_result = res
         return tokenizer_from_result(res, self.special_tokens)
 
@@ -139,12 +146,24 @@ class FIGBPE:
         batch_key: str = "actions",
         max_sequences: Optional[int] = None,
     ) -> FIGBPEState:
-        """Reference :100-151: encode batches (offset-free mp tokens) on the GPU, then train."""
+        """Reference :100-151: encode batches (offset-free mp tokens) on the GPU, then train.
+
+        With ``process_group`` and ``update_bounds`` every encode widens the bounds by the
+        extremes of all ranks' current batches (one all-reduce per step), so
+        the ranks' bounds stay identical and the union of their corpora is the one a single
+        process builds from the global batches; a rank whose batches run out keeps taking
+        part in those steps with no rows until every rank is done."""
         rows: List[torch.Tensor] = []
         collected = 0
         encode_fn = getattr(tokenizer, "encode_to_mp_tokens", None)
         if encode_fn is None:
             encode_fn = tokenizer.encode
+        group = self.process_group if update_bounds else None
+        if group is not None:
+            enc = encode_fn
+
+            def encode_fn(data, update_bounds):  # noqa: F811 - the collective form
+                return enc(data, update_bounds=update_bounds, process_group=group)
         progress_bar = None
         if self.show_progress and tqdm is not None:
             progress_bar = tqdm(total=max_sequences, desc="Collecting BEAST sequences for BPE", unit="seq",
@@ -170,6 +189,9 @@ class FIGBPE:
                 break
         if progress_bar is not None:
             progress_bar.close()
+        if group is not None:   # match the other ranks' remaining bounds all-reduces, then stop together
+            while bool(tokenizer.update_weights_bounds_per_batch(None, process_group=group)):
+                pass
         if not rows or collected == 0:
             if self.process_group is None:
                 raise ValueError("No non-empty sequences provided for BPE training.")

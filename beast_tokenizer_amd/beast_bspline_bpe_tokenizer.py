@@ -150,14 +150,16 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
                               update_bounds: bool = False, batch_key: str = "actions",
                               max_sequences: Optional[int] = None, min_frequency: int = 2,
                               special_tokens: Optional[Sequence[str]] = None, show_progress: bool = True,
-                              max_token_length: int = 10000, process_group=None) -> "FIGBPEState":
+                              max_token_length: int = 10000, process_group=None,
+                              replicate: bool = True) -> "FIGBPEState":
         """Train the internal BPE model on BEAST bins (reference :111-146), on the GPU.
-        ``process_group`` (extension) shards the corpus over ranks."""
+        ``process_group`` / ``replicate`` (extensions) shard the corpus over ranks (DESIGN.md
+        §7); with ``update_bounds`` the ranks' bounds follow the global batches."""
         from .beast_bpe_trainer import FIGBPE
         trainer = FIGBPE(vocab_size=self.bpe_vocab_size, min_frequency=min_frequency,
                          special_tokens=special_tokens, show_progress=show_progress,
                          max_token_length=max_token_length, device=self._dev(),
-                         process_group=process_group)
+                         process_group=process_group, replicate=replicate)
         state = trainer.fit_from_trajectories(self, trajectories, update_bounds=update_bounds,
                                               batch_key=batch_key, max_sequences=max_sequences)
         self.set_bpe_tokenizer(state.tokenizer, min_token=state.min_token, max_token=state.max_token)
@@ -227,17 +229,20 @@ class BEASTBsplineBPETokenizer(BEASTBsplineTokenizer):
 
     # ------------------------------------------------------------------ BEAST API with BPE
 
-    def encode_to_mp_tokens(self, trajs: torch.Tensor, update_bounds: bool = False) -> tuple:
-        """Expose the underlying MP-token encoding without BPE."""
+    def encode_to_mp_tokens(self, trajs: torch.Tensor, update_bounds: bool = False, *,
+                            process_group=None) -> tuple:
+        """Expose the underlying MP-token encoding without BPE.  ``process_group``: see
+        :meth:`BEASTBsplineTokenizer.encode` (global-batch bounds with ``update_bounds``)."""
         return BEASTBsplineTokenizer.encode(self, trajs, update_bounds=update_bounds,
-                                            respect_llm_vocab_size=False)
+                                            respect_llm_vocab_size=False, process_group=process_group)
 
     def encode(self, trajs: torch.Tensor, update_bounds: bool = False, *,
-               return_mp_tokens: bool = False, return_tensors: bool = False) -> tuple:
+               return_mp_tokens: bool = False, return_tensors: bool = False, process_group=None) -> tuple:
         """return_tensors (an extension): the BPE ids as ``BpeIds(ids, lengths)`` -- a device
         block padded with ``PAD_ID`` that ``decode`` / ``bpe_to_mp_tokens`` take as is --
         instead of ``List[List[int]]``; the ids are the same."""
-        mp_tokens, params = self.encode_to_mp_tokens(trajs, update_bounds=update_bounds)
+        mp_tokens, params = self.encode_to_mp_tokens(trajs, update_bounds=update_bounds,
+                                                     process_group=process_group)
         out = (self._discrete_to_bpe(mp_tokens, as_tensors=return_tensors), params)
         return out + (mp_tokens,) if return_mp_tokens else out
 

@@ -64,6 +64,19 @@ class _MPInfo:
                 f"tau={self.tau:.6g})")
 
 
+def widen_bounds(w_min: torch.Tensor, w_max: torch.Tensor, batch_min: torch.Tensor, batch_max: torch.Tensor) -> None:
+    """In place: take a batch extreme where it lies beyond the bound by more than 1e-4
+    (reference beast_bspline_tokenizer.py:384-389: the masks, then ``masked_scatter_``; a
+    ``where`` writes the same values).  Pure torch: the device-agnostic step after the
+    (all-reduced) batch min/max."""
+    wmin = w_min.to(batch_min.device)
+    wmax = w_max.to(batch_max.device)
+    smaller_mask = batch_min < (wmin - 1e-4)
+    larger_mask = batch_max > (wmax + 1e-4)
+    w_min.copy_(torch.where(smaller_mask, batch_min, wmin).to(w_min.device))
+    w_max.copy_(torch.where(larger_mask, batch_max, wmax).to(w_max.device))
+
+
 _FAST = None
 
 
@@ -599,27 +612,46 @@ class BEASTBsplineTokenizer(TokenizerBase):
         params, _ = self._fit(demos, None, p)
         return params
 
+    def _batch_minmax(self, weights, process_group, active=True):
+        """Column (min, max) of ``weights`` [rows, D*N] on this rank, all-reduced over
+        ``process_group`` (None: this process only; True: the default group) so every rank
+        holds the extremes of the global batch.  ``weights=None`` (or
+        ``active=False``) takes part in the collective without rows.  Returns
+        (mn, mx, any_rank_active)."""
+        from .quantile import allreduce_minmax, column_minmax
+        from .bpe_train import no_reduce, torch_dist_reducer
+        cols = self.num_dof * self.num_basis
+        if weights is not None and active:
+            mn, mx = column_minmax(weights.reshape(-1, cols))
+        else:
+            if process_group is None:
+                raise ValueError("an empty bounds update needs a process_group")
+            dev = self._dev()
+            mn = torch.full((cols,), float("inf"), dtype=torch.float32, device=dev)
+            mx = torch.full((cols,), float("-inf"), dtype=torch.float32, device=dev)
+            active = False
+        reduce = no_reduce if process_group is None else torch_dist_reducer(
+            None if process_group is True else process_group)
+        return allreduce_minmax(mn, mx, reduce, active)
+
     @torch.no_grad()
-    def update_weights_bounds(self, demos):
-        """w_min/w_max <- column min/max of the batch's params (reference :362-378)."""
-        from .quantile import column_minmax
+    def update_weights_bounds(self, demos, *, process_group=None):
+        """w_min/w_max <- column min/max of the batch's params (reference :362-378).
+        ``process_group`` (extension, a collective): the min/max of every rank's batch."""
         weights = self.compute_weights(demos)
-        mn, mx = column_minmax(weights)
+        mn, mx, _ = self._batch_minmax(weights, process_group)
         self.w_min.copy_(mn.to(self.w_min.device))
         self.w_max.copy_(mx.to(self.w_max.device))
 
     @torch.no_grad()
-    def update_weights_bounds_per_batch(self, weights):
-        """Widen w_min/w_max by the batch extremes beyond a 1e-4 margin (reference :379-389)."""
-        from .quantile import column_minmax
-        weights = weights.reshape(-1, self.num_dof * self.num_basis)
-        batch_min, batch_max = column_minmax(weights)
-        wmin = self.w_min.to(batch_min.device)
-        wmax = self.w_max.to(batch_max.device)
-        smaller_mask = batch_min < (wmin - 1e-4)
-        larger_mask = batch_max > (wmax + 1e-4)
-        self.w_min.copy_(torch.where(smaller_mask, batch_min, wmin).to(self.w_min.device))
-        self.w_max.copy_(torch.where(larger_mask, batch_max, wmax).to(self.w_max.device))
+    def update_weights_bounds_per_batch(self, weights, *, process_group=None):
+        """Widen w_min/w_max by the batch extremes beyond a 1e-4 margin (reference :379-389).
+        ``process_group`` (extension, a collective): the extremes of the global batch, so
+        every rank's bounds stay identical.  ``weights=None``: this rank has no batch this
+        step but takes part; returns whether any rank had one (a 0-d bool tensor)."""
+        batch_min, batch_max, any_active = self._batch_minmax(weights, process_group, weights is not None)
+        widen_bounds(self.w_min, self.w_max, batch_min, batch_max)
+        return any_active
 
     def update_times(self, times):
         self.times = times.to(self.device)
@@ -628,11 +660,14 @@ class BEASTBsplineTokenizer(TokenizerBase):
     #           - tokenizer encoding -
     # ===============================================
 
-    def encode(self, trajs, update_bounds=False, *, respect_llm_vocab_size=True):
+    def encode(self, trajs, update_bounds=False, *, respect_llm_vocab_size=True, process_group=None):
         """(tokens int64 [B, num_basis*num_dof], params_dict) -- reference :399-428.
 
         No autograd graph is recorded: the outputs are written by the kernel into fresh
-        tensors (the reference runs under ``torch.no_grad`` equivalently)."""
+        tensors (the reference runs under ``torch.no_grad`` equivalently).
+        ``process_group`` (extension): with ``update_bounds`` the bounds widen by the
+        extremes of every rank's batch (one all-reduce; a collective call), so all ranks
+        quantise with the same bounds -- those of one process encoding the global batch."""
         p = self._plan()
         offset = (self.llm_vocab_size - self.vocab_size
                   if respect_llm_vocab_size and self.llm_vocab_size is not None else 0)
@@ -643,7 +678,7 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if update_bounds:
             with torch.no_grad():
                 params, _ = self._fit(trajs, None, p)
-                self.update_weights_bounds_per_batch(params)
+                self.update_weights_bounds_per_batch(params, process_group=process_group)
                 tokens = self._quantize(params, offset, p.dev, mode=0)
         else:
             params, tokens = self._fit(trajs, offset, p)
@@ -665,12 +700,12 @@ class BEASTBsplineTokenizer(TokenizerBase):
         return out
 
     @torch.no_grad()
-    def encode_continuous(self, trajs, update_bounds=False):
+    def encode_continuous(self, trajs, update_bounds=False, *, process_group=None):
         """Normalised params in [-1, 1], (t d) order (reference :430-450)."""
         p = self._plan()
         params, _ = self._fit(trajs, None, p)
         if update_bounds:
-            self.update_weights_bounds_per_batch(params)
+            self.update_weights_bounds_per_batch(params, process_group=process_group)
         tokens = self._quantize(params, 0, p.dev, mode=1)
         params_dict = {"params": params, **self._cond_dict()}
         return tokens, params_dict

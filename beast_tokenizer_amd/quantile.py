@@ -110,6 +110,33 @@ def column_quantiles(x, qs: Sequence[float], reduce: Reducer = no_reduce, ops=No
     return ops.finalize()
 
 
+def allreduce_minmax(mn: torch.Tensor, mx: torch.Tensor, reduce: Reducer, active: bool = True):
+    """Column (min, max) of the union of all ranks' rows from each rank's own (min, max):
+    SURVEY.md §8e's allreduce(MIN)/allreduce(MAX) for the update_bounds paths
+    (beast/beast_bspline_tokenizer.py:362-389), packed into ONE MIN all-reduce of
+    ``[mn | -mx | nan flags | idle flag]`` (negation is exact, so -min(-x) = max(x) bitwise).
+
+    torch's ``min``/``max`` propagate NaN; an all-reduce's float MIN need not, so a column
+    that is NaN on any rank is carried as a flag and restored as NaN afterwards.  A rank
+    with no rows this step (``active=False``) contributes (+inf, -inf) and is neutral.
+    Returns ``(mn, mx, any_rank_active)``; with ``no_reduce`` it returns the inputs (and
+    ``active`` as given)."""
+    if reduce is no_reduce:
+        return mn, mx, active
+    cols = mn.numel()
+    nan = torch.isnan(mn) | torch.isnan(mx)
+    inf = torch.full_like(mn, float("inf"))
+    packed = torch.cat([torch.where(nan, inf, mn), torch.where(nan, inf, -mx),
+                        torch.where(nan, torch.zeros_like(mn), torch.ones_like(mn)),
+                        torch.tensor([0.0 if active else 1.0], dtype=mn.dtype, device=mn.device)])
+    reduce(packed, "min")
+    g_nan = packed[2 * cols: 3 * cols] == 0
+    nanv = torch.full_like(mn, float("nan"))
+    g_mn = torch.where(g_nan, nanv, packed[:cols])
+    g_mx = torch.where(g_nan, nanv, -packed[cols: 2 * cols])
+    return g_mn, g_mx, packed[3 * cols] == 0   # 0-d bool tensor: no host sync unless read
+
+
 def column_minmax(x: torch.Tensor):
     """(min, max) over dim 0 with torch's NaN propagation, fp32 [cols] each."""
     _lib.require_gpu(x, "weights")

@@ -218,6 +218,29 @@ def quantile_bounds(params: np.ndarray):
     return (np.quantile(params, 0.01, 0).astype(F32), np.quantile(params, 0.99, 0).astype(F32))
 
 
+def update_bounds(weights: np.ndarray):
+    """``update_weights_bounds`` (beast_bspline_tokenizer.py:362-378): column min / max of the
+    batch's params (torch's min / max propagate NaN, as numpy's do)."""
+    w = np.asarray(weights, F32).reshape(-1, weights.shape[-1])
+    return w.min(0), w.max(0)
+
+
+def update_bounds_per_batch(wmin: np.ndarray, wmax: np.ndarray, weights: np.ndarray):
+    """``update_weights_bounds_per_batch`` (beast_bspline_tokenizer.py:379-389): the batch
+    extremes replace a bound they pass by more than 1e-4 (fp32 compare against bound -/+ 1e-4,
+    the subtraction rounded in fp32 as torch does); returns the new (wmin, wmax)."""
+    bmin, bmax = update_bounds(weights)
+    wmin, wmax = np.asarray(wmin, F32), np.asarray(wmax, F32)
+    lo = torch.as_tensor(wmin) - 1e-4
+    hi = torch.as_tensor(wmax) + 1e-4
+    smaller = torch.as_tensor(bmin) < lo
+    larger = torch.as_tensor(bmax) > hi
+    out_lo, out_hi = wmin.copy(), wmax.copy()
+    out_lo[smaller.numpy()] = bmin[smaller.numpy()]
+    out_hi[larger.numpy()] = bmax[larger.numpy()]
+    return out_lo, out_hi
+
+
 def quantile_ranks(n: int, q: float):
     """numpy 2.x 'linear' method in the input dtype (float32): (lo, hi, gamma)."""
     vi = F32(n - 1) * F32(q)

@@ -27,6 +27,20 @@ def _free_port():
     return p
 
 
+def _bounds_steps():
+    """Four global batches of params [rows, 12]: growing spread, a column that moves by less
+    than the 1e-4 hysteresis, and a NaN in rank 0's part of step 2."""
+    rng = np.random.default_rng(11)
+    steps = []
+    for k in range(4):
+        g = (rng.standard_normal((16, 12)) * (0.01 + 0.02 * k)).astype(np.float32)
+        g[:, 5] = np.float32(0.02 + 5e-5 * k)          # inside the margin: never widens w_max
+        g[-1, 7] = np.float32(-0.5 - k)                 # the extreme sits on the last rank
+        steps.append(g)
+    steps[2][1, 9] = np.nan
+    return steps
+
+
 def _worker(rank, world, port, case, q):
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, HERE)
@@ -49,6 +63,40 @@ def _worker(rank, world, port, case, q):
             assert res.stats["sharded"] == (mode != "gather_words")
             assert res.stats["device_loop"] == (mode != "per_merge_allreduce")
             q.put((rank, res.vocab, [list(m) for m in res.merges], res.min_token, res.max_token))
+        elif case[0] == "bounds":
+            # the update_bounds collective: each step's global batch is split over the ranks
+            # (unevenly; rank 1 runs out one step early and takes part with no rows, as
+            # FIGBPE.fit_from_trajectories does); every rank must hold the bounds one process
+            # gets from the concatenated batches (oracle: reference :362-389)
+            from beast_tokenizer_amd.beast_bspline_tokenizer import widen_bounds
+            from beast_tokenizer_amd.quantile import allreduce_minmax
+            steps = _bounds_steps()
+            w_min = torch.full((12,), -0.02)
+            w_max = torch.full((12,), 0.02)
+            trace = []
+            for k, g in enumerate(steps):
+                cut = 3 + 2 * k
+                mine = g[:cut] if rank == 0 else g[cut:]
+                if rank == 1 and k == len(steps) - 1:
+                    mine = None
+                if mine is not None:
+                    t = torch.from_numpy(mine)
+                    mn, mx, act = allreduce_minmax(t.min(0)[0], t.max(0)[0], red, True)
+                else:
+                    mn, mx, act = allreduce_minmax(torch.full((12,), float("inf")),
+                                                   torch.full((12,), float("-inf")), red, False)
+                assert bool(act)
+                widen_bounds(w_min, w_max, mn, mx)
+                trace.append((w_min.numpy().copy(), w_max.numpy().copy()))
+            # the closing idle round every rank takes: nobody active -> all stop together
+            mn, mx, act = allreduce_minmax(torch.full((12,), float("inf")), torch.full((12,), float("-inf")),
+                                           red, False)
+            assert not bool(act)
+            g_mn, g_mx, _ = allreduce_minmax(torch.from_numpy(steps[0][:4]).min(0)[0] if rank == 0 else
+                                             torch.from_numpy(steps[0][4:]).min(0)[0],
+                                             torch.from_numpy(steps[0][:4]).max(0)[0] if rank == 0 else
+                                             torch.from_numpy(steps[0][4:]).max(0)[0], red)
+            q.put((rank, trace, (g_mn.numpy(), g_mx.numpy())))
         else:
             from beast_tokenizer_amd.quantile import column_quantiles
             rng = np.random.default_rng(5)
@@ -88,6 +136,36 @@ def test_bpe_two_ranks_matches_hf(cname, vs, mode):
     assert (lo0, hi0) == (ref["min_token"], ref["max_token"])
     assert v0 == ref["vocab"]
     assert m0 == ref["merges"]
+
+
+def test_update_bounds_two_ranks_match_one_process():
+    """SURVEY §8e's MIN/MAX all-reduce for the update_bounds paths: after every step both ranks
+    hold bitwise the bounds one process computes on the global batch (oracle restatement of
+    reference :379-389), including the NaN column and a rank with no rows; the plain
+    update_weights_bounds form gives the global column min / max."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    from oracle import beast_oracle as O
+    (_, t0, g0), (_, t1, g1) = _run(("bounds",))
+    lo, hi = np.full(12, -0.02, np.float32), np.full(12, 0.02, np.float32)
+    steps = _bounds_steps()
+    for k, g in enumerate(steps):
+        if k == len(steps) - 1:     # rank 1 had no rows: the global batch is rank 0's part
+            g = g[:3 + 2 * k]
+        lo, hi = O.update_bounds_per_batch(lo, hi, g)
+        for trace in (t0, t1):
+            assert np.array_equal(trace[k][0], lo, equal_nan=True), k
+            assert np.array_equal(trace[k][1], hi, equal_nan=True), k
+    want = O.update_bounds(_bounds_steps()[0])
+    for g in (g0, g1):
+        assert np.array_equal(g[0], want[0]) and np.array_equal(g[1], want[1])
+
+
+def test_allreduce_minmax_single_process_is_identity():
+    from beast_tokenizer_amd.bpe_train import no_reduce
+    from beast_tokenizer_amd.quantile import allreduce_minmax
+    mn, mx = torch.tensor([1.0, float("nan")]), torch.tensor([2.0, 3.0])
+    a, b, act = allreduce_minmax(mn, mx, no_reduce)
+    assert a is mn and b is mx and act is True
 
 
 def test_quantile_two_ranks_matches_numpy():
