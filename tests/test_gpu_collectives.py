@@ -162,7 +162,14 @@ def _nccl_worker(rank, world, port, q):
                 fig.fit_from_sequences(seqs)
                 r[f"bpe_{replicate}"] = (fig.last_result.vocab, [list(m) for m in fig.last_result.merges],
                                          fig.min_token, fig.max_token, fig.last_result.stats.get("replicated"))
-            t3 = _tok(dev)
+            t4 = _tok(dev)   # FIGBPE from trajectories with update_bounds: one bounds all-reduce per batch
+            st = t4.fit_from_trajectories([{"actions": x} for x in xs], update_bounds=True, show_progress=False,
+                                          process_group=group)
+            r["fit_traj"] = (t4._last_bpe_result.vocab, [list(m) for m in t4._last_bpe_result.merges],
+                             st.min_token, st.max_token, t4.w_min.cpu().numpy().tolist(), t4.w_max.cpu().numpy().tolist())
+            from beast_tokenizer_amd import BEASTBsplineTokenizer
+            t3 = BEASTBsplineTokenizer(num_dof=14, gripper_indices=[6, 13], gripper_zero_order=True,
+                                       llm_vocab_size=32000, device=str(dev))
             toks = [t3.encode(x, update_bounds=True, process_group=group)[0] for x in xs]
             t3.update_weights_bounds(xs[0], process_group=group)
             r["update_bounds"] = ([tk.cpu().numpy() for tk in toks], t3.w_min.cpu().numpy(), t3.w_max.cpu().numpy())
@@ -188,6 +195,7 @@ def test_rccl_world1_collectives_equal_no_group(gpu_device):
         vb, mb, lob, hib, rep = b[f"bpe_{replicate}"]
         assert (va, ma, loa, hia) == (vb, mb, lob, hib), replicate
         assert rep == replicate     # the group path took the requested multi-rank form
+    assert a["fit_traj"] == b["fit_traj"]
     ta, lo_a, hi_a = a["update_bounds"]
     tb, lo_b, hi_b = b["update_bounds"]
     assert all(np.array_equal(x, y) for x, y in zip(ta, tb))
