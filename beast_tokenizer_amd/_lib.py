@@ -79,6 +79,7 @@ SIGNATURES = {
     "beast_bpe_loop_batch": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
                                     _vp, _vp, _sz, _i32, _vp, _vp, _vp]),
     "beast_bpe_dedup_workspace_bytes": (_sz, [_i64]),
+    "beast_bpe_dedup_workspace_bytes_safe": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),
     "beast_bpe_repack_words": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -126,10 +126,13 @@ class GpuBpeModel:
         wm_host = np.zeros(wm_bytes // 4, dtype=np.uint32)
         arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in (ma, mb, mn)]
         lb = ctypes.c_int(0)
-        _lib.run("beast_bpe_wordmap_build_host", *[x.ctypes.data if self.n_merges else None for x in arrs],
-                 self.n_merges, wm_host.ctypes.data, wm_bytes, ctypes.byref(lb))
-        self.wordmap_log2b = lb.value
-        self.wordmap = torch.from_numpy(wm_host[:4 << lb.value].view(np.int32).copy()).to(device)
+        try:
+            _lib.run("beast_bpe_wordmap_build_host", *[x.ctypes.data if self.n_merges else None for x in arrs],
+                     self.n_merges, wm_host.ctypes.data, wm_bytes, ctypes.byref(lb))
+            self.wordmap_log2b = lb.value
+            self.wordmap = torch.from_numpy(wm_host[:4 << lb.value].view(np.int32).copy()).to(device)
+        except NotImplementedError:   # no cuckoo placement at either table size: per-row kernel only
+            self.wordmap_log2b, self.wordmap = 0, None
         self.monotone = rank_monotone(list(zip(ma, mb, mn)))
         self._max_id = max(vocab.values()) if vocab else 0   # 0xFFFF marks "no id" in k_bpe_words
 
@@ -222,12 +225,35 @@ class GpuBpeModel:
             out = self._encode_rows_words(tok, row_off, max_row, min_token, max_span)
         except NotImplementedError:   # rows too long for k_bpe_words' LDS image: the per-row kernel
             return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
-        if resolve and R and bool((out[2] == ST_FALLBACK).any()):
-            return self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+        if resolve and R:
+            fr = torch.nonzero(out[2] == ST_FALLBACK).flatten()
+            if fr.numel():
+                self._resolve_fallback(fr, *out, tok, row_off, max_row, min_token, max_span)
         return out
 
+    def _resolve_fallback(self, fr, ids, lens, status, tok, row_off, max_row, min_token, max_span) -> None:
+        """Re-encode only the rows ``fr`` (device indices) that k_bpe_words returned as ST_FALLBACK
+        (a word over 64 byte symbols) with the per-row kernel, in place: the other rows keep the
+        by-words result (the same ids; both are HF's)."""
+        dev = self.device
+        fr = fr.to(torch.int64)
+        starts = row_off[fr].to(torch.int64)
+        n = row_off[fr + 1].to(torch.int64) - starts
+        sub_off = torch.zeros(fr.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(n, 0, out=sub_off[1:])
+        total = int(sub_off[-1])
+        idx = torch.repeat_interleave(starts - sub_off[:-1], n, output_size=total) + \
+            torch.arange(total, dtype=torch.int64, device=dev)
+        i2, l2, s2 = self._encode_rows_kernel(tok[idx], sub_off, max_row, min_token, max_span)
+        if i2.shape[1] != ids.shape[1]:   # same max_row / max_span -> same width (both kernels size it so)
+            raise RuntimeError("BPE encode: fallback rows came back with a different id width")
+        ids[fr] = i2
+        lens[fr] = l2
+        status[fr] = s2
+
     def _words_ok(self) -> bool:
-        return _ENCODE_PATH["path"] == "auto" and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
+        return (_ENCODE_PATH["path"] == "auto" and self.n_spec == 0 and self.monotone and self._max_id < 0xFFFF
+                and self.wordmap is not None)
 
     def _encode_rows_kernel(self, tok, row_off, max_row, min_token, max_span):
         """The per-row kernel (k_bpe_encode): special tokens, fallback rows, non-monotone models
@@ -293,10 +319,10 @@ class GpuBpeModel:
         st_h.copy_(status, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         st_np = st_h.numpy()
-        if (st_np == ST_FALLBACK).any():   # a word over 64 byte symbols / a key collision: per-row kernel
-            ids, lens, status = self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
-            W = ids.shape[1]
-            ids_h = blk[:R * W].view(R, W)
+        fb = np.flatnonzero(st_np == ST_FALLBACK)
+        if fb.size:   # a word over 64 byte symbols: those rows (only) through the per-row kernel
+            self._resolve_fallback(torch.from_numpy(fb).to(self.device), ids, lens, status, tok, row_off, max_row,
+                                   min_token, max_span)
             ids_h.copy_(ids, non_blocking=True)
             lens_h.copy_(lens, non_blocking=True)
             st_h.copy_(status, non_blocking=True)
@@ -326,7 +352,8 @@ class GpuBpeModel:
         first_bad = torch.where(status != 0, torch.arange(R, device=self.device, dtype=torch.int32), R).min()
         summ = torch.stack([first_bad, lens.max(), (status == ST_FALLBACK).any().to(torch.int32)]).cpu()
         if int(summ[2]):
-            ids, lens, status = self._encode_rows_kernel(tok, row_off, max_row, min_token, max_span)
+            self._resolve_fallback(torch.nonzero(status == ST_FALLBACK).flatten(), ids, lens, status, tok, row_off,
+                                   max_row, min_token, max_span)
             first_bad = torch.where(status != 0, torch.arange(R, device=self.device, dtype=torch.int32), R).min()
             summ = torch.stack([first_bad, lens.max()]).cpu()
         r_bad, w = int(summ[0]), int(summ[1])

@@ -588,7 +588,8 @@ def fixed_rows_to_device(tokens: torch.Tensor) -> Tuple[torch.Tensor, torch.Tens
 
 
 def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
-                   special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000) -> BPEResult:
+                   special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
+                   vocab_bytes_cap: Optional[int] = None) -> BPEResult:
     """The same training through the one-call C-ABI ``beast_bpe_train`` (include/beast_hip.h):
     what a non-Python caller binds.  Single GPU; raises NotImplementedError where the C entry
     point defers to this module's driver (Vt > 4096, a string-hash collision)."""
@@ -601,18 +602,30 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
     n_base_max = 512 + len(special_tokens) + max(int(mm[1]) - int(mm[0]) + 1, 0)
     max_vocab = max(vocab_size, n_base_max)
     merges = np.zeros(2 * max(vocab_size, 1), dtype=np.int32)
-    vbytes = np.zeros(max(64 * max_vocab, 1024) + 8 * int(max_token_length or 10000), dtype=np.uint8)
+    vbytes = np.zeros(vocab_bytes_cap or (max(64 * max_vocab, 1024) + 8 * int(max_token_length or 10000)),
+                      dtype=np.uint8)
+    retried = False
     voff = np.zeros(max_vocab + 1, dtype=np.int64)
     out = [ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int(), ctypes.c_int()]
     specs = [t.encode("utf-8") for t in special_tokens]
     sarr = (ctypes.c_char_p * max(len(specs), 1))(*specs)
-    _lib.run("beast_bpe_train", tokens.data_ptr(), seq_off.data_ptr(), n_seq, lut.data_ptr(), lut.numel(),
-             int(vocab_size), int(min_frequency), int(max_token_length or 0), sarr, len(specs),
-             ctypes.byref(out[0]), ctypes.byref(out[1]), vbytes.ctypes.data, vbytes.nbytes, voff.ctypes.data,
-             max_vocab, ctypes.byref(out[2]), merges.ctypes.data, max(vocab_size, 1), ctypes.byref(out[3]),
-             _lib.stream_of(dev))
+    for attempt in range(2):
+        rc = _lib.call("beast_bpe_train", tokens.data_ptr(), seq_off.data_ptr(), n_seq, lut.data_ptr(), lut.numel(),
+                       int(vocab_size), int(min_frequency), int(max_token_length or 0), sarr, len(specs),
+                       ctypes.byref(out[0]), ctypes.byref(out[1]), vbytes.ctypes.data, vbytes.nbytes,
+                       voff.ctypes.data, max_vocab, ctypes.byref(out[2]), merges.ctypes.data, merges.size // 2,
+                       ctypes.byref(out[3]), _lib.stream_of(dev))
+        if rc != _lib.BEAST_E_WORKSPACE or attempt:
+            _lib.check(rc, "beast_bpe_train")
+            break
+        # an output was too small: the call reported the sizes it needs (include/beast_hip.h)
+        retried = True
+        max_vocab = max(max_vocab, out[2].value)
+        vbytes = np.zeros(max(vbytes.nbytes, int(voff[0])), dtype=np.uint8)
+        voff = np.zeros(max_vocab + 1, dtype=np.int64)
+        merges = np.zeros(2 * max(merges.size // 2, out[3].value), dtype=np.int32)
     nv, nm = out[2].value, out[3].value
     id2str = [bytes(vbytes[voff[i]:voff[i + 1]]).decode("utf-8") for i in range(nv)]
     pairs = [(id2str[int(merges[2 * m])], id2str[int(merges[2 * m + 1])]) for m in range(nm)]
     return BPEResult(vocab={t: i for i, t in enumerate(id2str)}, merges=pairs, min_token=out[0].value,
-                     max_token=out[1].value, stats={"capi": True, "n_merges": nm})
+                     max_token=out[1].value, stats={"capi": True, "n_merges": nm, "retried": retried})

@@ -418,6 +418,7 @@ struct DedupWs {
   uint32_t* slot;             // [n] distinct -> table slot
   unsigned long long* nu;     // distinct count; nu[1]: overflow flag
   uint64_t cap;
+  uint32_t max_probe;         // DEDUP_MAX_PROBE, or unbounded when cap > n_words (never full)
 };
 
 // Table of the distinct words (keys + counts, 12 B a slot).  Round 4: sized for a quarter of the
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(DEDUP_T) void k_dedup_insert(const uint16_t* __rest
         const unsigned long long mine = ((h >> 32) << 32) | (unsigned long long)(uint32_t)(w + 1);
         k = h & mask;
         for (int probe = 0;; ++probe) {
-          if (probe == DEDUP_MAX_PROBE) {   // table too full: the caller retries with a larger one
+          if ((uint32_t)probe == ws.max_probe) {   // table too full: the caller retries with a larger one
             ws.nu[1] = 1ull;
             have = false;
             break;
@@ -800,6 +801,13 @@ extern "C" int beast_bpe_word_signatures(const uint16_t* sym, const uint32_t* ws
 extern "C" size_t beast_bpe_dedup_workspace_bytes(int64_t n_words) {
   return (size_t)(dedup_cap(n_words > 0 ? n_words : 1) * 12) + dedup_fixed_bytes(n_words);
 }
+// a table of >= 2 n_words slots: it can never fill, so the probes are unbounded and *out_n is
+// always the distinct count (no retry)
+extern "C" size_t beast_bpe_dedup_workspace_bytes_safe(int64_t n_words) {
+  uint64_t c = 1024;
+  while (c < 2 * (uint64_t)(n_words > 0 ? n_words : 1)) c <<= 1;
+  return (size_t)(c * 12) + dedup_fixed_bytes(n_words);
+}
 extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen,
                                      int64_t n_words, void* workspace, size_t ws_bytes, uint32_t* out_wstart,
                                      uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_n, void* stream) {
@@ -813,6 +821,7 @@ extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart
   DedupWs ws;
   ws.cap = 1024;   // the largest power of two the workspace holds
   while ((ws.cap * 2) * 12 + dedup_fixed_bytes(n_words) <= ws_bytes) ws.cap *= 2;
+  ws.max_probe = ws.cap > (uint64_t)n_words ? 0xFFFFFFFFu : (uint32_t)DEDUP_MAX_PROBE;
   char* p = static_cast<char*>(workspace);
   ws.keys = reinterpret_cast<unsigned long long*>(p);  p += ws.cap * 8;
   ws.cnt = reinterpret_cast<uint32_t*>(p);              p += ws.cap * 4;

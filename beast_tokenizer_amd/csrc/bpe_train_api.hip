@@ -326,6 +326,7 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
 
   // ---- replay the log against the real strings (bpe_train.py replay_log)
   int n_merges = 0;
+  std::vector<int32_t> merge_ids;
   for (int i = 0; i < n_log; ++i) {
     const int a = log[4 * i], b = log[4 * i + 1], nid = log[4 * i + 2], reused = log[4 * i + 3];
     BEAST_REQUIRE_CODE(a >= 0 && b >= 0 && a < (int)id2str.size() && b < (int)id2str.size(), BEAST_E_UNSUPPORTED,
@@ -340,21 +341,29 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
       str2id.emplace(t, nid);
       id2str.push_back(t);
     }
-    BEAST_REQUIRE_CODE(n_merges < max_merges_out, BEAST_E_WORKSPACE, "beast_bpe_train: merge capacity %d too small",
-                       max_merges_out);
-    out_merges[2 * n_merges] = a;
-    out_merges[2 * n_merges + 1] = b;
+    merge_ids.push_back(a);
+    merge_ids.push_back(b);
     ++n_merges;
   }
 
-  // ---- outputs: the vocabulary's strings in id order, the merges, the token range
-  BEAST_REQUIRE_CODE((int)id2str.size() <= max_vocab, BEAST_E_WORKSPACE, "beast_bpe_train: vocab capacity %d < %zu",
-                     max_vocab, id2str.size());
+  // ---- outputs: the vocabulary's strings in id order, the merges, the token range.  Capacities
+  // are checked against the finished training: when one is short, the required sizes come back
+  // (*out_n_vocab, *out_n_merges, out_vocab_off[0] = vocabulary bytes) with BEAST_E_WORKSPACE
+  size_t need_bytes = 0;
+  for (const std::string& t : id2str) need_bytes += t.size();
+  if ((int)id2str.size() > max_vocab || n_merges > max_merges_out || need_bytes > vocab_bytes_cap) {
+    *out_n_vocab = (int)id2str.size();
+    *out_n_merges = n_merges;
+    out_vocab_off[0] = (int64_t)need_bytes;
+    BEAST_REQUIRE_CODE(false, BEAST_E_WORKSPACE,
+                       "beast_bpe_train: output capacity (vocab %d, merges %d, bytes %zu) below the result's (%zu, %d, "
+                       "%zu); the required sizes are in *out_n_vocab, *out_n_merges, out_vocab_off[0]",
+                       max_vocab, max_merges_out, vocab_bytes_cap, id2str.size(), n_merges, need_bytes);
+  }
+  std::memcpy(out_merges, merge_ids.data(), merge_ids.size() * sizeof(int32_t));
   size_t off = 0;
   for (size_t i = 0; i < id2str.size(); ++i) {
     out_vocab_off[i] = (int64_t)off;
-    BEAST_REQUIRE_CODE(off + id2str[i].size() <= vocab_bytes_cap, BEAST_E_WORKSPACE,
-                       "beast_bpe_train: vocab byte capacity %zu too small", vocab_bytes_cap);
     std::memcpy(out_vocab_bytes + off, id2str[i].data(), id2str[i].size());
     off += id2str[i].size();
   }

@@ -312,7 +312,10 @@ int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_
  * strings in id order (out_vocab_bytes[out_vocab_off[i] .. out_vocab_off[i+1])), the merges as
  * id pairs out_merges[2m], [2m+1] (merge m's token is their concatenation, the next new id
  * unless the string already had one).  Capacities: max_vocab >= max(vocab_size, alphabet),
- * max_merges_out >= vocab_size - alphabet.  Synchronises the stream.  BEAST_E_UNSUPPORTED for
+ * max_merges_out >= vocab_size - alphabet (checked up front), vocab_bytes_cap >= the strings'
+ * bytes (known only after training).  When an output is too small the call returns
+ * BEAST_E_WORKSPACE with the required sizes in *out_n_vocab, *out_n_merges and out_vocab_off[0]
+ * (vocabulary bytes); retry with those.  Synchronises the stream.  BEAST_E_UNSUPPORTED for
  * Vt > 4096, a full merge log or a 64-bit string-hash collision (the Python driver,
  * bpe_train.train_bpe, reruns those on its host-driven loop); one GPU (the multi-rank forms
  * are the Python driver's, over torch.distributed). */
@@ -327,8 +330,15 @@ int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),
  * out_wcount its multiplicity, *out_n (device int64) the number of distinct words.
  * Output order is unspecified (training results do not depend on it).  Words of 0 or 1
- * symbols are dropped (they hold no pair). out_* sized n_words. */
+ * symbols are dropped (they hold no pair). out_* sized n_words.
+ * Workspace: beast_bpe_dedup_workspace_bytes(n) sizes the hash table for n / 4 distinct words
+ * (trajectory corpora repeat their words; K5 is 13 % distinct, and the smaller table stays in the
+ * 256 MB Infinity Cache).  With more distinct words than that table holds the call still returns
+ * BEAST_OK but writes *out_n = -1 (the outputs are then undefined): retry with a larger workspace
+ * (the in-tree callers multiply it by 4).  beast_bpe_dedup_workspace_bytes_safe(n) sizes a table
+ * of >= 2 n slots, which can never fill: with it *out_n is always the distinct count. */
 size_t beast_bpe_dedup_workspace_bytes(int64_t n_words);
+size_t beast_bpe_dedup_workspace_bytes_safe(int64_t n_words);
 int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
                           void* workspace, size_t ws_bytes, uint32_t* out_wstart, uint32_t* out_wlen,
                           uint32_t* out_wcount, int64_t* out_n, void* stream);

@@ -52,6 +52,19 @@ def test_capi_train_options_match_live_hf(special, max_len, min_freq, gpu_device
 
 
 @pytest.mark.gpu
+def test_capi_train_reports_required_capacity(gpu_device):
+    """Too small a vocabulary byte buffer: beast_bpe_train returns BEAST_E_WORKSPACE with the sizes it
+    needs (*out_n_vocab, *out_n_merges, out_vocab_off[0]); train_bpe_capi retries once with them."""
+    arr = load_npz("bpe_corpora.npz")["skew"]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    want = train_bpe_capi(flat, off, 2048)
+    assert not want.stats["retried"]
+    got = train_bpe_capi(flat, off, 2048, vocab_bytes_cap=64)
+    assert got.stats["retried"]
+    assert got.vocab == want.vocab and got.merges == want.merges
+
+
+@pytest.mark.gpu
 def test_capi_train_rejects_empty_and_wide(gpu_device):
     from beast_tokenizer_amd import _lib
     flat = torch.zeros(0, dtype=torch.int64, device=gpu_device)

@@ -226,6 +226,30 @@ def test_words_fallback_rows_for_long_words(gpu_device):
     want = [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in rows], add_special_tokens=False)]
     assert got == want
     assert model.encode_to_lists(flat, off, width, 0, None) == want
+    ids, lens = model.encode_to_tensors(flat, off, width, 0, None)
+    ids, lens = ids.cpu().numpy(), lens.cpu().numpy()
+    assert [ids[i, :lens[i]].tolist() for i in range(len(rows))] == want
+
+
+def test_wordmap_build_failure_keeps_per_row_kernel(gpu_device, monkeypatch):
+    """A model whose cuckoo word map cannot be placed (forced here) is still built: encode takes the
+    per-row kernel (k_bpe_encode) instead of failing."""
+    from beast_tokenizer_amd import _lib, bpe_codec
+    tok, _, rng, _ = _trained_model(255, 400, 60, 700, 6, gpu_device)
+    real = _lib.run
+
+    def run(name, *args):
+        if name == "beast_bpe_wordmap_build_host":
+            raise NotImplementedError("word map: cuckoo insertion failed")
+        return real(name, *args)
+    monkeypatch.setattr(_lib, "run", run)
+    model = bpe_codec.GpuBpeModel(tok, gpu_device)
+    monkeypatch.setattr(_lib, "run", real)
+    assert model.wordmap is None and not model._words_ok()
+    rows = [rng.integers(0, 256, size=60) for _ in range(50)]
+    got, status = encode_rows(model, rows, gpu_device)
+    assert not status.any()
+    assert got == [e.ids for e in tok.encode_batch(["".join(map(chr, r)) for r in rows], add_special_tokens=False)]
 
 
 @pytest.mark.parametrize("bits", [3, 8, 20])

@@ -601,6 +601,19 @@ def test_bpe_dedup_table_overflow_retries(gpu_device):
     u = ops.dedup(w)
     got = dict(zip(words_of(u), u["wcount"].cpu().numpy()[: u["n_words"]].tolist()))
     assert got == dict(want)
+    # the C-ABI's never-full size (include/beast_hip.h): one call, *out_n the distinct count
+    from beast_tokenizer_amd import _lib
+    lib, n = _lib.load(), w["n_words"]
+    small, safe = lib.beast_bpe_dedup_workspace_bytes(n), lib.beast_bpe_dedup_workspace_bytes_safe(n)
+    assert safe > small
+    outs = [torch.empty(n, dtype=torch.int32, device=gpu_device) for _ in range(3)]
+    on = torch.empty(1, dtype=torch.int64, device=gpu_device)
+    for nbytes, ok in ((small, False), (safe, True)):
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=gpu_device)
+        _lib.run("beast_bpe_dedup_words", w["sym"].data_ptr(), w["wstart"].data_ptr(), w["wlen"].data_ptr(), n,
+                 ws.data_ptr(), ws.numel(), *[o.data_ptr() for o in outs], on.data_ptr(), ops.stream)
+        torch.cuda.synchronize()
+        assert (int(on.item()) == len(want)) == ok and (int(on.item()) == -1) == (not ok)
 
 
 def test_bpe_dedup_and_compact_match_counter(gpu_device):
