@@ -1054,22 +1054,10 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
                                                           0, 0);
         // f32 C/D map: col = lane & 15, row = (lane >> 4) * 4 + r
         if (ok) {
-#ifdef BEAST_REC_DIRECT
-          // (measurement variant) every lane stores its accumulators straight to HBM
-          float* gp = a.pos_out + (b0 + j) * (int64_t)Tout * ndo + min(max(dst[d], 0), ndo - 1);
-#pragma unroll
-          for (int i = 0; i < RT; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int t = i * 16 + lk * 4 + r;
-              if (t < Tout && (a.phases & 4)) st4<(S::W == 7) ? LAT_SP : 0>(gp + t * ndo, acc[i][r]);
-            }
-#else
 #pragma unroll
           for (int i = 0; i < RT; ++i)
 #pragma unroll
             for (int r = 0; r < 4; ++r) oc[(i * 16 + r) * ndo] = acc[i][r];
-#endif
         }
       } else {
         const float* Ph = phi + (kind * RTR + lr) * Np4 + lk * KS;
@@ -1097,19 +1085,187 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
       }
     }
     if (tile == blockIdx.x) STAMP(1, 5);
-#ifdef BEAST_REC_DIRECT
-    if constexpr (RT > 0) {
-      if (tile + gridDim.x < a.ntiles) __syncthreads();   // the next tile's DMA overwrites the tokens
-    } else {
-#endif
     __syncthreads();
     if (tile == blockIdx.x) STAMP(1, 6);
     if (a.phases & 4) rec_store<S>(a, a.pos_out + b0 * (int64_t)Tout * ndo, ob, nb, RTR);
-#ifdef BEAST_REC_DIRECT
-    }
-#endif
     if (tile == blockIdx.x) STAMP(1, 7);
   }
+#ifdef BEAST_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP(1, 8);
+  BSTAMP(1, 1);
+#endif
+}
+
+// ------------------------------------------------ reconstruct, per-trajectory waves --
+// Latency regime (<= 2 tiles per CU, e.g. the bench's B = 4,096), fixed shapes with
+// num_dof_out == D.  k_reconstruct computes pos^T (rows t, columns (trajectory, DoF)), so a
+// lane's accumulators are 4 rows of one output column, 4 * ndo bytes apart: they go through an
+// LDS image, a workgroup barrier and a cooperative store, and HBM sits idle while the whole chip
+// computes.  Here the MFMA computes pos[j] itself: wave j owns trajectory j of the tile, A = W
+// (16 rows = output columns c, K = basis n), B = Phi^T (columns t), so a lane's accumulator
+// holds columns c = 4 kk .. 4 kk + 3 of one row t -- contiguous bytes of pos[j][t][.] -- and each
+// wave stores its trajectory straight from registers as soon as its own chain is done (no LDS
+// image, no barrier): the stores of the first waves overlap the MFMAs of the others.
+// Same K mapping (n = kk * KS + s) and the same products summed in the same order as
+// k_reconstruct (a product's operands only swap roles), so positions are bit-identical.  With
+// gripper DoFs the rows of the other kind are zero in each kind's chain: the joint chain then
+// the gripper chain, each adding exact zeros to the other kind's rows.
+constexpr int RV_W = 8;   // waves = trajectories per tile
+
+struct RvSmem {
+  int tok, wlo, whi, dst, phi, lut, wimg, img, total;
+};
+template <class S>
+__host__ __device__ constexpr RvSmem rv_smem(int nkinds) {
+  RvSmem s{};
+  constexpr int per = S::D * S::N;
+  int o = 0;
+  s.tok = o;  o += round_up(RV_W * per * 8, 1024);           // DMA: whole wave-instructions
+  s.wlo = o;  o += round_up(per * 4, 256);
+  s.whi = o;  o += round_up(per * 4, 256);
+  s.dst = o;  o += round_up(S::D * 4, 256);
+  s.phi = o;  o += round_up(nkinds * S::T * S::N * 4, 1024);
+  s.lut = o;  o += round_up(LUT_MAX * 4, 16);
+  s.wimg = o; o += round_up(RV_W * per * 4, 16);              // W[j][d][n] (d n), one per wave
+  s.img = o;  o += RV_W * round_up(S::T * S::D * 4, 16);        // pos[j] [T][D], one per wave
+  s.total = o;
+  return s;
+}
+
+template <int KS, class S>
+__global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restrict__ tsrc, int64_t B, int esz,
+                                                             RecArgs a) {
+  static_assert(S::fixed && S::T > 0 && S::T <= 64 && S::D <= 16 && S::DL == S::D && 4 * KS >= S::N,
+                "per-trajectory reconstruct: fixed shape, T <= 64, D <= 16, ndo == D");
+  constexpr int NT = RV_W * 64, D = S::D, N = S::N, T = S::T, per = D * N;
+  constexpr int NJ = S::NJ;
+  constexpr int nkinds = NJ < D ? 2 : 1;
+  constexpr RvSmem L = rv_smem<S>(nkinds);
+  constexpr int RV_IMG = round_up(T * D * 4, 16) / 4;   // floats per wave's output image
+  static_assert((T * D) % 4 == 0, "per-trajectory reconstruct: whole 16-byte rows");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned char* tokl = smem + L.tok;
+  float* wlo = reinterpret_cast<float*>(smem + L.wlo);
+  float* whi = reinterpret_cast<float*>(smem + L.whi);
+  int* dst = reinterpret_cast<int*>(smem + L.dst);
+  float* phi = reinterpret_cast<float*>(smem + L.phi);
+  float* lut = reinterpret_cast<float*>(smem + L.lut);
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * RV_W;
+  STAMP(1, 0);
+  BSTAMP(1, 0);
+  // ---- prologue: the token tile, bounds, DoF map and raw basis by DMA, all in flight together
+  stage_rows<NT>(smem + L.tok, tsrc, B, esz, b0, per, RV_W);
+  STAMP(1, 9);
+  dma4<NT>(wlo, a.w_min, per);
+  dma4<NT>(whi, a.w_max, per);
+  dma4<NT>(dst, a.dof_dst, D);
+  {
+    constexpr int pbytes = nkinds * T * N * 4;
+    if ((pbytes & 15) == 0 && (((uintptr_t)a.basis) & 15) == 0) dma16<NT>(phi, a.basis, pbytes >> 4);
+    else dma4<NT>(phi, a.basis, pbytes >> 2);
+  }
+  const float vm1 = (float)(a.vocab - 1);
+  for (int t = tid; t < a.lut_n; t += NT) lut[t] = __fdiv_rn((float)t, vm1);
+  STAMP(1, 12);
+  __syncthreads();   // every DMA and the LUT are in place
+  STAMP(1, 2);
+  const int j = wave;
+  const int nb = (int)min<int64_t>(RV_W, B - b0);
+  if (j >= nb) return;   // no barrier follows
+  // ---- W[j][d][n] of this wave's trajectory (bit-exact discrete_to_continuous, init_p for n = 0 of
+  //      the joint DoFs: reference :505-510) into its LDS image
+  float* wimg = reinterpret_cast<float*>(smem + L.wimg) + j * per;
+  const long long* tk = reinterpret_cast<const long long*>(tokl) + j * per;
+#pragma unroll
+  for (int u = 0; u < (per + 63) / 64; ++u) {
+    const int e = u * 64 + lane;   // (n d) order
+    if (e < per) {
+      const int n = e / D, d = e - n * D, k = d * N + n;
+      const float lo = wlo[k], hi = whi[k];
+      const long long t = tk[e] - a.tok_offset;
+      const float nrm = (t >= 0 && t < a.lut_n) ? lut[(int)t] : __fdiv_rn((float)t, vm1);
+      float w = beast::clamp_t(__fadd_rn(__fmul_rn(nrm, __fsub_rn(hi, lo)), lo), lo, hi);
+      if (a.init_p != nullptr && n == 0 && d < NJ) w = a.init_p[(b0 + j) * a.init_p_sb + a.init_p_src[d]];
+      wimg[k] = w;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  STAMP(1, 3);
+  // ---- A = W: row c = lane & 15 is output column c, i.e. DoF d with dst[d] == c; K-step s holds
+  //      n = kk * KS + s (k_reconstruct's mapping), zero past N, past D and for the other kind
+  const int c = lane & 15, kk = lane >> 4;
+  int dsrc = -1;
+#pragma unroll
+  for (int d = 0; d < D; ++d) dsrc = dst[d] == c ? d : dsrc;
+  const bool row_ok = dsrc >= 0;
+  const int dd = row_ok ? dsrc : 0;
+  float av[KS];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) {
+    const int n = kk * KS + s2;
+    const float w = wimg[dd * N + min(n, N - 1)];
+    av[s2] = (row_ok && n < N) ? w : 0.0f;
+  }
+  // ---- B = Phi_kind^T: column t = 16 tt + (lane & 15), K-step s: n = kk * KS + s
+  float4_t acc[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) acc[tt] = float4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int kd = 0; kd < nkinds; ++kd) {
+    float bv[4][KS];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) {
+        const int t = tt * 16 + c, n = kk * KS + s2;
+        const float x = phi[(kd * T + min(t, T - 1)) * N + min(n, N - 1)];
+        bv[tt][s2] = (t < T && n < N) ? x : 0.0f;
+      }
+    const bool mine = nkinds == 1 || ((dd < NJ) == (kd == 0));
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      const float ak = mine ? av[s2] : 0.0f;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+        if (tt * 16 < T) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ak, bv[tt][s2], acc[tt], 0, 0, 0);
+    }
+  }
+  STAMP(1, 5);
+  // ---- f32 C/D map: row (column c of pos) = kk * 4 + r, column (t) = lane & 15: this lane holds
+  //      pos[j][16 tt + (lane & 15)][4 kk .. 4 kk + 3].  Those are 8-byte aligned (t * D * 4 is a
+  //      multiple of 16 only for even t), and 8-byte write-through stores are one fabric write each,
+  //      so the wave puts its trajectory's [T][D] image into LDS (its own region: no workgroup
+  //      barrier) and copies it out as 16-byte write-through stores.
+  float* img = reinterpret_cast<float*>(smem + L.img) + j * RV_IMG;
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const int t = tt * 16 + c;
+    if (tt * 16 < T && t < T) {
+      float* q = img + t * D + 4 * kk;
+      if (4 * kk + 1 < D) *reinterpret_cast<float2*>(q) = make_float2(acc[tt][0], acc[tt][1]);
+      else if (4 * kk < D) q[0] = acc[tt][0];
+      if (4 * kk + 3 < D) *reinterpret_cast<float2*>(q + 2) = make_float2(acc[tt][2], acc[tt][3]);
+      else if (4 * kk + 2 < D) q[2] = acc[tt][2];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  STAMP(1, 6);
+  if (a.phases & 4) {
+    constexpr int n4 = T * D / 4;
+    float4* gout = reinterpret_cast<float4*>(a.pos_out + (b0 + j) * (int64_t)T * D);
+#pragma unroll
+    for (int u = 0; u < (n4 + 63) / 64; ++u) {
+      const int i = u * 64 + lane;
+      if (i < n4) st16<LAT_SP>(gout + i, reinterpret_cast<const float4*>(img)[i]);
+    }
+  }
+  STAMP(1, 7);
 #ifdef BEAST_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(1, 8);
@@ -1377,6 +1533,26 @@ int launch_rec_mfma(RecArgs a, int D, int nj, int N, hipStream_t s) {
   }
 }
 
+// k_reconstruct_v takes the latency regime's fixed shapes unless BEAST_OPT_BLOCK_WAVES forces
+// the 7-wave (or 4-wave) k_reconstruct; positions only (no params_out), int64 tokens, one tile
+// per workgroup
+bool rec_v(const RecArgs& a) {
+  return (g_block_waves == 0 || g_block_waves == 8) && a.params_out == nullptr && a.ntokens == nullptr &&
+         a.ntiles <= 2 * (int64_t)cu_count() && (((uintptr_t)a.pos_out) & 15) == 0;
+}
+
+template <class S>
+int launch_rec_v(RecArgs a, hipStream_t s) {
+  constexpr int KS = (S::N + 3) / 4;
+  constexpr RvSmem L = rv_smem<S>(S::NJ < S::D ? 2 : 1);
+  static_assert(L.total <= 64 * 1024, "k_reconstruct_v LDS");
+  a.tbt = RV_W;
+  a.ntiles = (a.B + RV_W - 1) / RV_W;
+  static std::atomic<hipFunction_t> fn[16] = {};
+  return launch_fn(reinterpret_cast<const void*>(&k_reconstruct_v<KS, S>), fn, (unsigned)a.ntiles, RV_W * 64,
+                   L.total, s, "k_reconstruct_v", static_cast<const void*>(a.tokens), a.B, 8, a);
+}
+
 template <int TBT>
 int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t s) {
   a.g = make_geom<TBT>(D, nj, N, 1);
@@ -1391,6 +1567,8 @@ int launch_reconstruct(RecArgs a, int D, int nj, int N, bool shared, hipStream_t
   if (a.Tout <= 16 * RT_REG) {
     if (!g_generic_only && N == 10 && a.Tout == 50 && a.ndo == D) {
       const bool wide = wide_blocks(a.ntiles);
+      if (wide && rec_v(a) && D == 14 && nj == 14) return launch_rec_v<Shape<14, 14, 10, 50, 14>>(a, s);
+      if (wide && rec_v(a) && D == 14 && nj == 12) return launch_rec_v<Shape<14, 12, 10, 50, 14>>(a, s);
       if (D == 14 && nj == 14)
         return wide ? launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14, 7>>(a, D, nj, s)
                     : launch_rec_ks<TBT, 3, RT_REG, Shape<14, 14, 10, 50, 14>>(a, D, nj, s);
