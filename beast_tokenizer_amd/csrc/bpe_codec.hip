@@ -58,6 +58,8 @@ constexpr int ST_OK = 0, ST_BELOW_MIN = 1, ST_ABOVE_MAX = 2, ST_NOT_UNICODE = 3,
 // the stamps add no atomics and no shared address
 constexpr int BPE_RS = 4096;
 __device__ unsigned long long g_bpe_rs[BPE_RS][12];
+// k_bpe_words' merge tasks per row wave: [0..3) time in mid / short / tiny tasks, [3..6) their counts
+__device__ unsigned long long g_bpe_wt[BPE_RS][8];
 #define BPE_STAMP(k)                                                                          \
   do {                                                                                        \
     if (lane == 0 && r < BPE_RS) g_bpe_rs[r][k] = __builtin_amdgcn_s_memrealtime();          \
@@ -852,7 +854,8 @@ __device__ __forceinline__ uint32_t grp_down1(uint32_t v, uint32_t fill) {
     return (threadIdx.x & 7) == 7 ? fill : x;
   }
   if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x101, 0xF, 0xF, false);
-  else { const uint32_t x = (uint32_t)__shfl_down((int)v, 1); return (threadIdx.x & 63) == 63 ? fill : x; }
+  // wave_shl:1 (gfx9 DPP): lane 63 has no source and keeps `fill` -- no LDS permute on the round's chain
+  else return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xF, 0xF, false);
 }
 template <int GW>
 __device__ __forceinline__ uint32_t grp_up1(uint32_t v, uint32_t fill) {
@@ -861,7 +864,7 @@ __device__ __forceinline__ uint32_t grp_up1(uint32_t v, uint32_t fill) {
     return (threadIdx.x & 7) == 0 ? fill : x;
   }
   if constexpr (GW == 16) return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x111, 0xF, 0xF, false);
-  else { const uint32_t x = (uint32_t)__shfl_up((int)v, 1); return (threadIdx.x & 63) == 0 ? fill : x; }
+  else return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xF, 0xF, false);   // wave_shr:1
 }
 template <int GW>
 __device__ __forceinline__ uint32_t grp_min(uint32_t v) {   // every lane of the group gets the group's min
@@ -870,14 +873,20 @@ __device__ __forceinline__ uint32_t grp_min(uint32_t v) {   // every lane of the
     v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
     return min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
   }
+  if constexpr (GW == 64) {   // row_shr 1, 2, 4, 8 then row_bcast 15 / 31: lane 63 holds the min (DPP only)
+    constexpr int MX = (int)0xFFFFFFFFu;
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(MX, (int)v, 0x143, 0xC, 0xF, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  }
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));   // row_ror:8
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false));   // row_ror:4
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xF, 0xF, false));   // row_ror:2
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xF, 0xF, false));   // row_ror:1
-  if constexpr (GW == 64) {
-    v = min(v, (uint32_t)__shfl_xor((int)v, 16));
-    v = min(v, (uint32_t)__shfl_xor((int)v, 32));
-  }
   return v;
 }
 
@@ -939,6 +948,94 @@ __device__ __forceinline__ uint32_t dw_merge_word(const WordMap& mm, uint32_t ra
     sym = grp_compact<GW>(sym, gl < n && !dies, gl, gbase, n);
   }
   return sym;
+}
+
+// A word of <= ML byte symbols merged by ONE lane, in registers (round 5, the tiny words): HF's Word::merge_all
+// exactly -- repeatedly the pair of lowest (rank, position) among the word's current pairs (the
+// min-heap's order, without its stale entries), merged, and the two pairs it forms looked up --
+// for any model (no rank-monotone requirement).  Every index into the register arrays is a
+// compile-time one (select chains over the dynamic position), so nothing spills to scratch.  A
+// wave merges 64 words at once: the cross-lane steps of dw_merge_word (DPP min, ballots, a
+// ds_permute per round) are gone, and the map lookups of all lanes are in flight together.
+// c: the word's byte symbols in the row image (SYM_NONE: no vocab id); the ids are written back
+// over them.  Returns the word's final length.
+__device__ __forceinline__ uint32_t wm_rank(const WordMap& mm, uint32_t a, uint32_t b) {   // rank << 16 | new id
+  const uint32_t key = (a << 16) | b;
+  const uint4 b1 = mm.b[wm_h1(key, mm.log2b)], b2 = mm.b[wm_h2(key, mm.log2b)];
+  const uint32_t v = b1.x == key ? b1.y : b1.z == key ? b1.w : b2.x == key ? b2.y : b2.z == key ? b2.w : 0u;
+  return v ? v - 0x10000u : RK_NONE;
+}
+
+template <int ML>
+__device__ __forceinline__ int dw_merge_lane(const WordMap& mm, uint16_t* c, int blen, int unk_id, int fuse_unk,
+                                             int& rounds) {
+  uint32_t s[ML];
+  bool miss_any = false;
+#pragma unroll
+  for (int i = 0; i < ML; ++i) {
+    s[i] = i < blen ? (uint32_t)c[i] : SYM_NONE;
+    miss_any |= i < blen && s[i] == SYM_NONE;
+  }
+  int n = blen;
+  if (__any(miss_any)) {
+    // HF BPE::merge_word's unknown chars (rare): unk_id, consecutive ones fused when fuse_unk, or
+    // dropped without an unk token -- compacted by select chains
+    uint32_t t[ML];
+    bool pm = false;
+    n = 0;
+#pragma unroll
+    for (int i = 0; i < ML; ++i) t[i] = SYM_NONE;
+#pragma unroll
+    for (int i = 0; i < ML; ++i) {
+      if (i < blen) {
+        const bool miss = s[i] == SYM_NONE;
+        const bool live = !(miss && (unk_id < 0 || (fuse_unk && pm)));
+        const uint32_t id = miss ? (uint32_t)unk_id : s[i];
+#pragma unroll
+        for (int k = 0; k <= i; ++k) t[k] = (live && k == n) ? id : t[k];
+        n += live ? 1 : 0;
+        pm = miss;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ML; ++i) s[i] = t[i];
+  }
+  uint32_t rk[ML];   // rk[i]: the pair (s[i], s[i + 1]), RK_NONE when it is not a merge
+#pragma unroll
+  for (int i = 0; i < ML; ++i) rk[i] = i + 1 < n ? wm_rank(mm, s[i], s[i + 1]) : RK_NONE;
+  for (int it = 0; it < ML - 1; ++it) {
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i + 1 < ML; ++i)
+      best = min(best, rk[i] == RK_NONE ? 0xFFFFFFFFu : (((rk[i] >> 16) << 5) | (uint32_t)i));
+    if (best == 0xFFFFFFFFu) break;
+    ++rounds;
+    const int p = (int)(best & 31u);
+    uint32_t nid = 0, left = SYM_NONE, right = SYM_NONE;
+#pragma unroll
+    for (int i = 0; i < ML; ++i) {
+      nid = i == p ? (rk[i] & 0xFFFFu) : nid;
+      left = i + 1 == p ? s[i] : left;
+      right = i == p + 2 ? s[i] : right;
+    }
+#pragma unroll
+    for (int i = 0; i < ML; ++i) {   // s[p] <- the new id, the symbols after it move left by one
+      const uint32_t nx = i + 1 < ML ? s[i + 1] : SYM_NONE;
+      s[i] = i == p ? nid : (i > p ? nx : s[i]);
+    }
+    --n;
+    const uint32_t rl = p > 0 ? wm_rank(mm, left, nid) : RK_NONE;
+    const uint32_t rr = p + 1 < n ? wm_rank(mm, nid, right) : RK_NONE;
+#pragma unroll
+    for (int i = 0; i < ML; ++i) {
+      const uint32_t nx = i + 1 < ML ? rk[i + 1] : RK_NONE;
+      rk[i] = i + 1 == p ? rl : (i == p ? rr : (i > p ? nx : rk[i]));
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < ML; ++i)
+    if (i < n) c[i] = (uint16_t)s[i];
+  return n;
 }
 
 // ------------------------------------------------------- encode by words, one launch --
@@ -1060,19 +1157,24 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   }
   __syncthreads();
   if (r < a.n_rows) BPE_STAMP(5);
-  // 4. merges: a mid word (17..64 byte symbols) per wave, words of 9..16 four to a wave (16-lane
-  // rows), words of <= 8 eight to a wave (half rows)
+  // 4. merges: a mid word (17..64 byte symbols) per wave and words of 9..16 four to a wave (16-lane
+  // rows) by dw_merge_word's cooperative rounds; words of <= 8 one per lane, 64 to a task
+  // (dw_merge_lane: its select chains stay short, and the tiny words are most of them)
   // the cursor of length 17 has passed every longer word, that of length 9 every word of 9 or
   // more (clamped: the task count bounds the loop below, so it never exceeds the word count)
   const int nmid = min(max(s_hist[DW_SHORT + 1], 0), nd);
   const int n9 = min(max(s_hist[DW_TINY + 1], nmid), nd);
   const int t16 = nmid + (n9 - nmid + 3) / 4;
-  const int tasks = t16 + (nd - n9 + 7) / 8;
+  const int tasks = t16 + (nd - n9 + 63) / 64;
   int nrounds = 0;
   // tasks longest first, each wave taking the next one when it is done (an LDS counter): the
   // workgroup waits for its slowest wave at the barrier below (29.8 vs 33.0 us with tasks dealt
   // round-robin, profiles/r04/ab/encode_words_variants_r04d.txt)
   for (int t = wave; t < tasks;) {
+#ifdef BPE_STAMPS
+    const unsigned long long t_task0 = __builtin_amdgcn_s_memrealtime();
+    const int kind_task = t < nmid ? 0 : (t < t16 ? 1 : 2);
+#endif
     if (t < nmid) {
       const uint32_t v = ds[t];
       const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
@@ -1096,18 +1198,21 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
       if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
       if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
     } else {
-      const int j = n9 + 8 * (t - t16) + (lane >> 3), gl = lane & 7;
+      const int j = n9 + 64 * (t - t16) + lane;
       const bool valid = j < nd;
       const uint32_t v = valid ? ds[j] : 0u;
       const DwRow Rw = dw_carve(rows + (size_t)(v >> 22) * rb, a.Lc, a.S);
       const int k = (v >> 7) & 0x7FFF, blen = valid ? (int)(v & 127u) : 0;
-      const int bs = valid ? Rw.symoff[Rw.wcp[k]] : 0;
-      const uint32_t raw = gl < blen ? (uint32_t)Rw.c[bs + gl] : SYM_NONE;
-      int n;
-      const uint32_t id = dw_merge_word<DW_TINY>(lm, raw, blen, a.unk_id, a.fuse_unk, n, nrounds);
-      if (valid && gl < n) Rw.c[bs + gl] = (uint16_t)id;
-      if (valid && gl == 0) Rw.vis[k] = (uint8_t)n;
+      uint16_t* c = Rw.c + (valid ? Rw.symoff[Rw.wcp[k]] : 0);
+      const int n = dw_merge_lane<DW_TINY>(lm, c, blen, a.unk_id, a.fuse_unk, nrounds);
+      if (valid) Rw.vis[k] = (uint8_t)n;
     }
+#ifdef BPE_STAMPS
+    if (lane == 0 && r < BPE_RS) {
+      g_bpe_wt[r][kind_task] += __builtin_amdgcn_s_memrealtime() - t_task0;
+      g_bpe_wt[r][3 + kind_task] += 1;
+    }
+#endif
     int nt = 0;
     if (lane == 0) nt = atomicAdd(&s_next, 1);
     t = __builtin_amdgcn_readfirstlane(nt);
@@ -1351,6 +1456,13 @@ int grid_for(int64_t n_rows, int per_cu = 4) {
 #ifdef BPE_STAMPS
 extern "C" int beast_debug_bpe_stamps(unsigned long long* host) {   // [4096][12]
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_rs), sizeof(g_bpe_rs)) == hipSuccess ? 0 : -2;
+}
+extern "C" int beast_debug_bpe_task_times(unsigned long long* host, int clear) {   // [4096][8]
+  if (clear) {
+    static unsigned long long zero[BPE_RS][8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_bpe_wt), zero, sizeof(zero)) == hipSuccess ? 0 : -2;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bpe_wt), sizeof(g_bpe_wt)) == hipSuccess ? 0 : -2;
 }
 #endif
 

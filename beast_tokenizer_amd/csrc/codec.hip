@@ -512,260 +512,176 @@ __global__ __launch_bounds__(S::W * 64) void k_encode(EncArgs a) {
 #endif
 }
 
-// ------------------------------------------------------- encode, pipelined --
-// Latency regime (at most two 8-trajectory tiles per CU, e.g. B = 4096 on 256 CUs).  Every
-// workgroup issues its loads at once, so without a pipeline the whole chip loads, then
-// computes (memory idle), then stores: the MFMA phase adds to the HBM time instead of
-// hiding under it.  Here a workgroup (8 waves) splits its 8 trajectories into two
-// sub-tiles A, B of PIPE_SUB and overlaps:
-//
-//   waves 0-3 (DMA + MFMA):  DMA A, constants, DMA B | wait A | fit A | wait B | fit B  | store B
-//   waves 4-7 (store):                                | scale  |       | store A         | store B
-//
-// The waits are explicit vmcnt counts: the DMA waves issue exactly PIPE_Y_OPS wave-
-// instructions per sub-tile (sources clamped to the batch, destinations padded), and
-// nothing else after B's, so "vmcnt(PIPE_Y_OPS)" is "A and the constants have landed".
-// A and B sit in distinct static LDS arrays, which lets the compiler's own LDS-DMA
-// tracking tell them apart (a single array would make it wait for B before reading A).
-// Results are bit-identical to k_encode's: same MFMA chain (even / odd K-steps), same
-// epilogue arithmetic.
-constexpr int PIPE_SUB = 4;       // trajectories per sub-tile
-constexpr int PIPE_MW = 4;        // DMA + MFMA waves
-constexpr int PIPE_W = 8;         // waves per workgroup
-constexpr int PIPE_MT = PIPE_MW * 64;
-
+// Fixed shapes of the per-trajectory kernels (k_encode_v): the MFMA K-steps over Tp.
 template <class S>
-struct PipeShape {
-  static_assert(S::fixed && S::T > 0 && S::DL > 0 && ((S::T * S::DL) % 4) == 0, "pipelined encode: fixed shape");
+struct VShape {
+  static_assert(S::fixed && S::T > 0 && S::DL > 0 && ((S::T * S::DL) % 4) == 0, "per-trajectory encode: fixed shape");
   static constexpr int T = S::T, DL = S::DL, D = S::D, N = S::N, DN = S::D * S::N, Tp = round_up(S::T, 4);
-  static constexpr int NST = Tp / 4;                              // MFMA K-steps
-  static constexpr int Y16 = PIPE_SUB * T * DL / 4;               // float4 per sub-tile
-  static constexpr int Y_OPS = (Y16 + PIPE_MT - 1) / PIPE_MT;     // DMA wave-instructions per DMA wave
-  static constexpr int P_OPS = (2 * 4 * Tp + PIPE_MT - 1) / PIPE_MT;
+  static constexpr int NST = Tp / 4;   // MFMA K-steps
 };
 
-// s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8])
-template <int N>
-__device__ __forceinline__ void wait_vm_lgkm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | ((N >> 4) << 14));
-}
-// Workgroup barrier that does not wait for this wave's outstanding global memory (the
-// caller has waited for what must be visible); a compiler-level memory fence on each side.
-__device__ __forceinline__ void bar_only() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// OPS wave-instructions of 16-byte LDS-DMA from each of the PIPE_MW DMA waves: slot
-// i = op * PIPE_MT + tid of the destination <- source float4 min(first + i, last).
-template <int OPS>
-__device__ __forceinline__ void dma16_fixed(void* lds, const float4* src, int64_t first, int64_t last) {
-  const int tid = threadIdx.x, wb = tid & ~63;
-#pragma unroll
-  for (int op = 0; op < OPS; ++op)
-    __builtin_amdgcn_global_load_lds(src + min(first + op * PIPE_MT + tid, last),
-                                     (lds_void*)(static_cast<uint4*>(lds) + op * PIPE_MT + wb), 16, 0, 0);
-}
-
-// params[j][d][n] of one sub-tile = sum_t P_kind[n][t] y[j][t][d]: a DMA wave per MFMA
-// column tile; all operands of the tile's K-steps are read before the chain (one LDS round
-// trip), even / odd steps accumulate separately as in k_encode.
-template <class S>
-__device__ __forceinline__ void pipe_fit(const Geom& g, const Dims<S>& m, const float* P, const float* Y,
-                                         const int* lcol, float* pb, int nb, int wave, int lane) {
-  using PS = PipeShape<S>;
-  const int lr = lane & 15, lk = lane >> 4;
-  const int nq = n_coltiles<PIPE_SUB>(m);
-  for (int q = wave; q < nq; q += PIPE_MW) {
-    int j, d, k;
-    bool ok;
-    tile_col<PIPE_SUB>(g, m, q, lr, j, d, k, ok);
-    ok = ok && j < nb;
-    const int c = min(max(lcol[d], 0), PS::DL - 1);
-    const float* pa = P + (k * 16 + lr) * PS::Tp + lk;
-    const float* yc = Y + j * PS::T * PS::DL + c;
-    float xa[PS::NST], ya[PS::NST];
-#pragma unroll
-    for (int st = 0; st < PS::NST; ++st) {
-      xa[st] = pa[4 * st];
-      ya[st] = yc[min(4 * st + lk, PS::T - 1) * PS::DL];
-    }
-    float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0;
-#pragma unroll
-    for (int st = 0; st < PS::NST; ++st) {
-      if (st & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc1, 0, 0, 0);
-      else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = lk * 4 + r;
-      if (ok && n < PS::N) pb[j * PS::DN + d * PS::N + n] = __fadd_rn(acc0[r], acc1[r]);
-    }
-  }
-}
-
-// params (d n) and tokens (n d) of one sub-tile from its LDS params image, by threads
-// t in [0, nthr): k_encode's epilogue.
-template <class S>
-__device__ __forceinline__ void pipe_store(const EncArgs& a, const float* pb, const float4* kq, const float* wlo,
-                                           const float* whi, int64_t b0, int nb, int t, int nthr, float vm1) {
-  using PS = PipeShape<S>;
-  constexpr int per = PS::DN, D = PS::D, N = PS::N;
-  if (nb <= 0) return;
-  if (a.params_out != nullptr) {
-    float* dst = a.params_out + b0 * per;
-    const int count = nb * per;
-    if ((((uintptr_t)dst) & 15) == 0 && (per % 4) == 0) {
-      // params from the highest threads, tokens (below) from the lowest: a sub-tile's 140 param
-      // vectors and 280 token pairs land on different waves instead of both on the first ones
-      // (encode 4.72 -> 4.66 us at B = 4,096, profiles/r02/encode_params_top_ab.log)
-      for (int i = nthr - 1 - t; i < count / 4; i += nthr)
-        st16<LAT_SP>(reinterpret_cast<float4*>(dst) + i, reinterpret_cast<const float4*>(pb)[i]);
-    } else {
-      for (int i = t; i < count; i += nthr) dst[i] = pb[i];
-    }
-  }
-  if (a.tokens_out == nullptr) return;
-  const int total = nb * per;
-  long long* tout = a.tokens_out + b0 * per;
-  const unsigned long long off = (unsigned long long)a.tok_offset;
-  auto col_of = [&](int e, int& pj) {   // token e of the sub-tile -> (d n) column, trajectory
-    const int j = e / per, r = e - j * per, n = r / D;
-    pj = j * per;
-    return (r - n * D) * N + n;
-  };
-  int done = 0;
-  if ((((uintptr_t)tout) & 15) == 0) {
-    // two tokens per 16-byte store, consecutive pairs in consecutive lanes: a wave's store
-    // instruction covers one contiguous 1 KiB (whole lines for the write-through path)
-    const int n2 = total >> 1;
-    for (int i = t; i < n2; i += nthr) {
-      int bin[2], c[2], pj[2];
-      float pv[2];
-      float4 qv[2];
-      bool ex = false;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) c[u] = col_of(2 * i + u, pj[u]);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) { pv[u] = pb[pj[u] + c[u]]; qv[u] = kq[c[u]]; }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) bin[u] = beast::quantize_bin_k(pv[u], qv[u].x, qv[u].y, qv[u].z, vm1, ex);
-      if (ex) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) bin[u] = beast::quantize_bin(pv[u], qv[u].x, qv[u].y, vm1);
-      }
-      st16<LAT_SP>(tout + 2 * i, beast::widen_bin(bin[0], off), beast::widen_bin(bin[1], off));
-    }
-    done = n2 << 1;
-  }
-  for (int e = done + t; e < total; e += nthr) {
-    int pj;
-    const int c = col_of(e, pj);
-    tout[e] = beast::widen_bin(beast::quantize_bin(pb[pj + c], wlo[c], whi[c], vm1), off);
-  }
-}
-
-struct PipeSmem {
-  int P, pbA, pbB, kq, wlo, whi, lcol, total;
+// ------------------------------------------------------- encode, per-trajectory waves --
+constexpr int RV_W = 8;   // waves = trajectories per tile (k_encode_v, k_reconstruct_v)
+// Fixed shapes (the BEAST defaults), every batch size.  Wave j of the workgroup owns trajectory
+// j of the 8-trajectory tile: C[n][d] = sum_t P_kind[n][t] y[j][t][lcol[d]] on
+// v_mfma_f32_16x16x4_f32 (A = P, B = y[j]: the columns are the trajectory's DoFs), then the wave
+// quantises its own accumulators, writes its trajectory's params (d n) and tokens (n d) into an
+// LDS image of its own and copies both out with 16-byte write-through stores -- no workgroup
+// barrier after the prologue, so one wave's stores overlap the others' MFMAs.  It replaced round 2's
+// pipelined kernel (two sub-tiles, DMA / MFMA waves and store waves; 4.70 vs 4.44 us at B = 4,096,
+// 209 vs 214 us at B = 262,144, profiles/r05/).  Same products in the same K order with the same
+// even / odd accumulators as k_encode, and the same quantiser, so params and tokens are
+// bit-identical.  With gripper DoFs each kind's chain sees zero B columns for the other kind.
+struct EvSmem {
+  int Y, P, wlo, whi, lcol, pimg, timg, total;
 };
 template <class S>
-__host__ __device__ constexpr PipeSmem pipe_smem() {
-  using PS = PipeShape<S>;
-  PipeSmem s{};
+__host__ __device__ constexpr EvSmem ev_smem(int nkinds) {
+  using PS = VShape<S>;
+  EvSmem s{};
   int o = 0;
-  s.P = o;    o += PS::P_OPS * PIPE_MT * 16;
-  s.pbA = o;  o += round_up(PIPE_SUB * PS::DN * 4, 16);
-  s.pbB = o;  o += round_up(PIPE_SUB * PS::DN * 4, 16);
-  s.kq = o;   o += PS::DN * 16;
+  s.Y = o;    o += round_up(RV_W * PS::T * PS::DL * 4, 1024);
+  s.P = o;    o += round_up(nkinds * 16 * PS::Tp * 4, 1024);
   s.wlo = o;  o += round_up(PS::DN * 4, 256);
   s.whi = o;  o += round_up(PS::DN * 4, 256);
   s.lcol = o; o += round_up(PS::D * 4, 256);
+  s.pimg = o; o += RV_W * round_up(PS::DN * 4, 16);
+  s.timg = o; o += RV_W * round_up(PS::DN * 8, 16);
   s.total = o;
   return s;
 }
 
-// traj and B lead the argument list (the rest of EncArgs follows by value) so that a build with
-// kernarg preloading (-mllvm -amdgpu-kernarg-preload-count) has them in SGPRs at wave start and
-// the first DMA does not wait for a scalar load of the argument block.
-template <class S>
-__global__ __launch_bounds__(PIPE_W * 64) void k_encode_pipe(const float* __restrict__ traj, int64_t B, EncArgs a) {
-  using PS = PipeShape<S>;
+template <class S, int SP>
+__global__ __launch_bounds__(RV_W * 64) void k_encode_v(const float* __restrict__ traj, int64_t B, EncArgs a) {
+  using PS = VShape<S>;
+  static_assert(PS::D <= 16 && PS::N <= 16 && PS::DL == PS::D, "per-trajectory encode: D, N <= 16, rows of D");
+  constexpr int NT = RV_W * 64, D = PS::D, N = PS::N, T = PS::T, Tp = PS::Tp, DN = PS::DN, NST = PS::NST;
+  constexpr int NJ = S::NJ;
+  constexpr int nkinds = NJ < D ? 2 : 1;
+  constexpr EvSmem L = ev_smem<S>(nkinds);
+  constexpr int PIMG = round_up(DN * 4, 16) / 4, TIMG = round_up(DN * 8, 16) / 8;
+  static_assert((T * D) % 4 == 0 && (DN % 2) == 0, "per-trajectory encode: whole 16-byte rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ __attribute__((aligned(16))) float YA[PS::Y_OPS * PIPE_MT * 4];
-  __shared__ __attribute__((aligned(16))) float YB[PS::Y_OPS * PIPE_MT * 4];
-  const Geom& g = a.g;
-  const Dims<S> m(g);
-  constexpr PipeSmem L = pipe_smem<S>();
+  float* Y = reinterpret_cast<float*>(smem + L.Y);
   float* P = reinterpret_cast<float*>(smem + L.P);
-  float* pbA = reinterpret_cast<float*>(smem + L.pbA);
-  float* pbB = reinterpret_cast<float*>(smem + L.pbB);
-  float4* kq = reinterpret_cast<float4*>(smem + L.kq);
   float* wlo = reinterpret_cast<float*>(smem + L.wlo);
   float* whi = reinterpret_cast<float*>(smem + L.whi);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const bool mw = wave < PIPE_MW;   // wave-uniform role
-  BSTAMP(0, 0);
-  STAMP(0, 0);
+  const int64_t b0 = (int64_t)blockIdx.x * RV_W;
+  const int nb = (int)min<int64_t>(RV_W, B - b0);
   const bool quant = a.tokens_out != nullptr;
+  STAMP(0, 0);
+  BSTAMP(0, 0);
+  // ---- prologue: the tile and every constant HBM -> LDS by DMA, all in flight together
+  constexpr int tile16 = T * D / 4;   // float4 per trajectory
+  dma16<NT>(Y, reinterpret_cast<const float4*>(traj) + b0 * tile16, nb * tile16);
+  STAMP(0, 9);
+  dma16<NT>(P, a.proj, nkinds * 4 * Tp);
+  if (quant) {
+    dma4<NT>(wlo, a.w_min, DN);
+    dma4<NT>(whi, a.w_max, DN);
+  }
+  dma4<NT>(lcol, a.dof_src, D);
   const float vm1 = (float)(a.vocab - 1);
-  const int64_t b0 = (int64_t)blockIdx.x * (2 * PIPE_SUB);
-  const int nbA = (int)min<int64_t>(PIPE_SUB, B - b0);
-  const int nbB = (int)max<int64_t>(0, min<int64_t>(PIPE_SUB, B - b0 - PIPE_SUB));
-  constexpr int tile16 = PS::T * PS::DL / 4;   // float4 per trajectory
-
-  if (mw) {
-    const float4* src = reinterpret_cast<const float4*>(traj);
-    // sources clamped to the sub-tile's own last vector (the padding re-reads a line this
-    // workgroup already fetches, not the next workgroup's trajectories)
-    const int64_t last = B * tile16 - 1;
-    dma16_fixed<PS::Y_OPS>(YA, src, b0 * tile16, min(last, (b0 + PIPE_SUB) * tile16 - 1));
-    const int nk16 = ((m.nj < m.D) ? 2 : 1) * 4 * PS::Tp;
-    dma16_fixed<PS::P_OPS>(P, reinterpret_cast<const float4*>(a.proj), 0, nk16 - 1);
-    if (quant) {
-      dma4<PIPE_MT>(wlo, a.w_min, PS::DN);
-      dma4<PIPE_MT>(whi, a.w_max, PS::DN);
+  __syncthreads();
+  STAMP(0, 2);
+  const int j = wave;
+  if (j >= nb) return;   // no barrier follows
+  // ---- fit: lane (lr, lk): A = P_kind[n = lr][t = 4 st + lk], B = y[j][t][lcol[d = lr]] (t clamped
+  //      to T - 1: the zero-padded P columns meet those rows), even / odd steps accumulate apart
+  const int lr = lane & 15, lk = lane >> 4;
+  const bool dok = lr < D;
+  const int c = dok ? min(max(lcol[lr], 0), D - 1) : 0;
+  const float* yc = Y + j * T * D + c;
+  float4_t acc0 = {0.0f, 0.0f, 0.0f, 0.0f}, acc1 = acc0;
+#pragma unroll
+  for (int kd = 0; kd < nkinds; ++kd) {
+    const bool mine = dok && (nkinds == 1 || ((lr < NJ) == (kd == 0)));
+    const float* pa = P + (kd * 16 + lr) * Tp + lk;
+    float xa[NST], ya[NST];
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {   // every operand read before the chain (one LDS round trip)
+      xa[st] = pa[4 * st];
+      const float y = yc[min(4 * st + lk, T - 1) * D];
+      ya[st] = mine ? y : 0.0f;
     }
-    dma4<PIPE_MT>(lcol, a.dof_src, PS::D);
-    dma16_fixed<PS::Y_OPS>(YB, src, min(last, (b0 + PIPE_SUB) * tile16), min(last, (b0 + 2 * PIPE_SUB) * tile16 - 1));
-    STAMP(0, 1);
-    wait_vm_lgkm<PS::Y_OPS>();   // A and the constants have landed (B's DMA is the newest)
-    STAMP(0, 2);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      if (st & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc1, 0, 0, 0);
+      else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[st], ya[st], acc0, 0, 0, 0);
+    }
   }
-  bar_only();
-  if (mw) {
-    pipe_fit<S>(g, m, P, YA, lcol, pbA, nbA, wave, lane);
-    STAMP(0, 3);
-    wait_vm_lgkm<0>();           // B has landed; pbA written
-    STAMP(0, 4);
-  } else {
-    if (quant)
-      for (int i = tid - PIPE_MT; i < PS::DN; i += PIPE_MT)
-        kq[i] = make_float4(wlo[i], whi[i], beast::quantize_scale(wlo[i], whi[i], vm1), 0.0f);
-    wait_vm_lgkm<0>();
+  STAMP(0, 3);
+  // ---- C/D map: row n = lk * 4 + r, column d = lr.  Params (d n) and tokens (n d) of the trajectory
+  //      into this wave's images; the quantiser is k_encode's (fast bins, the exact chain near a
+  //      rounding boundary or for NaN / inf)
+  float* pimg = reinterpret_cast<float*>(smem + L.pimg) + j * PIMG;
+  long long* timg = reinterpret_cast<long long*>(smem + L.timg) + j * TIMG;
+  float pv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) pv[r] = __fadd_rn(acc0[r], acc1[r]);
+  if (dok) {
+    float* q = pimg + lr * N + 4 * lk;
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      if (4 * lk + r + 1 < N) *reinterpret_cast<float2*>(q + r) = make_float2(pv[r], pv[r + 1]);
+      else if (4 * lk + r < N) q[r] = pv[r];
+    }
   }
-  bar_only();
-  if (mw) {
-    pipe_fit<S>(g, m, P, YB, lcol, pbB, nbB, wave, lane);
-    wait_vm_lgkm<0>();
-    STAMP(0, 5);
-  } else {
-    pipe_store<S>(a, pbA, kq, wlo, whi, b0, nbA, tid - PIPE_MT, PIPE_MT, vm1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the LDS reads of pbA are done
-    STAMP(0, 5);
+  if (quant) {
+    const unsigned long long off = (unsigned long long)a.tok_offset;
+    float lo[4], hi[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = lr * N + min(4 * lk + r, N - 1);
+      lo[r] = wlo[min(k, DN - 1)];
+      hi[r] = whi[min(k, DN - 1)];
+    }
+    int bin[4];
+    bool ex = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bin[r] = beast::quantize_bin_k(pv[r], lo[r], hi[r], beast::quantize_scale(lo[r], hi[r], vm1), vm1, ex);
+    if (ex) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bin[r] = beast::quantize_bin(pv[r], lo[r], hi[r], vm1);
+    }
+    if (dok) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * lk + r < N) timg[(4 * lk + r) * D + lr] = beast::widen_bin(bin[r], off);
+    }
   }
-  bar_only();
-  STAMP(0, 6);
-  pipe_store<S>(a, pbB, kq, wlo, whi, b0 + PIPE_SUB, nbB, tid, PIPE_W * 64, vm1);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  STAMP(0, 5);
+  // ---- 16-byte write-through stores of the trajectory's params (DN floats) and tokens (DN int64)
+  if (a.phases & 4) {
+    if (a.params_out != nullptr) {
+      float4* gp = reinterpret_cast<float4*>(a.params_out + (b0 + j) * DN);
+#pragma unroll
+      for (int u = 0; u < (DN / 4 + 63) / 64; ++u) {
+        const int i = u * 64 + lane;
+        if (i < DN / 4) st16<SP>(gp + i, reinterpret_cast<const float4*>(pimg)[i]);
+      }
+    }
+    if (quant) {
+      long long* gt = a.tokens_out + (b0 + j) * DN;
+#pragma unroll
+      for (int u = 0; u < (DN / 2 + 63) / 64; ++u) {
+        const int i = u * 64 + lane;
+        if (i < DN / 2) st16<SP>(gt + 2 * i, timg[2 * i], timg[2 * i + 1]);
+      }
+    }
+  }
   STAMP(0, 7);
 #ifdef BEAST_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP(0, 8);
-  __syncthreads();
-#endif
   BSTAMP(0, 1);
+#endif
 }
 
 // ------------------------------------------------------------ reconstruct --
@@ -936,7 +852,7 @@ __device__ __forceinline__ void rec_store(const RecArgs& a, float* gout, const f
 }
 
 // tsrc (the token rows: a.tokens, or a.ntokens with esz 4), B and esz lead the argument list for
-// kernarg preloading, as in k_encode_pipe: the first tile's DMA needs nothing else.
+// kernarg preloading, as in k_encode_v: the first tile's DMA needs nothing else.
 template <int TBT, int KS, int RT, class S>
 __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restrict__ tsrc, int64_t B, int esz,
                                                            RecArgs a) {
@@ -1111,7 +1027,6 @@ __global__ __launch_bounds__(S::W * 64) void k_reconstruct(const void* __restric
 // k_reconstruct (a product's operands only swap roles), so positions are bit-identical.  With
 // gripper DoFs the rows of the other kind are zero in each kind's chain: the joint chain then
 // the gripper chain, each adding exact zeros to the other kind's rows.
-constexpr int RV_W = 8;   // waves = trajectories per tile
 
 struct RvSmem {
   int tok, wlo, whi, dst, phi, lut, wimg, img, total;
@@ -1133,7 +1048,7 @@ __host__ __device__ constexpr RvSmem rv_smem(int nkinds) {
   return s;
 }
 
-template <int KS, class S>
+template <int KS, class S, int SP>
 __global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restrict__ tsrc, int64_t B, int esz,
                                                              RecArgs a) {
   static_assert(S::fixed && S::T > 0 && S::T <= 64 && S::D <= 16 && S::DL == S::D && 4 * KS >= S::N,
@@ -1262,7 +1177,7 @@ __global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restr
 #pragma unroll
     for (int u = 0; u < (n4 + 63) / 64; ++u) {
       const int i = u * 64 + lane;
-      if (i < n4) st16<LAT_SP>(gout + i, reinterpret_cast<const float4*>(img)[i]);
+      if (i < n4) st16<SP>(gout + i, reinterpret_cast<const float4*>(img)[i]);
     }
   }
   STAMP(1, 7);
@@ -1410,9 +1325,11 @@ bool wide_blocks(int64_t ntiles) {
   if (g_block_waves == 4 || g_block_waves == 7 || g_block_waves == 8) return g_block_waves != 4;
   return ntiles <= 2 * (int64_t)cu_count();
 }
-// Encode in the latency regime: the pipelined 8-wave kernel (default; BEAST_OPT_BLOCK_WAVES
-// 8 forces it at any batch), or k_encode's 7-wave one (BEAST_OPT_BLOCK_WAVES 7).
-bool pipe_encode(int64_t ntiles) { return g_block_waves == 8 || (g_block_waves == 0 && wide_blocks(ntiles)); }
+// The per-trajectory kernels (k_encode_v, k_reconstruct_v) for the fixed shapes: encode at every
+// batch size, reconstruct in the latency regime (its 4-wave kernel is as fast for bulk launches,
+// profiles/r05/).  BEAST_OPT_BLOCK_WAVES 4 / 7 forces the 4- / 7-wave k_encode / k_reconstruct, 8
+// the per-trajectory kernels at any batch size.
+bool enc_v() { return g_block_waves == 0 || g_block_waves == 8; }
 
 // Host launch of a hot kernel through hipModuleLaunchKernel with a cached function handle (per
 // device): the runtime skips hipLaunchKernel's host-function lookup and the GGL template's
@@ -1442,13 +1359,17 @@ int launch_fn(const void* kernel, std::atomic<hipFunction_t> (&cache)[16], unsig
 }
 
 template <class S>
-int launch_encode_pipe(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
-  a.g = make_geom<PIPE_SUB>(D, nj, N, T);
-  a.ntiles = (a.B + 2 * PIPE_SUB - 1) / (2 * PIPE_SUB);
-  constexpr PipeSmem L = pipe_smem<S>();
-  static std::atomic<hipFunction_t> fn[16] = {};
-  return launch_fn(reinterpret_cast<const void*>(&k_encode_pipe<S>), fn, (unsigned)a.ntiles, PIPE_W * 64, L.total, s,
-                   "k_encode_pipe", a.traj, a.B, a);
+int launch_encode_v(EncArgs a, hipStream_t s) {
+  constexpr EvSmem L = ev_smem<S>(S::NJ < S::D ? 2 : 1);
+  static_assert(L.total <= 80 * 1024, "k_encode_v LDS");
+  a.g = make_geom<RV_W>(S::D, S::NJ, S::N, S::T);
+  a.ntiles = (a.B + RV_W - 1) / RV_W;
+  // write-through stores in the latency regime, write-back for bulk launches (as k_encode's widths)
+  static std::atomic<hipFunction_t> fn[2][16] = {};
+  const bool lat = a.ntiles <= 2 * (int64_t)cu_count();
+  return launch_fn(lat ? reinterpret_cast<const void*>(&k_encode_v<S, LAT_SP>)
+                       : reinterpret_cast<const void*>(&k_encode_v<S, 0>),
+                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_encode_v", a.traj, a.B, a);
 }
 
 template <int TBT, class S>
@@ -1486,9 +1407,9 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
                 "encode list: rows must be contiguous and rows per batch a multiple of %d", tbt);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
     const bool wide = wide_blocks((a.B + 7) / 8);
-    if (!a.traj_list && pipe_encode((a.B + 7) / 8)) {
-      if (D == 14 && nj == 14) return launch_encode_pipe<Shape<14, 14, 10, 50, 14>>(a, T, D, nj, N, s);
-      if (D == 14 && nj == 12) return launch_encode_pipe<Shape<14, 12, 10, 50, 14>>(a, T, D, nj, N, s);
+    if (!a.traj_list && enc_v()) {
+      if (D == 14 && nj == 14) return launch_encode_v<Shape<14, 14, 10, 50, 14>>(a, s);
+      if (D == 14 && nj == 12) return launch_encode_v<Shape<14, 12, 10, 50, 14>>(a, s);
     }
     if (D == 14 && nj == 14)
       return wide ? launch_encode_t<8, Shape<14, 14, 10, 50, 14, 7>>(a, T, D, nj, N, true, s)
@@ -1537,8 +1458,8 @@ int launch_rec_mfma(RecArgs a, int D, int nj, int N, hipStream_t s) {
 // the 7-wave (or 4-wave) k_reconstruct; positions only (no params_out), int64 tokens, one tile
 // per workgroup
 bool rec_v(const RecArgs& a) {
-  return (g_block_waves == 0 || g_block_waves == 8) && a.params_out == nullptr && a.ntokens == nullptr &&
-         a.ntiles <= 2 * (int64_t)cu_count() && (((uintptr_t)a.pos_out) & 15) == 0;
+  return (g_block_waves == 8 || (g_block_waves == 0 && a.ntiles <= 2 * (int64_t)cu_count())) &&
+         a.params_out == nullptr && a.ntokens == nullptr && (((uintptr_t)a.pos_out) & 15) == 0;
 }
 
 template <class S>
@@ -1548,9 +1469,12 @@ int launch_rec_v(RecArgs a, hipStream_t s) {
   static_assert(L.total <= 64 * 1024, "k_reconstruct_v LDS");
   a.tbt = RV_W;
   a.ntiles = (a.B + RV_W - 1) / RV_W;
-  static std::atomic<hipFunction_t> fn[16] = {};
-  return launch_fn(reinterpret_cast<const void*>(&k_reconstruct_v<KS, S>), fn, (unsigned)a.ntiles, RV_W * 64,
-                   L.total, s, "k_reconstruct_v", static_cast<const void*>(a.tokens), a.B, 8, a);
+  static std::atomic<hipFunction_t> fn[2][16] = {};
+  const bool lat = a.ntiles <= 2 * (int64_t)cu_count();
+  return launch_fn(lat ? reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, LAT_SP>)
+                       : reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, 0>),
+                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_reconstruct_v",
+                   static_cast<const void*>(a.tokens), a.B, 8, a);
 }
 
 template <int TBT>

@@ -167,8 +167,8 @@ def codec_roofline(prof, note, t_enc: float, t_rec: float, B: int) -> dict:
     fingerprint = this tree's) `traffic` is its PMC HBM bytes per launch and the rocprofv3 averages
     of the driver's own command sit beside the live numbers (`rocprof`), so the two can be compared;
     the fraction itself never comes from a stored number."""
-    algo = {"k_encode_pipe": ENC_BYTES * B, "k_reconstruct": REC_BYTES * B}
-    ev = {"k_encode_pipe": t_enc, "k_reconstruct": t_rec}
+    algo = {"k_encode_v": ENC_BYTES * B, "k_reconstruct_v": REC_BYTES * B}
+    ev = {"k_encode_v": t_enc, "k_reconstruct_v": t_rec}
     k = max(ev, key=ev.get)
     achieved = algo[k] / (ev[k] * 1e-6)
     kern = (prof or {}).get("kernels", {})
@@ -185,7 +185,7 @@ def codec_roofline(prof, note, t_enc: float, t_rec: float, B: int) -> dict:
             "traffic_unit": "HBM bytes per launch (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same tree)",
             "algo_bytes_per_launch": algo[k], "avg_launch_us": ev[k],
             "duration_source": "HIP events around back-to-back launches on the kernel's stream, this run",
-            "events_us": {"k_encode_pipe": t_enc, "k_reconstruct": t_rec},
+            "events_us": {"k_encode_v": t_enc, "k_reconstruct_v": t_rec},
             "other_kernel_frac": {kk: algo[kk] / (ev[kk] * 1e-6) / HBM_PEAK for kk in algo if kk != k},
             "profile": os.path.relpath(PROFILE, REPO) if prof else None, "profile_note": note,
             "profile_git_head": prof.get("git_head_measured") if prof else None,
@@ -247,17 +247,17 @@ def large_batch_roofline(tok, dev, stream, B: int):
 
 def mfma_utilisation(prof, note, times_us: dict) -> dict:
     """MFMA utilisation of the fit GEMM (north_star; reference GEMM mp/uni_bspline.py:564-586):
-    issued MFMA flops per launch (same-tree rocprofv3 --pmc SQ_INSTS_MFMA of k_encode_pipe at
+    issued MFMA flops per launch (same-tree rocprofv3 --pmc SQ_INSTS_MFMA of k_encode_v at
     B = 4,096, each v_mfma_f32_16x16x4_f32 = 16*16*4*2 flops) and the algorithmic 2*T*N*D flops per
     trajectory, both over the launch duration the roofline uses, against the dense f32 MFMA peak."""
-    pm = (prof or {}).get("pmc", {}).get("k_encode_pipe", {})
+    pm = (prof or {}).get("pmc", {}).get("k_encode_v", {})
     if not pm.get("mfma_insts_per_launch"):
         return {"error": f"no same-tree SQ_INSTS_MFMA pass ({note or 'profile lacks it'})"}
     us = times_us["encode_4096"]
     issued = pm["mfma_insts_per_launch"] * 2048
     algo = FIT_FLOPS * 4096
     return {"peak_tflops": F32_MFMA_PEAK / 1e12, "source": os.path.relpath(PROFILE, REPO), "flops_per_mfma": 2048,
-            "encode_4096": {"kernel": "k_encode_pipe", "batch": 4096, "avg_launch_us": us,
+            "encode_4096": {"kernel": "k_encode_v", "batch": 4096, "avg_launch_us": us,
                             "issued_flops_per_launch": issued, "algorithmic_flops_per_launch": algo,
                             "issued_tflops": issued / (us * 1e-6) / 1e12,
                             "util_issued": issued / (us * 1e-6) / F32_MFMA_PEAK,

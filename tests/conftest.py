@@ -63,7 +63,7 @@ def set_kernel_mode(mode):
 @pytest.fixture(params=["specialised", "specialised_w4", "specialised_w7", "specialised_w8", "generic"])
 def kernel_mode(request):
     """Run a parity test on the shape-specialised kernels (the width the batch size picks,
-    the 4-wave width large batches use, the 7-wave one-pass encode and the 8-wave pipelined
+    the 4-wave width large batches use, the 7-wave one-pass encode and the 8-wave per-trajectory
     encode forced at any batch) and on the runtime-shape ones."""
     set_kernel_mode(request.param)
     yield request.param

@@ -1,6 +1,6 @@
 """Interleaved A/B of the B = 4,096 codec kernels by BEAST_OPT_BLOCK_WAVES (same library): reconstruct
-7-wave k_reconstruct (7) vs the per-trajectory k_reconstruct_v (0 / 8), encode 7-wave k_encode (7) vs
-k_encode_pipe (0 / 8); HIP events over back-to-back launches (bench.kernel_time_us), and a check that
+7-wave k_reconstruct (7) vs the per-trajectory k_reconstruct_v (8, 0), encode 7-wave k_encode (7) vs
+k_encode_pipe (8) vs the per-trajectory k_encode_v (0); HIP events over back-to-back launches (bench.kernel_time_us), and a check that
 both modes give bit-identical outputs.   python tools/ab/rec_modes_ab.py [rounds]"""
 import json
 import os
@@ -24,10 +24,10 @@ x = torch.from_numpy(synth_trajectories(B, 50, 14, seed=100)).to(dev)
 stream = torch.cuda.current_stream(dev)
 lib = _lib.load()
 enc, rec = bench.launchers(tok, dev, stream, x, B)
-res = {"rec": {7: [], 0: []}, "enc": {7: [], 0: []}, "step_wall_us": {7: [], 0: []}}
+res = {"rec": {7: [], 8: [], 0: []}, "enc": {7: [], 8: [], 0: []}, "step_wall_us": {7: [], 8: [], 0: []}}
 outs = {}
 for r in range(rounds):
-    for mode in (7, 0):
+    for mode in (7, 8, 0):
         lib.beast_set_option(_lib.OPT_BLOCK_WAVES, mode)
         res["rec"][mode].append(bench.kernel_time_us(rec, stream))
         res["enc"][mode].append(bench.kernel_time_us(enc, stream))
@@ -45,7 +45,7 @@ for r in range(rounds):
         if r == 0:
             outs[mode] = (t.cpu().numpy(), p.cpu().numpy())
 lib.beast_set_option(_lib.OPT_BLOCK_WAVES, 0)
-same = all(np.array_equal(a, b) for a, b in zip(outs[7], outs[0]))
+same = all(np.array_equal(a, b) for m in (8, 0) for a, b in zip(outs[7], outs[m]))
 print(json.dumps({"rounds": rounds, "bitwise_equal": same,
                   "median": {k: {m: float(np.median(v)) for m, v in d.items()} for k, d in res.items()},
                   "all": res}, indent=1))

@@ -29,11 +29,17 @@ def main():
     buf = (C.c_ulonglong * (4096 * 12))()
     fn = lib.beast_debug_bpe_stamps
     fn.argtypes = [C.c_void_p]
+    tt = lib.beast_debug_bpe_task_times
+    tt.argtypes = [C.c_void_p, C.c_int]
+    tbuf = (C.c_ulonglong * (4096 * 8))()
+    assert tt(tbuf, 1) == 0
     t0 = time.perf_counter()
     model.encode_rows(*args, resolve=False)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     assert fn(buf) == 0
+    assert tt(tbuf, 0) == 0
+    wt = np.frombuffer(tbuf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
     st = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 12).astype(np.int64)
     t00 = st[:, 10].min()
     us = lambda v: np.round(v / 100.0, 2)   # noqa: E731  (100 MHz)
@@ -49,7 +55,15 @@ def main():
            "row_end_us_p50_max": [float(x) for x in us(np.percentile(st[:, 7] - t00, [50, 100]))],
            "distinct_words_per_wg_p50_max": [float(np.median(st[:, 8])), int(st[:, 8].max())],
            "words_per_row_p50_max": [float(np.median(st[:, 9])), int(st[:, 9].max())],
-           "merge_rounds_per_wave_p50_max": [float(np.median(st[:, 11])), int(st[:, 11].max())]}
+           "merge_rounds_per_wave_p50_max": [float(np.median(st[:, 11])), int(st[:, 11].max())],
+           # per row wave: time (us) in mid (17..64 symbols, one word a wave), short (9..16) and tiny
+           # (<= 8) merge tasks, and how many of each it took
+           "task_us_per_wave_p50_max": {k: [float(us(np.median(wt[:, i]))), float(us(wt[:, i].max()))]
+                                        for i, k in enumerate(("mid", "short", "tiny"))},
+           "tasks_per_wg": {k: float(wt[:, 3 + i].reshape(-1, 16).sum(1).mean())
+                            for i, k in enumerate(("mid", "short", "tiny"))},
+           "us_per_task_mean": {k: float(us(wt[:, i].sum() / max(1, wt[:, 3 + i].sum())))
+                                for i, k in enumerate(("mid", "short", "tiny"))}}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:

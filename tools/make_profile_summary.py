@@ -6,7 +6,7 @@
   --stats      rocprofv3 --kernel-trace --stats summary (kernel_stats.csv) of `python bench.py`, the
                driver's own command: each kernel's average launch duration under the profiler
   --codec-pmc  tools/gpu_pmc.sh output (FETCH_SIZE and WRITE_SIZE passes over tools/pmc_codec.py at
-               B = 4,096): HBM bytes per launch of k_encode_pipe / k_reconstruct
+               B = 4,096): HBM bytes per launch of k_encode_v / k_reconstruct_v
   --bpe-pmc    tools/bpe_pmc.sh output (FETCH_SIZE / WRITE_SIZE over tools/bpe_profile.py at K5):
                HBM bytes per launch of k_merge_batch / k_apply_batch
   --bench      the bench line printed by the same rocprof'd command (kept beside for reference)
@@ -37,8 +37,8 @@ from pmc_summary import summarise  # noqa: E402
 
 # short name -> predicate on the rocprof kernel name (the B = 4,096 instantiations bench.py times)
 KERNELS = {
-    "k_encode_pipe": lambda n: "k_encode_pipe<" in n,
-    "k_reconstruct": lambda n: "k_reconstruct<8, 3, 4," in n and "14, 7> >" in n,
+    "k_encode_v": lambda n: "k_encode_v<" in n and "14, 4>, 2>" in n,        # write-through: B = 4,096
+    "k_reconstruct_v": lambda n: "k_reconstruct_v<" in n and "14, 4>, 2>" in n,
     "k_merge_batch": lambda n: "k_merge_batch(" in n,
     "k_apply_batch": lambda n: "k_apply_batch<" in n,
     "k_bpe_encode": lambda n: "k_bpe_encode<" in n,
@@ -70,14 +70,15 @@ def main():
     ap.add_argument("--bpe-pmc")
     ap.add_argument("--bench")
     ap.add_argument("--head")
+    ap.add_argument("--gpu", help="the profiled box's GPU / driver (rocm-smi --showproductname --showdriverversion)")
     a = ap.parse_args()
     from beast_tokenizer_amd import _build
     head = a.head or subprocess.run(["git", "-C", REPO, "rev-parse", "HEAD"], capture_output=True,
                                     text=True).stdout.strip()
-    res = {"lib_fingerprint": _build._fingerprint(), "git_head_measured": head,
+    res = {"lib_fingerprint": _build._fingerprint(), "git_head_measured": head, "gpu": a.gpu,
            "stats_csv": os.path.relpath(a.stats, REPO), "kernels": stats(a.stats), "pmc": {}}
     if a.codec_pmc:
-        s = summarise(a.codec_pmc, ("k_encode_pipe", "k_reconstruct"))
+        s = summarise(a.codec_pmc, ("k_encode_v", "k_reconstruct_v"))
         for k, c in s.items():
             fetch, write = 2 * c.get("FETCH_SIZE", 0.0) * 1024, c.get("WRITE_SIZE", 0.0) * 1024
             res["pmc"][k] = {"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
