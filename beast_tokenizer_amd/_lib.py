@@ -82,6 +82,10 @@ SIGNATURES = {
     "beast_bpe_dedup_workspace_bytes_safe": (_sz, [_i64]),
     "beast_bpe_dedup_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_repack_workspace_bytes": (_sz, [_i64]),
+    "beast_bpe_pretok_dedup_workspace_bytes": (_sz, [_i64]),
+    "beast_bpe_pretok_dedup": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _sz, _vp, _vp]),
+    "beast_bpe_pretok_dedup_repack": (_i32, [_vp, _i64, _vp, _vp, _sz, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp,
+                                             _vp]),
     "beast_bpe_repack_words": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_compact_words": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "beast_bpe_mergemap_log2cap": (_i32, [_i32]),

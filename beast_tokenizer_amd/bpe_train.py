@@ -95,7 +95,7 @@ class GpuBpeOps:
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
         self.stream = _lib.stream_of(self.device)
-        self._host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        self._host = torch.empty(4, dtype=torch.int64, pin_memory=True)
 
     # -- small helpers
     def _read_i64(self, t: torch.Tensor, n: int) -> List[int]:
@@ -144,6 +144,53 @@ class GpuBpeOps:
                  lut_d.numel(), woff.data_ptr(), soff.data_ptr(), b2i.data_ptr(), sym.data_ptr(), wstart.data_ptr(),
                  wlen.data_ptr(), s)
         return {"sym": sym, "wstart": wstart, "wlen": wlen, "wcount": None, "n_words": nw, "n_syms": ns}
+
+    def pretok_dedup(self, tokens, seq_off, mn, lut: np.ndarray, byte2id: np.ndarray):
+        """The one-pass setup (beast_bpe_pretok_dedup): pre-tokenise every sequence and insert its
+        words straight into the distinct-word table, then repack the distinct words; returns
+        (words, n_words, n_syms) -- the same words as pretokenize + dedup -- or None when a row
+        needs the two-pass path (over 512 code points, code points outside [0, 2^31), 2^32 tokens
+        or more)."""
+        dev, s = self.device, self.stream
+        S = seq_off.numel() - 1
+        nt = tokens.numel()
+        if S <= 0 or nt >= 2 ** 32 - 1:
+            return None
+        lib = _lib.load()
+        lut_d = torch.from_numpy(np.ascontiguousarray(lut)).to(dev)
+        b2i = torch.from_numpy(np.ascontiguousarray(byte2id, dtype=np.uint16).view(np.int16)).to(dev)
+        info = torch.empty(4, dtype=torch.int64, device=dev)
+        nbytes = lib.beast_bpe_pretok_dedup_workspace_bytes(nt)
+        while True:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            _lib.run("beast_bpe_pretok_dedup", tokens.data_ptr(), seq_off.data_ptr(), S, mn, lut_d.data_ptr(),
+                     lut_d.numel(), ws.data_ptr(), ws.numel(), info.data_ptr(), s)
+            nu, nw, ns, flags = self._read_i64(info, 4)
+            if flags & 2:
+                return None
+            if not flags & 1:
+                break
+            del ws
+            nbytes = 4 * nbytes   # more distinct words than the table holds: a 4x larger one
+        if ns >= 2 ** 32:
+            raise NotImplementedError("BPE corpus has >= 2^32 byte symbols on one GPU; shard it over more ranks")
+        m = max(nu, 1)
+        rws = torch.empty(lib.beast_bpe_repack_workspace_bytes(nu) + 8 * (nu + 1), dtype=torch.uint8, device=dev)
+        sym2 = torch.empty(max(ns + 3 * nu, 1), dtype=torch.int16, device=dev)   # spans rounded up to 4
+        w2, l2, c2 = (torch.empty(m, dtype=torch.int32, device=dev) for _ in range(3))
+        on = torch.empty(1, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_pretok_dedup_repack", tokens.data_ptr(), mn, b2i.data_ptr(), ws.data_ptr(), ws.numel(), nu,
+                 rws.data_ptr(), rws.numel(), sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), c2.data_ptr(),
+                 on.data_ptr(), s)
+        nsp = self._read_i64(on, 1)[0]
+        del ws, rws
+        sym2 = sym2[:max(nsp, 1)].clone()
+        sig = torch.empty(m, dtype=torch.int64, device=dev)
+        _lib.run("beast_bpe_word_signatures", sym2.data_ptr(), w2.data_ptr(), l2.data_ptr(), nu, sig.data_ptr(), s)
+        live = int(l2[:nu].sum()) if nu else 0
+        words = dict(sym=sym2, wstart=w2, wlen=l2, wcount=c2, sig=sig, n_words=nu, n_distinct=nu,
+                     n_syms=nsp, n_syms_distinct=live, n_syms_padded=nsp)
+        return words, nw, ns
 
     def dedup(self, words):
         """Distinct words of >= 2 symbols x their counts (HF trains on word counts)."""
@@ -472,10 +519,14 @@ def train_bpe(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, m
     if Vt > 32768:
         raise NotImplementedError(f"dense pair table needs Vt <= 32768 (got {Vt})")
     lut = class_lut(n_cp)
-    words = ops.pretokenize(tokens, seq_off, mn, lut, byte2id)
-    n_words, n_syms = words["n_words"], words["n_syms"]
-    if hasattr(ops, "dedup"):
-        words = ops.dedup(words)
+    fused = ops.pretok_dedup(tokens, seq_off, mn, lut, byte2id) if hasattr(ops, "pretok_dedup") else None
+    if fused is not None:   # one pass: pre-tokenise straight into the distinct-word table
+        words, n_words, n_syms = fused
+    else:
+        words = ops.pretokenize(tokens, seq_off, mn, lut, byte2id)
+        n_words, n_syms = words["n_words"], words["n_syms"]
+        if hasattr(ops, "dedup"):
+            words = ops.dedup(words)
     gather = getattr(reduce, "gather", None)
     loop_reduce = reduce
     if replicate and gather is not None and hasattr(ops, "gather_words") and reduce is not no_reduce:

@@ -632,28 +632,41 @@ __device__ __forceinline__ int key_col(unsigned long long k, int x, int Vt) {
   return (int)(~(uint32_t)k - (uint32_t)x * (uint32_t)Vt);
 }
 
+constexpr int RT_LANE = 4;   // best counts kept per lane by the first pass over the row
 __device__ __forceinline__ void rank_row_top(const uint32_t* __restrict__ row, int x, int Vt, int vcur, int lane,
                                              unsigned long long* __restrict__ out) {
+  // Each lane keeps its RT_LANE best (count desc, column asc) from one pass -- round 5: four, not
+  // two; a lane owning more of the row's top keys than it kept rescans its counts (a 32-step loop
+  // per extra pop), and frequent rows put several of their top columns on one lane, which made
+  // the full re-ranks the apply launch's slowest waves (profiles/r05/)
   const int nst = (vcur + ROW_STRETCH - 1) / ROW_STRETCH;
   int32_t c[32];
-  int32_t c1 = 0, c2 = 0;
-  int i1 = -1, i2 = -1;
+  int32_t tc[RT_LANE];
+  int ti[RT_LANE];
+#pragma unroll
+  for (int q = 0; q < RT_LANE; ++q) { tc[q] = 0; ti[q] = -1; }
   for (int st = 0; st < nst; ++st) {
     row_counts(row, Vt, vcur, lane, st * ROW_STRETCH, c);
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const int32_t v = c[i];
       const int idx = st * 32 + i;
-      const bool g1 = v > c1, g2 = v > c2;
-      c2 = g1 ? c1 : (g2 ? v : c2);
-      i2 = g1 ? i1 : (g2 ? idx : i2);
-      c1 = g1 ? v : c1;
-      i1 = g1 ? idx : i1;
+      // insert into the sorted list; strict '>' keeps the earlier column first on equal counts
+      bool g[RT_LANE];
+#pragma unroll
+      for (int q = 0; q < RT_LANE; ++q) g[q] = v > tc[q];
+#pragma unroll
+      for (int q = RT_LANE - 1; q > 0; --q) {
+        tc[q] = g[q - 1] ? tc[q - 1] : (g[q] ? v : tc[q]);
+        ti[q] = g[q - 1] ? ti[q - 1] : (g[q] ? idx : ti[q]);
+      }
+      tc[0] = g[0] ? v : tc[0];
+      ti[0] = g[0] ? idx : ti[0];
     }
   }
-  int32_t cc = c1;
-  int ci = i1;
-  bool second = true;   // (c2, i2) is the lane's next
+  int32_t cc = tc[0];
+  int ci = ti[0];
+  int next = 1;   // (tc[next], ti[next]) is the lane's next while next < RT_LANE
   unsigned long long w = 0ull;
 #pragma unroll 1
   for (int r = 0; r < RT_K; ++r) {   // rolled: one copy of the body stays in the instruction cache
@@ -661,10 +674,17 @@ __device__ __forceinline__ void rank_row_top(const uint32_t* __restrict__ row, i
     w = wave_max_u64(k);
     if (lane == 0) out[r] = w;
     if (r + 1 < RT_K && w != 0ull && k == w) {   // the owner (keys are distinct) moves to its next
-      if (second) {
-        cc = c2;
-        ci = i2;
-        second = false;
+      if (next < RT_LANE) {
+        int32_t nc = tc[0];
+        int ni = ti[0];
+#pragma unroll
+        for (int q = 1; q < RT_LANE; ++q) {
+          nc = q == next ? tc[q] : nc;
+          ni = q == next ? ti[q] : ni;
+        }
+        cc = nc;
+        ci = ni;
+        ++next;
       } else {   // rare: its best below (cc, ci)
         int32_t nc = 0;
         int ni = -1;
@@ -752,7 +772,7 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
 // deciding apply workgroup at its phases, for 64 passes.
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][12];
-__device__ unsigned long long g_bpe_dstamps[64][8];
+__device__ unsigned long long g_bpe_dstamps[64][16];   // [8 ..): BPE_DECIDE_WARM's dry run
 __device__ unsigned long long g_bpe_batch[1024][2];   // every pass: merges decided, why the batch ended
 __device__ unsigned long long g_apply_stamps[64][256][12];
 #define ASTAMP(pi, k)                                                                                     \
@@ -1184,7 +1204,18 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   ASTAMP(KA_PI, 2);
   if (t != gridDim.x - 1) return;
   // ---- the last workgroup's wave 0: commit the batch just applied, decide the next one
-  DSTAMP(KA_PI, 0);
+#ifdef BPE_DECIDE_WARM
+  // measurement only: the decision runs twice, the first time without writing anything (stamps
+  // at [8 ..)), to split its time into instruction fetch and the work itself
+  for (int rep = 0; rep < 2; ++rep) {
+    const bool dry = rep == 0;
+#define KA_DS(k) (dry ? 8 + (k) : (k))
+#else
+  {
+    constexpr bool dry = false;
+#define KA_DS(k) (k)
+#endif
+  DSTAMP(KA_PI, KA_DS(0));
   // the loop state in registers (uniform): this wave writes only the record below.  The batch
   // just applied was committed by k_merge_batch's workgroup 0 (a kernel boundary ago).
   const int log2cap = loop->log2cap, target = loop->target, maxm = loop->max_merges;
@@ -1208,7 +1239,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     }
   };
   load_lists(0);
-  if (lane == 0) st_agent(&loop->ticket, 0u);
+  if (lane == 0 && !dry) st_agent(&loop->ticket, 0u);
   // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
   // rows each), then KM wave-max rounds hand it out
   unsigned long long K[KM], S[KM];
@@ -1220,7 +1251,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #pragma unroll
     for (int t = 0; t < 2; ++t) top_merge<KM>(K, S, LK[t], LS[t]);
   }
-  DSTAMP(KA_PI, 1);
+  DSTAMP(KA_PI, KA_DS(1));
   // KM rounds: the wave max of the lanes' list heads (DPP, no LDS), its owner pops it; lane r
   // keeps the r-th (best, second)
   unsigned long long ckey = 0, csec = 0;
@@ -1238,7 +1269,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
       K[KM - 1] = S[KM - 1] = 0ull;
     }
   }
-  DSTAMP(KA_PI, 2);
+  DSTAMP(KA_PI, KA_DS(2));
   // lanes j < KM: candidate j's string and its id if it exists (the probes run in parallel)
   int cand_a = 0, cand_b = 0, exist = -1;
   uint32_t clen = 0;
@@ -1257,7 +1288,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
       sl = (sl + 1) & hmask;
     }
   }
-  DSTAMP(KA_PI, 3);
+  DSTAMP(KA_PI, KA_DS(3));
   // HF's stopping rules per merge and the batch rules (see above), every candidate on its own
   // lane against the ones before it; the batch is the leading run of lanes that pass
   const unsigned long long count = ckey >> 32;
@@ -1292,7 +1323,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     }
     why |= !(sec < ckey) ? 64u : 0u;
     const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
-    if (lane == 0 && KA_PI < 1024) {
+    if (lane == 0 && KA_PI < 1024 && !dry) {
       g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
       g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
     }
@@ -1300,7 +1331,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #endif
   // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
   const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
-  if (lane < nb) {
+  if (lane < nb && !dry) {
     const bool reused = lane == 0 && exist >= 0;
     loop->ba[lane] = cand_a;
     loop->bb[lane] = cand_b;
@@ -1319,7 +1350,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
         (long long)(readlane_u64(ckey, j) >> 32) >= lds_min)
       kd = j + 1;
   }
-  if (lane == 0) {
+  if (lane == 0 && !dry) {
     loop->bn = nb;
     loop->bv0 = vnow;
     loop->bnm0 = nm;
@@ -1329,7 +1360,9 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     loop->passes += 1;
     if (nb == 0) loop->active = 0;
   }
-  DSTAMP(KA_PI, 4);
+  DSTAMP(KA_PI, KA_DS(4));
+  }
+#undef KA_DS
 #undef KA_PI
 }
 

@@ -168,15 +168,17 @@ __device__ void pretok_serial(const long long* __restrict__ tok, const int64_t* 
 // with code points outside [0, 2^31)) take pretok_serial on lane 0.
 constexpr int PT_LC = 512;
 constexpr int PT_WAVES = 4;
-struct PtLds {
-  int32_t cp[PT_LC];
-  int32_t e[PT_LC];         // end of the word starting at i
-  int32_t wcp[PT_LC + 1];   // first code point of word w
-  int16_t so[PT_LC + 1];    // byte-symbol offset of code point i
-  uint8_t cls[PT_LC];
-  uint8_t vis[PT_LC];       // word_starts' marks
+template <int LC>
+struct PtLdsT {
+  int32_t cp[LC];
+  int32_t e[LC];         // end of the word starting at i
+  int32_t wcp[LC + 1];   // first code point of word w
+  int16_t so[LC + 1];    // byte-symbol offset of code point i
+  uint8_t cls[LC];
+  uint8_t vis[LC];       // word_starts' marks
   int32_t nw;
 };
+using PtLds = PtLdsT<PT_LC>;
 
 __device__ __forceinline__ void pt_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -571,6 +573,205 @@ __global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict
 }
 
 
+// ---------------------------------------------- pre-tokenise + dedup, one pass --
+// (round 5) HF's BpeTrainer trains on distinct words x counts, yet the pipeline above writes every
+// word occurrence (K5: 36.9 M words, 210 MB of byte symbols and 295 MB of starts / lengths, after
+// a counting pass and two scans) only for k_dedup_insert to read them back.  k_pretok_dedup
+// pre-tokenises each sequence (one wave, k_pretok_wave's lane-parallel regex and word chain) and
+// inserts its words straight into the distinct-word table.  A word is identified by its code
+// points (UTF-8 and the byte -> symbol map are injective), so a table key is (22-bit hash tag,
+// code-point length, token offset of the word's first occurrence) and a tag match is confirmed
+// against that occurrence in the token array -- a read-only input, so no workgroup depends on
+// bytes another one has just written.  Only the distinct words get byte symbols, in the repack
+// (k_copy_words_cp).  Rows the lane-parallel pass does not take (over PT_LC code points, code
+// points outside [0, 2^31), token offsets from 2^32) set a flag and the host runs the two-pass
+// pipeline instead; a table that fills up sets another and the host retries with a larger one.
+struct PdWs {
+  unsigned long long* keys;   // [cap] tag << 42 | cp length << 32 | token offset; 0 = free
+  uint32_t* cnt;              // [cap] occurrences per slot
+  uint32_t* rep;              // [cap] distinct word -> token offset of its first occurrence
+  uint32_t* lens;             // [cap] distinct word -> cp length << 16 | byte-symbol length
+  uint32_t* slot;             // [cap] distinct word -> table slot
+  unsigned long long* info;   // [4] distinct words, words, byte symbols, flags (PD_OVERFLOW | PD_UNSUPPORTED)
+  uint64_t cap;
+  uint32_t max_probe;
+  int tag_bits;               // 22, or fewer (tests force tag collisions)
+};
+constexpr unsigned long long PD_OVERFLOW = 1, PD_UNSUPPORTED = 2, PD_LONG = 4;
+constexpr int PD_NEW = 128;     // per-wave LDS list of new distinct words, flushed with one atomic
+constexpr int PD_LDS = 2048;    // per-workgroup LDS occurrence counts (slot -> count)
+constexpr int PD_WAVES = 8;     // rows (waves) per workgroup
+
+__device__ __forceinline__ uint64_t cp_hash(const int32_t* cps, int cs, int ce) {
+  uint64_t h = 0xcbf29ce484222325ull ^ (uint64_t)(ce - cs);
+  for (int i = cs; i < ce; ++i) h = (h ^ (uint32_t)cps[i]) * 0x100000001b3ull;
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  return h;
+}
+
+// LC: the longest row the LDS image holds (256 first: four workgroups of 8 waves a CU for BEAST's
+// rows of D * N bins; a longer row flags PD_LONG and the host reruns with 512)
+template <int LC>
+__global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long* __restrict__ tok,
+                                                              const int64_t* __restrict__ seq_off, int64_t n_seq,
+                                                              long long mn, const uint8_t* __restrict__ lut,
+                                                              int64_t lut_n, PdWs ws) {
+  __shared__ PtLdsT<LC> lds[PD_WAVES];
+  __shared__ uint8_t s_lut[256];
+  __shared__ uint32_t lkey[PD_LDS], lcnt[PD_LDS];
+  __shared__ uint32_t nrep[PD_WAVES][PD_NEW], nlen[PD_WAVES][PD_NEW], nslot[PD_WAVES][PD_NEW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lut[i] = i < lut_n ? lut[i] : (uint8_t)CLS_OTHER;
+  for (int i = threadIdx.x; i < PD_LDS; i += blockDim.x) { lkey[i] = 0; lcnt[i] = 0; }
+  __syncthreads();
+  PtLdsT<LC>& L = lds[wv];
+  const uint64_t mask = ws.cap - 1;
+  const uint32_t tag_mask = (1u << ws.tag_bits) - 1u;
+  int ncnt = 0;                          // this wave's list length (uniform)
+  unsigned long long nwords = 0, nsyms = 0;
+  auto flush_new = [&]() {               // the wave's new distinct words -> the global list
+    if (ncnt == 0) return;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(&ws.info[0], (unsigned long long)ncnt);
+    b = __shfl(b, 0);
+    for (int i = lane; i < ncnt; i += 64) {
+      ws.rep[b + i] = nrep[wv][i];
+      ws.lens[b + i] = nlen[wv][i];
+      ws.slot[b + i] = nslot[wv][i];
+    }
+    ncnt = 0;
+    pt_wave_sync();
+  };
+  constexpr int PF = LC / 64;
+  // the 512 kernel runs after the 256 one and takes only the rows that one left (257..512 code
+  // points); it returns at once when there were none (the flag, a kernel boundary ago)
+  if (LC > 256 && !(ws.info[3] & PD_LONG)) return;   // uniform: before any barrier
+  for (int64_t sidx = (int64_t)blockIdx.x * PD_WAVES + wv; sidx < n_seq; sidx += (int64_t)gridDim.x * PD_WAVES) {
+    const int64_t r0 = seq_off[sidx], n64 = seq_off[sidx + 1] - r0;
+    if (LC > 256 && n64 <= 256) continue;   // the 256 kernel's
+    if (LC == 256 && n64 > LC && n64 <= PT_LC) {   // wave-uniform: the 512-code-point kernel takes it
+      if (lane == 0) atomicOr(&ws.info[3], PD_LONG);
+      continue;
+    }
+    bool bad = n64 > LC || r0 + n64 > 0xFFFFFFFFll;
+    const int n = bad ? 0 : (int)n64;
+    // 1. code points, classes, UTF-8 symbol offsets (k_pretok_wave)
+    long long tv[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) tv[k] = (lane + 64 * k < n) ? tok[r0 + lane + 64 * k] : 0;
+    int carry = 0;
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      if (64 * k >= n) break;
+      const int i = 64 * k + lane;
+      int len = 0;
+      if (i < n) {
+        const long long c = tv[k] - mn;
+        bad |= (c < 0) | (c > 0x7FFFFFFFLL);
+        L.cp[i] = (int32_t)c;
+        L.cls[i] = (c >= 0 && c < 256) ? s_lut[c] : (c >= 0 && c < lut_n) ? lut[c] : (uint8_t)CLS_OTHER;
+        len = utf8_len(c);
+      }
+      int tot;
+      const int ex = beast_pt::wave_excl_scan(len, lane, tot);
+      if (i < n) L.so[i] = (int16_t)(carry + ex);
+      carry += tot;
+    }
+    if (__any(bad)) {   // wave-uniform: the host takes the two-pass path
+      if (lane == 0) atomicOr(&ws.info[3], PD_UNSUPPORTED);
+      continue;
+    }
+    if (lane == 0) L.so[n] = (int16_t)carry;
+    pt_wave_sync();
+    // 2. word ends, 3. the word chain (csrc/pretok.h)
+    beast_pt::regex_ends(L.cp, L.cls, L.wcp, L.e, n, lane);
+    beast_pt::word_starts(L.e, L.vis, L.wcp, nullptr, &L.nw, n, lane);
+    const int nw = L.nw;
+    nwords += nw;
+    nsyms += carry;
+    // 4. the sequence's words into the distinct-word table, a lane per word
+    for (int wb = 0; wb < nw; wb += 64) {
+      if (ncnt > PD_NEW - 64) flush_new();   // uniform
+      const int w = wb + lane;
+      bool have = false, is_new = false;
+      uint64_t k = 0;
+      uint32_t lens = 0;
+      if (w < nw) {
+        const int cs = L.wcp[w], ce = L.wcp[w + 1];
+        const int blen = L.so[ce] - L.so[cs];
+        if (blen >= 2) {
+          have = true;
+          const int cl = ce - cs;
+          lens = ((uint32_t)cl << 16) | (uint32_t)blen;
+          const uint64_t h = cp_hash(L.cp, cs, ce);
+          const unsigned long long hi = ((unsigned long long)((uint32_t)(h >> 40) & tag_mask) << 42) |
+                                        ((unsigned long long)cl << 32);
+          const unsigned long long mine = hi | (unsigned long long)(uint32_t)(r0 + cs);
+          k = h & mask;
+          for (uint32_t probe = 0;; ++probe) {
+            if (probe == ws.max_probe) {   // table too full: the host retries with a larger one
+              atomicOr(&ws.info[3], PD_OVERFLOW);
+              have = false;
+              break;
+            }
+            unsigned long long v = ws.keys[k];
+            if (v == 0ull) {
+              v = atomicCAS(&ws.keys[k], 0ull, mine);
+              if (v == 0ull) { is_new = true; break; }
+            }
+            if ((v >> 32) == (hi >> 32)) {   // same tag and length: compare the code points
+              const long long* o = tok + (uint32_t)v;
+              bool eq = true;
+              for (int i = 0; i < cl && eq; ++i) eq = (o[i] - mn) == (long long)L.cp[cs + i];
+              if (eq) break;
+            }
+            k = (k + 1) & mask;
+          }
+        }
+      }
+      // new distinct words -> this wave's LDS list (a ballot, no atomics)
+      const unsigned long long nb = __ballot(is_new);
+      if (is_new) {
+        const int u = ncnt + (int)__popcll(nb & ((1ull << lane) - 1ull));
+        nrep[wv][u] = (uint32_t)(r0 + L.wcp[w]);
+        nlen[wv][u] = lens;
+        nslot[wv][u] = (uint32_t)k;
+      }
+      ncnt += (int)__popcll(nb);
+      // the occurrence, counted in LDS (the frequent words occur millions of times)
+      if (have) {
+        const uint32_t key = (uint32_t)k + 1u;
+        uint32_t j = (key * 0x9E3779B1u) >> (32 - 11);
+        bool done = false;
+        for (int probe = 0; probe < 8 && !done; ++probe) {
+          const uint32_t cur = atomicCAS(&lkey[j], 0u, key);
+          if (cur == 0u || cur == key) { atomicAdd(&lcnt[j], 1u); done = true; }
+          j = (j + 1) & (PD_LDS - 1);
+        }
+        if (!done) atomicAdd(&ws.cnt[k], 1u);
+      }
+    }
+    pt_wave_sync();   // LDS is reused by the next sequence
+  }
+  flush_new();
+  if (lane == 0) {
+    atomicAdd(&ws.info[1], nwords);
+    atomicAdd(&ws.info[2], nsyms);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < PD_LDS; i += blockDim.x)
+    if (lkey[i]) atomicAdd(&ws.cnt[lkey[i] - 1u], lcnt[i]);
+}
+
+// distinct word i -> (token offset, byte length, count) for the repack
+__global__ __launch_bounds__(256) void k_pd_gather(PdWs ws, int64_t nu, uint32_t* __restrict__ ol,
+                                                    uint32_t* __restrict__ oc) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nu; i += (int64_t)gridDim.x * blockDim.x) {
+    ol[i] = ws.lens[i] & 0xFFFFu;
+    oc[i] = ws.cnt[ws.slot[i]];
+  }
+}
+
 // keep the words that can still merge (>= 2 symbols); one atomic per wave
 __global__ __launch_bounds__(256) void k_compact_words(const uint32_t* __restrict__ wstart,
                                                        const uint32_t* __restrict__ wlen,
@@ -671,6 +872,40 @@ __global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__
     uint16_t* dst = osym + offs[i];
     for (uint32_t k = 0; k < L; ++k) dst[k] = src[k];
     for (uint32_t k = L; k & 3u; ++k) dst[k] = 0;   // the span's padding (never a symbol of the word)
+    ow[i] = (uint32_t)offs[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out_nsym = offs[nw];
+}
+
+// k_copy_words for the one-pass setup: a distinct word's byte symbols from its first occurrence's
+// code points (UTF-8 bytes -> vocab ids), same layout (length order, spans of 4)
+__global__ __launch_bounds__(256) void k_copy_words_cp(const uint32_t* __restrict__ order, const long long* __restrict__ tok,
+                                                       long long mn, const uint16_t* __restrict__ byte2id,
+                                                       const uint32_t* __restrict__ rep, const uint32_t* __restrict__ lens,
+                                                       const int64_t* __restrict__ offs, int64_t nw,
+                                                       uint16_t* __restrict__ osym, uint32_t* __restrict__ ow,
+                                                       int64_t* __restrict__ out_nsym) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = order[i], cl = lens[w] >> 16;
+    const long long* src = tok + rep[w];
+    uint16_t* dst = osym + offs[i];
+    uint32_t o = 0;
+    auto emit = [&](long long t) {
+      uint8_t b[4];
+      const long long cp = t - mn;
+      const int Lb = utf8_len(cp);
+      utf8_bytes(cp, b);
+      for (int q = 0; q < Lb; ++q) dst[o++] = byte2id[b[q]];
+    };
+    constexpr int CP_REG = 12;   // the first code points' loads all in flight (99.9 % of K5's words)
+    long long c[CP_REG];
+#pragma unroll
+    for (int k = 0; k < CP_REG; ++k) c[k] = (uint32_t)k < cl ? src[k] : 0;
+#pragma unroll
+    for (int k = 0; k < CP_REG; ++k)
+      if ((uint32_t)k < cl) emit(c[k]);
+    for (uint32_t k = CP_REG; k < cl; ++k) emit(src[k]);
+    for (; o & 3u; ++o) dst[o] = 0;   // the span's padding (never a symbol of the word)
     ow[i] = (uint32_t)offs[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *out_nsym = offs[nw];
@@ -839,6 +1074,98 @@ extern "C" int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart
   hipLaunchKernelGGL(k_dedup_gather, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, wstart, wlen, ws, out_wstart,
                      out_wlen, out_wcount, out_n);
   BEAST_LAUNCHED("k_dedup_gather");
+  return BEAST_OK;
+}
+
+// ---- one-pass setup (k_pretok_dedup): the table and the distinct-word list in one workspace
+static uint64_t pd_cap(int64_t n_tokens) {   // ~ n_tokens / 5 slots (K5: 4.85 M distinct words of 7e7 tokens)
+  uint64_t c = 1024;
+  while (c < (uint64_t)std::max<int64_t>(n_tokens, 1) / 5) c <<= 1;
+  return c;
+}
+static PdWs pd_view(void* workspace, size_t ws_bytes) {
+  PdWs w{};
+  w.cap = 1024;   // the largest power of two the workspace holds (24 bytes a slot)
+  while ((w.cap * 2) * 24 + 64 <= ws_bytes) w.cap *= 2;
+  char* p = static_cast<char*>(workspace);
+  w.keys = reinterpret_cast<unsigned long long*>(p);  p += w.cap * 8;
+  w.cnt = reinterpret_cast<uint32_t*>(p);             p += w.cap * 4;
+  w.rep = reinterpret_cast<uint32_t*>(p);             p += w.cap * 4;
+  w.lens = reinterpret_cast<uint32_t*>(p);            p += w.cap * 4;
+  w.slot = reinterpret_cast<uint32_t*>(p);            p += w.cap * 4;
+  w.info = reinterpret_cast<unsigned long long*>(p);
+  w.max_probe = DEDUP_MAX_PROBE;
+  w.tag_bits = std::min(22, std::max(1, beast::g_bpe_dedup_key_bits));
+  return w;
+}
+extern "C" size_t beast_bpe_pretok_dedup_workspace_bytes(int64_t n_tokens) { return pd_cap(n_tokens) * 24 + 64; }
+
+extern "C" int beast_bpe_pretok_dedup(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                                      const uint8_t* cls_lut, int64_t lut_n, void* workspace, size_t ws_bytes,
+                                      int64_t* out_info, void* stream) {
+  BEAST_REQUIRE(tok && seq_off && cls_lut && workspace && out_info, "beast_bpe_pretok_dedup: null pointer");
+  BEAST_REQUIRE(n_seq >= 0 && ws_bytes >= 1024 * 24 + 64, "beast_bpe_pretok_dedup: bad sizes");
+  hipStream_t s = beast::as_stream(stream);
+  PdWs w = pd_view(workspace, ws_bytes);
+  BEAST_HIP(hipMemsetAsync(w.keys, 0, w.cap * 12, s), "pretok_dedup memset");   // keys + counts
+  BEAST_HIP(hipMemsetAsync(w.info, 0, 32, s), "pretok_dedup memset");
+  if (n_seq > 0) {
+    // the waves walk the sequences grid-stride; rows of <= 256 code points first (37 KB of LDS a
+    // workgroup), rows of 257..512 by the 512 kernel only when some row needs it
+    hipLaunchKernelGGL(k_pretok_dedup<256>, dim3(grid_for(n_seq, PD_WAVES, 4 * 256)), dim3(64 * PD_WAVES), 0, s,
+                       reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n, w);
+    BEAST_LAUNCHED("k_pretok_dedup<256>");
+    hipLaunchKernelGGL(k_pretok_dedup<PT_LC>, dim3(grid_for(n_seq, PD_WAVES, 2 * 256)), dim3(64 * PD_WAVES), 0, s,
+                       reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n, w);
+    BEAST_LAUNCHED("k_pretok_dedup<512>");
+  }
+  BEAST_HIP(hipMemcpyAsync(out_info, w.info, 32, hipMemcpyDeviceToDevice, s), "pretok_dedup info");
+  return BEAST_OK;
+}
+
+extern "C" int beast_bpe_pretok_dedup_repack(const int64_t* tok, int64_t min_tok, const uint16_t* byte2id,
+                                             void* workspace, size_t ws_bytes, int64_t n_distinct, void* repack_ws,
+                                             size_t repack_ws_bytes, uint16_t* out_sym, uint32_t* out_wstart,
+                                             uint32_t* out_wlen, uint32_t* out_wcount, int64_t* out_nsym,
+                                             void* stream) {
+  BEAST_REQUIRE(tok && byte2id && workspace && repack_ws && out_sym && out_wstart && out_wlen && out_wcount && out_nsym,
+                "beast_bpe_pretok_dedup_repack: null pointer");
+  PdWs w = pd_view(workspace, ws_bytes);
+  BEAST_REQUIRE(n_distinct >= 0 && (uint64_t)n_distinct <= w.cap, "beast_bpe_pretok_dedup_repack: bad n_distinct");
+  BEAST_REQUIRE_CODE(repack_ws_bytes >= beast_bpe_repack_workspace_bytes(n_distinct) + 8 * (size_t)(n_distinct + 1),
+                     BEAST_E_WORKSPACE, "repack workspace %zu too small", repack_ws_bytes);
+  hipStream_t s = beast::as_stream(stream);
+  const int64_t n = n_distinct > 0 ? n_distinct : 1;
+  char* p = static_cast<char*>(repack_ws);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(p);   p += 256 * 4;
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(p); p += 256 * 4;
+  uint32_t* order = reinterpret_cast<uint32_t*>(p);  p += n * 4;
+  p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
+  int64_t* lens = reinterpret_cast<int64_t*>(p);     p += n * 8;
+  int64_t* offs = reinterpret_cast<int64_t*>(p);     p += (n + 1) * 8;
+  int64_t* sws = reinterpret_cast<int64_t*>(p);      p += beast_scan_workspace_bytes(n);
+  p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(p) + 7) & ~uintptr_t(7));
+  uint32_t* blen = reinterpret_cast<uint32_t*>(p);   p += n * 4;   // byte lengths / counts before the sort
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(p);
+  BEAST_HIP(hipMemsetAsync(hist, 0, 256 * 4, s), "repack memset");
+  if (n_distinct == 0) {
+    BEAST_HIP(hipMemsetAsync(out_nsym, 0, 8, s), "repack memset");
+    return BEAST_OK;
+  }
+  const int g = grid_for(n_distinct, 256, 8192);
+  hipLaunchKernelGGL(k_pd_gather, dim3(g), dim3(256), 0, s, w, n_distinct, blen, cnt);
+  hipLaunchKernelGGL(k_len_hist, dim3(g), dim3(256), 0, s, blen, n_distinct, hist);
+  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(256), 0, s, hist, cursor);
+  hipLaunchKernelGGL(k_len_scatter, dim3((n_distinct + RP_WPB - 1) / RP_WPB), dim3(256), 0, s, blen, n_distinct, cursor,
+                     order);
+  hipLaunchKernelGGL(k_gather_lens, dim3(g), dim3(256), 0, s, order, blen, cnt, n_distinct, lens, out_wlen, out_wcount);
+  BEAST_LAUNCHED("k_gather_lens");
+  int rc = scan_rec(lens, offs, n_distinct, sws, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_scan_total, dim3(1), dim3(64), 0, s, lens, offs, n_distinct);
+  hipLaunchKernelGGL(k_copy_words_cp, dim3(g), dim3(256), 0, s, order, reinterpret_cast<const long long*>(tok),
+                     (long long)min_tok, byte2id, w.rep, w.lens, offs, n_distinct, out_sym, out_wstart, out_nsym);
+  BEAST_LAUNCHED("k_copy_words_cp");
   return BEAST_OK;
 }
 

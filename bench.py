@@ -588,7 +588,15 @@ def hf_bpe_same_sample(rows: torch.Tensor, vocab: int):
     torch.cuda.synchronize()
     el_gpu = time.perf_counter() - t0
     same = [list(m) for m in g.merges] == model["merges"] and g.vocab == model["vocab"]
-    return {"value": nm / el, "unit": "merges/s", "kind": "reference",
+    full = None   # HF over the FULL K5 corpus, measured in the build container (tools/hf_k5_container.py)
+    fp = os.path.join(REPO, "profiles", "r05", "hf_k5_container.json")
+    if os.path.exists(fp):
+        with open(fp) as f:
+            fk = json.load(f)
+        full = {k: fk.get(k) for k in ("merges_per_s", "hf_seconds", "merges", "tokens", "rayon_threads",
+                                       "container_cpus", "hf_version")}
+        full["source"] = os.path.relpath(fp, REPO)
+    return {"value": nm / el, "unit": "merges/s", "kind": "reference", "full_k5_container": full,
             "cores": int(os.environ.get("RAYON_NUM_THREADS", "1")),
             "gpu_same_sample_merges_per_s": len(g.merges) / el_gpu, "gpu_same_sample_s": el_gpu,
             "hf_seconds": el, "merges_equal": bool(same),

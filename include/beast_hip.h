@@ -342,6 +342,26 @@ size_t beast_bpe_dedup_workspace_bytes_safe(int64_t n_words);
 int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uint32_t* wlen, int64_t n_words,
                           void* workspace, size_t ws_bytes, uint32_t* out_wstart, uint32_t* out_wlen,
                           uint32_t* out_wcount, int64_t* out_n, void* stream);
+/* One-pass setup (round 5): beast_bpe_pretok_count / _emit and beast_bpe_dedup_words fused.
+ * Every sequence is pre-tokenised (one wave each, as beast_bpe_pretok_emit) and its words of >= 2
+ * byte symbols go straight into the distinct-word table, identified by their code points (a
+ * match is confirmed against the first occurrence in `tok` itself); no per-occurrence symbol
+ * array is written.  out_info (device int64[4]): distinct words, words, byte symbols, flags --
+ * bit 0: the table filled up (retry with 4x the workspace), bit 1: a row the one-pass kernel does
+ * not take (over 512 code points, a code point outside [0, 2^31), token offsets from 2^32): run
+ * the two-pass functions above instead.  Workspace: beast_bpe_pretok_dedup_workspace_bytes(total
+ * tokens); it keeps the distinct-word list for beast_bpe_pretok_dedup_repack, which writes the
+ * same outputs as beast_bpe_dedup_words + beast_bpe_repack_words (words of >= 2 symbols in
+ * length order, their counts), byte symbols made from the code points (byte2id as pretok_emit).
+ * repack_ws_bytes >= beast_bpe_repack_workspace_bytes(n_distinct) + 8 * (n_distinct + 1). */
+size_t beast_bpe_pretok_dedup_workspace_bytes(int64_t n_tokens);
+int beast_bpe_pretok_dedup(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
+                           const uint8_t* cls_lut, int64_t lut_n, void* workspace, size_t ws_bytes, int64_t* out_info,
+                           void* stream);
+int beast_bpe_pretok_dedup_repack(const int64_t* tok, int64_t min_tok, const uint16_t* byte2id, void* workspace,
+                                  size_t ws_bytes, int64_t n_distinct, void* repack_ws, size_t repack_ws_bytes,
+                                  uint16_t* out_sym, uint32_t* out_wstart, uint32_t* out_wlen, uint32_t* out_wcount,
+                                  int64_t* out_nsym, void* stream);
 /* Copy words into one symbol array ordered by length (min(L, 255) buckets, order inside a
  * bucket unspecified); each word starts at a multiple of 4 symbols (8 bytes) and owns its length
  * rounded up to 4 (the padding is zero): the layout the merge loops read and write in 8-byte

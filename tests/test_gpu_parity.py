@@ -660,6 +660,78 @@ def test_bpe_dedup_and_compact_match_counter(gpu_device):
     assert got_c == sorted(keep)
 
 
+@pytest.mark.parametrize("mode", ["plain", "tag3", "overflow", "mixed_utf8"])
+def test_bpe_pretok_dedup_equals_two_pass(gpu_device, mode):
+    """The one-pass setup (k_pretok_dedup + repack from code points) gives exactly the two-pass
+    pipeline's distinct words x counts, in the same layout (length order, 4-symbol spans), and the
+    same word / symbol totals: with forced 3-bit hash tags (every tag collides; the code-point
+    compare keeps words apart), with a table too small for the words (the retry), and over
+    code points of 1-3 UTF-8 bytes."""
+    from collections import Counter
+    from beast_tokenizer_amd import _lib
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, fixed_rows_to_device
+    from beast_tokenizer_amd.pretok import class_lut
+    rng = np.random.default_rng(23)
+    hi = 3000 if mode == "mixed_utf8" else 300
+    base = rng.integers(0, hi, size=9)
+    arr = base[rng.integers(0, 9, size=(4000, 60))]
+    arr[::7] = rng.integers(0, hi, size=(arr[::7].shape[0], 60))
+    arr[::11, ::5] = 32   # spaces: more, shorter words
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64) + 17).to(gpu_device))
+    present = np.zeros(hi, dtype=bool)
+    present[np.unique(arr)] = True
+    _, _, byte2id = build_alphabet(present, [chr(i) for i in range(hi)], [])
+    ops = GpuBpeOps(gpu_device)
+    lut = class_lut(hi)
+
+    def counted(d):
+        sym = d["sym"].cpu().numpy().view(np.uint16)
+        ws, wl = d["wstart"].cpu().numpy(), d["wlen"].cpu().numpy()
+        wc = d["wcount"].cpu().numpy()
+        return {tuple(sym[a:a + n]): int(c) for a, n, c in zip(ws[: d["n_words"]], wl[: d["n_words"]],
+                                                                wc[: d["n_words"]])}
+    w = ops.pretokenize(flat, off, 17, lut, byte2id)
+    want = counted(ops.dedup(w))
+    lib = _lib.load()
+    saved = lib.beast_bpe_pretok_dedup_workspace_bytes
+    try:
+        if mode == "tag3":
+            lib.beast_set_option(_lib.OPT_BPE_DEDUP_KEY_BITS, 3)
+        if mode == "overflow":   # 2,048 slots for thousands of distinct words: the kernel flags it, ops retries
+            ops_lib = _lib.load()
+            ops_lib.beast_bpe_pretok_dedup_workspace_bytes = lambda n: 2048 * 24 + 64
+        res = ops.pretok_dedup(flat, off, 17, lut, byte2id)
+    finally:
+        lib.beast_set_option(_lib.OPT_BPE_DEDUP_KEY_BITS, 64)
+        lib.beast_bpe_pretok_dedup_workspace_bytes = saved
+    assert res is not None
+    u, nw, ns = res
+    assert (nw, ns) == (w["n_words"], w["n_syms"])
+    if mode == "overflow":
+        assert u["n_words"] > 2048 * 0.5
+    got = counted(u)
+    assert len(got) == u["n_words"] == len(want) and got == want
+    lens = u["wlen"].cpu().numpy()[: u["n_words"]]
+    assert np.all(np.diff(np.minimum(lens, 255)) >= 0)
+    ws = u["wstart"].cpu().numpy()[: u["n_words"]]
+    assert np.array_equal(ws[1:], ws[:-1] + (lens[:-1] + 3) // 4 * 4)
+    assert u["n_syms_distinct"] == int(lens.sum()) and u["n_syms_padded"] == int(((lens + 3) // 4 * 4).sum())
+
+
+def test_bpe_pretok_dedup_declines_long_rows(gpu_device):
+    """A row over 512 code points is not the one-pass kernel's: it reports it and train_bpe runs the
+    two-pass pipeline (HF's merges either way, tests/golden ragged corpora)."""
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, sequences_to_device
+    from beast_tokenizer_amd.pretok import class_lut
+    rng = np.random.default_rng(3)
+    seqs = [rng.integers(0, 200, size=n) for n in (40, 700, 90)]
+    flat, off = sequences_to_device(seqs, gpu_device)
+    present = np.zeros(200, dtype=bool)
+    present[np.unique(np.concatenate(seqs))] = True
+    _, _, byte2id = build_alphabet(present, [chr(i) for i in range(200)], [])
+    assert GpuBpeOps(gpu_device).pretok_dedup(flat, off, 0, class_lut(200), byte2id) is None
+
+
 def test_bpe_tokenizer_end_to_end(gpu_device):
     g = load_npz("bspline_k2.npz")
     tok = make_tok("k2", g, gpu_device, cls=BEASTBsplineBPETokenizer, bpe_vocab_size=512)

@@ -74,7 +74,7 @@ def run(out_json=None) -> None:
     res = train_bpe(flat, off, 2048, ops=Ops(dev))
     torch.cuda.synchronize()
     ms = _read(lib, "beast_debug_merge_stamps", (64, 1024, 12))
-    ds = _read(lib, "beast_debug_decide_stamps", (64, 8))
+    ds = _read(lib, "beast_debug_decide_stamps", (64, 16))
     aps = _read(lib, "beast_debug_apply_stamps", (64, 256, 12))
     us = lambda v: round(float(v) / 100.0, 2)   # noqa: E731
     passes = []
@@ -134,6 +134,11 @@ def run(out_json=None) -> None:
         if d[0] > 0:
             rec.update({"decide_start": us(d[0] - t0), "decide_lists_merged": us(d[1] - t0),
                         "decide_rounds": us(d[2] - t0), "decide_probed": us(d[3] - t0), "decide_end": us(d[4] - t0)})
+        if d[8] > 0:   # -DBPE_DECIDE_WARM: the dry first run of the same decision (times from its start)
+            rec.update({"dry_lists_merged": us(d[9] - d[8]), "dry_rounds": us(d[10] - d[8]),
+                        "dry_probed": us(d[11] - d[8]), "dry_end": us(d[12] - d[8]),
+                        "warm_lists_merged": us(d[1] - d[0]), "warm_rounds": us(d[2] - d[0]),
+                        "warm_probed": us(d[3] - d[0]), "warm_end": us(d[4] - d[0])})
         passes.append(rec)
     keys = list(dict.fromkeys(k for r in passes for k in r if k != "wg"))
     summary = {k: float(np.median([r[k] for r in passes if k in r])) for k in keys}
