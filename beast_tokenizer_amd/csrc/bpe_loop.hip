@@ -439,41 +439,30 @@ constexpr int BK = 8;                 // merges per batch at most
 constexpr int BATCH_LDS = 32768;      // bytes of LDS delta vectors per workgroup (k_merge's 4 * Vt int32 at Vt 2048)
 constexpr int BATCH_WG_LANE = 4;      // apply-workgroup lists per lane of the deciding wave (Vt <= 4096)
 
-// One decided batch.  Every k_merge_batch workgroup decides the batch it applies (the same one:
-// same inputs); its workgroup 0 writes it here for k_apply_batch, the next decision and the host.
-struct BatchRec {
-  int32_t n;             // merges (0: none; the loop has stopped)
-  int32_t v0, nm0;       // vocabulary size and merges logged before the batch
-  int32_t vcur;          // vocabulary size after the batch
-  int32_t kd;            // merges 0 .. kd-1 sum their pair-count changes in LDS first
-  int32_t mt;            // longest token a word can hold during the batch (its new ones included)
-  int32_t a[BK], b[BK], nid[BK], reused[BK];
-  uint32_t len[BK];
-  unsigned long long h[BK];
-};
-static_assert(sizeof(BatchRec) % 4 == 0, "copied as 32-bit words");
-constexpr int32_t LOOP_FAULT = 0x46415531;   // a value no earlier state word at this offset takes
-
-// The loop's device state.  rec[passes & 1] is the latest decided batch (for pass 0: k_loop_init's
-// empty one).  k_merge_batch reads it at entry, decides the next batch into LDS and its
-// workgroup 0 writes that batch to the other slot right away (no other workgroup reads it), then
-// commits it (string hash table, token lengths, log); once every workgroup has taken its decision
-// (`decided` reaches the grid) workgroup 0 advances `passes` and the host view (vcur, n_merges,
-// maxtlen).  k_apply_batch reads rec[passes & 1]: the batch the merge launch before it applied.
+// The loop's device state: counters, the string hash table's geometry and the batch the next
+// k_merge_batch applies.  The batch record (b*) is written by the deciding wave of k_apply_batch
+// (or k_loop_init); the counters (vcur, n_merges, maxtlen) by workgroup 0 of k_merge_batch when
+// it commits the batch; every other reader is in a later kernel.
 struct LoopState {
   int32_t active;        // 0 once the loop has stopped (later launches are no-ops)
-  int32_t vcur;          // vocabulary size (committed merges)          -- host view
-  int32_t n_merges;      // merges logged                               -- host view
+  int32_t vcur;          // vocabulary size (committed merges)
+  int32_t n_merges;      // merges logged
   int32_t target;        // vocab_size
   int32_t min_freq;
   int32_t log2cap;       // token-string hash table
   int32_t max_merges;    // log capacity
-  int32_t maxtlen;       // longest committed token (HF length units)   -- host view
-  uint32_t decided;      // k_merge_batch workgroups past their decision in this launch
+  int32_t maxtlen;       // longest committed token (HF length units)
+  uint32_t ticket;       // k_apply_batch workgroups arrived in this launch
   int32_t passes;        // batches decided
-  int32_t fault;         // LOOP_FAULT: a merge launch's decision barrier timed out (the host raises)
-  int32_t pad_;
-  BatchRec rec[2];
+  // the batch the next k_merge_batch applies (and commits: its workgroup 0)
+  int32_t bn;            // merges (0: none; the loop has stopped)
+  int32_t bv0, bnm0;     // vocabulary size and merges logged before the batch
+  int32_t bvcur;         // vocabulary size after the batch
+  int32_t bkd;           // merges 0 .. bkd-1 sum their pair-count changes in LDS first
+  int32_t bmt;           // longest token a word can hold during the batch (its new ones included)
+  int32_t ba[BK], bb[BK], bnid[BK], breused[BK];
+  uint32_t blen[BK];
+  unsigned long long bh[BK];
 };
 
 // Token strings are identified by (64-bit polynomial hash of their UTF-8 bytes, byte length):
@@ -779,11 +768,11 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
 
 // Per-pass phase stamps (tools builds with -DBPE_MERGE_STAMPS=<first pass>; the product library
 // compiles them out): s_memrealtime (100 MHz) of thread 0 of the first 1024 merge workgroups at
-// entry, after the decision, after the scan, before the delta flush and at exit, of every apply
-// workgroup, and of merge workgroup 0's decision at its phases, for 64 passes.
+// entry, after the record, after the scan, before the delta flush and at exit, and of the
+// deciding apply workgroup at its phases, for 64 passes.
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][12];
-__device__ unsigned long long g_bpe_dstamps[64][16];
+__device__ unsigned long long g_bpe_dstamps[64][16];   // [8 ..): BPE_DECIDE_WARM's dry run
 __device__ unsigned long long g_bpe_batch[1024][2];   // every pass: merges decided, why the batch ended
 __device__ unsigned long long g_apply_stamps[64][256][12];
 #define ASTAMP(pi, k)                                                                                     \
@@ -798,7 +787,7 @@ __device__ unsigned long long g_apply_stamps[64][256][12];
   } while (0)
 #define DSTAMP(pi, k)                                                                                     \
   do {                                                                                                    \
-    if (lane == 0 && blockIdx.x == 0 && (pi) >= BPE_MERGE_STAMPS && (pi) < BPE_MERGE_STAMPS + 64)         \
+    if (lane == 0 && (pi) >= BPE_MERGE_STAMPS && (pi) < BPE_MERGE_STAMPS + 64)                            \
       g_bpe_dstamps[(pi) - BPE_MERGE_STAMPS][k] = __builtin_amdgcn_s_memrealtime();                       \
   } while (0)
 #else
@@ -807,229 +796,64 @@ __device__ unsigned long long g_apply_stamps[64][256][12];
 #define ASTAMP(pi, k) do { } while (0)
 #endif
 
-// The next batch, decided by one wave from the apply workgroups' lists (bw.wgkey / wgsec: each
-// its BK best candidates, best first, with their rows' bounds) and the previous batch's record P:
-// the global order (lane l merges the sorted lists of apply workgroups l, l + 64, ...; KM wave-max
-// rounds hand out the top KM), each candidate's string and its id if it exists (the probes in
-// parallel), HF's stopping rules per merge and the batch rules, every candidate on its own lane
-// against the ones before it -- the batch is the leading run of lanes that pass.  Writes the batch
-// into R (LDS).  Every k_merge_batch workgroup runs this on the same inputs and gets the same
-// batch.  While it runs, workgroup 0 may already be committing this launch's batch into the
-// string table: such entries carry ids >= vnow, and the probe skips them -- the table as it was
-// before the batch is what the rules ask about.
-template <int KM>
-__device__ __forceinline__ void decide_batch(const LoopState* __restrict__ loop, const BatchRec* __restrict__ P,
-                                             const LoopHash& lh, const BatchWs& bw,
-                                             const uint32_t* __restrict__ tlen, int Vt, long long lds_min, int lane,
-                                             BatchRec& R, int pi) {
-  DSTAMP(pi, 0);
-  const int log2cap = loop->log2cap, target = loop->target, maxm = loop->max_merges;
-  const unsigned long long minf = (unsigned long long)loop->min_freq;
-  const int nm = P->nm0 + P->n;
-  int mt = P->mt;
-  const int vnow = P->vcur;
-  const uint64_t hmask = (1ull << log2cap) - 1;
-  const int nwg = batch_nwg(Vt);
-  unsigned long long LK[2][KM], LS[2][KM];
-  auto load_lists = [&](int t0) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int g = (t0 + t) * 64 + lane;
-#pragma unroll
-      for (int i = 0; i < KM; ++i) {
-        LK[t][i] = g < nwg ? ld_agent(&bw.wgkey[(size_t)i * nwg + g]) : 0ull;
-        LS[t][i] = g < nwg ? ld_agent(&bw.wgsec[(size_t)i * nwg + g]) : 0ull;
-      }
-    }
-  };
-  load_lists(0);
-  // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
-  // rows each), then KM wave-max rounds hand it out
-  unsigned long long K[KM], S[KM];
-#pragma unroll
-  for (int i = 0; i < KM; ++i) K[i] = S[i] = 0ull;
-  for (int t0 = 0; t0 < BATCH_WG_LANE; t0 += 2) {
-    if (t0 * 64 >= nwg) break;
-    if (t0 > 0) load_lists(t0);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) top_merge<KM>(K, S, LK[t], LS[t]);
-  }
-  DSTAMP(pi, 1);
-  // KM rounds: the wave max of the lanes' list heads (DPP, no LDS), its owner pops it; lane r
-  // keeps the r-th (best, second)
-  unsigned long long ckey = 0, csec = 0;
-#pragma unroll
-  for (int r = 0; r < KM; ++r) {
-    const unsigned long long m = wave_max_u64(K[0]);
-    const bool mine = m != 0ull && K[0] == m;   // keys are distinct: one owner
-    const unsigned long long ball = __ballot(mine);
-    const int src = ball ? (int)__builtin_ctzll(ball) : 0;
-    const unsigned long long sec = readlane_u64(S[0], src);
-    if (lane == r) { ckey = m; csec = ball ? sec : 0ull; }
-    if (mine) {
-#pragma unroll
-      for (int i = 0; i < KM - 1; ++i) { K[i] = K[i + 1]; S[i] = S[i + 1]; }
-      K[KM - 1] = S[KM - 1] = 0ull;
-    }
-  }
-  DSTAMP(pi, 2);
-  // lanes j < KM: candidate j's string and its id if it exists (the probes run in parallel)
-  int cand_a = 0, cand_b = 0, exist = -1;
-  uint32_t clen = 0;
-  unsigned long long ch = 0;
-  if (lane < KM && ckey) {
-    const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(ckey & 0xFFFFFFFFull);
-    cand_a = (int)(idx / (uint32_t)Vt);
-    cand_b = (int)(idx % (uint32_t)Vt);
-    ch = ld_agent(&lh.th[cand_a]) * ld_agent(&lh.tp[cand_b]) + ld_agent(&lh.th[cand_b]);
-    clen = ld_agent(&tlen[cand_a]) + ld_agent(&tlen[cand_b]);
-    uint64_t sl = loop_slot(ch, clen, log2cap);
-    while (true) {
-      const unsigned long long li = ld_agent(&lh.lid[sl]), ki = ld_agent(&lh.key[sl]);
-      if (li == LOOP_EMPTY) break;
-      // ids >= vnow: this launch's own commit, racing with the probe -- not part of the table the
-      // decision reads (its key may not even be written yet)
-      if ((uint32_t)li < (uint32_t)vnow && (uint32_t)(li >> 32) == clen && ki == ch) { exist = (int)(uint32_t)li; break; }
-      sl = (sl + 1) & hmask;
-    }
-  }
-  DSTAMP(pi, 3);
-  // HF's stopping rules per merge and the batch rules (see above), every candidate on its own
-  // lane against the ones before it; the batch is the leading run of lanes that pass
-  const unsigned long long count = ckey >> 32;
-  bool ok = lane < KM && count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm;
-  if (lane > 0) ok &= exist < 0;   // only the first may re-use an id
-  unsigned long long sec = 0;
-#pragma unroll
-  for (int i = 0; i < KM - 1; ++i) {
-    const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
-    const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)clen, i);
-    const unsigned long long hi = readlane_u64(ch, i), si = readlane_u64(csec, i);
-    const bool ends = ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0);   // self-pair / re-use
-    // a later pair must not chain onto an earlier one (b_j == a_i: (x, a_i) loses count; a_j ==
-    // b_i: (b_i, y) does); sharing a_i as its left or b_i as its right symbol is fine
-    if (i < lane) ok &= !ends && cand_b != ai && cand_a != bi && !(ch == hi && clen == li);
-    if (i < lane) sec = umax64(sec, si);
-  }
-  ok &= sec < ckey;   // a taken row's second-best would come first
-  const unsigned long long pass = __ballot(ok);
-  const int nb = (int)__builtin_ctzll(~pass);   // leading lanes that pass (<= KM)
-#ifdef BPE_MERGE_STAMPS
-  {   // why the batch ended: the first failing lane's rules (bit 0 list end, 1 HF stop, 2 re-use,
-      // 3 after a self-pair / re-use, 4 chaining, 5 same string, 6 a taken row's bound)
-    uint32_t why = lane >= KM ? 1u : 0u;
-    why |= !(count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm) ? 2u : 0u;
-    why |= lane > 0 && exist >= 0 ? 4u : 0u;
-    for (int i = 0; i < KM - 1 && i < lane; ++i) {
-      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
-      why |= ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0) ? 8u : 0u;
-      why |= cand_b == ai || cand_a == bi ? 16u : 0u;
-      why |= ch == readlane_u64(ch, i) && clen == (uint32_t)__builtin_amdgcn_readlane((int)clen, i) ? 32u : 0u;
-    }
-    why |= !(sec < ckey) ? 64u : 0u;
-    const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
-    if (lane == 0 && blockIdx.x == 0 && pi >= 0 && pi < 1024) {
-      g_bpe_batch[pi][0] = (unsigned long long)nb;
-      g_bpe_batch[pi][1] = nb < KM ? w_nb : 1u;
-    }
-  }
-#endif
-  // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
-  const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
-  if (lane < BK) {   // every slot: the batch's merges, then empty ones
-    const bool in = lane < nb;
-    const bool reused = in && lane == 0 && exist >= 0;
-    R.a[lane] = in ? cand_a : -1;
-    R.b[lane] = in ? cand_b : -1;
-    R.nid[lane] = in ? (reused ? exist : vnow + lane) : -1;
-    R.reused[lane] = reused ? 1 : 0;
-    R.len[lane] = in ? clen : 0u;
-    R.h[lane] = in ? ch : 0ull;
-  }
-  // merges 0 .. kd-1 sum their changes in LDS: the frequent ones whose vectors fit
-  const int stride = vnow + nb;
-  int kd = 0;
-#pragma unroll
-  for (int j = 0; j < KM; ++j) {
-    if (j < nb) mt = max(mt, (int)__builtin_amdgcn_readlane((int)clen, j));
-    if (kd == j && j < nb && (j + 1) * 16 * stride <= BATCH_LDS &&
-        (long long)(readlane_u64(ckey, j) >> 32) >= lds_min)
-      kd = j + 1;
-  }
-  if (lane == 0) {
-    R.n = nb;
-    R.v0 = vnow;
-    R.nm0 = nm;
-    R.vcur = vnow + nb - (reused0 ? 1 : 0);
-    R.kd = kd;
-    R.mt = mt;
-  }
-  DSTAMP(pi, 4);
-}
-
-// One pass: decide the batch (every workgroup, wave 0, from the lists the last k_apply_batch
-// published -- no serial last-workgroup decision at the end of the apply launch), then apply its
-// merges over every word: one scan of the word signatures for the union of the batch's pairs,
-// each candidate word read once into registers; the merges it holds are known up front (batch
-// pairs never chain, so one merge neither makes nor breaks another's pair) and applied with the
-// op per lane, so a wave whose lanes hold different merges runs one pass, not one per merge.
-// The first signature loads are in flight while the batch is decided.  apps (nullable, tools /
-// byte accounting): pair occurrences rewritten per merge, unweighted, at apps[n_merges + j].
-template <int KM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_merge_batch(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
+// The merges of the batch the last k_apply_batch decided, over every word: one scan of the word
+// signatures for the union of the batch's pairs, each candidate word read once into registers;
+// the merges it holds are known up front (batch pairs are symbol-disjoint, so one merge neither
+// makes nor breaks another's pair) and applied with the op per lane, so a wave whose lanes hold
+// different merges runs one pass, not one per merge.  The first signature loads are in flight
+// before the batch record arrives.  apps (nullable, tools / byte accounting): pair occurrences
+// rewritten per merge, unweighted, at apps[n_merges + j].
+__global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym, const uint32_t* __restrict__ wstart,
                                                      uint32_t* __restrict__ wlen, const uint32_t* __restrict__ wcount,
                                                      int64_t nw, uint32_t* __restrict__ tlen, int max_len,
                                                      int Vt, unsigned long long* __restrict__ sig,
-                                                     LoopState* __restrict__ loop, LoopHash lh, BatchWs bw,
+                                                     LoopState* __restrict__ loop, LoopHash lh,
                                                      uint32_t* __restrict__ table, uint32_t* __restrict__ clean,
-                                                     int32_t* __restrict__ deltas, uint32_t* __restrict__ apps,
-                                                     long long lds_min) {
+                                                     int32_t* __restrict__ deltas, uint32_t* __restrict__ apps) {
   __shared__ __attribute__((aligned(16))) int32_t dl[BATCH_LDS / 4];
   __shared__ uint32_t clist[BATCH_CLIST];
   __shared__ int cn, touched;
-  __shared__ BatchRec R;   // this pass's batch
-  __shared__ uint32_t s_apps[BK];
+  __shared__ int s_a[BK], s_b[BK], s_nid[BK];
+  __shared__ uint32_t s_len[BK], s_apps[BK];
   __shared__ unsigned long long s_need[BK];
-  // the state the launch starts from: `passes` and rec[passes & 1] do not change until every
-  // workgroup has decided
-  const int active = loop->active, pp = loop->passes;
-#define KB_PI pp
+#ifdef BPE_MERGE_STAMPS
+  const int st_pi = loop->passes;
+#define KB_PI st_pi
+#else
+#define KB_PI 0
+#endif
   MSTAMP(KB_PI, 0);
-  unsigned long long sgv[MERGE_SCAN];   // the first signature batch of the two-phase scan
+  // the batch record (threads < BK), then the first signature batch of the two-phase scan
+  int ra = 0, rb = 0, rn = 0;
+  uint32_t rl = 0;
+  if (threadIdx.x < BK) {
+    ra = loop->ba[threadIdx.x];
+    rb = loop->bb[threadIdx.x];
+    rn = loop->bnid[threadIdx.x];
+    rl = loop->blen[threadIdx.x];
+  }
+  // the record's fields all in one round trip (no load waits on the n == 0 test)
+  const int n = loop->bn, vcur = loop->bv0, kd = loop->bkd, mt = loop->bmt, nm0 = loop->bnm0;
+  unsigned long long sgv[MERGE_SCAN];
   const int64_t nchunks = (nw + 255) / 256;
 #pragma unroll
   for (int u = 0; u < MERGE_SCAN; ++u) {
     const int64_t w = (blockIdx.x + (int64_t)u * gridDim.x) * 256 + threadIdx.x;
     sgv[u] = w < nw ? sig[w] : 0ull;
   }
-  // the LDS delta vectors cleared whole while the batch is decided (16-byte stores)
+  // the LDS delta vectors cleared whole while the record is in flight (16-byte stores)
   for (int i = threadIdx.x; i < BATCH_LDS / 16; i += 256) reinterpret_cast<int4*>(dl)[i] = make_int4(0, 0, 0, 0);
-  if (!active) return;   // the loop has stopped (uniform)
-  if (threadIdx.x < 64) {
-    decide_batch<KM>(loop, &loop->rec[pp & 1], lh, bw, tlen, Vt, lds_min, (int)threadIdx.x, R, pp);
-    if (threadIdx.x == 0) atomicAdd(&loop->decided, 1u);   // after the decision's last load returned
-  }
-  __syncthreads();
-  const int n = R.n, vcur = R.v0, kd = R.kd, mt = R.mt, nm0 = R.nm0;
-  if (n == 0) {   // HF's stop (same in every workgroup): nothing is written but the flag
-    if (blockIdx.x == 0 && threadIdx.x == 0) st_agent(&loop->active, 0);
-    return;
-  }
-  if (blockIdx.x == 0) {
-    // the record for k_apply_batch, the host and the next decision, into the slot no workgroup of
-    // this launch reads; then the commit, merge j on lane j: its string into the hash table
-    // (distinct strings, so concurrent inserts only race for free slots), the new token's hash /
-    // P^len / length, its log entry.  The other workgroups take the vocabulary before the batch
-    // and the new tokens' lengths from their own decision, and their probes skip ids >= v0.
-    const int32_t* src = reinterpret_cast<const int32_t*>(&R);
-    int32_t* dst = reinterpret_cast<int32_t*>(&loop->rec[(pp + 1) & 1]);
-    for (int i = threadIdx.x; i < (int)(sizeof(BatchRec) / 4); i += 256) dst[i] = src[i];
+  if (n == 0) return;   // the loop has stopped (uniform)
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // commit the batch, merge j on lane j: its string into the hash table (distinct strings, so
+    // concurrent inserts only race for free slots), the new token's hash / P^len / length, its log
+    // entry; then the counters.  No other workgroup of this launch reads what this writes: they
+    // take the vocabulary before the batch from bv0 and the new tokens' lengths from the record.
     const int j = threadIdx.x;
     if (j < n) {
-      const int ra = R.a[j], rb = R.b[j], rn = R.nid[j], reused = R.reused[j];
-      const uint32_t rl = R.len[j];
+      const int reused = loop->breused[j];
       if (!reused) {
-        const unsigned long long h = R.h[j];
+        const unsigned long long h = loop->bh[j];
         const unsigned long long pa = lh.tp[ra], pb = lh.tp[rb];
         const uint64_t hmask = (1ull << loop->log2cap) - 1;
         uint64_t sl = loop_slot(h, rl, loop->log2cap);
@@ -1042,17 +866,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       int32_t* lg = lh.log + 4 * (int64_t)(nm0 + j);
       lg[0] = ra; lg[1] = rb; lg[2] = rn; lg[3] = reused;
     }
+    if (j == 0) {
+      loop->n_merges = nm0 + n;
+      loop->vcur = loop->bvcur;
+      loop->maxtlen = mt;
+    }
   }
   if (threadIdx.x < BK) {
+    s_a[threadIdx.x] = ra;
+    s_b[threadIdx.x] = rb;
+    s_nid[threadIdx.x] = rn;
+    s_len[threadIdx.x] = rl;
     s_apps[threadIdx.x] = 0;
-    s_need[threadIdx.x] = (int)threadIdx.x < n ? sig_bit((uint32_t)R.a[threadIdx.x]) | sig_bit((uint32_t)R.b[threadIdx.x])
-                                               : ~0ull;
+    s_need[threadIdx.x] = (int)threadIdx.x < n ? sig_bit((uint32_t)ra) | sig_bit((uint32_t)rb) : ~0ull;
   }
   if (threadIdx.x == 0) { cn = 0; touched = 0; }
-  const int* s_a = R.a;
-  const int* s_b = R.b;
-  const int* s_nid = R.nid;
-  const uint32_t* s_len = R.len;
   const int stride = vcur + n;
   const int nl = kd * 4 * stride;   // LDS entries in use (<= BATCH_LDS / 4: the decider's rule)
   __syncthreads();
@@ -1064,7 +892,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
   for (int j = 0; j < BK; ++j) need[j] = s_need[j];
   bool any = false;
-  const uint32_t nmask = (1u << n) - 1u;
   auto op_of = [&](int j) {
     return BatchOp{s_a[j], s_b[j], s_nid[j], max_len, Vt, vbase, nnew, stride, mt + (int)s_len[j] < max_len,
                    s_len[j], tlen, nlen, j < kd ? dl + j * 4 * stride : nullptr,
@@ -1101,7 +928,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       uint32_t cand = 0;   // the merges whose pair the signature admits (need[j] = ~0 past n)
 #pragma unroll
       for (int j = 0; j < BK; ++j) cand |= (uint32_t)((sgw & need[j]) == need[j]) << j;
-      cand &= nmask;       // a saturated signature admits ~0 too
       uint32_t hits = 0;
       for (; cand; cand &= cand - 1) {
         const int j = __builtin_ctz(cand);
@@ -1201,58 +1027,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   MSTAMP(KB_PI, 3);
   if (apps != nullptr && threadIdx.x < n && s_apps[threadIdx.x])
     atomicAdd(&apps[nm0 + threadIdx.x], s_apps[threadIdx.x]);
-  if (kd > 0) {
-    if (any) touched = 1;
-    __syncthreads();
-    if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> the table (or the delta vectors)
-      for (int i = threadIdx.x; i < nl; i += 256) {
-        const int32_t v = dl[i];
-        if (v) {
-          const int jk = i / stride;
-          const int j = jk >> 2;
-          BatchOp op = op_of(j);
-          op.dl = nullptr;
-          op.table_add(jk & 3, (uint32_t)(i - jk * stride), v);
-        }
+  if (kd == 0) { MSTAMP(KB_PI, 4); return; }
+  if (any) touched = 1;
+  __syncthreads();
+  if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> the table (or the delta vectors)
+    for (int i = threadIdx.x; i < nl; i += 256) {
+      const int32_t v = dl[i];
+      if (v) {
+        const int jk = i / stride;
+        const int j = jk >> 2;
+        BatchOp op = op_of(j);
+        op.dl = nullptr;
+        op.table_add(jk & 3, (uint32_t)(i - jk * stride), v);
       }
-  }
+    }
   MSTAMP(KB_PI, 4);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // every workgroup has read rec[pp & 1] and `passes` (each counts itself right after its
-    // decision, at its start, so the count is complete long before this): the pass advances.  The
-    // wait is bounded; a timeout stops the loop and is reported (fault), it never hangs.
-    uint32_t spins = 0;
-    bool ok = true;
-    while (ld_agent(&loop->decided) < gridDim.x) {
-      if (++spins > (1u << 22)) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    if (!ok) {
-      st_agent(&loop->fault, LOOP_FAULT);
-      st_agent(&loop->active, 0);
-    } else {
-      st_agent(&loop->decided, 0u);
-      loop->n_merges = nm0 + n;
-      loop->vcur = R.vcur;
-      loop->maxtlen = mt;
-      loop->passes = pp + 1;
-    }
-  }
 #undef KB_PI
 }
 
 // After a batch: (sharded: add the all-reduced delta vectors to the table,) retire the merged
-// pairs, re-rank every changed row and publish this workgroup's BK best candidates for the next
-// k_merge_batch's decision.  init: no batch, every row < vcur ranked.  The batch is
-// rec[passes & 1], which the merge launch before this one wrote (and counted).
+// pairs, re-rank every changed row (best and second-best) and publish this workgroup's BK best
+// rows.  The workgroup that arrives last then commits the batch (string hash table, token
+// lengths, log, vcur) and decides the next one, so the next k_merge_batch reads a finished
+// record.  init: no batch, every row < vcur ranked, then the first decision.
+//
+// The hand-off of the per-workgroup lists to the deciding workgroup: the lists are stored
+// write-through (sc1) by wave 0, which waits for them (vmcnt(0)) before its lane 0 adds to the
+// ticket; the workgroup whose add returns gridDim.x - 1 reads them with sc1 loads
+// (MI355X_MICROARCH.md, hand-off table row 1).  Everything else the decision reads -- the hash
+// table, tlen, th, tp, the loop state -- only the deciding lane writes.
+template <int KM>
 __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __restrict__ table, int Vt, ArgWs aw,
-                                                                 BatchWs bw, const LoopState* __restrict__ loop,
-                                                                 int nrows, int init, int32_t* __restrict__ deltas) {
+                                                                 BatchWs bw, uint32_t* __restrict__ tlen,
+                                                                 LoopState* __restrict__ loop, LoopHash lh, int nrows,
+                                                                 int init, int32_t* __restrict__ deltas,
+                                                                 long long lds_min) {
   __shared__ unsigned long long s_top[APPLY_ROWS][RT_STRIDE];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int pp = loop->passes;
-#define KA_PI (pp - 1)
+#ifdef BPE_MERGE_STAMPS
+  const int st_pi = loop->passes;
+#define KA_PI st_pi
+#else
+#define KA_PI 0
+#endif
   ASTAMP(KA_PI, 0);
+  // rows interleaved over the workgroups (x = blockIdx + wave * grid): the rows a batch touches
+  // -- neighbours of its pairs, often a run of early, frequent ids -- spread over the grid
+  // instead of filling a few workgroups' waves (a workgroup re-ranking 14 of its 16 rows was the
+  // pass's last ticket, 8.4 us against 4.4 for the median re-ranking one)
   const int x = (int)blockIdx.x + wave * (int)gridDim.x;
   // the row's clean flag and cached keys do not depend on the batch record: in flight with it
   uint32_t pre_clean = 0u;
@@ -1263,17 +1085,16 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     pre_k = lane < RT_K ? g[lane] : 0ull;
     pre_F = g[RT_F];
   }
-  const BatchRec* Rb = &loop->rec[pp & 1];
-  const int n = init ? 0 : Rb->n;
+  const int n = init ? 0 : loop->bn;
   if (!init && (n == 0 || !loop->active)) return;   // uniform over the grid
   int A[BK], B[BK], N[BK];
 #pragma unroll
   for (int j = 0; j < BK; ++j) {
-    A[j] = j < n ? Rb->a[j] : -1;
-    B[j] = j < n ? Rb->b[j] : -1;
-    N[j] = j < n ? Rb->nid[j] : -1;
+    A[j] = j < n ? loop->ba[j] : -1;
+    B[j] = j < n ? loop->bb[j] : -1;
+    N[j] = j < n ? loop->bnid[j] : -1;
   }
-  const int vcur = init ? loop->vcur : Rb->vcur;
+  const int vcur = init ? loop->vcur : loop->bvcur;
   // rows the merges changed: b_j, new_j entirely (re-ranked); other rows x only at columns a_j,
   // new_j (k_merge_batch's adds: clean[x] == 0; or the sharded deltas: touched) and, for x = a_j,
   // b_j (retired below)
@@ -1376,7 +1197,172 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
       st_agent(&bw.wgsec[(size_t)rank * nwg + blockIdx.x], kw ? s_top[w][KR] : 0ull);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(&loop->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   ASTAMP(KA_PI, 2);
+  if (t != gridDim.x - 1) return;
+  // ---- the last workgroup's wave 0: commit the batch just applied, decide the next one
+#ifdef BPE_DECIDE_WARM
+  // measurement only: the decision runs twice, the first time without writing anything (stamps
+  // at [8 ..)), to split its time into instruction fetch and the work itself
+  for (int rep = 0; rep < 2; ++rep) {
+    const bool dry = rep == 0;
+#define KA_DS(k) (dry ? 8 + (k) : (k))
+#else
+  {
+    constexpr bool dry = false;
+#define KA_DS(k) (k)
+#endif
+  DSTAMP(KA_PI, KA_DS(0));
+  // the loop state in registers (uniform): this wave writes only the record below.  The batch
+  // just applied was committed by k_merge_batch's workgroup 0 (a kernel boundary ago).
+  const int log2cap = loop->log2cap, target = loop->target, maxm = loop->max_merges;
+  const unsigned long long minf = (unsigned long long)loop->min_freq;
+  const int nm = loop->n_merges;
+  int mt = loop->maxtlen;
+  const int vnow = loop->vcur;
+  const uint64_t hmask = (1ull << log2cap) - 1;
+  // the workgroups' lists (the first 128: the whole table up to Vt = 2,048) first: they do not
+  // depend on the commit, so their round trip overlaps it
+  unsigned long long LK[2][KM], LS[2][KM];
+  auto load_lists = [&](int t0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int g = (t0 + t) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < KM; ++i) {
+        LK[t][i] = g < nwg ? ld_agent(&bw.wgkey[(size_t)i * nwg + g]) : 0ull;
+        LS[t][i] = g < nwg ? ld_agent(&bw.wgsec[(size_t)i * nwg + g]) : 0ull;
+      }
+    }
+  };
+  load_lists(0);
+  if (lane == 0 && !dry) st_agent(&loop->ticket, 0u);
+  // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
+  // rows each), then KM wave-max rounds hand it out
+  unsigned long long K[KM], S[KM];
+#pragma unroll
+  for (int i = 0; i < KM; ++i) K[i] = S[i] = 0ull;
+  for (int t0 = 0; t0 < BATCH_WG_LANE; t0 += 2) {
+    if (t0 * 64 >= nwg) break;
+    if (t0 > 0) load_lists(t0);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) top_merge<KM>(K, S, LK[t], LS[t]);
+  }
+  DSTAMP(KA_PI, KA_DS(1));
+  // KM rounds: the wave max of the lanes' list heads (DPP, no LDS), its owner pops it; lane r
+  // keeps the r-th (best, second)
+  unsigned long long ckey = 0, csec = 0;
+#pragma unroll
+  for (int r = 0; r < KM; ++r) {
+    const unsigned long long m = wave_max_u64(K[0]);
+    const bool mine = m != 0ull && K[0] == m;   // keys are distinct: one owner
+    const unsigned long long ball = __ballot(mine);
+    const int src = ball ? (int)__builtin_ctzll(ball) : 0;
+    const unsigned long long sec = readlane_u64(S[0], src);
+    if (lane == r) { ckey = m; csec = ball ? sec : 0ull; }
+    if (mine) {
+#pragma unroll
+      for (int i = 0; i < KM - 1; ++i) { K[i] = K[i + 1]; S[i] = S[i + 1]; }
+      K[KM - 1] = S[KM - 1] = 0ull;
+    }
+  }
+  DSTAMP(KA_PI, KA_DS(2));
+  // lanes j < KM: candidate j's string and its id if it exists (the probes run in parallel)
+  int cand_a = 0, cand_b = 0, exist = -1;
+  uint32_t clen = 0;
+  unsigned long long ch = 0;
+  if (lane < KM && ckey) {
+    const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(ckey & 0xFFFFFFFFull);
+    cand_a = (int)(idx / (uint32_t)Vt);
+    cand_b = (int)(idx % (uint32_t)Vt);
+    ch = ld_agent(&lh.th[cand_a]) * ld_agent(&lh.tp[cand_b]) + ld_agent(&lh.th[cand_b]);
+    clen = ld_agent(&tlen[cand_a]) + ld_agent(&tlen[cand_b]);
+    uint64_t sl = loop_slot(ch, clen, log2cap);
+    while (true) {
+      const unsigned long long li = ld_agent(&lh.lid[sl]), ki = ld_agent(&lh.key[sl]);
+      if (li == LOOP_EMPTY) break;
+      if ((uint32_t)(li >> 32) == clen && ki == ch) { exist = (int)(uint32_t)li; break; }
+      sl = (sl + 1) & hmask;
+    }
+  }
+  DSTAMP(KA_PI, KA_DS(3));
+  // HF's stopping rules per merge and the batch rules (see above), every candidate on its own
+  // lane against the ones before it; the batch is the leading run of lanes that pass
+  const unsigned long long count = ckey >> 32;
+  bool ok = lane < KM && count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm;
+  if (lane > 0) ok &= exist < 0;   // only the first may re-use an id
+  unsigned long long sec = 0;
+#pragma unroll
+  for (int i = 0; i < KM - 1; ++i) {
+    const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
+    const uint32_t li = (uint32_t)__builtin_amdgcn_readlane((int)clen, i);
+    const unsigned long long hi = readlane_u64(ch, i), si = readlane_u64(csec, i);
+    const bool ends = ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0);   // self-pair / re-use
+    // a later pair must not chain onto an earlier one (b_j == a_i: (x, a_i) loses count; a_j ==
+    // b_i: (b_i, y) does); sharing a_i as its left or b_i as its right symbol is fine
+    if (i < lane) ok &= !ends && cand_b != ai && cand_a != bi && !(ch == hi && clen == li);
+    if (i < lane) sec = umax64(sec, si);
+  }
+  ok &= sec < ckey;   // a taken row's second-best would come first
+  const unsigned long long pass = __ballot(ok);
+  const int nb = (int)__builtin_ctzll(~pass);   // leading lanes that pass (<= KM)
+#ifdef BPE_MERGE_STAMPS
+  {   // why the batch ended: the first failing lane's rules (bit 0 list end, 1 HF stop, 2 re-use,
+      // 3 after a self-pair / re-use, 4 chaining, 5 same string, 6 a taken row's bound)
+    uint32_t why = lane >= KM ? 1u : 0u;
+    why |= !(count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm) ? 2u : 0u;
+    why |= lane > 0 && exist >= 0 ? 4u : 0u;
+    for (int i = 0; i < KM - 1 && i < lane; ++i) {
+      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
+      why |= ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0) ? 8u : 0u;
+      why |= cand_b == ai || cand_a == bi ? 16u : 0u;
+      why |= ch == readlane_u64(ch, i) && clen == (uint32_t)__builtin_amdgcn_readlane((int)clen, i) ? 32u : 0u;
+    }
+    why |= !(sec < ckey) ? 64u : 0u;
+    const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
+    if (lane == 0 && KA_PI < 1024 && !dry) {
+      g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
+      g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
+    }
+  }
+#endif
+  // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
+  const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
+  if (lane < nb && !dry) {
+    const bool reused = lane == 0 && exist >= 0;
+    loop->ba[lane] = cand_a;
+    loop->bb[lane] = cand_b;
+    loop->bnid[lane] = reused ? exist : vnow + lane;
+    loop->breused[lane] = reused ? 1 : 0;
+    loop->blen[lane] = clen;
+    loop->bh[lane] = ch;
+  }
+  // merges 0 .. kd-1 sum their changes in LDS: the frequent ones whose vectors fit
+  const int stride = vnow + nb;
+  int kd = 0;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    if (j < nb) mt = max(mt, (int)__builtin_amdgcn_readlane((int)clen, j));
+    if (kd == j && j < nb && (j + 1) * 16 * stride <= BATCH_LDS &&
+        (long long)(readlane_u64(ckey, j) >> 32) >= lds_min)
+      kd = j + 1;
+  }
+  if (lane == 0 && !dry) {
+    loop->bn = nb;
+    loop->bv0 = vnow;
+    loop->bnm0 = nm;
+    loop->bvcur = vnow + nb - (reused0 ? 1 : 0);
+    loop->bkd = kd;
+    loop->bmt = mt;
+    loop->passes += 1;
+    if (nb == 0) loop->active = 0;
+  }
+  DSTAMP(KA_PI, KA_DS(4));
+  }
+#undef KA_DS
 #undef KA_PI
 }
 
@@ -1543,8 +1529,6 @@ extern "C" int beast_bpe_loop_init(void* ws, size_t ws_bytes, int Vt, int max_me
   init.log2cap = loop_log2cap(Vt);
   init.max_merges = max_merges;
   init.maxtlen = max_tlen;
-  init.rec[0].v0 = init.rec[0].vcur = n_tokens;   // the empty batch before the first one
-  init.rec[0].mt = max_tlen;
   const int n = n_tokens > 0 ? n_tokens : 1;
   hipLaunchKernelGGL(k_loop_init, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<LoopState*>(w + L.st), init,
                      loop_hash_view(ws, Vt, max_merges), n_tokens, init.log2cap,
@@ -1566,23 +1550,12 @@ extern "C" size_t beast_bpe_batch_workspace_bytes(int Vt) { return batch_ws_byte
 
 extern "C" size_t beast_bpe_batch_delta_count(int Vt) { return (size_t)BK * 4 * (size_t)(Vt > 0 ? Vt : 1); }
 
-static int launch_apply(LoopState* st, BatchWs bw, ArgWs aw, int Vt, uint32_t* table, int rows, int init,
-                        int32_t* deltas, hipStream_t s) {
-  hipLaunchKernelGGL(k_apply_batch, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s, table,
-                     Vt, aw, bw, st, rows, init, deltas);
-  BEAST_LAUNCHED("k_apply_batch");
-  return BEAST_OK;
-}
-
 template <int KM>
-static int launch_merge_batch(int grid, uint16_t* sym, const uint32_t* wstart, uint32_t* wlen, const uint32_t* wcount,
-                              int64_t n_words, uint32_t* tlen, int max_token_length, int Vt, uint64_t* sig,
-                              LoopState* st, const LoopHash& lh, BatchWs bw, uint32_t* table, uint32_t* clean,
-                              int32_t* deltas, uint32_t* apps, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge_batch<KM>, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, tlen,
-                     max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, bw, table, clean,
-                     deltas, apps, (long long)beast::g_merge_lds_min);
-  BEAST_LAUNCHED("k_merge_batch");
+static int launch_apply(LoopState* st, const LoopHash& lh, BatchWs bw, ArgWs aw, int Vt, uint32_t* tlen,
+                        uint32_t* table, int rows, int init, int32_t* deltas, hipStream_t s) {
+  hipLaunchKernelGGL(k_apply_batch<KM>, dim3((rows + APPLY_ROWS - 1) / APPLY_ROWS), dim3(64 * APPLY_ROWS), 0, s, table,
+                     Vt, aw, bw, tlen, st, lh, rows, init, deltas, (long long)beast::g_merge_lds_min);
+  BEAST_LAUNCHED("k_apply_batch");
   return BEAST_OK;
 }
 
@@ -1607,31 +1580,26 @@ extern "C" int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_step
   const ArgWs aw = argws_view(argws, Vt);
   const BatchWs bw = batch_view(batch_ws, Vt);
   const int rows = std::min(Vt, std::max(vocab_size, 1));
-  auto apply = [&](int init) { return launch_apply(st, bw, aw, Vt, table, rows, init, deltas, s); };
-  if (flags & BEAST_BPE_BATCH_INIT) {   // every row's cached keys and the workgroups' lists for the first decision
+  auto apply = [&](int init) {
+    switch (max_batch) {
+      case 2: return launch_apply<2>(st, lh, bw, aw, Vt, tlen, table, rows, init, deltas, s);
+      case 4: return launch_apply<4>(st, lh, bw, aw, Vt, tlen, table, rows, init, deltas, s);
+      default: return launch_apply<8>(st, lh, bw, aw, Vt, tlen, table, rows, init, deltas, s);
+    }
+  };
+  if (flags & BEAST_BPE_BATCH_INIT) {   // every row's best and second-best, then the first batch
     BEAST_HIP(hipMemsetAsync(batch_ws, 0, batch_ws_bytes(Vt), s), "batch workspace memset");
     if (int rc = apply(1)) return rc;
   }
-  // the grid: as many workgroups as the device holds at once (the pass's decision barrier waits
-  // for all of them to have started), from the occupancy of the instantiation launched
-  static int resident[3] = {0, 0, 0};
-  const int ki = max_batch == 2 ? 0 : max_batch == 4 ? 1 : 2;
-  if (resident[ki] == 0)
-    resident[ki] = ki == 0 ? resident_grid(k_merge_batch<2>, 256, 0, 2)
-                 : ki == 1 ? resident_grid(k_merge_batch<4>, 256, 0, 2) : resident_grid(k_merge_batch<8>, 256, 0, 2);
-  const int grid = grid_for(n_words > 0 ? n_words : 1, MERGE_SCAN * 256, resident[ki]);
+  static int resident = 0;
+  if (resident == 0) resident = resident_grid(k_merge_batch, 256, 0, 2);
+  const int grid = grid_for(n_words > 0 ? n_words : 1, MERGE_SCAN * 256, resident);
   for (int i = 0; i < n_steps; ++i) {
     if (!(flags & BEAST_BPE_BATCH_NO_MERGE)) {
-      int rc;
-      switch (max_batch) {
-        case 2: rc = launch_merge_batch<2>(grid, sym, wstart, wlen, wcount, n_words, tlen, max_token_length, Vt, sig, st,
-                                           lh, bw, table, aw.clean, deltas, apps, s); break;
-        case 4: rc = launch_merge_batch<4>(grid, sym, wstart, wlen, wcount, n_words, tlen, max_token_length, Vt, sig, st,
-                                           lh, bw, table, aw.clean, deltas, apps, s); break;
-        default: rc = launch_merge_batch<8>(grid, sym, wstart, wlen, wcount, n_words, tlen, max_token_length, Vt, sig,
-                                            st, lh, bw, table, aw.clean, deltas, apps, s);
-      }
-      if (rc) return rc;
+      hipLaunchKernelGGL(k_merge_batch, dim3(grid), dim3(256), 0, s, sym, wstart, wlen, wcount, n_words, tlen,
+                         max_token_length, Vt, reinterpret_cast<unsigned long long*>(sig), st, lh, table, aw.clean,
+                         deltas, apps);
+      BEAST_LAUNCHED("k_merge_batch");
     }
     if (!(flags & BEAST_BPE_BATCH_NO_APPLY))
       if (int rc = apply(0)) return rc;

@@ -79,7 +79,7 @@ struct HostPinned {
 };
 
 constexpr uint64_t LOOP_P = 0x9E3779B97F4A7C15ull;   // bpe_train.py GpuBpeOps.LOOP_P
-constexpr int ST_ACTIVE = 0, ST_VCUR = 1, ST_NMERGES = 2, ST_FAULT = 10;
+constexpr int ST_ACTIVE = 0, ST_VCUR = 1, ST_NMERGES = 2;
 constexpr int KMAX = 8, CHUNK = 64;
 
 }  // namespace
@@ -315,8 +315,6 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
   int32_t state[16];
   BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
   BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  BEAST_REQUIRE_CODE(state[ST_FAULT] != 0x46415531, BEAST_E_HIP,   // bpe_loop.hip LOOP_FAULT
-                     "beast_bpe_train: a k_merge_batch launch timed out waiting for its workgroups' decisions");
   const int n_log = state[ST_NMERGES];
   BEAST_REQUIRE_CODE(n_log < max_merges, BEAST_E_UNSUPPORTED,
                      "beast_bpe_train: merge log full; use the Python driver's host-driven loop");
