@@ -890,35 +890,14 @@ __device__ __forceinline__ uint32_t grp_min(uint32_t v) {   // every lane of the
   return v;
 }
 
-// The word's symbols move to the first n lanes of the group, in order (one forward permute).  The
-// live lanes below each lane come from v_mbcnt over the wave's ballot, rebased to the group with a
-// DPP row broadcast (row_newbcast) of its first lane's count: a handful of VALU ops, not the 64-bit
-// mask arithmetic per lane (k_bpe_words is VALU-issue bound, profiles/r04/encode_words_pmc_r04d.json)
+// The word's symbols move to the first n lanes of the group, in order (one forward permute).
 template <int GW>
 __device__ __forceinline__ uint32_t grp_compact(uint32_t sym, bool live, int gl, int gbase, int& n) {
   const unsigned long long bal = __ballot(live);
-  const uint32_t bw = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-  int below;
-#ifdef BPE_WORDS_OLD_COMPACT   // A/B only (round 5): the round-4 mask arithmetic
-  constexpr bool FAST = false;
-#else
-  constexpr bool FAST = true;
-#endif
-  if constexpr (FAST && GW == 64) {
-    below = (int)bw;
-    n = __popcll(bal);
-  } else if constexpr (FAST && GW == 16) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bw, 0x150, 0xF, 0xF, false);      // row_newbcast:0
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(bw + (live ? 1u : 0u)), 0x15F, 0xF, 0xF, false);  // :15
-    below = (int)(bw - lo);
-    n = (int)(hi - lo);
-  } else {
-    const unsigned long long gm = (bal >> gbase) & ((1ull << GW) - 1ull);
-    const unsigned long long bm = gl == 0 ? 0ull : (gm & ((1ull << gl) - 1ull));
-    n = __popcll(gm);
-    below = __popcll(bm);
-  }
-  const int dst = gbase + (live ? below : GW - 1);   // a dead lane only exists when n < GW
+  const unsigned long long gm = GW == 64 ? bal : ((bal >> gbase) & ((1ull << GW) - 1ull));
+  const unsigned long long below = gl == 0 ? 0ull : (gm & ((1ull << gl) - 1ull));
+  n = __popcll(gm);
+  const int dst = gbase + (live ? __popcll(below) : GW - 1);   // a dead lane only exists when n < GW
   const uint32_t got = (uint32_t)__builtin_amdgcn_ds_permute(dst * 4, (int)sym);
   return gl < n ? got : SYM_NONE;
 }

@@ -9,4 +9,3 @@ timeout -k 10 200 python -u tools/codec/words_ab.py 50 > gpurun_out/words_ab.jso
 grep -A1 '"auto' gpurun_out/words_ab.json | grep us_per_call
 timeout -k 10 200 python -u tools/codec/dw_phases.py gpurun_out/dw_phases.json > gpurun_out/dw_phases.log 2>&1 || exit 1
 python -c "import json; d=json.load(open('gpurun_out/dw_phases.json')); print(json.dumps({k: d[k] for k in ('phase_us_p50_p90_p99_max', 'task_us_per_wave_p50_max', 'tasks_per_wg', 'us_per_task_mean')}))"
-bash tools/codec/words_variants.sh r05c tools/ab/lib_oldcompact.so
