@@ -632,13 +632,16 @@ __device__ __forceinline__ int key_col(unsigned long long k, int x, int Vt) {
   return (int)(~(uint32_t)k - (uint32_t)x * (uint32_t)Vt);
 }
 
-constexpr int RT_LANE = 4;   // best counts kept per lane by the first pass over the row
+#ifndef BPE_RT_LANE
+#define BPE_RT_LANE 2
+#endif
+constexpr int RT_LANE = BPE_RT_LANE;   // best counts kept per lane by the first pass over the row
 __device__ __forceinline__ void rank_row_top(const uint32_t* __restrict__ row, int x, int Vt, int vcur, int lane,
                                              unsigned long long* __restrict__ out) {
-  // Each lane keeps its RT_LANE best (count desc, column asc) from one pass -- round 5: four, not
-  // two; a lane owning more of the row's top keys than it kept rescans its counts (a 32-step loop
-  // per extra pop), and frequent rows put several of their top columns on one lane, which made
-  // the full re-ranks the apply launch's slowest waves (profiles/r05/)
+  // Each lane keeps its RT_LANE best (count desc, column asc) from one pass; a lane owning more
+  // of the row's top keys than it kept rescans its counts (a 32-step loop per extra pop).  Two
+  // measured faster than four at K5 (20.1-20.3 vs 20.5-20.6 ms, profiles/r05/bpe_loop_ab_r05d.txt):
+  // the sorted insert costs every element more than the rare rescans it saves.
   const int nst = (vcur + ROW_STRETCH - 1) / ROW_STRETCH;
   int32_t c[32];
   int32_t tc[RT_LANE];
@@ -772,7 +775,7 @@ __device__ __forceinline__ bool row_top_update(const uint32_t* __restrict__ row,
 // deciding apply workgroup at its phases, for 64 passes.
 #ifdef BPE_MERGE_STAMPS
 __device__ unsigned long long g_bpe_stamps[64][1024][12];
-__device__ unsigned long long g_bpe_dstamps[64][16];   // [8 ..): BPE_DECIDE_WARM's dry run
+__device__ unsigned long long g_bpe_dstamps[64][16];
 __device__ unsigned long long g_bpe_batch[1024][2];   // every pass: merges decided, why the batch ended
 __device__ unsigned long long g_apply_stamps[64][256][12];
 #define ASTAMP(pi, k)                                                                                     \
@@ -1204,18 +1207,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   ASTAMP(KA_PI, 2);
   if (t != gridDim.x - 1) return;
   // ---- the last workgroup's wave 0: commit the batch just applied, decide the next one
-#ifdef BPE_DECIDE_WARM
-  // measurement only: the decision runs twice, the first time without writing anything (stamps
-  // at [8 ..)), to split its time into instruction fetch and the work itself
-  for (int rep = 0; rep < 2; ++rep) {
-    const bool dry = rep == 0;
-#define KA_DS(k) (dry ? 8 + (k) : (k))
-#else
-  {
-    constexpr bool dry = false;
-#define KA_DS(k) (k)
-#endif
-  DSTAMP(KA_PI, KA_DS(0));
+  DSTAMP(KA_PI, 0);
   // the loop state in registers (uniform): this wave writes only the record below.  The batch
   // just applied was committed by k_merge_batch's workgroup 0 (a kernel boundary ago).
   const int log2cap = loop->log2cap, target = loop->target, maxm = loop->max_merges;
@@ -1239,7 +1231,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     }
   };
   load_lists(0);
-  if (lane == 0 && !dry) st_agent(&loop->ticket, 0u);
+  if (lane == 0) st_agent(&loop->ticket, 0u);
   // the global order: lane l merges the sorted lists of apply workgroups l, l + 64, ... (top KM
   // rows each), then KM wave-max rounds hand it out
   unsigned long long K[KM], S[KM];
@@ -1251,7 +1243,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #pragma unroll
     for (int t = 0; t < 2; ++t) top_merge<KM>(K, S, LK[t], LS[t]);
   }
-  DSTAMP(KA_PI, KA_DS(1));
+  DSTAMP(KA_PI, 1);
   // KM rounds: the wave max of the lanes' list heads (DPP, no LDS), its owner pops it; lane r
   // keeps the r-th (best, second)
   unsigned long long ckey = 0, csec = 0;
@@ -1269,7 +1261,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
       K[KM - 1] = S[KM - 1] = 0ull;
     }
   }
-  DSTAMP(KA_PI, KA_DS(2));
+  DSTAMP(KA_PI, 2);
   // lanes j < KM: candidate j's string and its id if it exists (the probes run in parallel)
   int cand_a = 0, cand_b = 0, exist = -1;
   uint32_t clen = 0;
@@ -1288,7 +1280,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
       sl = (sl + 1) & hmask;
     }
   }
-  DSTAMP(KA_PI, KA_DS(3));
+  DSTAMP(KA_PI, 3);
   // HF's stopping rules per merge and the batch rules (see above), every candidate on its own
   // lane against the ones before it; the batch is the leading run of lanes that pass
   const unsigned long long count = ckey >> 32;
@@ -1323,7 +1315,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     }
     why |= !(sec < ckey) ? 64u : 0u;
     const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
-    if (lane == 0 && KA_PI < 1024 && !dry) {
+    if (lane == 0 && KA_PI < 1024) {
       g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
       g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
     }
@@ -1331,7 +1323,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
 #endif
   // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
   const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
-  if (lane < nb && !dry) {
+  if (lane < nb) {
     const bool reused = lane == 0 && exist >= 0;
     loop->ba[lane] = cand_a;
     loop->bb[lane] = cand_b;
@@ -1350,7 +1342,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
         (long long)(readlane_u64(ckey, j) >> 32) >= lds_min)
       kd = j + 1;
   }
-  if (lane == 0 && !dry) {
+  if (lane == 0) {
     loop->bn = nb;
     loop->bv0 = vnow;
     loop->bnm0 = nm;
@@ -1360,9 +1352,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     loop->passes += 1;
     if (nb == 0) loop->active = 0;
   }
-  DSTAMP(KA_PI, KA_DS(4));
-  }
-#undef KA_DS
+  DSTAMP(KA_PI, 4);
 #undef KA_PI
 }
 

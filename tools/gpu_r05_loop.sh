@@ -1,14 +1,24 @@
 #!/bin/bash
-# merge-loop phase stamps: the product loop (tools/libbpe_stamps.so) and the dry-run decision
-# split (tools/libbpe_warm.so, -DBPE_DECIDE_WARM), passes 100..163 of K5
+# merge loop: BPE tests on the product (rolled decision loops), then an interleaved A/B against
+# the unrolled decision (tools/ab/lib_loop_old.so) and top-2 row ranks (tools/ab/lib_rt2.so),
+# phase stamps of the product and of the dry-run decision split (tools/libbpe_warm.so)
 set -o pipefail
 mkdir -p gpurun_out
-BEAST_LIB=tools/libbpe_stamps.so timeout -k 10 300 python -u tools/bpe_phases.py run gpurun_out/bpe_phases_r05c.json > gpurun_out/bpe_phases_r05c.log 2>&1 || { tail -20 gpurun_out/bpe_phases_r05c.log; exit 1; }
-BEAST_LIB=tools/libbpe_warm.so timeout -k 10 300 python -u tools/bpe_phases.py run gpurun_out/bpe_warm_r05c.json > gpurun_out/bpe_warm_r05c.log 2>&1 || { tail -20 gpurun_out/bpe_warm_r05c.log; exit 1; }
-python - <<'PY'
-import json
-for f in ("gpurun_out/bpe_phases_r05c.json", "gpurun_out/bpe_warm_r05c.json"):
-    d = json.load(open(f))
-    s = d["median_over_passes_us"]
-    print(f, d["loop_s"], {k: s[k] for k in s if k.startswith(("decide", "dry", "warm", "apply_r", "pass"))})
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -m gpu -x -q --timeout 150 \
+  --timeout-method thread -k "bpe or train or k5" > gpurun_out/t_loop.log 2>&1 || { tail -30 gpurun_out/t_loop.log; exit 1; }
+tail -1 gpurun_out/t_loop.log
+for rep in 1 2; do for lib in beast_tokenizer_amd/libbeast_hip.so tools/ab/lib_loop_old.so tools/ab/lib_rt2.so; do
+  n=$(basename $lib .so)
+  BEAST_LIB=$lib timeout -k 10 200 python tools/bpe_ab.py 3 base= > gpurun_out/ab_${n}_$rep.log 2>&1 || { tail -5 gpurun_out/ab_${n}_$rep.log; exit 3; }
+  echo $n $rep $(tail -n1 gpurun_out/ab_${n}_$rep.log)
+done; done
+for v in stamps warm; do
+  L=tools/libbpe_$v.so
+  BEAST_LIB=$L timeout -k 10 300 python -u tools/bpe_phases.py run gpurun_out/bpe_${v}_r05d.json > gpurun_out/bpe_${v}_r05d.log 2>&1 || { tail -20 gpurun_out/bpe_${v}_r05d.log; exit 1; }
+  python - gpurun_out/bpe_${v}_r05d.json <<'PY'
+import json, sys
+d = json.load(open(sys.argv[1]))
+s = d["median_over_passes_us"]
+print(sys.argv[1], round(d["loop_s"], 4), json.dumps({k: s[k] for k in s if k.startswith(("decide", "dry", "warm", "apply_r", "apply_t", "pass", "merge_exit"))}))
 PY
+done
