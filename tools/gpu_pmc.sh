@@ -12,7 +12,7 @@ i=0
 while read -r group; do
   [ -z "$group" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-include-regex "k_encode_pipe|k_reconstruct" --pmc $group --kernel-trace --output-format csv -d "$OUT/p$i" -o run \
+  timeout -k 10 300 rocprofv3 --kernel-include-regex "k_encode|k_reconstruct" --pmc $group --kernel-trace --output-format csv -d "$OUT/p$i" -o run \
     -- python3 "$R/tools/pmc_codec.py" "$B" "$REPS" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done <<GROUPS
 ${PMC_GROUPS:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS
