@@ -1110,7 +1110,13 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   __syncthreads();   // every row's code points, word starts and symbols are readable workgroup-wide
   if (r < a.n_rows) BPE_STAMP(4);
   // 2. exact dedup; L.e[k] = the word's first occurrence (wave << 16 | word)
+#ifdef BPE_WORDS_SKIP_DEDUP   // counter attribution only (wrong ids): no dedup, sort or merges
+  if (r < a.n_rows && st == ST_OK)
+    for (int k = lane; k < nw; k += 64) { L.e[k] = (int32_t)(((uint32_t)wave << 16) | (uint32_t)k); L.vis[k] = 0; }
+  if (false) {
+#else
   if (r < a.n_rows && st == ST_OK) {
+#endif
     const uint32_t lmask = (uint32_t)lcap - 1u;
     for (int k = lane; k < nw; k += 64) {
       const int cs = L.wcp[k], ce = L.wcp[k + 1], len = ce - cs;
@@ -1167,10 +1173,16 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   const int t16 = nmid + (n9 - nmid + 3) / 4;
   const int tasks = t16 + (nd - n9 + 63) / 64;
   int nrounds = 0;
+#if defined(BPE_WORDS_SKIP_MERGES) || defined(BPE_WORDS_SKIP_DEDUP)   // counter attribution only (wrong ids)
+  if (r < a.n_rows && st == ST_OK)
+    for (int k = lane; k < nw; k += 64) L.vis[k] = 0;
+  for (int t = tasks; t < tasks;) {
+#else
   // tasks longest first, each wave taking the next one when it is done (an LDS counter): the
   // workgroup waits for its slowest wave at the barrier below (29.8 vs 33.0 us with tasks dealt
   // round-robin, profiles/r04/ab/encode_words_variants_r04d.txt)
   for (int t = wave; t < tasks;) {
+#endif
 #ifdef BPE_STAMPS
     const unsigned long long t_task0 = __builtin_amdgcn_s_memrealtime();
     const int kind_task = t < nmid ? 0 : (t < t16 ? 1 : 2);
