@@ -570,14 +570,28 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));    // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));    // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));    // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));    // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));   // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// The wave max of 64-bit keys (count << 32 | tie-break) as 32-bit DPP steps: the largest high word
+// first, then the largest low word among the lanes holding it -- one lane in the common case (a
+// readlane), a second 32-bit max only on ties.  Keys of count 0 are 0 in every caller.  K5 loop
+// 19.8 vs 19.9-20.0 ms with the 64-bit DPP form (profiles/r05/bpe_loop_ab_r05f.txt).
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-  v = umax64(v, dpp_u64<0x111, 0xF, true>(v));    // row_shr:1
-  v = umax64(v, dpp_u64<0x112, 0xF, true>(v));    // row_shr:2
-  v = umax64(v, dpp_u64<0x114, 0xF, true>(v));    // row_shr:4
-  v = umax64(v, dpp_u64<0x118, 0xF, true>(v));    // row_shr:8: lane 15 of a row holds its max
-  v = umax64(v, dpp_u64<0x142, 0xA, false>(v));   // row_bcast:15 into rows 1, 3
-  v = umax64(v, dpp_u64<0x143, 0xC, false>(v));   // row_bcast:31 into rows 2, 3
-  return readlane_u64(v, 63);
+  const uint32_t hi = (uint32_t)(v >> 32);
+  const uint32_t mh = wave_max_u32(hi);
+  const bool cand = hi == mh;
+  const unsigned long long b = __ballot(cand);
+  const uint32_t lo = cand ? (uint32_t)v : 0u;
+  const uint32_t ml = __popcll(b) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)__builtin_ctzll(b))
+                                       : wave_max_u32(lo);
+  return ((unsigned long long)mh << 32) | ml;
 }
 
 // Two descending (key, second) lists of KM -> the top KM of both, descending: the elementwise
@@ -847,34 +861,6 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   // the LDS delta vectors cleared whole while the record is in flight (16-byte stores)
   for (int i = threadIdx.x; i < BATCH_LDS / 16; i += 256) reinterpret_cast<int4*>(dl)[i] = make_int4(0, 0, 0, 0);
   if (n == 0) return;   // the loop has stopped (uniform)
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
-    // commit the batch, merge j on lane j: its string into the hash table (distinct strings, so
-    // concurrent inserts only race for free slots), the new token's hash / P^len / length, its log
-    // entry; then the counters.  No other workgroup of this launch reads what this writes: they
-    // take the vocabulary before the batch from bv0 and the new tokens' lengths from the record.
-    const int j = threadIdx.x;
-    if (j < n) {
-      const int reused = loop->breused[j];
-      if (!reused) {
-        const unsigned long long h = loop->bh[j];
-        const unsigned long long pa = lh.tp[ra], pb = lh.tp[rb];
-        const uint64_t hmask = (1ull << loop->log2cap) - 1;
-        uint64_t sl = loop_slot(h, rl, loop->log2cap);
-        while (atomicCAS(&lh.lid[sl], LOOP_EMPTY, lid_of(rl, rn)) != LOOP_EMPTY) sl = (sl + 1) & hmask;
-        lh.key[sl] = h;
-        lh.th[rn] = h;
-        lh.tp[rn] = pa * pb;
-        tlen[rn] = rl;
-      }
-      int32_t* lg = lh.log + 4 * (int64_t)(nm0 + j);
-      lg[0] = ra; lg[1] = rb; lg[2] = rn; lg[3] = reused;
-    }
-    if (j == 0) {
-      loop->n_merges = nm0 + n;
-      loop->vcur = loop->bvcur;
-      loop->maxtlen = mt;
-    }
-  }
   if (threadIdx.x < BK) {
     s_a[threadIdx.x] = ra;
     s_b[threadIdx.x] = rb;
@@ -1030,21 +1016,54 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
   MSTAMP(KB_PI, 3);
   if (apps != nullptr && threadIdx.x < n && s_apps[threadIdx.x])
     atomicAdd(&apps[nm0 + threadIdx.x], s_apps[threadIdx.x]);
-  if (kd == 0) { MSTAMP(KB_PI, 4); return; }
-  if (any) touched = 1;
-  __syncthreads();
-  if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> the table (or the delta vectors)
-    for (int i = threadIdx.x; i < nl; i += 256) {
-      const int32_t v = dl[i];
-      if (v) {
-        const int jk = i / stride;
-        const int j = jk >> 2;
-        BatchOp op = op_of(j);
-        op.dl = nullptr;
-        op.table_add(jk & 3, (uint32_t)(i - jk * stride), v);
+  if (kd > 0) {
+    if (any) touched = 1;
+    __syncthreads();
+    if (touched)   // LDS entry i = (j * 4 + kind) * stride + x -> the table (or the delta vectors)
+      for (int i = threadIdx.x; i < nl; i += 256) {
+        const int32_t v = dl[i];
+        if (v) {
+          const int jk = i / stride;
+          const int j = jk >> 2;
+          BatchOp op = op_of(j);
+          op.dl = nullptr;
+          op.table_add(jk & 3, (uint32_t)(i - jk * stride), v);
+        }
       }
-    }
+  }
   MSTAMP(KB_PI, 4);
+  // the commit last (round 5): its compare-and-swap round trips no longer hold workgroup 0's scan,
+  // which made it one of the pass's last workgroups (profiles/r05/bpe_phases_r05a.json, raw; 19.8
+  // vs 19.8-19.9 ms, profiles/r05/bpe_loop_ab_r05f.txt)
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // commit the batch, merge j on lane j: its string into the hash table (distinct strings, so
+    // concurrent inserts only race for free slots), the new token's hash / P^len / length, its log
+    // entry; then the counters.  No other workgroup of this launch reads what this writes: they
+    // take the vocabulary before the batch from bv0 and the new tokens' lengths from the record.
+    const int j = threadIdx.x;
+    if (j < n) {
+      const int reused = loop->breused[j];
+      if (!reused) {
+        const unsigned long long h = loop->bh[j];
+        const unsigned long long pa = lh.tp[ra], pb = lh.tp[rb];
+        const uint64_t hmask = (1ull << loop->log2cap) - 1;
+        uint64_t sl = loop_slot(h, rl, loop->log2cap);
+        while (atomicCAS(&lh.lid[sl], LOOP_EMPTY, lid_of(rl, rn)) != LOOP_EMPTY) sl = (sl + 1) & hmask;
+        lh.key[sl] = h;
+        lh.th[rn] = h;
+        lh.tp[rn] = pa * pb;
+        tlen[rn] = rl;
+      }
+      int32_t* lg = lh.log + 4 * (int64_t)(nm0 + j);
+      lg[0] = ra; lg[1] = rb; lg[2] = rn; lg[3] = reused;
+    }
+    if (j == 0) {
+      loop->n_merges = nm0 + n;
+      loop->vcur = loop->bvcur;
+      loop->maxtlen = mt;
+    }
+  }
+
 #undef KB_PI
 }
 
