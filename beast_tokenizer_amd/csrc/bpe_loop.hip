@@ -1320,26 +1320,7 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
   ok &= sec < ckey;   // a taken row's second-best would come first
   const unsigned long long pass = __ballot(ok);
   const int nb = (int)__builtin_ctzll(~pass);   // leading lanes that pass (<= KM)
-#ifdef BPE_MERGE_STAMPS
-  {   // why the batch ended: the first failing lane's rules (bit 0 list end, 1 HF stop, 2 re-use,
-      // 3 after a self-pair / re-use, 4 chaining, 5 same string, 6 a taken row's bound)
-    uint32_t why = lane >= KM ? 1u : 0u;
-    why |= !(count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm) ? 2u : 0u;
-    why |= lane > 0 && exist >= 0 ? 4u : 0u;
-    for (int i = 0; i < KM - 1 && i < lane; ++i) {
-      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
-      why |= ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0) ? 8u : 0u;
-      why |= cand_b == ai || cand_a == bi ? 16u : 0u;
-      why |= ch == readlane_u64(ch, i) && clen == (uint32_t)__builtin_amdgcn_readlane((int)clen, i) ? 32u : 0u;
-    }
-    why |= !(sec < ckey) ? 64u : 0u;
-    const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
-    if (lane == 0 && KA_PI < 1024) {
-      g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
-      g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
-    }
-  }
-#endif
+  DSTAMP(KA_PI, 5);   // rules and ballot done
   // a re-used id ends the batch at its first merge, so the new ids are vnow, vnow + 1, ...
   const int reused0 = nb > 0 && __builtin_amdgcn_readlane(exist, 0) >= 0;
   if (lane < nb) {
@@ -1372,6 +1353,26 @@ __global__ __launch_bounds__(64 * APPLY_ROWS) void k_apply_batch(uint32_t* __res
     if (nb == 0) loop->active = 0;
   }
   DSTAMP(KA_PI, 4);
+#ifdef BPE_MERGE_STAMPS
+  {   // why the batch ended (after the last stamp: tools only): the first failing lane's rules (bit 0 list end, 1 HF stop, 2 re-use,
+      // 3 after a self-pair / re-use, 4 chaining, 5 same string, 6 a taken row's bound)
+    uint32_t why = lane >= KM ? 1u : 0u;
+    why |= !(count >= 1 && count >= minf && vnow + lane < target && nm + lane < maxm) ? 2u : 0u;
+    why |= lane > 0 && exist >= 0 ? 4u : 0u;
+    for (int i = 0; i < KM - 1 && i < lane; ++i) {
+      const int ai = __builtin_amdgcn_readlane(cand_a, i), bi = __builtin_amdgcn_readlane(cand_b, i);
+      why |= ai == bi || (i == 0 && __builtin_amdgcn_readlane(exist, 0) >= 0) ? 8u : 0u;
+      why |= cand_b == ai || cand_a == bi ? 16u : 0u;
+      why |= ch == readlane_u64(ch, i) && clen == (uint32_t)__builtin_amdgcn_readlane((int)clen, i) ? 32u : 0u;
+    }
+    why |= !(sec < ckey) ? 64u : 0u;
+    const uint32_t w_nb = (uint32_t)__builtin_amdgcn_readlane((int)why, nb < 64 ? nb : 63);
+    if (lane == 0 && KA_PI < 1024) {
+      g_bpe_batch[KA_PI][0] = (unsigned long long)nb;
+      g_bpe_batch[KA_PI][1] = nb < KM ? w_nb : 1u;
+    }
+  }
+#endif
 #undef KA_PI
 }
 

@@ -134,6 +134,8 @@ def run(out_json=None) -> None:
         if d[0] > 0:
             rec.update({"decide_start": us(d[0] - t0), "decide_lists_merged": us(d[1] - t0),
                         "decide_rounds": us(d[2] - t0), "decide_probed": us(d[3] - t0), "decide_end": us(d[4] - t0)})
+            if d[5] > 0:   # rules + ballot done, before the batch record is written
+                rec["decide_ruled"] = us(d[5] - t0)
         if d[8] > 0:   # -DBPE_DECIDE_WARM: the dry first run of the same decision (times from its start)
             rec.update({"dry_lists_merged": us(d[9] - d[8]), "dry_rounds": us(d[10] - d[8]),
                         "dry_probed": us(d[11] - d[8]), "dry_end": us(d[12] - d[8]),
