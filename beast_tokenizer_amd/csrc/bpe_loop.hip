@@ -490,10 +490,17 @@ __device__ __forceinline__ uint64_t loop_slot(unsigned long long h, uint32_t len
 
 constexpr int KR = 4;   // candidate pairs per table row: its KR best, in HF order
 // Each row's cached keys: rowtop[x][0 .. RT_K) descending (0 past them) are exactly the row's keys
-// >= rowtop[x][RT_F] (the floor; 1 when they are all its positive keys).  A batch changes a row
+// >= rowtop[x][RT_F] (the floor; 1 when they are all its positive keys).  RT_K = 8 (round 5): a
+// full re-rank runs RT_K wave-max rounds, and 8 keys measured faster at K5 than 6, 10, 12 or 14
+// (19.5 vs 19.5-20.2 ms, profiles/r05/bpe_loop_ab_rtk_r05k.txt) -- fewer rounds per re-rank
+// against re-ranks a little more often.  A batch changes a row
 // outside b_j / new_j only at known columns, so re-reading those keeps the invariant; the row is
 // re-ranked in full only when fewer than KR + 1 keys stay above a floor > 1.
-constexpr int RT_K = 12, RT_F = 15, RT_STRIDE = 16;
+#ifndef BPE_RT_K
+#define BPE_RT_K 8
+#endif
+constexpr int RT_K = BPE_RT_K, RT_F = 15, RT_STRIDE = 16;
+static_assert(RT_K < RT_F, "the floor's slot follows the cached keys");
 struct BatchWs {
   unsigned long long* rowtop;         // [Vt][RT_STRIDE]: the row caches above
   unsigned long long* wgkey;          // [BK][nwg] each apply workgroup's BK best candidates, best first (k-major:
