@@ -194,6 +194,9 @@ __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2
     uint32_t lv = nid, rv = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < MERGE_REG; ++k) {
+      // past every active lane's word the registers hold the sentinel rv starts with: stop there
+      // (round 5: the chains ran all MERGE_REG positions for words of ~8 symbols)
+      WORD_SWEEP_EXIT(k, L);
       lv = k + 1 == i ? v[k] : lv;
       rv = k == i + 2 ? v[k] : rv;
     }
