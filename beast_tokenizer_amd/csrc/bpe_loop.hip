@@ -128,17 +128,19 @@ __device__ __forceinline__ uint32_t merge_global(uint16_t* __restrict__ s, uint3
 __device__ __forceinline__ void load_word(const uint16_t* __restrict__ s, uint32_t L, uint32_t (&v)[MERGE_REG + 2]) {
   const uint2* __restrict__ p = reinterpret_cast<const uint2*>(s);
 #pragma unroll
+  for (int i = 0; i < MERGE_REG + 2; ++i) v[i] = 0xFFFFFFFFu;   // the sentinel everywhere first
+  // then the units some active lane's word reaches, its positions past L kept at the sentinel (the
+  // padding of a word's last unit is zero, a valid id): no select over all MERGE_REG positions
+#pragma unroll
   for (int q = 0; q < MERGE_REG / 4; ++q) {
+    if (__builtin_amdgcn_ballot_w64((uint32_t)(4 * q) < L) == 0ull) break;
     uint2 u = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
     if ((uint32_t)(4 * q) < L) u = p[q];
-    v[4 * q] = u.x & 0xFFFFu;
-    v[4 * q + 1] = u.x >> 16;
-    v[4 * q + 2] = u.y & 0xFFFFu;
-    v[4 * q + 3] = u.y >> 16;
+    v[4 * q] = (uint32_t)(4 * q) < L ? (u.x & 0xFFFFu) : 0xFFFFFFFFu;
+    v[4 * q + 1] = (uint32_t)(4 * q + 1) < L ? (u.x >> 16) : 0xFFFFFFFFu;
+    v[4 * q + 2] = (uint32_t)(4 * q + 2) < L ? (u.y & 0xFFFFu) : 0xFFFFFFFFu;
+    v[4 * q + 3] = (uint32_t)(4 * q + 3) < L ? (u.y >> 16) : 0xFFFFFFFFu;
   }
-#pragma unroll
-  for (int i = 0; i < MERGE_REG; ++i) v[i] = (uint32_t)i < L ? v[i] : 0xFFFFFFFFu;
-  v[MERGE_REG] = v[MERGE_REG + 1] = 0xFFFFFFFFu;
 }
 // Wave-uniform exit from the unrolled sweeps once no active lane's word reaches position i.
 #define WORD_SWEEP_EXIT(i, L)                                                                  \
