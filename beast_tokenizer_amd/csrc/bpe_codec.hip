@@ -1167,11 +1167,16 @@ __global__ __launch_bounds__(64 * DW_WAVES) void k_bpe_words(EncArgs a, WordMap 
   // rows) by dw_merge_word's cooperative rounds; words of <= 8 one per lane, 64 to a task
   // (dw_merge_lane: its select chains stay short, and the tiny words are most of them)
   // the cursor of length 17 has passed every longer word, that of length 9 every word of 9 or
-  // more (clamped: the task count bounds the loop below, so it never exceeds the word count)
-  const int nmid = min(max(s_hist[DW_SHORT + 1], 0), nd);
-  const int n9 = min(max(s_hist[DW_TINY + 1], nmid), nd);
+  // more.  Cursors out of order would be a corrupt sort: the workgroup's rows then report
+  // ST_FALLBACK (the host re-encodes them with the per-row kernel) and no task runs, instead of a
+  // clamp quietly merging whatever the cursors point at (round 5)
+  const int c17 = s_hist[DW_SHORT + 1], c9 = s_hist[DW_TINY + 1];
+  const bool sane = 0 <= c17 && c17 <= c9 && c9 <= nd;
+  if (!sane && st == ST_OK) st = ST_FALLBACK;
+  const int nmid = sane ? c17 : 0;
+  const int n9 = sane ? c9 : 0;
   const int t16 = nmid + (n9 - nmid + 3) / 4;
-  const int tasks = t16 + (nd - n9 + 63) / 64;
+  const int tasks = sane ? t16 + (nd - n9 + 63) / 64 : 0;
   int nrounds = 0;
 #if defined(BPE_WORDS_SKIP_MERGES) || defined(BPE_WORDS_SKIP_DEDUP)   // counter attribution only (wrong ids)
   if (r < a.n_rows && st == ST_OK)
