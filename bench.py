@@ -596,7 +596,16 @@ def hf_bpe_same_sample(rows: torch.Tensor, vocab: int):
         full = {k: fk.get(k) for k in ("merges_per_s", "hf_seconds", "merges", "tokens", "rayon_threads",
                                        "container_cpus", "hf_version")}
         full["source"] = os.path.relpath(fp, REPO)
+    box = []   # the same full-size HF run on the GPU box's host at two thread counts (tools/hf_k5_container.py)
+    for t in (16, 64):
+        fb = os.path.join(REPO, "profiles", "r05", f"hf_k5_box_t{t}.json")
+        if os.path.exists(fb):
+            with open(fb) as f:
+                fk = json.load(f)
+            box.append({k: fk.get(k) for k in ("merges_per_s", "hf_seconds", "rayon_threads")} |
+                       {"source": os.path.relpath(fb, REPO)})
     return {"value": nm / el, "unit": "merges/s", "kind": "reference", "full_k5_container": full,
+            "full_k5_box_host": box,
             "cores": int(os.environ.get("RAYON_NUM_THREADS", "1")),
             "gpu_same_sample_merges_per_s": len(g.merges) / el_gpu, "gpu_same_sample_s": el_gpu,
             "hf_seconds": el, "merges_equal": bool(same),
