@@ -96,6 +96,17 @@ SIGNATURES = {
                                      _i32, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp]),
     "beast_bpe_train": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _sz, _vp,
                                _i32, _vp, _vp, _i32, _vp, _vp]),
+    "beast_comm_id_bytes": (_sz, []),
+    "beast_comm_unique_id": (_i32, [_vp]),
+    "beast_comm_init_rank": (_i32, [_i32, _i32, _vp, _i32, _vp]),
+    "beast_comm_init": (_i32, [_i32, _vp, _vp]),
+    "beast_comm_destroy": (_i32, [_vp]),
+    "beast_comm_info": (_i32, [_vp, _vp, _vp, _vp]),
+    "beast_comm_allreduce": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp]),
+    "beast_comm_allgather": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "beast_comm_allgatherv": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "beast_bpe_train_comm": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _sz, _vp,
+                                    _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
     "beast_bpe_wordmap_log2buckets": (_i32, [_i32]),
     "beast_bpe_wordmap_bytes": (_sz, [_i32]),
     "beast_bpe_wordmap_build_host": (_i32, [_vp, _vp, _vp, _i32, _vp, _sz, _vp]),

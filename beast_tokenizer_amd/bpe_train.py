@@ -640,15 +640,26 @@ def fixed_rows_to_device(tokens: torch.Tensor) -> Tuple[torch.Tensor, torch.Tens
 
 def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
                    special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
-                   vocab_bytes_cap: Optional[int] = None) -> BPEResult:
+                   vocab_bytes_cap: Optional[int] = None, comm=None) -> BPEResult:
     """The same training through the one-call C-ABI ``beast_bpe_train`` (include/beast_hip.h):
-    what a non-Python caller binds.  Single GPU; raises NotImplementedError where the C entry
-    point defers to this module's driver (Vt > 4096, a string-hash collision)."""
+    what a non-Python caller binds.  ``comm`` (a :class:`beast_tokenizer_amd.comm.Communicator`)
+    trains over every rank's shard with ``beast_bpe_train_comm`` (the replicated form: one
+    all-gather of the distinct words, every rank returns the same result).  Raises
+    NotImplementedError where the C entry point defers to this module's driver (Vt > 4096, a
+    string-hash collision)."""
     import ctypes
     dev = tokens.device
     _lib.require_gpu(tokens, "tokens")
     n_seq = seq_off.numel() - 1
-    mm = torch.stack([tokens.min(), tokens.max()]).tolist() if tokens.numel() else [0, -1]
+    if comm is not None:   # the class LUT must cover the corpus's range, not this shard's
+        big = 2 ** 62
+        lo_nhi = torch.tensor([int(tokens.min()) if tokens.numel() else big,
+                               -int(tokens.max()) if tokens.numel() else big], dtype=torch.int64, device=dev)
+        comm.allreduce(lo_nhi, "min")
+        lo, nhi = lo_nhi.tolist()
+        mm = [lo, -nhi] if lo != big else [0, -1]
+    else:
+        mm = torch.stack([tokens.min(), tokens.max()]).tolist() if tokens.numel() else [0, -1]
     lut = torch.from_numpy(np.ascontiguousarray(class_lut(max(int(mm[1]) - int(mm[0]) + 1, 1)))).to(dev)
     n_base_max = 512 + len(special_tokens) + max(int(mm[1]) - int(mm[0]) + 1, 0)
     max_vocab = max(vocab_size, n_base_max)
@@ -661,11 +672,14 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
     specs = [t.encode("utf-8") for t in special_tokens]
     sarr = (ctypes.c_char_p * max(len(specs), 1))(*specs)
     for attempt in range(2):
-        rc = _lib.call("beast_bpe_train", tokens.data_ptr(), seq_off.data_ptr(), n_seq, lut.data_ptr(), lut.numel(),
-                       int(vocab_size), int(min_frequency), int(max_token_length or 0), sarr, len(specs),
-                       ctypes.byref(out[0]), ctypes.byref(out[1]), vbytes.ctypes.data, vbytes.nbytes,
-                       voff.ctypes.data, max_vocab, ctypes.byref(out[2]), merges.ctypes.data, merges.size // 2,
-                       ctypes.byref(out[3]), _lib.stream_of(dev))
+        args = (tokens.data_ptr(), seq_off.data_ptr(), n_seq, lut.data_ptr(), lut.numel(), int(vocab_size),
+                int(min_frequency), int(max_token_length or 0), sarr, len(specs), ctypes.byref(out[0]),
+                ctypes.byref(out[1]), vbytes.ctypes.data, vbytes.nbytes, voff.ctypes.data, max_vocab,
+                ctypes.byref(out[2]), merges.ctypes.data, merges.size // 2, ctypes.byref(out[3]))
+        if comm is None:
+            rc = _lib.call("beast_bpe_train", *args, _lib.stream_of(dev))
+        else:
+            rc = _lib.call("beast_bpe_train_comm", *args, comm.handle, _lib.stream_of(dev))
         if rc != _lib.BEAST_E_WORKSPACE or attempt:
             _lib.check(rc, "beast_bpe_train")
             break
@@ -679,4 +693,5 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
     id2str = [bytes(vbytes[voff[i]:voff[i + 1]]).decode("utf-8") for i in range(nv)]
     pairs = [(id2str[int(merges[2 * m])], id2str[int(merges[2 * m + 1])]) for m in range(nm)]
     return BPEResult(vocab={t: i for i, t in enumerate(id2str)}, merges=pairs, min_token=out[0].value,
-                     max_token=out[1].value, stats={"capi": True, "n_merges": nm, "retried": retried})
+                     max_token=out[1].value, stats={"capi": True, "n_merges": nm, "retried": retried,
+                                                    "world": comm.world if comm is not None else 1})

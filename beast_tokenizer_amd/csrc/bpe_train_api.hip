@@ -7,9 +7,11 @@
 // chars by code point), pre-tokenisation (count, scan, emit), distinct words x counts, the
 // length-ordered repack + word signatures, the pair table, then the device-driven batched
 // merge loop with two chunks of passes in flight, and the host replay of its merge log against
-// the real strings.  Single device, Vt <= 4,096 (the batched loop); a 64-bit string-hash
-// collision or a full merge log comes back BEAST_E_UNSUPPORTED (the Python driver then reruns
-// on its host-driven loop).
+// the real strings.  Vt <= 4,096 (the batched loop); a 64-bit string-hash collision or a full
+// merge log comes back BEAST_E_UNSUPPORTED (the Python driver then reruns on its host-driven
+// loop).  beast_bpe_train_comm is the same over several GPUs with the library's communicator
+// (comm.hip): bpe_train.py's replicated form -- the range and presence all-reduced, the shards'
+// distinct words all-gathered once, the loop run on the union on every rank.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -94,12 +96,144 @@ constexpr int KMAX = 8, CHUNK = 64;
   BEAST_REQUIRE_CODE(var != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of %zu x %zu bytes failed", \
                      (size_t)(n), sizeof(T))
 
-extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
-                               int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
-                               const char* const* special_tokens, int n_special, int64_t* out_min_token,
-                               int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
-                               int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
-                               int max_merges_out, int* out_n_merges, void* stream) {
+namespace {
+
+// rank r's word starts index its own symbols: shift them by where its symbols land in the union
+__global__ void k_offset_starts(uint32_t* __restrict__ w, int64_t n, uint32_t off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) w[i] += off;
+}
+
+// this shard's words: pre-tokenisation (count, scan, emit), the distinct words x counts (the
+// table grows 4x while it overflows) and their length-ordered repack
+int shard_words(DevMem& mem, const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, int64_t mn,
+                const uint8_t* cls_lut, int64_t lut_n, const uint16_t* byte2id, uint16_t*& sym2, uint32_t*& w2,
+                uint32_t*& l2, uint32_t*& c2, int64_t& nu, int64_t& nsp, hipStream_t s) {
+  void* stream = s;
+  ALLOC(wps, int64_t, n_seq);
+  ALLOC(sps, int64_t, n_seq);
+  TRY(beast_bpe_pretok_count(tokens, seq_off, n_seq, mn, cls_lut, lut_n, wps, sps, stream));
+  ALLOC(scan_ws, uint8_t, beast_scan_workspace_bytes(n_seq));
+  ALLOC(woff, int64_t, n_seq + 1);
+  ALLOC(soff, int64_t, n_seq + 1);
+  TRY(beast_exclusive_scan_i64(wps, woff, n_seq, scan_ws, stream));
+  TRY(beast_exclusive_scan_i64(sps, soff, n_seq, scan_ws, stream));
+  int64_t nw = 0, ns = 0;
+  BEAST_HIP(hipMemcpyAsync(&nw, woff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "word count read");
+  BEAST_HIP(hipMemcpyAsync(&ns, soff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "symbol count read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  BEAST_REQUIRE_CODE(ns < (int64_t(1) << 32), BEAST_E_UNSUPPORTED,
+                     "BPE corpus has >= 2^32 byte symbols on one GPU; shard it over more ranks");
+  ALLOC(b2i_d, uint16_t, 256);
+  BEAST_HIP(hipMemcpyAsync(b2i_d, byte2id, 256 * sizeof(uint16_t), hipMemcpyHostToDevice, s), "byte2id upload");
+  ALLOC(sym, uint16_t, ns);
+  ALLOC(wstart, uint32_t, nw);
+  ALLOC(wlen, uint32_t, nw);
+  TRY(beast_bpe_pretok_emit(tokens, seq_off, n_seq, mn, cls_lut, lut_n, woff, soff, b2i_d, sym, wstart, wlen, stream));
+  ALLOC(ow, uint32_t, nw);
+  ALLOC(ol, uint32_t, nw);
+  ALLOC(oc, uint32_t, nw);
+  ALLOC(on, int64_t, 1);
+  nu = -1;
+  for (size_t nbytes = beast_bpe_dedup_workspace_bytes(nw); nu < 0; nbytes *= 4) {
+    void* dws = nullptr;
+    BEAST_HIP(hipMalloc(&dws, nbytes), "dedup workspace");
+    const int rc = beast_bpe_dedup_words(sym, wstart, wlen, nw, dws, nbytes, ow, ol, oc, on, stream);
+    if (rc == BEAST_OK) {
+      const hipError_t e1 = hipMemcpyAsync(&nu, on, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+      const hipError_t e2 = hipStreamSynchronize(s);
+      (void)hipFree(dws);
+      BEAST_HIP(e1, "distinct count read");
+      BEAST_HIP(e2, "stream sync");
+    } else {
+      (void)hipFree(dws);
+      return rc;
+    }
+  }
+  ALLOC(rp_ws, uint8_t, beast_bpe_repack_workspace_bytes(nu));
+  sym2 = mem.get<uint16_t>(ns + 3 * nu);   // spans rounded up to 4
+  w2 = mem.get<uint32_t>(nu);
+  l2 = mem.get<uint32_t>(nu);
+  c2 = mem.get<uint32_t>(nu);
+  BEAST_REQUIRE_CODE(sym2 && w2 && l2 && c2, BEAST_E_HIP, "beast_bpe_train: hipMalloc of the repacked words failed");
+  TRY(beast_bpe_repack_words(sym, ow, ol, oc, nu, rp_ws, beast_bpe_repack_workspace_bytes(nu), sym2, w2, l2, c2, on,
+                             stream));
+  BEAST_HIP(hipMemcpyAsync(&nsp, on, sizeof(int64_t), hipMemcpyDeviceToHost, s), "symbol count read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  return BEAST_OK;
+}
+
+// every rank's distinct words x counts on every rank, in rank order, repacked for the loop
+// (bpe_train.py GpuBpeOps.gather_words): one all-gather of the sizes, then one all-gather-v per
+// array.  A word repeated across shards appears once per shard with its shard count, which
+// leaves every pair count (and so every merge) unchanged.
+int union_words(DevMem& mem, beast_comm* comm, uint16_t*& sym2, uint32_t*& w2, uint32_t*& l2, uint32_t*& c2,
+                int64_t& nu, int64_t& nsp, hipStream_t s) {
+  void* stream = s;
+  int world = 0, rank = 0;
+  TRY(beast_comm_info(comm, &world, &rank, nullptr));
+  ALLOC(sz, int64_t, 2 + 2 * (size_t)world);
+  const int64_t mine[2] = {nu, nsp};
+  BEAST_HIP(hipMemcpyAsync(sz, mine, sizeof(mine), hipMemcpyHostToDevice, s), "size upload");
+  TRY(beast_comm_allgather(comm, sz, sz + 2, 2, BEAST_DT_I64, stream));
+  std::vector<int64_t> all(2 * (size_t)world);
+  BEAST_HIP(hipMemcpyAsync(all.data(), sz + 2, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s), "size read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  std::vector<int64_t> wc(world), wd(world), bc(world), bd(world);   // words; symbol bytes
+  int64_t NU = 0, NS = 0;
+  for (int r = 0; r < world; ++r) {
+    wc[r] = all[2 * r];
+    wd[r] = NU;
+    bc[r] = 2 * all[2 * r + 1];
+    bd[r] = 2 * NS;
+    NU += all[2 * r];
+    NS += all[2 * r + 1];
+  }
+  BEAST_REQUIRE_CODE(NS + 3 * NU < (int64_t(1) << 32), BEAST_E_UNSUPPORTED,
+                     "beast_bpe_train: the shards' distinct words hold >= 2^32 symbols; the replicated loop keeps them on "
+                     "every GPU");
+  if (NU == 0) {
+    sym2 = nullptr;
+    nu = nsp = 0;
+    return BEAST_OK;
+  }
+  ALLOC(gsym, uint16_t, NS);
+  ALLOC(gw, uint32_t, NU);
+  ALLOC(gl, uint32_t, NU);
+  ALLOC(gc, uint32_t, NU);
+  TRY(beast_comm_allgatherv(comm, sym2, gsym, bc.data(), bd.data(), BEAST_DT_U8, stream));
+  TRY(beast_comm_allgatherv(comm, w2, gw, wc.data(), wd.data(), BEAST_DT_U32, stream));
+  TRY(beast_comm_allgatherv(comm, l2, gl, wc.data(), wd.data(), BEAST_DT_U32, stream));
+  TRY(beast_comm_allgatherv(comm, c2, gc, wc.data(), wd.data(), BEAST_DT_U32, stream));
+  for (int r = 0; r < world; ++r)
+    if (wc[r] > 0 && bd[r] > 0) {
+      hipLaunchKernelGGL(k_offset_starts, dim3((unsigned)((wc[r] + 255) / 256)), dim3(256), 0, s, gw + wd[r], wc[r],
+                         (uint32_t)(bd[r] / 2));
+      BEAST_LAUNCHED("k_offset_starts");
+    }
+  const size_t rp_bytes = beast_bpe_repack_workspace_bytes(NU);
+  ALLOC(rp_ws, uint8_t, rp_bytes);
+  ALLOC(on, int64_t, 1);
+  sym2 = mem.get<uint16_t>(NS + 3 * NU);   // spans rounded up to 4
+  w2 = mem.get<uint32_t>(NU);
+  l2 = mem.get<uint32_t>(NU);
+  c2 = mem.get<uint32_t>(NU);
+  BEAST_REQUIRE_CODE(sym2 && w2 && l2 && c2, BEAST_E_HIP, "beast_bpe_train: hipMalloc of the union's words failed");
+  TRY(beast_bpe_repack_words(gsym, gw, gl, gc, NU, rp_ws, rp_bytes, sym2, w2, l2, c2, on, stream));
+  BEAST_HIP(hipMemcpyAsync(&nsp, on, sizeof(int64_t), hipMemcpyDeviceToHost, s), "symbol count read");
+  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  nu = NU;
+  return BEAST_OK;
+}
+
+}  // namespace
+
+static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                          int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                          const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                          int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
+                          int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
+                          int max_merges_out, int* out_n_merges, beast_comm* comm, void* stream) {
   BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
                     out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
                 "beast_bpe_train: null pointer argument");
@@ -109,15 +243,38 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
   int64_t n_tok = 0;
   BEAST_HIP(hipMemcpyAsync(&n_tok, seq_off + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "seq_off read");
   BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  BEAST_REQUIRE(n_tok > 0, "No non-empty sequences provided for BPE training.");   // reference :84-85
-  BEAST_REQUIRE(tokens != nullptr, "beast_bpe_train: null pointer argument");
+  BEAST_REQUIRE(n_tok >= 0 && (n_tok == 0 || tokens != nullptr), "beast_bpe_train: null pointer argument");
+  // with a communicator: the shards' token count, range and code points are the corpus's
+  ALLOC(red, int64_t, 2);
+  if (comm != nullptr) {
+    BEAST_HIP(hipMemcpyAsync(red, &n_tok, sizeof(int64_t), hipMemcpyHostToDevice, s), "token count upload");
+    TRY(beast_comm_allreduce(comm, red, red, 1, BEAST_DT_I64, BEAST_OP_SUM, stream));
+    int64_t total = 0;
+    BEAST_HIP(hipMemcpyAsync(&total, red, sizeof(int64_t), hipMemcpyDeviceToHost, s), "token count read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    BEAST_REQUIRE(total > 0, "No non-empty sequences provided for BPE training.");   // reference :84-85
+  } else {
+    BEAST_REQUIRE(n_tok > 0, "No non-empty sequences provided for BPE training.");   // reference :84-85
+  }
 
   // ---- min / max (reference :86-87), the code points present
-  ALLOC(mm, int64_t, 2);
-  TRY(beast_i64_minmax(tokens, n_tok, mm, stream));
-  int64_t mmh[2];
-  BEAST_HIP(hipMemcpyAsync(mmh, mm, sizeof(mmh), hipMemcpyDeviceToHost, s), "minmax read");
-  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  constexpr int64_t NONE = int64_t(1) << 62;   // an empty shard's (min, -max)
+  int64_t mmh[2] = {NONE, -NONE};
+  if (n_tok > 0) {
+    ALLOC(mm, int64_t, 2);
+    TRY(beast_i64_minmax(tokens, n_tok, mm, stream));
+    BEAST_HIP(hipMemcpyAsync(mmh, mm, sizeof(mmh), hipMemcpyDeviceToHost, s), "minmax read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  }
+  if (comm != nullptr) {   // one MIN over (min, -max)
+    int64_t lo_nhi[2] = {mmh[0], -mmh[1]};
+    BEAST_HIP(hipMemcpyAsync(red, lo_nhi, sizeof(lo_nhi), hipMemcpyHostToDevice, s), "range upload");
+    TRY(beast_comm_allreduce(comm, red, red, 2, BEAST_DT_I64, BEAST_OP_MIN, stream));
+    BEAST_HIP(hipMemcpyAsync(lo_nhi, red, sizeof(lo_nhi), hipMemcpyDeviceToHost, s), "range read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    mmh[0] = lo_nhi[0];
+    mmh[1] = -lo_nhi[1];
+  }
   const int64_t mn = mmh[0], mx = mmh[1], K = mx - mn;
   BEAST_REQUIRE_CODE(K < 0xD800, BEAST_E_UNSUPPORTED,
                      "BPE alphabet reaches the UTF-16 surrogate range (max - min token >= 55296)");
@@ -125,7 +282,12 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
                 (long long)lut_n, (long long)(K + 1));
   const int64_t n_cp = K + 1;
   ALLOC(pr, uint8_t, n_cp);
-  TRY(beast_bpe_cp_presence(tokens, n_tok, mn, pr, n_cp, stream));
+  if (n_tok > 0) {
+    TRY(beast_bpe_cp_presence(tokens, n_tok, mn, pr, n_cp, stream));
+  } else {
+    BEAST_HIP(hipMemsetAsync(pr, 0, n_cp, s), "presence memset");
+  }
+  if (comm != nullptr) TRY(beast_comm_allreduce(comm, pr, pr, n_cp, BEAST_DT_U8, BEAST_OP_MAX, stream));
   std::vector<uint8_t> present(n_cp);
   BEAST_HIP(hipMemcpyAsync(present.data(), pr, n_cp, hipMemcpyDeviceToHost, s), "presence read");
   BEAST_HIP(hipStreamSynchronize(s), "stream sync");
@@ -177,58 +339,22 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
                      "beast_bpe_train: output capacity (vocab %d, merges %d) below the vocabulary size %d", max_vocab,
                      max_merges_out, Vt);
 
-  // ---- pre-tokenisation: words per sequence, offsets, then the byte symbols
-  ALLOC(wps, int64_t, n_seq);
-  ALLOC(sps, int64_t, n_seq);
-  TRY(beast_bpe_pretok_count(tokens, seq_off, n_seq, mn, cls_lut, lut_n, wps, sps, stream));
-  ALLOC(scan_ws, uint8_t, beast_scan_workspace_bytes(n_seq));
-  ALLOC(woff, int64_t, n_seq + 1);
-  ALLOC(soff, int64_t, n_seq + 1);
-  TRY(beast_exclusive_scan_i64(wps, woff, n_seq, scan_ws, stream));
-  TRY(beast_exclusive_scan_i64(sps, soff, n_seq, scan_ws, stream));
-  int64_t nw = 0, ns = 0;
-  BEAST_HIP(hipMemcpyAsync(&nw, woff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "word count read");
-  BEAST_HIP(hipMemcpyAsync(&ns, soff + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "symbol count read");
-  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  BEAST_REQUIRE_CODE(ns < (int64_t(1) << 32), BEAST_E_UNSUPPORTED,
-                     "BPE corpus has >= 2^32 byte symbols on one GPU; shard it over more ranks");
-  ALLOC(b2i_d, uint16_t, 256);
-  BEAST_HIP(hipMemcpyAsync(b2i_d, byte2id, sizeof(byte2id), hipMemcpyHostToDevice, s), "byte2id upload");
-  ALLOC(sym, uint16_t, ns);
-  ALLOC(wstart, uint32_t, nw);
-  ALLOC(wlen, uint32_t, nw);
-  TRY(beast_bpe_pretok_emit(tokens, seq_off, n_seq, mn, cls_lut, lut_n, woff, soff, b2i_d, sym, wstart, wlen, stream));
-
-  // ---- distinct words x counts (the table grows 4x while it overflows), repack, signatures
-  ALLOC(ow, uint32_t, nw);
-  ALLOC(ol, uint32_t, nw);
-  ALLOC(oc, uint32_t, nw);
-  ALLOC(on, int64_t, 1);
-  int64_t nu = -1;
-  for (size_t nbytes = beast_bpe_dedup_workspace_bytes(nw); nu < 0; nbytes *= 4) {
-    void* dws = nullptr;
-    BEAST_HIP(hipMalloc(&dws, nbytes), "dedup workspace");
-    const int rc = beast_bpe_dedup_words(sym, wstart, wlen, nw, dws, nbytes, ow, ol, oc, on, stream);
-    if (rc == BEAST_OK) {
-      const hipError_t e1 = hipMemcpyAsync(&nu, on, sizeof(int64_t), hipMemcpyDeviceToHost, s);
-      const hipError_t e2 = hipStreamSynchronize(s);
-      (void)hipFree(dws);
-      BEAST_HIP(e1, "distinct count read");
-      BEAST_HIP(e2, "stream sync");
-    } else {
-      (void)hipFree(dws);
-      return rc;
-    }
+  // ---- this shard's distinct words x counts, length-ordered (sym2 / w2 / l2 / c2, nu words,
+  // nsp padded symbols), then with a communicator the union of every rank's
+  uint16_t* sym2 = nullptr;
+  uint32_t *w2 = nullptr, *l2 = nullptr, *c2 = nullptr;
+  int64_t nu = 0, nsp = 0;
+  if (n_tok > 0) TRY(shard_words(mem, tokens, seq_off, n_seq, mn, cls_lut, lut_n, byte2id, sym2, w2, l2, c2, nu, nsp, s));
+  if (comm != nullptr) TRY(union_words(mem, comm, sym2, w2, l2, c2, nu, nsp, s));
+  if (sym2 == nullptr) {   // no words anywhere: an empty table, the loop stops at once
+    ALLOC(z16, uint16_t, 4);
+    ALLOC(z32, uint32_t, 3);
+    BEAST_HIP(hipMemsetAsync(z16, 0, 8, s), "empty words");
+    BEAST_HIP(hipMemsetAsync(z32, 0, 12, s), "empty words");
+    sym2 = z16, w2 = z32, l2 = z32 + 1, c2 = z32 + 2;
   }
-  ALLOC(rp_ws, uint8_t, beast_bpe_repack_workspace_bytes(nu));
-  ALLOC(sym2, uint16_t, ns + 3 * nu);   // spans rounded up to 4
-  ALLOC(w2, uint32_t, nu);
-  ALLOC(l2, uint32_t, nu);
-  ALLOC(c2, uint32_t, nu);
-  TRY(beast_bpe_repack_words(sym, ow, ol, oc, nu, rp_ws, beast_bpe_repack_workspace_bytes(nu), sym2, w2, l2, c2, on,
-                             stream));
   ALLOC(sig, uint64_t, nu);
-  TRY(beast_bpe_word_signatures(sym2, w2, l2, nu, sig, stream));
+  if (nu > 0) TRY(beast_bpe_word_signatures(sym2, w2, l2, nu, sig, stream));
 
   // ---- the pair table and the loop state
   ALLOC(table, uint32_t, (size_t)Vt * Vt);
@@ -373,4 +499,27 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
   *out_min_token = mn;
   *out_max_token = mx;
   return BEAST_OK;
+}
+
+extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                               int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                               const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                               int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
+                               int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
+                               int max_merges_out, int* out_n_merges, void* stream) {
+  return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                        special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, stream);
+}
+
+extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq,
+                                    const uint8_t* cls_lut, int64_t lut_n, int vocab_size, int min_frequency,
+                                    int max_token_length, const char* const* special_tokens, int n_special,
+                                    int64_t* out_min_token, int64_t* out_max_token, char* out_vocab_bytes,
+                                    size_t vocab_bytes_cap, int64_t* out_vocab_off, int max_vocab, int* out_n_vocab,
+                                    int32_t* out_merges, int max_merges_out, int* out_n_merges, beast_comm* comm,
+                                    void* stream) {
+  return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                        special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, stream);
 }

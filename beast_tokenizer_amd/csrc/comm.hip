@@ -1,0 +1,225 @@
+// beast_comm_*: the library's own RCCL communicator (beast_comm_init / destroy and
+// the comm argument of the training call), for a caller that drives several GPUs without
+// torch.distributed.  The collectives are the ones this path needs and nothing more:
+//   * all-reduce MIN / MAX / SUM -- §8e's running bounds (update_weights_bounds*,
+//     beast/beast_bspline_tokenizer.py:362-389), the quantile histograms (fit_parameters,
+//     :428 process_group) and the BPE setup's token range / code-point presence;
+//   * all-gather and all-gather-v -- the replicated BPE loop's one exchange of every rank's
+//     distinct words (beast_tokenizer_amd/bpe_train.py GpuBpeOps.gather_words).
+// RCCL is bound at run time (dlopen of librccl.so.1 on the first communicator), so the library
+// itself needs no RCCL to load, and inside a torch process the RCCL torch already mapped is the
+// one used (same soname) rather than a second copy.  One process per GPU is the intended form
+// (beast_comm_init_rank over a unique id the caller distributes); beast_comm_init is SURVEY's
+// single-process form (ncclCommInitAll: one handle per listed device).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+struct beast_comm {
+  ncclComm_t nc;
+  int world, rank, device;
+};
+
+namespace {
+
+struct Rccl {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*);
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*init_all)(ncclComm_t*, int, const int*);
+  ncclResult_t (*destroy)(ncclComm_t);
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*group_start)();
+  ncclResult_t (*group_end)();
+  const char* (*error_string)(ncclResult_t);
+  bool ok = false;
+};
+
+Rccl g_rccl;
+std::once_flag g_rccl_once;
+
+void rccl_load() {
+  // the copy already mapped (torch's), else the system one
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return;
+  bool all = true;
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+    all = all && fn != nullptr;
+  };
+  sym(g_rccl.get_unique_id, "ncclGetUniqueId");
+  sym(g_rccl.init_rank, "ncclCommInitRank");
+  sym(g_rccl.init_all, "ncclCommInitAll");
+  sym(g_rccl.destroy, "ncclCommDestroy");
+  sym(g_rccl.all_reduce, "ncclAllReduce");
+  sym(g_rccl.all_gather, "ncclAllGather");
+  sym(g_rccl.broadcast, "ncclBroadcast");
+  sym(g_rccl.group_start, "ncclGroupStart");
+  sym(g_rccl.group_end, "ncclGroupEnd");
+  sym(g_rccl.error_string, "ncclGetErrorString");
+  g_rccl.ok = all;
+}
+
+const Rccl* rccl() {
+  std::call_once(g_rccl_once, rccl_load);
+  return g_rccl.ok ? &g_rccl : nullptr;
+}
+
+int nccl_fail(ncclResult_t r, const char* what) {
+  beast::set_error("%s: RCCL error %d (%s)", what, (int)r, g_rccl.error_string ? g_rccl.error_string(r) : "?");
+  return BEAST_E_HIP;
+}
+
+#define BEAST_NCCL(call, what)                          \
+  do {                                                  \
+    const ncclResult_t r_ = (call);                     \
+    if (r_ != ncclSuccess) return nccl_fail(r_, what);  \
+  } while (0)
+
+#define BEAST_NEED_RCCL(R)                                                                           \
+  const Rccl* R = rccl();                                                                            \
+  BEAST_REQUIRE_CODE(R != nullptr, BEAST_E_UNSUPPORTED, "beast_comm: librccl.so.1 could not be loaded")
+
+bool dtype_of(int dt, ncclDataType_t* out, size_t* bytes) {
+  switch (dt) {
+    case BEAST_DT_U8: *out = ncclUint8; *bytes = 1; return true;
+    case BEAST_DT_I32: *out = ncclInt32; *bytes = 4; return true;
+    case BEAST_DT_U32: *out = ncclUint32; *bytes = 4; return true;
+    case BEAST_DT_I64: *out = ncclInt64; *bytes = 8; return true;
+    case BEAST_DT_U64: *out = ncclUint64; *bytes = 8; return true;
+    case BEAST_DT_F32: *out = ncclFloat32; *bytes = 4; return true;
+    case BEAST_DT_F64: *out = ncclFloat64; *bytes = 8; return true;
+    default: return false;
+  }
+}
+
+bool op_of(int op, ncclRedOp_t* out) {
+  switch (op) {
+    case BEAST_OP_SUM: *out = ncclSum; return true;
+    case BEAST_OP_MIN: *out = ncclMin; return true;
+    case BEAST_OP_MAX: *out = ncclMax; return true;
+    default: return false;
+  }
+}
+
+}  // namespace
+
+extern "C" size_t beast_comm_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
+
+extern "C" int beast_comm_unique_id(void* id_out) {
+  BEAST_REQUIRE(id_out != nullptr, "beast_comm_unique_id: null pointer");
+  BEAST_NEED_RCCL(R);
+  ncclUniqueId id;
+  BEAST_NCCL(R->get_unique_id(&id), "ncclGetUniqueId");
+  std::memcpy(id_out, &id, sizeof(id));
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_init_rank(int world, int rank, const void* id, int device, beast_comm** out) {
+  BEAST_REQUIRE(id != nullptr && out != nullptr, "beast_comm_init_rank: null pointer");
+  BEAST_REQUIRE(world >= 1 && rank >= 0 && rank < world && device >= 0,
+                "beast_comm_init_rank: bad rank %d of world %d on device %d", rank, world, device);
+  *out = nullptr;
+  BEAST_NEED_RCCL(R);
+  BEAST_HIP(hipSetDevice(device), "hipSetDevice");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t nc = nullptr;
+  BEAST_NCCL(R->init_rank(&nc, world, uid, rank), "ncclCommInitRank");
+  *out = new beast_comm{nc, world, rank, device};
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_init(int ndev, const int* devs, beast_comm** out) {
+  BEAST_REQUIRE(ndev >= 1 && devs != nullptr && out != nullptr, "beast_comm_init: bad arguments");
+  BEAST_NEED_RCCL(R);
+  std::vector<ncclComm_t> nc(ndev, nullptr);
+  BEAST_NCCL(R->init_all(nc.data(), ndev, devs), "ncclCommInitAll");
+  for (int i = 0; i < ndev; ++i) out[i] = new beast_comm{nc[i], ndev, i, devs[i]};
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_destroy(beast_comm* c) {
+  if (c == nullptr) return BEAST_OK;
+  BEAST_NEED_RCCL(R);
+  const ncclResult_t r = R->destroy(c->nc);
+  delete c;
+  BEAST_NCCL(r, "ncclCommDestroy");
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_info(const beast_comm* c, int* world, int* rank, int* device) {
+  BEAST_REQUIRE(c != nullptr, "beast_comm_info: null communicator");
+  if (world) *world = c->world;
+  if (rank) *rank = c->rank;
+  if (device) *device = c->device;
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_allreduce(beast_comm* c, const void* send, void* recv, int64_t count, int dtype, int op,
+                                    void* stream) {
+  BEAST_REQUIRE(c != nullptr && count >= 0 && (count == 0 || (send && recv)), "beast_comm_allreduce: bad arguments");
+  ncclDataType_t dt;
+  ncclRedOp_t ro;
+  size_t eb;
+  BEAST_REQUIRE(dtype_of(dtype, &dt, &eb) && op_of(op, &ro), "beast_comm_allreduce: unknown dtype %d / op %d", dtype, op);
+  if (count == 0) return BEAST_OK;
+  BEAST_NEED_RCCL(R);
+  BEAST_NCCL(R->all_reduce(send, recv, (size_t)count, dt, ro, c->nc, beast::as_stream(stream)), "ncclAllReduce");
+  return BEAST_OK;
+}
+
+extern "C" int beast_comm_allgather(beast_comm* c, const void* send, void* recv, int64_t count, int dtype,
+                                    void* stream) {
+  BEAST_REQUIRE(c != nullptr && count >= 0 && (count == 0 || (send && recv)), "beast_comm_allgather: bad arguments");
+  ncclDataType_t dt;
+  size_t eb;
+  BEAST_REQUIRE(dtype_of(dtype, &dt, &eb), "beast_comm_allgather: unknown dtype %d", dtype);
+  if (count == 0) return BEAST_OK;
+  BEAST_NEED_RCCL(R);
+  BEAST_NCCL(R->all_gather(send, recv, (size_t)count, dt, c->nc, beast::as_stream(stream)), "ncclAllGather");
+  return BEAST_OK;
+}
+
+// rank r's counts[r] elements land at recv + displs[r] on every rank: one broadcast per rank in
+// one group (RCCL has no all-gather-v); counts / displs are HOST arrays [world], the same on
+// every rank.  A rank with nothing to send is skipped by all ranks alike.
+extern "C" int beast_comm_allgatherv(beast_comm* c, const void* send, void* recv, const int64_t* counts,
+                                     const int64_t* displs, int dtype, void* stream) {
+  BEAST_REQUIRE(c != nullptr && counts != nullptr && displs != nullptr, "beast_comm_allgatherv: null pointer");
+  ncclDataType_t dt;
+  size_t eb;
+  BEAST_REQUIRE(dtype_of(dtype, &dt, &eb), "beast_comm_allgatherv: unknown dtype %d", dtype);
+  bool any = false;
+  for (int r = 0; r < c->world; ++r) {
+    BEAST_REQUIRE(counts[r] >= 0 && displs[r] >= 0, "beast_comm_allgatherv: negative count / displacement");
+    any = any || counts[r] > 0;
+  }
+  if (!any) return BEAST_OK;
+  BEAST_REQUIRE(recv != nullptr && (counts[c->rank] == 0 || send != nullptr), "beast_comm_allgatherv: null buffer");
+  BEAST_NEED_RCCL(R);
+  hipStream_t s = beast::as_stream(stream);
+  BEAST_NCCL(R->group_start(), "ncclGroupStart");
+  ncclResult_t first = ncclSuccess;
+  for (int r = 0; r < c->world; ++r) {
+    if (counts[r] == 0) continue;
+    char* dst = static_cast<char*>(recv) + (size_t)displs[r] * eb;
+    const ncclResult_t e = R->broadcast(r == c->rank ? send : dst, dst, (size_t)counts[r], dt, r, c->nc, s);
+    if (first == ncclSuccess) first = e;
+  }
+  const ncclResult_t e = R->group_end();
+  BEAST_NCCL(first, "ncclBroadcast");
+  BEAST_NCCL(e, "ncclGroupEnd");
+  return BEAST_OK;
+}

@@ -325,6 +325,54 @@ int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq
                     int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap, int64_t* out_vocab_off,
                     int max_vocab, int* out_n_vocab, int32_t* out_merges, int max_merges_out, int* out_n_merges,
                     void* stream);
+
+/* ---- The library's own RCCL communicator (round 5; SURVEY.md §8b's beast_comm_init / destroy
+ * and the comm argument of the training call), for a multi-GPU caller without torch.distributed.
+ * RCCL is bound at run time (librccl.so.1; inside a torch process the copy torch mapped), so the
+ * library loads without it; every entry point returns BEAST_E_UNSUPPORTED when it is absent.
+ * One process per GPU: rank 0 makes an id (beast_comm_unique_id, beast_comm_id_bytes() bytes),
+ * the caller hands it to every rank, each calls beast_comm_init_rank with its own device.
+ * beast_comm_init is the single-process form (one handle per listed device, out[ndev]). */
+typedef struct beast_comm beast_comm;
+#define BEAST_DT_U8 0
+#define BEAST_DT_I32 1
+#define BEAST_DT_U32 2
+#define BEAST_DT_I64 3
+#define BEAST_DT_U64 4
+#define BEAST_DT_F32 5
+#define BEAST_DT_F64 6
+#define BEAST_OP_SUM 0
+#define BEAST_OP_MIN 1
+#define BEAST_OP_MAX 2
+size_t beast_comm_id_bytes(void);
+int beast_comm_unique_id(void* id_out);
+int beast_comm_init_rank(int world, int rank, const void* id, int device, beast_comm** out);
+int beast_comm_init(int ndev, const int* devs, beast_comm** out);
+int beast_comm_destroy(beast_comm* comm);
+int beast_comm_info(const beast_comm* comm, int* world, int* rank, int* device);
+/* §8e's reductions on device buffers (in place when send == recv), stream-ordered: the running
+ * bounds (MIN / MAX over [D*N] f32, beast/beast_bspline_tokenizer.py:362-389), the quantile
+ * histograms and BPE pair tables (SUM). */
+int beast_comm_allreduce(beast_comm* comm, const void* send, void* recv, int64_t count, int dtype, int op,
+                         void* stream);
+int beast_comm_allgather(beast_comm* comm, const void* send, void* recv, int64_t count, int dtype, void* stream);
+/* rank r's counts[r] elements at recv + displs[r] on every rank; counts / displs HOST [world],
+ * equal on every rank */
+int beast_comm_allgatherv(beast_comm* comm, const void* send, void* recv, const int64_t* counts,
+                          const int64_t* displs, int dtype, void* stream);
+/* beast_bpe_train over every rank's shard of the sequences (SURVEY.md §8b's comm argument;
+ * FIGBPE.fit_from_sequences with process_group, beast/beast_bpe_trainer.py:61-98): the token
+ * range is all-reduced (MIN / MAX), the code-point presence (MAX), each rank pre-tokenises and
+ * deduplicates its shard, the distinct words x counts are all-gathered once (rank order) and
+ * every rank runs the batched loop on the union -- bpe_train.py's replicated form, no per-pass
+ * collective.  Every rank returns the same vocabulary and merges; a shard may be empty.  All
+ * ranks must call it with the same options.  comm == NULL is beast_bpe_train. */
+int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                         int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                         const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                         int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap, int64_t* out_vocab_off,
+                         int max_vocab, int* out_n_vocab, int32_t* out_merges, int max_merges_out, int* out_n_merges,
+                         beast_comm* comm, void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),
