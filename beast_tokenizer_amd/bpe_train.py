@@ -644,9 +644,8 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
     """The same training through the one-call C-ABI ``beast_bpe_train`` (include/beast_hip.h):
     what a non-Python caller binds.  ``comm`` (a :class:`beast_tokenizer_amd.comm.Communicator`)
     trains over every rank's shard with ``beast_bpe_train_comm`` (the replicated form: one
-    all-gather of the distinct words, every rank returns the same result).  Raises
-    NotImplementedError where the C entry point defers to this module's driver (Vt > 4096, a
-    string-hash collision)."""
+    all-gather of the distinct words, every rank returns the same result).  Vt > 4096 runs the
+    C++ host-driven loop; raises NotImplementedError above 32768 (the dense pair table)."""
     import ctypes
     dev = tokens.device
     _lib.require_gpu(tokens, "tokens")

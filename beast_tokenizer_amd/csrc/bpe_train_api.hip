@@ -7,9 +7,10 @@
 // chars by code point), pre-tokenisation (count, scan, emit), distinct words x counts, the
 // length-ordered repack + word signatures, the pair table, then the device-driven batched
 // merge loop with two chunks of passes in flight, and the host replay of its merge log against
-// the real strings.  Vt <= 4,096 (the batched loop); a 64-bit string-hash collision or a full
-// merge log comes back BEAST_E_UNSUPPORTED (the Python driver then reruns on its host-driven
-// loop).  beast_bpe_train_comm is the same over several GPUs with the library's communicator
+// the real strings.  Vt <= 4,096 runs the batched loop; larger vocabularies (Vt <= 32,768, the
+// dense pair table) the host-driven one (one merge per host round trip, bpe_train.py's loop
+// below the device loop), as does a rerun after a 64-bit string-hash collision or a full merge
+// log of the batched loop.  beast_bpe_train_comm is the same over several GPUs with the library's communicator
 // (comm.hip): bpe_train.py's replicated form -- the range and presence all-reduced, the shards'
 // distinct words all-gathered once, the loop run on the union on every rank.
 #include <hip/hip_runtime.h>
@@ -233,7 +234,8 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
                           const char* const* special_tokens, int n_special, int64_t* out_min_token,
                           int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
                           int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
-                          int max_merges_out, int* out_n_merges, beast_comm* comm, void* stream) {
+                          int max_merges_out, int* out_n_merges, beast_comm* comm, bool host_loop,
+                          void* stream) {
   BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
                     out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
                 "beast_bpe_train: null pointer argument");
@@ -333,8 +335,8 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   }
   const int n_base = (int)id2str.size();
   const int Vt = std::max(vocab_size, n_base);
-  BEAST_REQUIRE_CODE(Vt <= 4096, BEAST_E_UNSUPPORTED,
-                     "beast_bpe_train: Vt %d > 4096 (the batched device loop); use the Python driver", Vt);
+  BEAST_REQUIRE_CODE(Vt <= 32768, BEAST_E_UNSUPPORTED,
+                     "beast_bpe_train: Vt %d > 32768 (the dense pair table)", Vt);
   BEAST_REQUIRE_CODE(max_vocab >= Vt && max_merges_out >= std::max(vocab_size - n_base, 0), BEAST_E_WORKSPACE,
                      "beast_bpe_train: output capacity (vocab %d, merges %d) below the vocabulary size %d", max_vocab,
                      max_merges_out, Vt);
@@ -378,76 +380,135 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   ALLOC(tlen_d, uint32_t, Vt);
   BEAST_HIP(hipMemcpyAsync(hp_d, hp.data(), sizeof(uint64_t) * hp.size(), hipMemcpyHostToDevice, s), "hash upload");
   BEAST_HIP(hipMemcpyAsync(tlen_d, tlen.data(), sizeof(uint32_t) * Vt, hipMemcpyHostToDevice, s), "tlen upload");
-  const int max_merges = 4 * std::max(vocab_size - n_base, 0) + 1024;
-  const size_t lws_bytes = beast_bpe_loop_workspace_bytes(Vt, max_merges);
-  ALLOC(lws, uint8_t, lws_bytes);
-  TRY(beast_bpe_loop_init(lws, lws_bytes, Vt, max_merges, n_base, vocab_size, min_frequency, hp_d, hp_d + n_base,
-                          tlen_d, max_tlen, stream));
-  const void* st_p = nullptr;
-  const void* log_p = nullptr;
-  TRY(beast_bpe_loop_state(lws, Vt, max_merges, &st_p, &log_p));
-  const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
-  ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
-  BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
-  const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
-  ALLOC(bws, uint8_t, bw_bytes);
   const int max_len = max_token_length > 0 ? max_token_length : 0x7FFFFFFF;
-  auto run = [&](int steps, int flags) {
-    return beast_bpe_loop_batch(lws, Vt, max_merges, steps, KMAX, flags, sym2, w2, l2, c2, nu, tlen_d, max_len, sig,
-                                table, argws, bws, bw_bytes, vocab_size, nullptr, nullptr, stream);
+  // the same training from scratch on the host-driven loop (a string-hash collision or a full
+  // merge log of the batched one); every rank of a communicator takes the same decision
+  auto rerun_on_host = [&]() {
+    return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                          special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                          out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, true,
+                          stream);
   };
-
-  // ---- the loop: two chunks of passes in flight, the host reads the state the older one left
-  HostPinned stage;
-  BEAST_HIP(hipHostMalloc(&stage.p, 2 * 64, hipHostMallocDefault), "pinned state");
-  int32_t* st_host = static_cast<int32_t*>(stage.p);
-  struct Inflight { hipEvent_t ev; int slot; int passes; };
-  std::vector<Inflight> inflight;
-  auto release = [&]() {
-    for (auto& f : inflight) (void)hipEventDestroy(f.ev);
-    inflight.clear();
-  };
-  auto launch = [&](int steps, int flags) -> int {
-    if (int rc = run(steps, flags)) return rc;
-    const int slot = inflight.empty() ? 0 : 1 - inflight.back().slot;
-    if (hipMemcpyAsync(st_host + 16 * slot, st_p, 64, hipMemcpyDeviceToHost, s) != hipSuccess)
-      return beast::hip_fail(hipGetLastError(), "loop state copy");
-    hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return beast::hip_fail(hipGetLastError(), "event");
-    (void)hipEventRecord(ev, s);
-    inflight.push_back({ev, slot, steps});
-    return BEAST_OK;
-  };
-  int vcur = n_base, rc = BEAST_OK;
-  rc = launch(std::max(1, std::min(CHUNK, (vocab_size - vcur + KMAX - 1) / KMAX)), 1 /* BATCH_INIT */);
-  while (rc == BEAST_OK) {
-    int queued = 0;
-    for (auto& f : inflight) queued += f.passes;
-    const int left = vocab_size - vcur - 4 * queued;
-    if (left > 0 && (rc = launch(std::min(CHUNK, (left + KMAX - 1) / KMAX), 0)) != BEAST_OK) break;
-    Inflight f = inflight.front();
-    inflight.erase(inflight.begin());
-    const hipError_t e = hipEventSynchronize(f.ev);
-    (void)hipEventDestroy(f.ev);
-    if (e != hipSuccess) { rc = beast::hip_fail(e, "loop event"); break; }
-    const int32_t* h = st_host + 16 * f.slot;
-    const int active = h[ST_ACTIVE];
-    vcur = h[ST_VCUR];
-    if (!active || vcur >= vocab_size) break;
-    if (inflight.empty() && (rc = launch(1, 0)) != BEAST_OK) break;
-  }
-  release();
-  if (rc != BEAST_OK) return rc;
-  int32_t state[16];
-  BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
-  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  const int n_log = state[ST_NMERGES];
-  BEAST_REQUIRE_CODE(n_log < max_merges, BEAST_E_UNSUPPORTED,
-                     "beast_bpe_train: merge log full; use the Python driver's host-driven loop");
-  std::vector<int32_t> log(4 * (size_t)std::max(n_log, 1));
-  if (n_log > 0) {
-    BEAST_HIP(hipMemcpyAsync(log.data(), log_p, sizeof(int32_t) * 4 * n_log, hipMemcpyDeviceToHost, s), "log read");
+  std::vector<int32_t> log;
+  int n_log = 0;
+  if (host_loop || Vt > 4096) {
+    // ---- host-driven loop (bpe_train.py train_bpe below the device loop): argmax, merge in
+    // every word, apply + next argmax; one host read of the decided pair per merge
+    const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
+    ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
+    BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
+    ALLOC(deltas, int32_t, 4 * (size_t)Vt);
+    BEAST_HIP(hipMemsetAsync(deltas, 0, sizeof(int32_t) * 4 * (size_t)Vt, s), "deltas memset");
+    HostPinned kh;
+    BEAST_HIP(hipHostMalloc(&kh.p, 64, hipHostMallocDefault), "pinned key");
+    uint64_t* key_h = static_cast<uint64_t*>(kh.p);
+    auto read_key = [&](int call, uint64_t& key) -> int {
+      BEAST_HIP(hipMemcpyAsync(key_h, argws + 2 + (call & 1), sizeof(uint64_t), hipMemcpyDeviceToHost, s),
+                "argmax read");
+      BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+      key = *key_h;
+      return BEAST_OK;
+    };
+    std::vector<std::string> ids = id2str;
+    std::unordered_map<std::string, int> ix = str2id;
+    int call = 0;
+    uint64_t key = 0;
+    TRY(beast_bpe_argmax(table, Vt, n_base, argws, call, stream));
+    TRY(read_key(call++, key));
+    while ((int)ids.size() < vocab_size) {
+      const uint64_t count = key >> 32;
+      if (count < 1 || count < (uint64_t)std::max(min_frequency, 0)) break;
+      const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu);
+      const int a = (int)(idx / (uint32_t)Vt), b = (int)(idx % (uint32_t)Vt);
+      BEAST_REQUIRE_CODE(a < (int)ids.size() && b < (int)ids.size(), BEAST_E_HIP,
+                         "beast_bpe_train: argmax returned pair (%d, %d) outside the vocabulary", a, b);
+      std::string t = ids[a] + ids[b];
+      auto it = ix.find(t);
+      const bool reused = it != ix.end();
+      const int nid = reused ? it->second : (int)ids.size();
+      if (!reused) {
+        ix.emplace(t, nid);
+        ids.push_back(std::move(t));
+      }
+      log.insert(log.end(), {a, b, nid, reused ? 1 : 0});
+      ++n_log;
+      TRY(beast_bpe_merge(sym2, w2, l2, c2, nu, a, b, nid, tlen_d, max_len, deltas, Vt, sig, (int64_t)count, stream));
+      const int k = call++;
+      TRY(beast_bpe_apply_argmax(table, deltas, Vt, (int)ids.size(), a, b, nid, tlen_d, argws, k, stream));
+      if ((int)ids.size() >= vocab_size) break;   // last merge: applied without searching again
+      TRY(read_key(k, key));
+    }
     BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+  } else {
+    const int max_merges = 4 * std::max(vocab_size - n_base, 0) + 1024;
+    const size_t lws_bytes = beast_bpe_loop_workspace_bytes(Vt, max_merges);
+    ALLOC(lws, uint8_t, lws_bytes);
+    TRY(beast_bpe_loop_init(lws, lws_bytes, Vt, max_merges, n_base, vocab_size, min_frequency, hp_d, hp_d + n_base,
+                            tlen_d, max_tlen, stream));
+    const void* st_p = nullptr;
+    const void* log_p = nullptr;
+    TRY(beast_bpe_loop_state(lws, Vt, max_merges, &st_p, &log_p));
+    const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
+    ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
+    BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
+    const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
+    ALLOC(bws, uint8_t, bw_bytes);
+    auto run = [&](int steps, int flags) {
+      return beast_bpe_loop_batch(lws, Vt, max_merges, steps, KMAX, flags, sym2, w2, l2, c2, nu, tlen_d, max_len, sig,
+                                  table, argws, bws, bw_bytes, vocab_size, nullptr, nullptr, stream);
+    };
+
+    // ---- the loop: two chunks of passes in flight, the host reads the state the older one left
+    HostPinned stage;
+    BEAST_HIP(hipHostMalloc(&stage.p, 2 * 64, hipHostMallocDefault), "pinned state");
+    int32_t* st_host = static_cast<int32_t*>(stage.p);
+    struct Inflight { hipEvent_t ev; int slot; int passes; };
+    std::vector<Inflight> inflight;
+    auto release = [&]() {
+      for (auto& f : inflight) (void)hipEventDestroy(f.ev);
+      inflight.clear();
+    };
+    auto launch = [&](int steps, int flags) -> int {
+      if (int rc = run(steps, flags)) return rc;
+      const int slot = inflight.empty() ? 0 : 1 - inflight.back().slot;
+      if (hipMemcpyAsync(st_host + 16 * slot, st_p, 64, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return beast::hip_fail(hipGetLastError(), "loop state copy");
+      hipEvent_t ev;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return beast::hip_fail(hipGetLastError(), "event");
+      (void)hipEventRecord(ev, s);
+      inflight.push_back({ev, slot, steps});
+      return BEAST_OK;
+    };
+    int vcur = n_base, rc = BEAST_OK;
+    rc = launch(std::max(1, std::min(CHUNK, (vocab_size - vcur + KMAX - 1) / KMAX)), 1 /* BATCH_INIT */);
+    while (rc == BEAST_OK) {
+      int queued = 0;
+      for (auto& f : inflight) queued += f.passes;
+      const int left = vocab_size - vcur - 4 * queued;
+      if (left > 0 && (rc = launch(std::min(CHUNK, (left + KMAX - 1) / KMAX), 0)) != BEAST_OK) break;
+      Inflight f = inflight.front();
+      inflight.erase(inflight.begin());
+      const hipError_t e = hipEventSynchronize(f.ev);
+      (void)hipEventDestroy(f.ev);
+      if (e != hipSuccess) { rc = beast::hip_fail(e, "loop event"); break; }
+      const int32_t* h = st_host + 16 * f.slot;
+      const int active = h[ST_ACTIVE];
+      vcur = h[ST_VCUR];
+      if (!active || vcur >= vocab_size) break;
+      if (inflight.empty() && (rc = launch(1, 0)) != BEAST_OK) break;
+    }
+    release();
+    if (rc != BEAST_OK) return rc;
+    int32_t state[16];
+    BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    n_log = state[ST_NMERGES];
+    if (n_log >= max_merges) return rerun_on_host();   // merge log full
+    log.resize(4 * (size_t)std::max(n_log, 1));
+    if (n_log > 0) {
+      BEAST_HIP(hipMemcpyAsync(log.data(), log_p, sizeof(int32_t) * 4 * n_log, hipMemcpyDeviceToHost, s), "log read");
+      BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    }
   }
 
   // ---- replay the log against the real strings (bpe_train.py replay_log)
@@ -460,9 +521,10 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     const std::string t = id2str[a] + id2str[b];
     auto it = str2id.find(t);
     const bool have = it != str2id.end();
+    if (!host_loop && !(have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size())))
+      return rerun_on_host();   // a 64-bit string-hash collision in the batched loop
     BEAST_REQUIRE_CODE(have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size()),
-                       BEAST_E_UNSUPPORTED,
-                       "beast_bpe_train: 64-bit string-hash collision at merge %d; use the Python driver", i);
+                       BEAST_E_HIP, "beast_bpe_train: merge %d disagrees with the strings", i);
     if (!have) {
       str2id.emplace(t, nid);
       id2str.push_back(t);
@@ -509,7 +571,8 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
                                int max_merges_out, int* out_n_merges, void* stream) {
   return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, stream);
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, false,
+                        stream);
 }
 
 extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq,
@@ -521,5 +584,6 @@ extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_of
                                     void* stream) {
   return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, stream);
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, false,
+                        stream);
 }

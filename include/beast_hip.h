@@ -315,10 +315,11 @@ int beast_bpe_loop_batch(void* ws, int Vt, int max_merges, int n_steps, int max_
  * max_merges_out >= vocab_size - alphabet (checked up front), vocab_bytes_cap >= the strings'
  * bytes (known only after training).  When an output is too small the call returns
  * BEAST_E_WORKSPACE with the required sizes in *out_n_vocab, *out_n_merges and out_vocab_off[0]
- * (vocabulary bytes); retry with those.  Synchronises the stream.  BEAST_E_UNSUPPORTED for
- * Vt > 4096, a full merge log or a 64-bit string-hash collision (the Python driver,
- * bpe_train.train_bpe, reruns those on its host-driven loop); one GPU (the multi-rank forms
- * are the Python driver's, over torch.distributed). */
+ * (vocabulary bytes); retry with those.  Synchronises the stream.  Vt <= 4096 runs the batched
+ * device loop; 4096 < Vt <= 32768 the host-driven one (beast_bpe_argmax / _merge / _apply_argmax,
+ * one host read per merge), as does a rerun after a full merge log or a 64-bit string-hash
+ * collision of the batched loop; BEAST_E_UNSUPPORTED above 32768 (the dense pair table).  One
+ * GPU; beast_bpe_train_comm below is the multi-rank form. */
 int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                     int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
                     const char* const* special_tokens, int n_special, int64_t* out_min_token,

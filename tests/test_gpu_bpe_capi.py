@@ -65,14 +65,41 @@ def test_capi_train_reports_required_capacity(gpu_device):
 
 
 @pytest.mark.gpu
-def test_capi_train_rejects_empty_and_wide(gpu_device):
+def test_capi_train_rejects_empty_and_too_wide(gpu_device):
     from beast_tokenizer_amd import _lib
     flat = torch.zeros(0, dtype=torch.int64, device=gpu_device)
     off = torch.zeros(2, dtype=torch.int64, device=gpu_device)
     with pytest.raises(ValueError, match="No non-empty sequences"):
         train_bpe_capi(flat, off, 300)
-    arr = np.arange(0, 6000, dtype=np.int64).reshape(60, 100)   # alphabet > 4096: the Python driver's loop
+    arr = np.arange(0, 40000, dtype=np.int64).reshape(400, 100)   # alphabet > 32768: no dense pair table
     flat, off = fixed_rows_to_device(torch.from_numpy(arr).to(gpu_device))
-    with pytest.raises(NotImplementedError, match="4096"):
-        train_bpe_capi(flat, off, 6500)
+    with pytest.raises(NotImplementedError, match="32768"):
+        train_bpe_capi(flat, off, 40500)
     assert _lib.load() is not None
+
+
+@pytest.mark.gpu
+def test_capi_train_wide_alphabet_host_loop_matches_live_hf(gpu_device):
+    """Vt > 4096: beast_bpe_train runs the host-driven loop (one merge per round trip) -- equal to
+    live HF and to the Python driver (the same loop)."""
+    tokenizers = pytest.importorskip("tokenizers")
+    from tokenizers.trainers import BpeTrainer
+    rng = np.random.default_rng(11)
+    wide = np.arange(0, 5000, dtype=np.int64).reshape(50, 100)       # every code point once
+    base = rng.integers(0, 400, size=9)
+    rep = base[rng.integers(0, 9, size=(60, 100))]                   # repeated structure to merge
+    arr = np.concatenate([wide, rep])
+    lo, hi = int(arr.min()), int(arr.max())
+    vs = 5400
+    bpe = tokenizers.ByteLevelBPETokenizer()
+    tr = BpeTrainer(vocab_size=vs, min_frequency=2, show_progress=False,
+                    initial_alphabet=[chr(i) for i in range(hi - lo + 1)], max_token_length=10000)
+    bpe._tokenizer.train_from_iterator(["".join(map(chr, r - lo)) for r in arr], trainer=tr)
+    m = json.loads(bpe._tokenizer.to_str())["model"]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr).to(gpu_device))
+    res = train_bpe_capi(flat, off, vs)
+    assert len(res.vocab) > 5000 + 50          # the host loop merged
+    assert res.vocab == m["vocab"]
+    assert [list(x) for x in res.merges] == [list(x) for x in m["merges"]]
+    py = train_bpe(flat, off, vs)
+    assert py.vocab == res.vocab and py.merges == res.merges
