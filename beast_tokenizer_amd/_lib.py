@@ -27,6 +27,7 @@ OPT_BLOCK_WAVES = 2
 OPT_MERGE_LDS_MIN = 3
 OPT_BPE_ENCODE_MODE = 5
 OPT_BPE_DEDUP_KEY_BITS = 6
+OPT_BPE_TRAIN_HOST_LOOP = 7
 
 _vp, _i64, _i32, _f32, _f64, _sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_double, C.c_size_t
 

@@ -229,6 +229,10 @@ int union_words(DevMem& mem, beast_comm* comm, uint16_t*& sym2, uint32_t*& w2, u
 
 }  // namespace
 
+namespace beast {
+int g_bpe_train_host = 0;
+}
+
 static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                           int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
                           const char* const* special_tokens, int n_special, int64_t* out_min_token,
@@ -391,7 +395,7 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   };
   std::vector<int32_t> log;
   int n_log = 0;
-  if (host_loop || Vt > 4096) {
+  if (host_loop || Vt > 4096 || beast::g_bpe_train_host == 1) {
     // ---- host-driven loop (bpe_train.py train_bpe below the device loop): argmax, merge in
     // every word, apply + next argmax; one host read of the decided pair per merge
     const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
@@ -521,10 +525,10 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     const std::string t = id2str[a] + id2str[b];
     auto it = str2id.find(t);
     const bool have = it != str2id.end();
-    if (!host_loop && !(have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size())))
+    const bool agree = have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size());
+    if (!host_loop && (!agree || beast::g_bpe_train_host == 2))
       return rerun_on_host();   // a 64-bit string-hash collision in the batched loop
-    BEAST_REQUIRE_CODE(have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size()),
-                       BEAST_E_HIP, "beast_bpe_train: merge %d disagrees with the strings", i);
+    BEAST_REQUIRE_CODE(agree, BEAST_E_HIP, "beast_bpe_train: merge %d disagrees with the strings", i);
     if (!have) {
       str2id.emplace(t, nid);
       id2str.push_back(t);

@@ -1612,6 +1612,11 @@ extern "C" int beast_set_option(int option, int value) {
     beast::g_bpe_dedup_key_bits = value;
     return BEAST_OK;
   }
+  if (option == BEAST_OPT_BPE_TRAIN_HOST_LOOP) {
+    BEAST_REQUIRE(value >= 0 && value <= 2, "BEAST_OPT_BPE_TRAIN_HOST_LOOP: %d is not 0..2", value);
+    beast::g_bpe_train_host = value;
+    return BEAST_OK;
+  }
   BEAST_REQUIRE(false, "unknown option %d", option);
   return BEAST_E_INVALID;
 }
@@ -1622,6 +1627,7 @@ extern "C" int beast_get_option(int option) {
   if (option == BEAST_OPT_MERGE_LDS_MIN) return (int)beast::g_merge_lds_min;
   if (option == BEAST_OPT_BPE_ENCODE_MODE) return beast::g_bpe_encode_mode;
   if (option == BEAST_OPT_BPE_DEDUP_KEY_BITS) return beast::g_bpe_dedup_key_bits;
+  if (option == BEAST_OPT_BPE_TRAIN_HOST_LOOP) return beast::g_bpe_train_host;
   beast::set_error("unknown option %d", option);
   return BEAST_E_INVALID;
 }

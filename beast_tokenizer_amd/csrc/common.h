@@ -19,6 +19,9 @@ extern int64_t g_merge_lds_min;
 extern int g_bpe_encode_mode;
 // BEAST_OPT_BPE_DEDUP_KEY_BITS: width of the dedup encode's word keys (tests force collisions)
 extern int g_bpe_dedup_key_bits;
+// BEAST_OPT_BPE_TRAIN_HOST_LOOP: beast_bpe_train's loop (tests: 1 host-driven, 2 rerun as after a
+// string-hash collision of the batched loop)
+extern int g_bpe_train_host;
 int hip_fail(hipError_t e, const char* what);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

@@ -56,12 +56,15 @@ const char* beast_last_error(void);
  * BEAST_OPT_BPE_DEDUP_KEY_BITS = k (tests): beast_bpe_encode_rows_words keeps only k bits of its
  * 32-bit word hashes, so different words share hashes; the code-point compare behind every hash
  * match keeps them apart (same ids).
+ * BEAST_OPT_BPE_TRAIN_HOST_LOOP = 1 (tests): beast_bpe_train runs the host-driven loop at any Vt;
+ * 2 reruns it after the batched loop as a string-hash collision would.  Results are identical.
  * Options are process-wide and not synchronised: set them before launching, not concurrently. */
 #define BEAST_OPT_GENERIC_KERNELS 1
 #define BEAST_OPT_BLOCK_WAVES 2
 #define BEAST_OPT_MERGE_LDS_MIN 3
 #define BEAST_OPT_BPE_ENCODE_MODE 5
 #define BEAST_OPT_BPE_DEDUP_KEY_BITS 6
+#define BEAST_OPT_BPE_TRAIN_HOST_LOOP 7
 int beast_set_option(int option, int value);
 /* the option's current value (BEAST_E_INVALID for an unknown option) */
 int beast_get_option(int option);

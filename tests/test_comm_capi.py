@@ -78,6 +78,16 @@ def _child(q):
                          (a.min_token, a.max_token) == (ref["min_token"], ref["max_token"]),
                          a.vocab == b.vocab and a.merges == b.merges, a.stats["world"])
         out["bpe"] = bpe
+        from beast_tokenizer_amd import _lib   # the rerun after a collision repeats the collectives
+        lib = _lib.load()
+        lib.beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, 2)
+        try:
+            ref = load_json("bpe_hf.json")["skew/2048"]
+            flat, off = fixed_rows_to_device(torch.from_numpy(corpora["skew"].astype(np.int64)).to(dev))
+            a = train_bpe_capi(flat, off, 2048, comm=comm)
+            out["rerun"] = (a.vocab == ref["vocab"], [list(m) for m in a.merges] == ref["merges"])
+        finally:
+            lib.beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, 0)
         try:   # an empty corpus over the communicator: the reference's error (:84-85)
             train_bpe_capi(torch.zeros(0, dtype=torch.int64, device=dev), torch.zeros(2, dtype=torch.int64, device=dev),
                            300, comm=comm)
@@ -118,5 +128,6 @@ def test_comm_world1_collectives_and_training(gpu_device):
     assert len(out["bpe"]) >= 3, out["bpe"]
     for case, flags in out["bpe"].items():
         assert flags == (True, True, True, True, 1), (case, flags)
+    assert out["rerun"] == (True, True)
     assert "No non-empty sequences" in out["empty"], out["empty"]
     assert out["init_all"] == (1, 1, 0, [1.0] * 5)

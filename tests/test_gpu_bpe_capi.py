@@ -103,3 +103,26 @@ def test_capi_train_wide_alphabet_host_loop_matches_live_hf(gpu_device):
     assert [list(x) for x in res.merges] == [list(x) for x in m["merges"]]
     py = train_bpe(flat, off, vs)
     assert py.vocab == res.vocab and py.merges == res.merges
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("case", ["skew/2048", "traj_k3/700"])
+def test_capi_train_host_loop_and_rerun_match_hf_golden(case, mode, gpu_device):
+    """BEAST_OPT_BPE_TRAIN_HOST_LOOP: 1 runs beast_bpe_train's host-driven loop at a small Vt, 2
+    reruns the training on it after the batched loop as a string-hash collision would -- both
+    equal to the HF golden."""
+    from beast_tokenizer_amd import _lib
+    ref = load_json("bpe_hf.json")[case]
+    cname, vs = case.split("/")
+    arr = load_npz("bpe_corpora.npz")[cname]
+    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64)).to(gpu_device))
+    lib = _lib.load()
+    lib.beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, mode)
+    try:
+        res = train_bpe_capi(flat, off, int(vs))
+    finally:
+        lib.beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, 0)
+    assert res.vocab == ref["vocab"]
+    assert [list(m) for m in res.merges] == ref["merges"]
+
