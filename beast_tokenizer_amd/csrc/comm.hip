@@ -132,11 +132,17 @@ extern "C" int beast_comm_init_rank(int world, int rank, const void* id, int dev
                 "beast_comm_init_rank: bad rank %d of world %d on device %d", rank, world, device);
   *out = nullptr;
   BEAST_NEED_RCCL(R);
+  // RCCL binds the communicator to the current device: switch for the init, then restore the
+  // caller's
+  int prev = 0;
+  BEAST_HIP(hipGetDevice(&prev), "hipGetDevice");
   BEAST_HIP(hipSetDevice(device), "hipSetDevice");
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclComm_t nc = nullptr;
-  BEAST_NCCL(R->init_rank(&nc, world, uid, rank), "ncclCommInitRank");
+  const ncclResult_t r = R->init_rank(&nc, world, uid, rank);
+  (void)hipSetDevice(prev);
+  BEAST_NCCL(r, "ncclCommInitRank");
   *out = new beast_comm{nc, world, rank, device};
   return BEAST_OK;
 }
