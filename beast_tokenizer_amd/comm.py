@@ -108,6 +108,33 @@ class Communicator:
                  DT[t.dtype], s)
         return out[:off]
 
+    def reducer(self):
+        """This communicator as ``bpe_train``'s ``Reducer`` (``red(t, op)`` in place, plus
+        ``red.gather(t)`` -> every rank's 1-D ``t`` in rank order), so ``train_bpe(...,
+        reduce=comm.reducer(), replicate=False)`` runs the sharded loop -- the per-pass delta
+        all-reduce between the merge and apply launches -- over the library's own RCCL
+        communicator instead of torch.distributed."""
+        def red(t: torch.Tensor, op: str) -> None:
+            if t.dtype == torch.bool:
+                u = t.to(torch.uint8)
+                self.allreduce(u, op)
+                t.copy_(u.bool())
+            else:
+                self.allreduce(t, op)
+
+        def gather(t: torch.Tensor) -> List[torch.Tensor]:
+            t = t.contiguous()
+            n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+            sizes = [int(v) for v in self.allgather(n).reshape(-1).tolist()]
+            flat = self.allgatherv(t.reshape(-1), sizes)
+            out, off = [], 0
+            for k in sizes:
+                out.append(flat[off:off + k])
+                off += k
+            return out
+        red.gather = gather
+        return red
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None:
             h, self._h = self._h, None

@@ -7,7 +7,9 @@ training call over it (``beast_bpe_train_comm``).
   (``beast_comm_init``); every reduction (SUM / MIN / MAX over u8 / i32 / i64 / f32 / f64), the
   all-gather and the all-gather-v run on the box's GPU, and ``beast_bpe_train_comm`` -- range and
   presence all-reduced, the distinct words all-gathered and repacked as a union -- returns the
-  HF golden vocabularies / merges of tests/golden/bpe_hf.json, equal to ``beast_bpe_train``.
+  HF golden vocabularies / merges of tests/golden/bpe_hf.json, equal to ``beast_bpe_train``; the
+  Python driver over the same communicator (``Communicator.reducer``), replicated and sharded,
+  matches the golden too.
   Ranks > 1 need one GPU each; the same exchange is rehearsed over gloo by
   tests/test_gpu_collectives.py (the Python driver's form).
 """
@@ -78,6 +80,17 @@ def _child(q):
                          (a.min_token, a.max_token) == (ref["min_token"], ref["max_token"]),
                          a.vocab == b.vocab and a.merges == b.merges, a.stats["world"])
         out["bpe"] = bpe
+        # the Python driver over this communicator: replicated (one gather) and sharded (per-pass
+        # delta all-reduce between the merge and apply launches)
+        from beast_tokenizer_amd.bpe_train import train_bpe
+        ref = load_json("bpe_hf.json")["skew/2048"]
+        flat, off = fixed_rows_to_device(torch.from_numpy(corpora["skew"].astype(np.int64)).to(dev))
+        py = {}
+        for replicate in (True, False):
+            r = train_bpe(flat, off, 2048, reduce=comm.reducer(), replicate=replicate)
+            py[replicate] = (r.vocab == ref["vocab"], [list(m) for m in r.merges] == ref["merges"],
+                             bool(r.stats.get("replicated")), bool(r.stats.get("sharded")))
+        out["py"] = py
         from beast_tokenizer_amd import _lib   # the rerun after a collision repeats the collectives
         lib = _lib.load()
         lib.beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, 2)
@@ -128,6 +141,8 @@ def test_comm_world1_collectives_and_training(gpu_device):
     assert len(out["bpe"]) >= 3, out["bpe"]
     for case, flags in out["bpe"].items():
         assert flags == (True, True, True, True, 1), (case, flags)
+    assert out["py"][True] == (True, True, True, False), out["py"]
+    assert out["py"][False] == (True, True, False, True), out["py"]
     assert out["rerun"] == (True, True)
     assert "No non-empty sequences" in out["empty"], out["empty"]
     assert out["init_all"] == (1, 1, 0, [1.0] * 5)
