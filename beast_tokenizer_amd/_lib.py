@@ -107,7 +107,7 @@ SIGNATURES = {
     "beast_comm_allgather": (_i32, [_vp, _vp, _vp, _i64, _i32, _vp]),
     "beast_comm_allgatherv": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "beast_bpe_train_comm": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _sz, _vp,
-                                    _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
+                                    _i32, _vp, _vp, _i32, _vp, _vp, _i32, _vp]),
     "beast_bpe_wordmap_log2buckets": (_i32, [_i32]),
     "beast_bpe_wordmap_bytes": (_sz, [_i32]),
     "beast_bpe_wordmap_build_host": (_i32, [_vp, _vp, _vp, _i32, _vp, _sz, _vp]),

@@ -640,11 +640,12 @@ def fixed_rows_to_device(tokens: torch.Tensor) -> Tuple[torch.Tensor, torch.Tens
 
 def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int, *, min_frequency: int = 2,
                    special_tokens: Sequence[str] = (), max_token_length: Optional[int] = 10000,
-                   vocab_bytes_cap: Optional[int] = None, comm=None) -> BPEResult:
+                   vocab_bytes_cap: Optional[int] = None, comm=None, replicate: bool = True) -> BPEResult:
     """The same training through the one-call C-ABI ``beast_bpe_train`` (include/beast_hip.h):
     what a non-Python caller binds.  ``comm`` (a :class:`beast_tokenizer_amd.comm.Communicator`)
-    trains over every rank's shard with ``beast_bpe_train_comm`` (the replicated form: one
-    all-gather of the distinct words, every rank returns the same result).  Vt > 4096 runs the
+    trains over every rank's shard with ``beast_bpe_train_comm``: replicated (one all-gather of
+    the distinct words) or, ``replicate=False``, sharded (a per-pass delta all-reduce); every
+    rank returns the same result.  Vt > 4096 runs the
     C++ host-driven loop; raises NotImplementedError above 32768 (the dense pair table)."""
     import ctypes
     dev = tokens.device
@@ -678,7 +679,7 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
         if comm is None:
             rc = _lib.call("beast_bpe_train", *args, _lib.stream_of(dev))
         else:
-            rc = _lib.call("beast_bpe_train_comm", *args, comm.handle, _lib.stream_of(dev))
+            rc = _lib.call("beast_bpe_train_comm", *args, comm.handle, int(bool(replicate)), _lib.stream_of(dev))
         if rc != _lib.BEAST_E_WORKSPACE or attempt:
             _lib.check(rc, "beast_bpe_train")
             break
@@ -693,4 +694,5 @@ def train_bpe_capi(tokens: torch.Tensor, seq_off: torch.Tensor, vocab_size: int,
     pairs = [(id2str[int(merges[2 * m])], id2str[int(merges[2 * m + 1])]) for m in range(nm)]
     return BPEResult(vocab={t: i for i, t in enumerate(id2str)}, merges=pairs, min_token=out[0].value,
                      max_token=out[1].value, stats={"capi": True, "n_merges": nm, "retried": retried,
-                                                    "world": comm.world if comm is not None else 1})
+                                                    "world": comm.world if comm is not None else 1,
+                                                    "replicated": comm is None or bool(replicate)})

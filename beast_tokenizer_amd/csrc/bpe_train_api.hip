@@ -238,8 +238,8 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
                           const char* const* special_tokens, int n_special, int64_t* out_min_token,
                           int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
                           int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
-                          int max_merges_out, int* out_n_merges, beast_comm* comm, bool host_loop,
-                          void* stream) {
+                          int max_merges_out, int* out_n_merges, beast_comm* comm, bool replicate,
+                          bool host_loop, void* stream) {
   BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
                     out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
                 "beast_bpe_train: null pointer argument");
@@ -351,7 +351,8 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   uint32_t *w2 = nullptr, *l2 = nullptr, *c2 = nullptr;
   int64_t nu = 0, nsp = 0;
   if (n_tok > 0) TRY(shard_words(mem, tokens, seq_off, n_seq, mn, cls_lut, lut_n, byte2id, sym2, w2, l2, c2, nu, nsp, s));
-  if (comm != nullptr) TRY(union_words(mem, comm, sym2, w2, l2, c2, nu, nsp, s));
+  const bool sharded = comm != nullptr && !replicate;   // every rank keeps its shard of the words
+  if (comm != nullptr && replicate) TRY(union_words(mem, comm, sym2, w2, l2, c2, nu, nsp, s));
   if (sym2 == nullptr) {   // no words anywhere: an empty table, the loop stops at once
     ALLOC(z16, uint16_t, 4);
     ALLOC(z32, uint32_t, 3);
@@ -366,6 +367,7 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   ALLOC(table, uint32_t, (size_t)Vt * Vt);
   BEAST_HIP(hipMemsetAsync(table, 0, sizeof(uint32_t) * (size_t)Vt * Vt, s), "pair table memset");
   TRY(beast_bpe_count_pairs(sym2, w2, l2, c2, nu, table, Vt, n_base, stream));
+  if (sharded) TRY(beast_comm_allreduce(comm, table, table, (int64_t)Vt * Vt, BEAST_DT_U32, BEAST_OP_SUM, stream));
   std::vector<uint64_t> hp(2 * (size_t)n_base);   // [0, n): string hash, [n, 2n): P^bytes
   std::vector<uint32_t> tlen(Vt, 0u);
   int max_tlen = 0;
@@ -390,8 +392,8 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   auto rerun_on_host = [&]() {
     return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
                           special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                          out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, true,
-                          stream);
+                          out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
+                          replicate, true, stream);
   };
   std::vector<int32_t> log;
   int n_log = 0;
@@ -437,6 +439,7 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
       log.insert(log.end(), {a, b, nid, reused ? 1 : 0});
       ++n_log;
       TRY(beast_bpe_merge(sym2, w2, l2, c2, nu, a, b, nid, tlen_d, max_len, deltas, Vt, sig, (int64_t)count, stream));
+      if (sharded) TRY(beast_comm_allreduce(comm, deltas, deltas, 4 * (int64_t)Vt, BEAST_DT_I32, BEAST_OP_SUM, stream));
       const int k = call++;
       TRY(beast_bpe_apply_argmax(table, deltas, Vt, (int)ids.size(), a, b, nid, tlen_d, argws, k, stream));
       if ((int)ids.size() >= vocab_size) break;   // last merge: applied without searching again
@@ -457,9 +460,16 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
     const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
     ALLOC(bws, uint8_t, bw_bytes);
+    int32_t* bdeltas = nullptr;   // sharded: each pass's pair-count changes, summed over the ranks
+    const size_t nbd = beast_bpe_batch_delta_count(Vt);
+    if (sharded) {
+      bdeltas = mem.get<int32_t>(nbd);
+      BEAST_REQUIRE_CODE(bdeltas != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of the pass deltas failed");
+      BEAST_HIP(hipMemsetAsync(bdeltas, 0, sizeof(int32_t) * nbd, s), "pass deltas memset");
+    }
     auto run = [&](int steps, int flags) {
       return beast_bpe_loop_batch(lws, Vt, max_merges, steps, KMAX, flags, sym2, w2, l2, c2, nu, tlen_d, max_len, sig,
-                                  table, argws, bws, bw_bytes, vocab_size, nullptr, nullptr, stream);
+                                  table, argws, bws, bw_bytes, vocab_size, bdeltas, nullptr, stream);
     };
 
     // ---- the loop: two chunks of passes in flight, the host reads the state the older one left
@@ -484,8 +494,26 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
       return BEAST_OK;
     };
     int vcur = n_base, rc = BEAST_OK;
-    rc = launch(std::max(1, std::min(CHUNK, (vocab_size - vcur + KMAX - 1) / KMAX)), 1 /* BATCH_INIT */);
-    while (rc == BEAST_OK) {
+    if (sharded) {
+      // every rank holds the same table and takes the same decisions, so every rank runs the same
+      // passes and collectives: merge on the shard, SUM of the pass's deltas, apply (bpe_train.py)
+      TRY(run(0, 1 /* BATCH_INIT */));
+      while (true) {
+        const int steps = std::max(1, std::min(CHUNK, (vocab_size - vcur + 1) / 2));
+        for (int i = 0; i < steps; ++i) {
+          TRY(run(1, BEAST_BPE_BATCH_NO_APPLY));
+          TRY(beast_comm_allreduce(comm, bdeltas, bdeltas, (int64_t)nbd, BEAST_DT_I32, BEAST_OP_SUM, stream));
+          TRY(run(1, BEAST_BPE_BATCH_NO_MERGE));
+        }
+        int32_t st[16];
+        BEAST_HIP(hipMemcpyAsync(st, st_p, sizeof(st), hipMemcpyDeviceToHost, s), "loop state read");
+        BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+        vcur = st[ST_VCUR];
+        if (!st[ST_ACTIVE] || vcur >= vocab_size) break;
+      }
+    }
+    if (!sharded) rc = launch(std::max(1, std::min(CHUNK, (vocab_size - vcur + KMAX - 1) / KMAX)), 1 /* BATCH_INIT */);
+    while (!sharded && rc == BEAST_OK) {
       int queued = 0;
       for (auto& f : inflight) queued += f.passes;
       const int left = vocab_size - vcur - 4 * queued;
@@ -575,8 +603,8 @@ extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, in
                                int max_merges_out, int* out_n_merges, void* stream) {
   return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, false,
-                        stream);
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, true,
+                        false, stream);
 }
 
 extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq,
@@ -585,9 +613,9 @@ extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_of
                                     int64_t* out_min_token, int64_t* out_max_token, char* out_vocab_bytes,
                                     size_t vocab_bytes_cap, int64_t* out_vocab_off, int max_vocab, int* out_n_vocab,
                                     int32_t* out_merges, int max_merges_out, int* out_n_merges, beast_comm* comm,
-                                    void* stream) {
+                                    int replicate, void* stream) {
   return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm, false,
-                        stream);
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
+                        replicate != 0, false, stream);
 }

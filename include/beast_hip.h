@@ -369,14 +369,18 @@ int beast_comm_allgatherv(beast_comm* comm, const void* send, void* recv, const 
  * range is all-reduced (MIN / MAX), the code-point presence (MAX), each rank pre-tokenises and
  * deduplicates its shard, the distinct words x counts are all-gathered once (rank order) and
  * every rank runs the batched loop on the union -- bpe_train.py's replicated form, no per-pass
- * collective.  Every rank returns the same vocabulary and merges; a shard may be empty.  All
- * ranks must call it with the same options.  comm == NULL is beast_bpe_train. */
+ * collective (replicate != 0).  replicate == 0 is the sharded form: every rank keeps its own
+ * words, the pair table is SUM-reduced once and each pass's pair-count changes are SUM-reduced
+ * between its merge and apply launches (the host-driven loop: each merge's), so the words of
+ * no single GPU need to hold the corpus.  Every rank returns the same vocabulary and merges; a
+ * shard may be empty (replicated form).  All ranks must call it with the same options.
+ * comm == NULL is beast_bpe_train. */
 int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                          int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
                          const char* const* special_tokens, int n_special, int64_t* out_min_token,
                          int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap, int64_t* out_vocab_off,
                          int max_vocab, int* out_n_vocab, int32_t* out_merges, int max_merges_out, int* out_n_merges,
-                         beast_comm* comm, void* stream);
+                         beast_comm* comm, int replicate, void* stream);
 /* Distinct words (HF BpeTrainer trains on word -> count): every word of >= 2 symbols is
  * matched by content (hash tag + symbol-by-symbol compare, so collisions never merge
  * different words); out_* get one entry per distinct word (its first-seen copy in sym),

@@ -9,7 +9,8 @@ training call over it (``beast_bpe_train_comm``).
   presence all-reduced, the distinct words all-gathered and repacked as a union -- returns the
   HF golden vocabularies / merges of tests/golden/bpe_hf.json, equal to ``beast_bpe_train``; the
   Python driver over the same communicator (``Communicator.reducer``), replicated and sharded,
-  matches the golden too.
+  and the C call's sharded form (``replicate=0``: batched and host-driven loops) match the golden
+  too.
   Ranks > 1 need one GPU each; the same exchange is rehearsed over gloo by
   tests/test_gpu_collectives.py (the Python driver's form).
 """
@@ -80,6 +81,23 @@ def _child(q):
                          (a.min_token, a.max_token) == (ref["min_token"], ref["max_token"]),
                          a.vocab == b.vocab and a.merges == b.merges, a.stats["world"])
         out["bpe"] = bpe
+        # the sharded form in C: batched loop (pass deltas all-reduced) and host-driven loop
+        # (each merge's deltas all-reduced; BEAST_OPT_BPE_TRAIN_HOST_LOOP = 1)
+        from beast_tokenizer_amd import _lib
+        sh = {}
+        for case in ("skew/2048", "traj_k3/700"):
+            ref = load_json("bpe_hf.json")[case]
+            cname, vs = case.split("/")
+            flat, off = fixed_rows_to_device(torch.from_numpy(corpora[cname].astype(np.int64)).to(dev))
+            for mode in (0, 1):
+                _lib.load().beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, mode)
+                try:
+                    a = train_bpe_capi(flat, off, int(vs), comm=comm, replicate=False)
+                finally:
+                    _lib.load().beast_set_option(_lib.OPT_BPE_TRAIN_HOST_LOOP, 0)
+                sh[(case, mode)] = (a.vocab == ref["vocab"], [list(m) for m in a.merges] == ref["merges"],
+                                    a.stats["replicated"])
+        out["sharded"] = sh
         # the Python driver over this communicator: replicated (one gather) and sharded (per-pass
         # delta all-reduce between the merge and apply launches)
         from beast_tokenizer_amd.bpe_train import train_bpe
@@ -144,5 +162,7 @@ def test_comm_world1_collectives_and_training(gpu_device):
     assert out["py"][True] == (True, True, True, False), out["py"]
     assert out["py"][False] == (True, True, False, True), out["py"]
     assert out["rerun"] == (True, True)
+    assert len(out["sharded"]) == 4 and all(v == (True, True, False) for v in out["sharded"].values()), \
+        out["sharded"]
     assert "No non-empty sequences" in out["empty"], out["empty"]
     assert out["init_all"] == (1, 1, 0, [1.0] * 5)
