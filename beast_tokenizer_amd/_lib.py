@@ -101,6 +101,9 @@ SIGNATURES = {
     "beast_comm_unique_id": (_i32, [_vp]),
     "beast_comm_init_rank": (_i32, [_i32, _i32, _vp, _i32, _vp]),
     "beast_comm_init": (_i32, [_i32, _vp, _vp]),
+    "beast_comm_init_virtual": (_i32, [_i32, _i32, _vp]),
+    "beast_comm_group_start": (_i32, []),
+    "beast_comm_group_end": (_i32, []),
     "beast_comm_destroy": (_i32, [_vp]),
     "beast_comm_info": (_i32, [_vp, _vp, _vp, _vp]),
     "beast_comm_allreduce": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp]),

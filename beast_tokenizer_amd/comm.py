@@ -13,9 +13,16 @@ One process per GPU::
     comm.allreduce(w_min, "min")            # §8e running bounds, in place
     result = train_bpe_capi(tokens, seq_off, vocab, comm=comm)   # bpe_train.py
     comm.close()
+
+Several devices from one process (``init_all``): issue each round of collectives inside
+``with Communicator.group():`` -- or drive every handle from its own thread, which is also how
+``train_bpe_capi(..., comm=...)`` must be called on such handles.  ``init_virtual(n)`` gives n
+ranks on one device (one thread each), which is how the tests run the multi-rank paths on a
+one-GPU box.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from typing import List, Sequence
 
@@ -63,6 +70,28 @@ class Communicator:
         hs = (C.c_void_p * n)()
         _lib.check(lib.beast_comm_init(n, devs, hs), "beast_comm_init")
         return [cls(n, i, b"", d, _handle=hs[i]) for i, d in enumerate(devices)]
+
+    @classmethod
+    def init_virtual(cls, n: int, device: int = 0) -> List["Communicator"]:
+        """``n`` virtual ranks on one device (``beast_comm_init_virtual``; SURVEY §4.3's "N
+        virtual ranks on one device"): drive handle ``r`` from its own host thread; collectives
+        meet in host memory.  For tests and rehearsal on a one-GPU box."""
+        lib = _lib.load()
+        hs = (C.c_void_p * n)()
+        _lib.check(lib.beast_comm_init_virtual(n, device, hs), "beast_comm_init_virtual")
+        return [cls(n, i, b"", device, _handle=hs[i]) for i in range(n)]
+
+    @staticmethod
+    @contextlib.contextmanager
+    def group():
+        """``beast_comm_group_start`` / ``_end`` around the collectives of the single-process form
+        (``init_all`` with several devices driven from one thread), as RCCL requires."""
+        lib = _lib.load()
+        _lib.check(lib.beast_comm_group_start(), "beast_comm_group_start")
+        try:
+            yield
+        finally:
+            _lib.check(lib.beast_comm_group_end(), "beast_comm_group_end")
 
     @property
     def handle(self) -> C.c_void_p:

@@ -96,6 +96,22 @@ constexpr int KMAX = 8, CHUNK = 64;
   T* var = mem.get<T>(n);                                                        \
   BEAST_REQUIRE_CODE(var != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of %zu x %zu bytes failed", \
                      (size_t)(n), sizeof(T))
+#define ALLOC_TO(var, T, n)                                                                                \
+  do {                                                                                                     \
+    var = mem.get<T>(n);                                                                                   \
+    BEAST_REQUIRE_CODE(var != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of %zu x %zu bytes failed", \
+                       (size_t)(n), sizeof(T));                                                            \
+  } while (0)
+// Every rank of a communicator must issue the same collectives in the same order.  A local phase
+// that fails on one rank therefore still reaches the agreement that ends it (the status all-reduced
+// with MAX, beast::comm_agree), where every rank learns of the failure and returns it together --
+// a rank returning alone would leave the others blocked in the next collective.  Without a
+// communicator AGREE is TRY.
+#define AGREE(...)   /* variadic: a lambda argument may hold commas */ \
+  do {                                                              \
+    const int a_ = beast::comm_agree(comm, (__VA_ARGS__), s);       \
+    if (a_ != BEAST_OK) return a_;                                  \
+  } while (0)
 
 namespace {
 
@@ -173,9 +189,13 @@ int union_words(DevMem& mem, beast_comm* comm, uint16_t*& sym2, uint32_t*& w2, u
   void* stream = s;
   int world = 0, rank = 0;
   TRY(beast_comm_info(comm, &world, &rank, nullptr));
-  ALLOC(sz, int64_t, 2 + 2 * (size_t)world);
+  int64_t* sz = nullptr;
   const int64_t mine[2] = {nu, nsp};
-  BEAST_HIP(hipMemcpyAsync(sz, mine, sizeof(mine), hipMemcpyHostToDevice, s), "size upload");
+  AGREE([&]() -> int {
+    ALLOC_TO(sz, int64_t, 2 + 2 * (size_t)world);
+    BEAST_HIP(hipMemcpyAsync(sz, mine, sizeof(mine), hipMemcpyHostToDevice, s), "size upload");
+    return BEAST_OK;
+  }());
   TRY(beast_comm_allgather(comm, sz, sz + 2, 2, BEAST_DT_I64, stream));
   std::vector<int64_t> all(2 * (size_t)world);
   BEAST_HIP(hipMemcpyAsync(all.data(), sz + 2, sizeof(int64_t) * all.size(), hipMemcpyDeviceToHost, s), "size read");
@@ -190,6 +210,7 @@ int union_words(DevMem& mem, beast_comm* comm, uint16_t*& sym2, uint32_t*& w2, u
     NU += all[2 * r];
     NS += all[2 * r + 1];
   }
+  // the sizes are every rank's alike: so is this check's outcome
   BEAST_REQUIRE_CODE(NS + 3 * NU < (int64_t(1) << 32), BEAST_E_UNSUPPORTED,
                      "beast_bpe_train: the shards' distinct words hold >= 2^32 symbols; the replicated loop keeps them on "
                      "every GPU");
@@ -198,14 +219,20 @@ int union_words(DevMem& mem, beast_comm* comm, uint16_t*& sym2, uint32_t*& w2, u
     nu = nsp = 0;
     return BEAST_OK;
   }
-  ALLOC(gsym, uint16_t, NS);
-  ALLOC(gw, uint32_t, NU);
-  ALLOC(gl, uint32_t, NU);
-  ALLOC(gc, uint32_t, NU);
+  uint16_t* gsym = nullptr;
+  uint32_t *gw = nullptr, *gl = nullptr, *gc = nullptr;
+  AGREE([&]() -> int {
+    ALLOC_TO(gsym, uint16_t, NS);
+    ALLOC_TO(gw, uint32_t, NU);
+    ALLOC_TO(gl, uint32_t, NU);
+    ALLOC_TO(gc, uint32_t, NU);
+    return BEAST_OK;
+  }());
   TRY(beast_comm_allgatherv(comm, sym2, gsym, bc.data(), bd.data(), BEAST_DT_U8, stream));
   TRY(beast_comm_allgatherv(comm, w2, gw, wc.data(), wd.data(), BEAST_DT_U32, stream));
   TRY(beast_comm_allgatherv(comm, l2, gl, wc.data(), wd.data(), BEAST_DT_U32, stream));
   TRY(beast_comm_allgatherv(comm, c2, gc, wc.data(), wd.data(), BEAST_DT_U32, stream));
+  // local from here on: the caller agrees before its next collective
   for (int r = 0; r < world; ++r)
     if (wc[r] > 0 && bd[r] > 0) {
       hipLaunchKernelGGL(k_offset_starts, dim3((unsigned)((wc[r] + 255) / 256)), dim3(256), 0, s, gw + wd[r], wc[r],
@@ -233,6 +260,11 @@ namespace beast {
 int g_bpe_train_host = 0;
 }
 
+// the batched loop asks for the host-driven one (a 64-bit string-hash collision, or a full merge
+// log): bpe_train_impl returns RERUN after releasing every device buffer of the attempt, and the
+// entry points train again with host_loop set -- the peak memory stays one training's
+constexpr int RERUN = 1;
+
 static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                           int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
                           const char* const* special_tokens, int n_special, int64_t* out_min_token,
@@ -240,18 +272,23 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
                           int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
                           int max_merges_out, int* out_n_merges, beast_comm* comm, bool replicate,
                           bool host_loop, void* stream) {
-  BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
-                    out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
-                "beast_bpe_train: null pointer argument");
-  BEAST_REQUIRE(n_seq >= 1 && vocab_size >= 1 && n_special >= 0, "beast_bpe_train: bad sizes");
   hipStream_t s = beast::as_stream(stream);
   DevMem mem;
+  // ---- arguments, this shard's token count
   int64_t n_tok = 0;
-  BEAST_HIP(hipMemcpyAsync(&n_tok, seq_off + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "seq_off read");
-  BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  BEAST_REQUIRE(n_tok >= 0 && (n_tok == 0 || tokens != nullptr), "beast_bpe_train: null pointer argument");
+  int64_t* red = nullptr;
+  AGREE([&]() -> int {
+    BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
+                      out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
+                  "beast_bpe_train: null pointer argument");
+    BEAST_REQUIRE(n_seq >= 1 && vocab_size >= 1 && n_special >= 0, "beast_bpe_train: bad sizes");
+    BEAST_HIP(hipMemcpyAsync(&n_tok, seq_off + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "seq_off read");
+    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    BEAST_REQUIRE(n_tok >= 0 && (n_tok == 0 || tokens != nullptr), "beast_bpe_train: null pointer argument");
+    ALLOC_TO(red, int64_t, 2);
+    return BEAST_OK;
+  }());
   // with a communicator: the shards' token count, range and code points are the corpus's
-  ALLOC(red, int64_t, 2);
   if (comm != nullptr) {
     BEAST_HIP(hipMemcpyAsync(red, &n_tok, sizeof(int64_t), hipMemcpyHostToDevice, s), "token count upload");
     TRY(beast_comm_allreduce(comm, red, red, 1, BEAST_DT_I64, BEAST_OP_SUM, stream));
@@ -266,12 +303,15 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   // ---- min / max (reference :86-87), the code points present
   constexpr int64_t NONE = int64_t(1) << 62;   // an empty shard's (min, -max)
   int64_t mmh[2] = {NONE, -NONE};
-  if (n_tok > 0) {
-    ALLOC(mm, int64_t, 2);
-    TRY(beast_i64_minmax(tokens, n_tok, mm, stream));
-    BEAST_HIP(hipMemcpyAsync(mmh, mm, sizeof(mmh), hipMemcpyDeviceToHost, s), "minmax read");
-    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-  }
+  AGREE([&]() -> int {
+    if (n_tok > 0) {
+      ALLOC(mm, int64_t, 2);
+      TRY(beast_i64_minmax(tokens, n_tok, mm, stream));
+      BEAST_HIP(hipMemcpyAsync(mmh, mm, sizeof(mmh), hipMemcpyDeviceToHost, s), "minmax read");
+      BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+    }
+    return BEAST_OK;
+  }());
   if (comm != nullptr) {   // one MIN over (min, -max)
     int64_t lo_nhi[2] = {mmh[0], -mmh[1]};
     BEAST_HIP(hipMemcpyAsync(red, lo_nhi, sizeof(lo_nhi), hipMemcpyHostToDevice, s), "range upload");
@@ -282,17 +322,21 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     mmh[1] = -lo_nhi[1];
   }
   const int64_t mn = mmh[0], mx = mmh[1], K = mx - mn;
-  BEAST_REQUIRE_CODE(K < 0xD800, BEAST_E_UNSUPPORTED,
-                     "BPE alphabet reaches the UTF-16 surrogate range (max - min token >= 55296)");
-  BEAST_REQUIRE(lut_n >= K + 1, "beast_bpe_train: class LUT covers %lld code points, the corpus needs %lld",
-                (long long)lut_n, (long long)(K + 1));
   const int64_t n_cp = K + 1;
-  ALLOC(pr, uint8_t, n_cp);
-  if (n_tok > 0) {
-    TRY(beast_bpe_cp_presence(tokens, n_tok, mn, pr, n_cp, stream));
-  } else {
-    BEAST_HIP(hipMemsetAsync(pr, 0, n_cp, s), "presence memset");
-  }
+  uint8_t* pr = nullptr;
+  AGREE([&]() -> int {
+    BEAST_REQUIRE_CODE(K < 0xD800, BEAST_E_UNSUPPORTED,
+                       "BPE alphabet reaches the UTF-16 surrogate range (max - min token >= 55296)");
+    BEAST_REQUIRE(lut_n >= K + 1, "beast_bpe_train: class LUT covers %lld code points, the corpus needs %lld",
+                  (long long)lut_n, (long long)(K + 1));
+    ALLOC_TO(pr, uint8_t, n_cp);
+    if (n_tok > 0) {
+      TRY(beast_bpe_cp_presence(tokens, n_tok, mn, pr, n_cp, stream));
+    } else {
+      BEAST_HIP(hipMemsetAsync(pr, 0, n_cp, s), "presence memset");
+    }
+    return BEAST_OK;
+  }());
   if (comm != nullptr) TRY(beast_comm_allreduce(comm, pr, pr, n_cp, BEAST_DT_U8, BEAST_OP_MAX, stream));
   std::vector<uint8_t> present(n_cp);
   BEAST_HIP(hipMemcpyAsync(present.data(), pr, n_cp, hipMemcpyDeviceToHost, s), "presence read");
@@ -339,34 +383,47 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   }
   const int n_base = (int)id2str.size();
   const int Vt = std::max(vocab_size, n_base);
-  BEAST_REQUIRE_CODE(Vt <= 32768, BEAST_E_UNSUPPORTED,
-                     "beast_bpe_train: Vt %d > 32768 (the dense pair table)", Vt);
-  BEAST_REQUIRE_CODE(max_vocab >= Vt && max_merges_out >= std::max(vocab_size - n_base, 0), BEAST_E_WORKSPACE,
-                     "beast_bpe_train: output capacity (vocab %d, merges %d) below the vocabulary size %d", max_vocab,
-                     max_merges_out, Vt);
 
   // ---- this shard's distinct words x counts, length-ordered (sym2 / w2 / l2 / c2, nu words,
   // nsp padded symbols), then with a communicator the union of every rank's
   uint16_t* sym2 = nullptr;
   uint32_t *w2 = nullptr, *l2 = nullptr, *c2 = nullptr;
   int64_t nu = 0, nsp = 0;
-  if (n_tok > 0) TRY(shard_words(mem, tokens, seq_off, n_seq, mn, cls_lut, lut_n, byte2id, sym2, w2, l2, c2, nu, nsp, s));
+  AGREE([&]() -> int {
+    BEAST_REQUIRE_CODE(Vt <= 32768, BEAST_E_UNSUPPORTED, "beast_bpe_train: Vt %d > 32768 (the dense pair table)", Vt);
+    if (max_vocab < Vt || max_merges_out < std::max(vocab_size - n_base, 0)) {
+      // the sizes a retry needs (upper bounds until the training has run)
+      *out_n_vocab = Vt;
+      *out_n_merges = std::max(vocab_size - n_base, 0);
+      BEAST_REQUIRE_CODE(false, BEAST_E_WORKSPACE,
+                         "beast_bpe_train: output capacity (vocab %d, merges %d) below the vocabulary size %d; the "
+                         "required sizes are in *out_n_vocab, *out_n_merges",
+                         max_vocab, max_merges_out, Vt);
+    }
+    if (n_tok > 0) TRY(shard_words(mem, tokens, seq_off, n_seq, mn, cls_lut, lut_n, byte2id, sym2, w2, l2, c2, nu, nsp, s));
+    return BEAST_OK;
+  }());
   const bool sharded = comm != nullptr && !replicate;   // every rank keeps its shard of the words
   if (comm != nullptr && replicate) TRY(union_words(mem, comm, sym2, w2, l2, c2, nu, nsp, s));
-  if (sym2 == nullptr) {   // no words anywhere: an empty table, the loop stops at once
-    ALLOC(z16, uint16_t, 4);
-    ALLOC(z32, uint32_t, 3);
-    BEAST_HIP(hipMemsetAsync(z16, 0, 8, s), "empty words");
-    BEAST_HIP(hipMemsetAsync(z32, 0, 12, s), "empty words");
-    sym2 = z16, w2 = z32, l2 = z32 + 1, c2 = z32 + 2;
-  }
-  ALLOC(sig, uint64_t, nu);
-  if (nu > 0) TRY(beast_bpe_word_signatures(sym2, w2, l2, nu, sig, stream));
 
   // ---- the pair table and the loop state
-  ALLOC(table, uint32_t, (size_t)Vt * Vt);
-  BEAST_HIP(hipMemsetAsync(table, 0, sizeof(uint32_t) * (size_t)Vt * Vt, s), "pair table memset");
-  TRY(beast_bpe_count_pairs(sym2, w2, l2, c2, nu, table, Vt, n_base, stream));
+  uint64_t* sig = nullptr;
+  uint32_t* table = nullptr;
+  AGREE([&]() -> int {
+    if (sym2 == nullptr) {   // no words anywhere: an empty table, the loop stops at once
+      ALLOC(z16, uint16_t, 4);
+      ALLOC(z32, uint32_t, 3);
+      BEAST_HIP(hipMemsetAsync(z16, 0, 8, s), "empty words");
+      BEAST_HIP(hipMemsetAsync(z32, 0, 12, s), "empty words");
+      sym2 = z16, w2 = z32, l2 = z32 + 1, c2 = z32 + 2;
+    }
+    ALLOC_TO(sig, uint64_t, nu);
+    if (nu > 0) TRY(beast_bpe_word_signatures(sym2, w2, l2, nu, sig, stream));
+    ALLOC_TO(table, uint32_t, (size_t)Vt * Vt);
+    BEAST_HIP(hipMemsetAsync(table, 0, sizeof(uint32_t) * (size_t)Vt * Vt, s), "pair table memset");
+    TRY(beast_bpe_count_pairs(sym2, w2, l2, c2, nu, table, Vt, n_base, stream));
+    return BEAST_OK;
+  }());
   if (sharded) TRY(beast_comm_allreduce(comm, table, table, (int64_t)Vt * Vt, BEAST_DT_U32, BEAST_OP_SUM, stream));
   std::vector<uint64_t> hp(2 * (size_t)n_base);   // [0, n): string hash, [n, 2n): P^bytes
   std::vector<uint32_t> tlen(Vt, 0u);
@@ -382,46 +439,47 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     tlen[i] = (uint32_t)utf8_chars(id2str[i]);
     max_tlen = std::max(max_tlen, (int)tlen[i]);
   }
-  ALLOC(hp_d, uint64_t, hp.size());
-  ALLOC(tlen_d, uint32_t, Vt);
-  BEAST_HIP(hipMemcpyAsync(hp_d, hp.data(), sizeof(uint64_t) * hp.size(), hipMemcpyHostToDevice, s), "hash upload");
-  BEAST_HIP(hipMemcpyAsync(tlen_d, tlen.data(), sizeof(uint32_t) * Vt, hipMemcpyHostToDevice, s), "tlen upload");
   const int max_len = max_token_length > 0 ? max_token_length : 0x7FFFFFFF;
-  // the same training from scratch on the host-driven loop (a string-hash collision or a full
-  // merge log of the batched one); every rank of a communicator takes the same decision
-  auto rerun_on_host = [&]() {
-    return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
-                          special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                          out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
-                          replicate, true, stream);
-  };
   std::vector<int32_t> log;
   int n_log = 0;
   if (host_loop || Vt > 4096 || beast::g_bpe_train_host == 1) {
     // ---- host-driven loop (bpe_train.py train_bpe below the device loop): argmax, merge in
     // every word, apply + next argmax; one host read of the decided pair per merge
-    const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
-    ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
-    BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
-    ALLOC(deltas, int32_t, 4 * (size_t)Vt);
-    BEAST_HIP(hipMemsetAsync(deltas, 0, sizeof(int32_t) * 4 * (size_t)Vt, s), "deltas memset");
+    uint64_t* hp_d = nullptr;
+    uint32_t* tlen_d = nullptr;
+    uint64_t* argws = nullptr;
+    int32_t* deltas = nullptr;
     HostPinned kh;
-    BEAST_HIP(hipHostMalloc(&kh.p, 64, hipHostMallocDefault), "pinned key");
-    uint64_t* key_h = static_cast<uint64_t*>(kh.p);
-    auto read_key = [&](int call, uint64_t& key) -> int {
-      BEAST_HIP(hipMemcpyAsync(key_h, argws + 2 + (call & 1), sizeof(uint64_t), hipMemcpyDeviceToHost, s),
-                "argmax read");
+    uint64_t key = 0;
+    int call = 0;
+    auto read_key = [&](int k, uint64_t& out) -> int {
+      uint64_t* key_h = static_cast<uint64_t*>(kh.p);
+      BEAST_HIP(hipMemcpyAsync(key_h, argws + 2 + (k & 1), sizeof(uint64_t), hipMemcpyDeviceToHost, s), "argmax read");
       BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-      key = *key_h;
+      out = *key_h;
       return BEAST_OK;
     };
+    AGREE([&]() -> int {
+      ALLOC_TO(hp_d, uint64_t, hp.size());
+      ALLOC_TO(tlen_d, uint32_t, Vt);
+      BEAST_HIP(hipMemcpyAsync(hp_d, hp.data(), sizeof(uint64_t) * hp.size(), hipMemcpyHostToDevice, s), "hash upload");
+      BEAST_HIP(hipMemcpyAsync(tlen_d, tlen.data(), sizeof(uint32_t) * Vt, hipMemcpyHostToDevice, s), "tlen upload");
+      const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
+      ALLOC_TO(argws, uint64_t, (aw_bytes + 7) / 8);
+      BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
+      ALLOC_TO(deltas, int32_t, 4 * (size_t)Vt);
+      BEAST_HIP(hipMemsetAsync(deltas, 0, sizeof(int32_t) * 4 * (size_t)Vt, s), "deltas memset");
+      BEAST_HIP(hipHostMalloc(&kh.p, 64, hipHostMallocDefault), "pinned key");
+      TRY(beast_bpe_argmax(table, Vt, n_base, argws, call, stream));
+      TRY(read_key(call++, key));
+      return BEAST_OK;
+    }());
     std::vector<std::string> ids = id2str;
     std::unordered_map<std::string, int> ix = str2id;
-    int call = 0;
-    uint64_t key = 0;
-    TRY(beast_bpe_argmax(table, Vt, n_base, argws, call, stream));
-    TRY(read_key(call++, key));
-    while ((int)ids.size() < vocab_size) {
+    int lrc = BEAST_OK;   // sharded: a failure is agreed at the top of the next merge, before its collective
+    while (true) {
+      AGREE(lrc);
+      if ((int)ids.size() >= vocab_size) break;
       const uint64_t count = key >> 32;
       if (count < 1 || count < (uint64_t)std::max(min_frequency, 0)) break;
       const uint32_t idx = 0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFu);
@@ -438,43 +496,53 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
       }
       log.insert(log.end(), {a, b, nid, reused ? 1 : 0});
       ++n_log;
-      TRY(beast_bpe_merge(sym2, w2, l2, c2, nu, a, b, nid, tlen_d, max_len, deltas, Vt, sig, (int64_t)count, stream));
+      lrc = beast_bpe_merge(sym2, w2, l2, c2, nu, a, b, nid, tlen_d, max_len, deltas, Vt, sig, (int64_t)count, stream);
       if (sharded) TRY(beast_comm_allreduce(comm, deltas, deltas, 4 * (int64_t)Vt, BEAST_DT_I32, BEAST_OP_SUM, stream));
       const int k = call++;
-      TRY(beast_bpe_apply_argmax(table, deltas, Vt, (int)ids.size(), a, b, nid, tlen_d, argws, k, stream));
-      if ((int)ids.size() >= vocab_size) break;   // last merge: applied without searching again
-      TRY(read_key(k, key));
+      if (lrc == BEAST_OK)
+        lrc = beast_bpe_apply_argmax(table, deltas, Vt, (int)ids.size(), a, b, nid, tlen_d, argws, k, stream);
+      if (lrc == BEAST_OK && (int)ids.size() < vocab_size) lrc = read_key(k, key);   // the last merge: no search
     }
     BEAST_HIP(hipStreamSynchronize(s), "stream sync");
   } else {
     const int max_merges = 4 * std::max(vocab_size - n_base, 0) + 1024;
     const size_t lws_bytes = beast_bpe_loop_workspace_bytes(Vt, max_merges);
-    ALLOC(lws, uint8_t, lws_bytes);
-    TRY(beast_bpe_loop_init(lws, lws_bytes, Vt, max_merges, n_base, vocab_size, min_frequency, hp_d, hp_d + n_base,
-                            tlen_d, max_tlen, stream));
+    const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
+    const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
+    const size_t nbd = beast_bpe_batch_delta_count(Vt);
+    uint64_t* hp_d = nullptr;
+    uint32_t* tlen_d = nullptr;
+    uint8_t *lws = nullptr, *bws = nullptr;
+    uint64_t* argws = nullptr;
+    int32_t* bdeltas = nullptr;   // sharded: each pass's pair-count changes, summed over the ranks
     const void* st_p = nullptr;
     const void* log_p = nullptr;
-    TRY(beast_bpe_loop_state(lws, Vt, max_merges, &st_p, &log_p));
-    const size_t aw_bytes = beast_bpe_argmax_workspace_bytes(Vt);
-    ALLOC(argws, uint64_t, (aw_bytes + 7) / 8);
-    BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
-    const size_t bw_bytes = beast_bpe_batch_workspace_bytes(Vt);
-    ALLOC(bws, uint8_t, bw_bytes);
-    int32_t* bdeltas = nullptr;   // sharded: each pass's pair-count changes, summed over the ranks
-    const size_t nbd = beast_bpe_batch_delta_count(Vt);
-    if (sharded) {
-      bdeltas = mem.get<int32_t>(nbd);
-      BEAST_REQUIRE_CODE(bdeltas != nullptr, BEAST_E_HIP, "beast_bpe_train: hipMalloc of the pass deltas failed");
-      BEAST_HIP(hipMemsetAsync(bdeltas, 0, sizeof(int32_t) * nbd, s), "pass deltas memset");
-    }
+    HostPinned stage;
+    AGREE([&]() -> int {
+      ALLOC_TO(hp_d, uint64_t, hp.size());
+      ALLOC_TO(tlen_d, uint32_t, Vt);
+      BEAST_HIP(hipMemcpyAsync(hp_d, hp.data(), sizeof(uint64_t) * hp.size(), hipMemcpyHostToDevice, s), "hash upload");
+      BEAST_HIP(hipMemcpyAsync(tlen_d, tlen.data(), sizeof(uint32_t) * Vt, hipMemcpyHostToDevice, s), "tlen upload");
+      ALLOC_TO(lws, uint8_t, lws_bytes);
+      TRY(beast_bpe_loop_init(lws, lws_bytes, Vt, max_merges, n_base, vocab_size, min_frequency, hp_d, hp_d + n_base,
+                              tlen_d, max_tlen, stream));
+      TRY(beast_bpe_loop_state(lws, Vt, max_merges, &st_p, &log_p));
+      ALLOC_TO(argws, uint64_t, (aw_bytes + 7) / 8);
+      BEAST_HIP(hipMemsetAsync(argws, 0, ((aw_bytes + 7) / 8) * 8, s), "argmax workspace memset");
+      ALLOC_TO(bws, uint8_t, bw_bytes);
+      if (sharded) {
+        ALLOC_TO(bdeltas, int32_t, nbd);
+        BEAST_HIP(hipMemsetAsync(bdeltas, 0, sizeof(int32_t) * nbd, s), "pass deltas memset");
+      }
+      BEAST_HIP(hipHostMalloc(&stage.p, 2 * 64, hipHostMallocDefault), "pinned state");
+      return BEAST_OK;
+    }());
     auto run = [&](int steps, int flags) {
       return beast_bpe_loop_batch(lws, Vt, max_merges, steps, KMAX, flags, sym2, w2, l2, c2, nu, tlen_d, max_len, sig,
                                   table, argws, bws, bw_bytes, vocab_size, bdeltas, nullptr, stream);
     };
 
     // ---- the loop: two chunks of passes in flight, the host reads the state the older one left
-    HostPinned stage;
-    BEAST_HIP(hipHostMalloc(&stage.p, 2 * 64, hipHostMallocDefault), "pinned state");
     int32_t* st_host = static_cast<int32_t*>(stage.p);
     struct Inflight { hipEvent_t ev; int slot; int passes; };
     std::vector<Inflight> inflight;
@@ -496,15 +564,18 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     int vcur = n_base, rc = BEAST_OK;
     if (sharded) {
       // every rank holds the same table and takes the same decisions, so every rank runs the same
-      // passes and collectives: merge on the shard, SUM of the pass's deltas, apply (bpe_train.py)
-      TRY(run(0, 1 /* BATCH_INIT */));
+      // passes and collectives: merge on the shard, SUM of the pass's deltas, apply (bpe_train.py).
+      // A launch that fails on one rank still joins every collective of its chunk; the chunk's end
+      // agrees on the status before anyone reads the state.
+      rc = run(0, 1 /* BATCH_INIT */);
       while (true) {
         const int steps = std::max(1, std::min(CHUNK, (vocab_size - vcur + 1) / 2));
         for (int i = 0; i < steps; ++i) {
-          TRY(run(1, BEAST_BPE_BATCH_NO_APPLY));
+          if (rc == BEAST_OK) rc = run(1, BEAST_BPE_BATCH_NO_APPLY);
           TRY(beast_comm_allreduce(comm, bdeltas, bdeltas, (int64_t)nbd, BEAST_DT_I32, BEAST_OP_SUM, stream));
-          TRY(run(1, BEAST_BPE_BATCH_NO_MERGE));
+          if (rc == BEAST_OK) rc = run(1, BEAST_BPE_BATCH_NO_MERGE);
         }
+        AGREE(rc);
         int32_t st[16];
         BEAST_HIP(hipMemcpyAsync(st, st_p, sizeof(st), hipMemcpyDeviceToHost, s), "loop state read");
         BEAST_HIP(hipStreamSynchronize(s), "stream sync");
@@ -530,23 +601,31 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
       if (inflight.empty() && (rc = launch(1, 0)) != BEAST_OK) break;
     }
     release();
-    if (rc != BEAST_OK) return rc;
-    int32_t state[16];
-    BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
-    BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-    n_log = state[ST_NMERGES];
-    if (n_log >= max_merges) return rerun_on_host();   // merge log full
-    log.resize(4 * (size_t)std::max(n_log, 1));
-    if (n_log > 0) {
-      BEAST_HIP(hipMemcpyAsync(log.data(), log_p, sizeof(int32_t) * 4 * n_log, hipMemcpyDeviceToHost, s), "log read");
+    // the rerun decision below is a collective point too (replicated ranks ran the loop alone)
+    AGREE([&]() -> int {
+      if (rc != BEAST_OK) return rc;
+      int32_t state[16];
+      BEAST_HIP(hipMemcpyAsync(state, st_p, sizeof(state), hipMemcpyDeviceToHost, s), "loop state read");
       BEAST_HIP(hipStreamSynchronize(s), "stream sync");
-    }
+      n_log = state[ST_NMERGES];
+      if (n_log < max_merges) {
+        log.resize(4 * (size_t)std::max(n_log, 1));
+        if (n_log > 0) {
+          BEAST_HIP(hipMemcpyAsync(log.data(), log_p, sizeof(int32_t) * 4 * n_log, hipMemcpyDeviceToHost, s), "log read");
+          BEAST_HIP(hipStreamSynchronize(s), "stream sync");
+        }
+      }
+      return BEAST_OK;
+    }());
   }
 
-  // ---- replay the log against the real strings (bpe_train.py replay_log)
+  // ---- replay the log against the real strings (bpe_train.py replay_log); a disagreement of the
+  // batched loop's log (a 64-bit string-hash collision) or its full log reruns on the host-driven
+  // loop -- every rank together
   int n_merges = 0;
   std::vector<int32_t> merge_ids;
-  for (int i = 0; i < n_log; ++i) {
+  bool rerun = !host_loop && (n_log >= 4 * std::max(vocab_size - n_base, 0) + 1024 || beast::g_bpe_train_host == 2);
+  for (int i = 0; i < n_log && !rerun; ++i) {
     const int a = log[4 * i], b = log[4 * i + 1], nid = log[4 * i + 2], reused = log[4 * i + 3];
     BEAST_REQUIRE_CODE(a >= 0 && b >= 0 && a < (int)id2str.size() && b < (int)id2str.size(), BEAST_E_UNSUPPORTED,
                        "beast_bpe_train: merge log entry %d out of range", i);
@@ -554,8 +633,10 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     auto it = str2id.find(t);
     const bool have = it != str2id.end();
     const bool agree = have == (reused != 0) && (!have || it->second == nid) && (have || nid == (int)id2str.size());
-    if (!host_loop && (!agree || beast::g_bpe_train_host == 2))
-      return rerun_on_host();   // a 64-bit string-hash collision in the batched loop
+    if (!host_loop && !agree) {
+      rerun = true;
+      break;
+    }
     BEAST_REQUIRE_CODE(agree, BEAST_E_HIP, "beast_bpe_train: merge %d disagrees with the strings", i);
     if (!have) {
       str2id.emplace(t, nid);
@@ -564,6 +645,11 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     merge_ids.push_back(a);
     merge_ids.push_back(b);
     ++n_merges;
+  }
+  if (!host_loop) {
+    int any = rerun ? 1 : 0;
+    TRY(beast::comm_max_i32(comm, any, &any, s));
+    if (any) return RERUN;
   }
 
   // ---- outputs: the vocabulary's strings in id order, the merges, the token range.  Capacities
@@ -595,16 +681,32 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
   return BEAST_OK;
 }
 
+// the batched attempt, then (RERUN) the host-driven one with the first attempt's memory released
+static int bpe_train_entry(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
+                           int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
+                           const char* const* special_tokens, int n_special, int64_t* out_min_token,
+                           int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
+                           int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
+                           int max_merges_out, int* out_n_merges, beast_comm* comm, bool replicate, void* stream) {
+  int rc = RERUN;
+  for (int attempt = 0; attempt < 2 && rc == RERUN; ++attempt)
+    rc = bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                        special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
+                        replicate, attempt == 1, stream);
+  return rc;
+}
+
 extern "C" int beast_bpe_train(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                                int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,
                                const char* const* special_tokens, int n_special, int64_t* out_min_token,
                                int64_t* out_max_token, char* out_vocab_bytes, size_t vocab_bytes_cap,
                                int64_t* out_vocab_off, int max_vocab, int* out_n_vocab, int32_t* out_merges,
                                int max_merges_out, int* out_n_merges, void* stream) {
-  return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
-                        special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, true,
-                        false, stream);
+  return bpe_train_entry(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                         out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, nullptr, true,
+                         stream);
 }
 
 extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq,
@@ -614,8 +716,8 @@ extern "C" int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_of
                                     size_t vocab_bytes_cap, int64_t* out_vocab_off, int max_vocab, int* out_n_vocab,
                                     int32_t* out_merges, int max_merges_out, int* out_n_merges, beast_comm* comm,
                                     int replicate, void* stream) {
-  return bpe_train_impl(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
-                        special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
-                        out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
-                        replicate != 0, false, stream);
+  return bpe_train_entry(tokens, seq_off, n_seq, cls_lut, lut_n, vocab_size, min_frequency, max_token_length,
+                         special_tokens, n_special, out_min_token, out_max_token, out_vocab_bytes, vocab_bytes_cap,
+                         out_vocab_off, max_vocab, out_n_vocab, out_merges, max_merges_out, out_n_merges, comm,
+                         replicate != 0, stream);
 }

@@ -1407,7 +1407,9 @@ int launch_encode(EncArgs a, int T, int D, int nj, int N, hipStream_t s) {
                 "encode list: rows must be contiguous and rows per batch a multiple of %d", tbt);
   if (fast && tbt == 8 && !g_generic_only && T == 50 && N == 10 && a.row_elems == D) {
     const bool wide = wide_blocks((a.B + 7) / 8);
-    if (!a.traj_list && enc_v()) {
+    // k_encode_v stores its outputs with unconditional 16-byte stores: other alignments take k_encode
+    const bool out16 = (((uintptr_t)a.params_out | (uintptr_t)a.tokens_out) & 15) == 0;
+    if (!a.traj_list && enc_v() && out16) {
       if (D == 14 && nj == 14) return launch_encode_v<Shape<14, 14, 10, 50, 14>>(a, s);
       if (D == 14 && nj == 12) return launch_encode_v<Shape<14, 12, 10, 50, 14>>(a, s);
     }

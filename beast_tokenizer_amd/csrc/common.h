@@ -23,6 +23,12 @@ extern int g_bpe_dedup_key_bits;
 // string-hash collision of the batched loop)
 extern int g_bpe_train_host;
 int hip_fail(hipError_t e, const char* what);
+// comm.hip: a rank's status agreed over the communicator (every rank must call it at the same
+// point).  Returns rc when it failed locally, the failing rank's code (message: which rank) when
+// another rank failed, BEAST_OK when all succeeded; comm == nullptr returns rc.
+int comm_agree(beast_comm* comm, int rc, hipStream_t s);
+// comm.hip: max over the ranks of a non-negative int (every rank calls it at the same point)
+int comm_max_i32(beast_comm* comm, int v, int* out, hipStream_t s);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -4,10 +4,16 @@
 
 One step = BEASTBsplineTokenizer.encode(x) -> reconstruct_traj(tokens) over one
 synthetic batch already resident in HBM (config "1xMI355X: num_dof=14
-num_basis=10 seq_len=50 vocab=256, B=4096").  For N > 1 the driver launches one
-rank per GPU (torch.distributed.run); every rank processes its own B
-trajectories (data-parallel, no collective on this path: weak scaling); the time
-is the max over ranks.  rank 0 prints ONE JSON line.
+num_basis=10 seq_len=50 vocab=256, B=4096").  For N > 1 there is one rank per GPU:
+either torch.distributed.run starts them (WORLD_SIZE set; it must equal --gpus) or
+``python bench.py --gpus N`` spawns them itself (``launch()``); every rank processes its own
+B trajectories (data-parallel, no collective on this path: weak scaling); the time
+is the max over ranks.  rank 0 prints ONE JSON line.  At N > 1 the BPE leg times both
+multi-rank trainer forms (replicated: one all-gather of the distinct words; sharded: a
+per-pass all-reduce of the pair-count deltas) and checks both against the K5 golden.
+
+``timing.host_issue_us_per_step`` / ``gpu_busy_us_per_step`` split a step into the host's
+cost of issuing it and the GPU's cost of running it (``host_issue_split``).
 
 Timing: W untimed warm-up steps, then ``--windows`` windows of exactly K steps, each
 bracketed by barrier + device synchronize (wall clock, max over ranks) and by HIP events
@@ -191,6 +197,61 @@ def codec_roofline(prof, note, t_enc: float, t_rec: float, B: int) -> dict:
             "profile_git_head": prof.get("git_head_measured") if prof else None,
             "lib_fingerprint": prof.get("lib_fingerprint") if prof else None,
             "rocprof": rp}
+
+
+def host_issue_split(step, stream: torch.cuda.Stream, K: int, rounds: int = 7) -> dict:
+    """Host cost and GPU cost of one step, measured apart.  The stream is held behind a sleep kernel
+    long enough that no launch of the K steps can wait for the GPU: the wall time of enqueuing them
+    is then the host's issue cost alone, and HIP events around them (they start when the sleep
+    ends) time the GPU running the K steps back to back with no host gap.  A round whose sleep
+    ended before the last launch was issued is discarded (its GPU time would include host gaps)."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0 = torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            step()
+        est = (time.perf_counter() - t0) * 1e6 / K
+        torch.cuda.synchronize()
+        # a sleep of ~10x the estimated issue time (>= 2 ms), its duration measured on the GPU
+        cycles = 100000
+        for _ in range(4):
+            s0.record(stream)
+            torch.cuda._sleep(cycles)
+            s.record(stream)
+            s.synchronize()
+            sleep_us = s0.elapsed_time(s) * 1e3
+            if sleep_us >= max(10.0 * est * K, 2000.0):
+                break
+            cycles = int(cycles * max(2.0, 1.2 * max(10.0 * est * K, 2000.0) / max(sleep_us, 1.0)))
+        host, gpu, dropped = [], [], 0
+        for _ in range(rounds):
+            torch.cuda.synchronize()
+            s0.record(stream)
+            torch.cuda._sleep(cycles)
+            s.record(stream)
+            t0 = time.perf_counter()
+            for _ in range(K):
+                step()
+            t1 = time.perf_counter()
+            e.record(stream)
+            torch.cuda.synchronize()
+            # the launches were all queued while the sleep still ran (it started no earlier than t0
+            # minus a launch, and lasted sleep_us): otherwise the GPU time may hold host gaps
+            if (t1 - t0) * 1e6 > 0.8 * s0.elapsed_time(s) * 1e3:
+                dropped += 1
+                continue
+            host.append((t1 - t0) * 1e6 / K)
+            gpu.append(s.elapsed_time(e) * 1e3 / K)
+    out = {"host_issue_us_per_step": float(np.median(host)) if host else None,
+           "gpu_busy_us_per_step": float(np.median(gpu)) if gpu else None,
+           "host_issue_runs_us": host, "gpu_busy_runs_us": gpu, "rounds_dropped": dropped, "steps_per_round": K,
+           "method": "K steps enqueued behind a sleep kernel: host = wall time of the enqueue, gpu = HIP events "
+                     "around the K steps on the kernels' stream (back to back, no host gap)"}
+    if host and gpu:
+        out["bound"] = "host" if out["host_issue_us_per_step"] > out["gpu_busy_us_per_step"] else "gpu"
+    return out
 
 
 def max_over_ranks(v: float, world: int, dev) -> float:
@@ -440,17 +501,37 @@ def bpe_bench(dev, args, world, rank, reduce, prof=None, prof_note=None):
     allrows = k5_corpus(dev, args.bpe_seqs, rank, world, golden)
     sha = hashlib.sha256(allrows.to(torch.uint8).cpu().numpy().tobytes()).hexdigest() \
         if world == 1 and int(allrows.max()) < 256 else None
-    times, res = [], None
-    for _ in range(2):            # first run pays one-time allocator growth; report the second
-        sync(world)
-        t0 = time.perf_counter()
-        flat, off = fixed_rows_to_device(allrows)
-        res = train_bpe(flat, off, args.bpe_vocab, reduce=reduce)
-        torch.cuda.synchronize()
-        times.append(max_over_ranks(time.perf_counter() - t0, world, dev))
-        del flat, off
+    def timed(replicate: bool):
+        times, res = [], None
+        for _ in range(2):            # first run pays one-time allocator growth; report the second
+            sync(world)
+            t0 = time.perf_counter()
+            flat, off = fixed_rows_to_device(allrows)
+            res = train_bpe(flat, off, args.bpe_vocab, reduce=reduce, replicate=replicate)
+            torch.cuda.synchronize()
+            times.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+            del flat, off
+        return times, res
+
+    times, res = timed(True)
     el = times[-1]
     st = res.stats
+    forms = None
+    if world > 1:
+        # the two multi-rank forms of the trainer over the same shards -- one all-gather
+        # of the distinct words then the loop on every rank (replicated, the default), and the
+        # sharded loop (each pass's pair-count deltas all-reduced between its launches)
+        s_times, s_res = timed(False)
+        forms = {}
+        for name, tt, rr in (("replicated", times, res), ("sharded", s_times, s_res)):
+            forms[name] = {"value": rr.stats["n_merges"] / tt[-1], "unit": "merges/s", "seconds": tt[-1],
+                           "seconds_runs": tt, "setup_s": rr.stats["setup_s"],
+                           "merge_loop_s": rr.stats["merge_loop_s"], "passes": rr.stats.get("passes"),
+                           "loop": rr.stats.get("loop"), "replicated": rr.stats.get("replicated"),
+                           "sharded": rr.stats.get("sharded")}
+        forms["sharded_merges_equal_replicated"] = bool(s_res.merges == res.merges and s_res.vocab == res.vocab)
+        RANK_INFO["bpe_merges_sharded"] = [list(m) for m in s_res.merges]
+        assert forms["sharded_merges_equal_replicated"], "sharded BPE merges differ from the replicated form's"
     RANK_INFO["bpe_merges"] = [list(m) for m in res.merges]
     RANK_INFO["bpe_vocab"] = res.vocab
     if world == 1:
@@ -467,7 +548,9 @@ def bpe_bench(dev, args, world, rank, reduce, prof=None, prof_note=None):
            "vocab_size": args.bpe_vocab, "setup_s": st["setup_s"], "merge_loop_s": st["merge_loop_s"],
            "us_per_merge": st["merge_loop_s"] / max(st["n_merges"], 1) * 1e6, "loop": st.get("loop"),
            "words": st["n_words"], "symbols": st["n_syms"], "distinct_words": st.get("n_distinct"),
-           "corpus_sha256": sha}
+           "corpus_sha256": sha, "world_size": world}
+    if forms is not None:
+        out["forms"] = forms
     # roofline of the merge loop: the HBM bytes its two kernels move per launch (same-tree rocprofv3
     # --pmc FETCH_SIZE + WRITE_SIZE of k_merge_batch and k_apply_batch at K5) times the passes this run
     # took, over the loop's wall time; §8d's notional count (a full scan of the live symbols per
@@ -501,6 +584,9 @@ def bpe_bench(dev, args, world, rank, reduce, prof=None, prof_note=None):
         got = [list(m) for m in res.merges]
         same = got == golden["merges"] and res.vocab == golden["vocab"]
         out["parity"] = {"golden": os.path.relpath(K5_GOLDEN, REPO), "merges_equal_hf": bool(same),
+                         # world > 1: the union of the ranks' shards is the golden's corpus, and both
+                         # multi-rank forms are checked against its merges
+                         "forms_checked": ["replicated", "sharded"] if forms else ["single rank"],
                          "corpus_sha256_equal": (sha == golden["corpus_sha256"]) if sha else None,
                          "hf": golden.get("hf_version"),
                          "scope": "bit-exact vs HF BpeTrainer given identical bins (this corpus: the GPU encode of "
@@ -768,6 +854,7 @@ def main():
         gpu_ms.append(max_over_ranks(s_ev.elapsed_time(e_ev), world, dev))
     el = float(np.median(walls))
     value = B * world * args.steps / el
+    split = host_issue_split(step, stream, args.steps)
     gpu_tokens = tok.encode(x)[0].cpu().numpy()
 
     # ---- dominant-kernel roofline: the same-tree rocprofv3 average when the profile matches this
@@ -808,7 +895,8 @@ def main():
                                    "seq_len=50 vocab=256 degree_p=4", "global_batch": B * world,
                        "per_gpu_batch": B, "seq_len": T, "parallelism": f"dp{world}"},
             "timing": {"windows": len(walls), "window_wall_s": walls, "window_gpu_event_ms": gpu_ms,
-                       "median_gpu_event_us_per_step": float(np.median(gpu_ms)) / args.steps * 1e3},
+                       "median_gpu_event_us_per_step": float(np.median(gpu_ms)) / args.steps * 1e3,
+                       "wall_us_per_step": el / args.steps * 1e6, **split},
             "roofline": roof, "mfma": mfma, "cpu_baseline": cpu, "token_parity": parity,
             "host": host_info(), "fit": fitb, "bpe": bpe,
             "dist": {"world_size": world, "backend": torch.distributed.get_backend() if world > 1 else None,
@@ -823,5 +911,75 @@ def main():
     return dict(RANK_INFO, rank=rank, world=world)
 
 
-if __name__ == "__main__":
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(rank: int, world: int, port: int, argv: list) -> None:
+    """One spawned rank of ``python bench.py --gpus N`` (a fresh interpreter: nothing in it has
+    touched the GPU before ``main()``)."""
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    sys.argv = list(argv)
     main()
+
+
+def launch(argv=None) -> int:
+    """``--gpus N`` is the number of ranks.  Under torch.distributed.run (WORLD_SIZE set) this
+    process is one of them and WORLD_SIZE must equal N.  Without it and N > 1, this process starts
+    N ranks itself -- multiprocessing "spawn", before anything here touches the GPU (no process
+    that initialised HIP is ever re-exec'd) -- one per GPU over RCCL, waits for them, and exits
+    with the first failing rank's code (the others are stopped: a rank left waiting in a collective
+    would never end)."""
+    argv = list(sys.argv if argv is None else argv)
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (one rank per GPU: they must agree)",
+                  file=sys.stderr)
+            return 2
+        main()
+        return 0
+    if args.gpus <= 1:
+        main()
+        return 0
+    one_device = os.environ.get("BEAST_BENCH_ONE_DEVICE") == "1"
+    ndev = torch.cuda.device_count()      # counts devices without initialising HIP on this image
+    if not one_device and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, {ndev} found", file=sys.stderr)
+        return 2
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, argv), name=f"bench-rank{r}")
+             for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            p.join(timeout=0.2)
+            if p.exitcode is None:
+                continue
+            live.remove(p)
+            if p.exitcode != 0 and rc == 0:
+                rc = p.exitcode if p.exitcode > 0 else 128 - p.exitcode
+                print(f"bench.py: {p.name} exited with {p.exitcode}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    q.join(timeout=15)
+                    if q.exitcode is None:
+                        q.kill()
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(launch())

@@ -351,7 +351,19 @@ typedef struct beast_comm beast_comm;
 size_t beast_comm_id_bytes(void);
 int beast_comm_unique_id(void* id_out);
 int beast_comm_init_rank(int world, int rank, const void* id, int device, beast_comm** out);
+/* The single-process form's collectives (beast_comm_init with ndev > 1, one host thread driving
+ * every handle) must be issued between beast_comm_group_start() and beast_comm_group_end(), as
+ * ncclGroupStart / ncclGroupEnd require; otherwise drive each handle from its own host thread.
+ * beast_bpe_train_comm issues collectives of its own: call it from one host thread per handle. */
 int beast_comm_init(int ndev, const int* devs, beast_comm** out);
+int beast_comm_group_start(void);
+int beast_comm_group_end(void);
+/* n virtual ranks on one device (SURVEY.md §4.3's "N virtual ranks on one device"; tests and
+ * rehearsal on a one-GPU box): out[n] handles of a world of n, each driven by its own host thread.
+ * Every collective synchronises the caller's stream and meets the other ranks in host memory
+ * (rank-ordered reductions), so the library's multi-rank code paths run where RCCL cannot form a
+ * world > 1.  A rank that does not arrive within 120 s fails the collective on every rank. */
+int beast_comm_init_virtual(int n, int device, beast_comm** out);
 int beast_comm_destroy(beast_comm* comm);
 int beast_comm_info(const beast_comm* comm, int* world, int* rank, int* device);
 /* §8e's reductions on device buffers (in place when send == recv), stream-ordered: the running
@@ -373,7 +385,10 @@ int beast_comm_allgatherv(beast_comm* comm, const void* send, void* recv, const 
  * words, the pair table is SUM-reduced once and each pass's pair-count changes are SUM-reduced
  * between its merge and apply launches (the host-driven loop: each merge's), so the words of
  * no single GPU need to hold the corpus.  Every rank returns the same vocabulary and merges; a
- * shard may be empty (replicated form).  All ranks must call it with the same options.
+ * shard may be empty (replicated form).  All ranks must call it with the same options.  A failure
+ * on one rank (an allocation, a launch, a shard over 2^32 symbols) is agreed over the communicator
+ * before the next collective (the status all-reduced with MAX), so every rank returns an error
+ * together: the failing rank its own, the others its code with a message naming the cause.
  * comm == NULL is beast_bpe_train. */
 int beast_bpe_train_comm(const int64_t* tokens, const int64_t* seq_off, int64_t n_seq, const uint8_t* cls_lut,
                          int64_t lut_n, int vocab_size, int min_frequency, int max_token_length,

@@ -103,6 +103,38 @@ def test_bench_main_two_ranks_rehearsal(gpu_device):
 
 
 @pytest.mark.gpu
+def test_bench_gpus_2_spawns_its_ranks():
+    """``python bench.py --gpus 2`` with no launcher: bench.py spawns the two ranks itself
+    (here both on cuda:0 over gloo) and prints one line with n_gpus 2; the BPE leg trains the full
+    K5 corpus sharded over the two ranks in both multi-rank forms (replicated and sharded), and
+    both equal the golden HF merges of the union (tests/golden/k5_bpe.json)."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"BEAST_BENCH_ONE_DEVICE": "1", "BEAST_BENCH_BACKEND": "gloo"})
+    args = ["--gpus", "2", "--steps", "5", "--warmup", "2", "--windows", "2", "--no-cpu", "--no-large",
+            "--no-bpe-api", "--fit-trajs", "65536"]
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "bench.py"), *args], env=env, cwd=REPO,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["dist"]["world_size"] == 2 and line["dist"]["backend"] == "gloo"
+    assert line["config"]["global_batch"] == 2 * 4096 and line["config"]["parallelism"] == "dp2"
+    bpe = line["bpe"]
+    assert bpe["world_size"] == 2 and bpe["parity"]["merges_equal_hf"] is True
+    assert bpe["parity"]["forms_checked"] == ["replicated", "sharded"]
+    forms = bpe["forms"]
+    assert forms["sharded_merges_equal_replicated"] is True
+    assert forms["replicated"]["replicated"] is True and forms["sharded"]["sharded"] is True
+    assert forms["replicated"]["value"] > 0 and forms["sharded"]["value"] > 0
+    assert line["timing"]["host_issue_us_per_step"] is not None
+
+
+@pytest.mark.gpu
 def test_tokenizer_on_non_current_device(gpu_device):
     """A tokenizer on cuda:1 while cuda:0 is current: every launch must resolve its device from
     its own stream and buffers (round-2 advice); results equal cuda:0's.  Needs 2 GPUs (the

@@ -13,6 +13,15 @@ __global__ void k_spin(long long cycles) {
   while (clock64() - t0 < cycles) {}
 }
 
+struct Args8 { long long p; };
+struct Args64 { char pad[64]; };
+__global__ void k_noop8(Args8 a) {
+  if (a.p == 123 && threadIdx.x == 9999) __builtin_amdgcn_s_sleep(1);
+}
+__global__ void k_noop64(Args64 a) {
+  if (a.pad[0] == 123 && threadIdx.x == 9999) a.pad[1] = 0;
+}
+
 __global__ void k_noop(Args a) {
   if (a.pad[0] == 123 && threadIdx.x == 9999) a.pad[1] = 0;
 }
@@ -86,6 +95,50 @@ int main() {
     hipEventSynchronize(e1);
     hipEventElapsedTime(&ms, e0, e1);
     printf("\"gpu_us_per_noop_queued_grid%d\": %.3f, ", grid, ms * 1000 / 1000);
+  }
+  // host cost alone: the stream held behind a long spin, so no launch can wait for the GPU
+  {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 20000000LL);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 2000; ++i) hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+    auto t1 = std::chrono::steady_clock::now();
+    printf("\"host_us_module_launch_blocked\": %.3f, ", std::chrono::duration<double, std::micro>(t1 - t0).count() / 2000);
+    hipDeviceSynchronize();
+    // the same with 8- and 64-byte argument blocks (host cost of the kernarg copy)
+    hipFunction_t f8, f64;
+    hipGetFuncBySymbol(&f8, (const void*)k_noop8);
+    hipGetFuncBySymbol(&f64, (const void*)k_noop64);
+    Args8 a8{0};
+    Args64 a64;
+    memset(&a64, 0, sizeof(a64));
+    void* args8[] = {&a8};
+    void* args64[] = {&a64};
+    for (int rep = 0; rep < 2; ++rep) {
+      hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 20000000LL);
+      t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < 2000; ++i) hipModuleLaunchKernel(f8, 512, 1, 1, 256, 1, 1, 0, s, args8, nullptr);
+      t1 = std::chrono::steady_clock::now();
+      if (rep) printf("\"host_us_module_launch_blocked_8B\": %.3f, ", std::chrono::duration<double, std::micro>(t1 - t0).count() / 2000);
+      hipDeviceSynchronize();
+      hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 20000000LL);
+      t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < 2000; ++i) hipModuleLaunchKernel(f64, 512, 1, 1, 256, 1, 1, 0, s, args64, nullptr);
+      t1 = std::chrono::steady_clock::now();
+      if (rep) printf("\"host_us_module_launch_blocked_64B\": %.3f, ", std::chrono::duration<double, std::micro>(t1 - t0).count() / 2000);
+      hipDeviceSynchronize();
+      hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 20000000LL);
+      t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < 2000; ++i) hipModuleLaunchKernel(f, 512, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+      t1 = std::chrono::steady_clock::now();
+      if (rep) printf("\"host_us_module_launch_blocked_224B\": %.3f, ", std::chrono::duration<double, std::micro>(t1 - t0).count() / 2000);
+      hipDeviceSynchronize();
+    }
+    int dev = 0;
+    t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 20000; ++i) hipStreamGetDevice(s, &dev);
+    t1 = std::chrono::steady_clock::now();
+    printf("\"host_us_stream_get_device\": %.4f, ", std::chrono::duration<double, std::micro>(t1 - t0).count() / 20000);
+    hipDeviceSynchronize();
   }
   printf("\"end\": 0}\n");
   return 0;
