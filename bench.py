@@ -16,9 +16,10 @@ per-pass all-reduce of the pair-count deltas) and checks both against the K5 gol
 cost of issuing it and the GPU's cost of running it (``host_issue_split``).
 
 Timing: W untimed warm-up steps, then ``--windows`` windows of exactly K steps, each
-bracketed by barrier + device synchronize (wall clock, max over ranks) and by HIP events
-on the stream the kernels run on; ``value`` / ``ms_per_step`` come from the median window
-(one 20-step window is ~0.3 ms of wall clock: start-up jitter would dominate a single one).
+bracketed by barrier + device synchronize (wall clock, max over ranks); ``value`` /
+``ms_per_step`` come from the median window (one 20-step window is ~0.2 ms of wall clock:
+start-up jitter would dominate a single one).  Nothing else runs inside a timed window; the
+HIP-event times of the same windows are taken in separate, untimed windows.
 
 Extra objects in that line:
   roofline      dominant kernel: algorithmic bytes / its average launch duration measured live in
@@ -840,19 +841,28 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    walls, gpu_ms = [], []
+    # the timed windows hold the K steps and nothing else: HIP events recorded inside a window cost
+    # the step ~15 % of wall time on the box (tools/window_probe.py: 12.75 vs 10.81 us per step at
+    # K = 20), so the GPU-side times come from windows of their own below
+    walls = []
     for _ in range(max(args.windows, 1)):
         sync(world)
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync(world)
+        walls.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+    el = float(np.median(walls))
+    gpu_ms = []
+    for _ in range(5):   # untimed: the same windows with HIP events on the kernels' stream
+        sync(world)
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record(stream)
         for _ in range(args.steps):
             step()
         e_ev.record(stream)
         sync(world)
-        walls.append(max_over_ranks(time.perf_counter() - t0, world, dev))
         gpu_ms.append(max_over_ranks(s_ev.elapsed_time(e_ev), world, dev))
-    el = float(np.median(walls))
     value = B * world * args.steps / el
     split = host_issue_split(step, stream, args.steps)
     gpu_tokens = tok.encode(x)[0].cpu().numpy()
