@@ -283,6 +283,16 @@ struct EncArgs {
   int64_t list_rows;               //   (a multiple of the tile, so no tile straddles two batches)
 };
 
+struct EncVArgs {
+  const int32_t* dof_src;
+  const float* proj;
+  const float* w_min;
+  const float* w_max;
+  long long* tokens_out;
+  float* params_out;
+  int64_t tok_offset;
+  int vocab, phases;
+};
 // First trajectory of tile row b0 (FAST path: contiguous rows of stride sb)
 __device__ __forceinline__ const float* enc_tile_src(const EncArgs& a, int64_t b0) {
   if (a.traj_list == nullptr) return a.traj + b0 * a.sb;
@@ -552,7 +562,7 @@ __host__ __device__ constexpr EvSmem ev_smem(int nkinds) {
 }
 
 template <class S, int SP>
-__global__ __launch_bounds__(RV_W * 64) void k_encode_v(const float* __restrict__ traj, int64_t B, EncArgs a) {
+__global__ __launch_bounds__(RV_W * 64) void k_encode_v(const float* __restrict__ traj, int64_t B, EncVArgs a) {
   using PS = VShape<S>;
   static_assert(PS::D <= 16 && PS::N <= 16 && PS::DL == PS::D, "per-trajectory encode: D, N <= 16, rows of D");
   constexpr int NT = RV_W * 64, D = PS::D, N = PS::N, T = PS::T, Tp = PS::Tp, DN = PS::DN, NST = PS::NST;
@@ -700,6 +710,22 @@ struct RecArgs {
   float* pos_out;
   Geom g;
   FastDiv fd_row;          // Tout * ndo
+};
+
+// The per-trajectory kernels' argument blocks: only what k_encode_v / k_reconstruct_v read (their
+// shapes are compile-time), 64 / 88 bytes instead of EncArgs' / RecArgs' ~260.  The runtime copies
+// every launch's argument block into the kernarg ring, and a 224-byte block costs the host ~0.28 us
+// more per launch than an 8- or 64-byte one (tools/launch/launch_bench.hip, profiles/r06/).
+struct RecVArgs {
+  const float* w_min;
+  const float* w_max;
+  const float* basis;
+  const int32_t* dof_dst;
+  const float* init_p;
+  const int32_t* init_p_src;
+  float* pos_out;
+  int64_t tok_offset, init_p_sb;
+  int vocab, lut_n, phases;
 };
 
 constexpr int LUT_MAX = 4096;   // dequantise LUT tok / (vocab - 1), IEEE-divided once
@@ -1050,7 +1076,7 @@ __host__ __device__ constexpr RvSmem rv_smem(int nkinds) {
 
 template <int KS, class S, int SP>
 __global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restrict__ tsrc, int64_t B, int esz,
-                                                             RecArgs a) {
+                                                             RecVArgs a) {
   static_assert(S::fixed && S::T > 0 && S::T <= 64 && S::D <= 16 && S::DL == S::D && 4 * KS >= S::N,
                 "per-trajectory reconstruct: fixed shape, T <= 64, D <= 16, ndo == D");
   constexpr int NT = RV_W * 64, D = S::D, N = S::N, T = S::T, per = D * N;
@@ -1369,7 +1395,9 @@ int launch_encode_v(EncArgs a, hipStream_t s) {
   const bool lat = a.ntiles <= 2 * (int64_t)cu_count();
   return launch_fn(lat ? reinterpret_cast<const void*>(&k_encode_v<S, LAT_SP>)
                        : reinterpret_cast<const void*>(&k_encode_v<S, 0>),
-                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_encode_v", a.traj, a.B, a);
+                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_encode_v", a.traj, a.B,
+                   EncVArgs{a.dof_src, a.proj, a.w_min, a.w_max, a.tokens_out, a.params_out, a.tok_offset, a.vocab,
+                            a.phases});
 }
 
 template <int TBT, class S>
@@ -1476,7 +1504,9 @@ int launch_rec_v(RecArgs a, hipStream_t s) {
   return launch_fn(lat ? reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, LAT_SP>)
                        : reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, 0>),
                    fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_reconstruct_v",
-                   static_cast<const void*>(a.tokens), a.B, 8, a);
+                   static_cast<const void*>(a.tokens), a.B, 8,
+                   RecVArgs{a.w_min, a.w_max, a.basis, a.dof_dst, a.init_p, a.init_p_src, a.pos_out, a.tok_offset,
+                            a.init_p_sb, a.vocab, a.lut_n, a.phases});
 }
 
 template <int TBT>
