@@ -531,7 +531,21 @@ struct VShape {
 };
 
 // ------------------------------------------------------- encode, per-trajectory waves --
-constexpr int RV_W = 8;   // waves = trajectories per tile (k_encode_v, k_reconstruct_v)
+// waves = trajectories per tile of k_encode_v / k_reconstruct_v.  Round 6: 16 (one 1,024-thread
+// workgroup per CU at B = 4,096) for both -- the encode -> reconstruct step is 2.4 % shorter than
+// with 8-wave tiles (9.49-9.51 vs 9.70-9.75 us per step, outputs bitwise equal), although either
+// kernel alone, launched back to back with itself, is 0.1 us slower; 16 / 8 mixed is slower than
+// both (profiles/r06/codec_tile_width_ab_r06k.txt).  BEAST_RV_WE / _WR override (measurements).
+// Bulk encode launches (more than one 16-trajectory tile per CU) keep 8-wave tiles: their 45 KB of
+// LDS fit three workgroups -- 24 waves -- per CU, where a 16-wave tile's 84 KB fits one
+// (B = 262,144: 232 vs 242 us, profiles/r06/).
+#ifndef BEAST_RV_WE
+#define BEAST_RV_WE 16
+#endif
+#ifndef BEAST_RV_WR
+#define BEAST_RV_WR 16
+#endif
+constexpr int RV_WE = BEAST_RV_WE, RV_WR = BEAST_RV_WR, RV_WE_BULK = 8;
 // Fixed shapes (the BEAST defaults), every batch size.  Wave j of the workgroup owns trajectory
 // j of the 8-trajectory tile: C[n][d] = sum_t P_kind[n][t] y[j][t][lcol[d]] on
 // v_mfma_f32_16x16x4_f32 (A = P, B = y[j]: the columns are the trajectory's DoFs), then the wave
@@ -545,30 +559,30 @@ constexpr int RV_W = 8;   // waves = trajectories per tile (k_encode_v, k_recons
 struct EvSmem {
   int Y, P, wlo, whi, lcol, pimg, timg, total;
 };
-template <class S>
+template <class S, int W>
 __host__ __device__ constexpr EvSmem ev_smem(int nkinds) {
   using PS = VShape<S>;
   EvSmem s{};
   int o = 0;
-  s.Y = o;    o += round_up(RV_W * PS::T * PS::DL * 4, 1024);
+  s.Y = o;    o += round_up(W * PS::T * PS::DL * 4, 1024);
   s.P = o;    o += round_up(nkinds * 16 * PS::Tp * 4, 1024);
   s.wlo = o;  o += round_up(PS::DN * 4, 256);
   s.whi = o;  o += round_up(PS::DN * 4, 256);
   s.lcol = o; o += round_up(PS::D * 4, 256);
-  s.pimg = o; o += RV_W * round_up(PS::DN * 4, 16);
-  s.timg = o; o += RV_W * round_up(PS::DN * 8, 16);
+  s.pimg = o; o += W * round_up(PS::DN * 4, 16);
+  s.timg = o; o += W * round_up(PS::DN * 8, 16);
   s.total = o;
   return s;
 }
 
-template <class S, int SP>
-__global__ __launch_bounds__(RV_W * 64) void k_encode_v(const float* __restrict__ traj, int64_t B, EncVArgs a) {
+template <class S, int SP, int W>
+__global__ __launch_bounds__(W * 64) void k_encode_v(const float* __restrict__ traj, int64_t B, EncVArgs a) {
   using PS = VShape<S>;
   static_assert(PS::D <= 16 && PS::N <= 16 && PS::DL == PS::D, "per-trajectory encode: D, N <= 16, rows of D");
-  constexpr int NT = RV_W * 64, D = PS::D, N = PS::N, T = PS::T, Tp = PS::Tp, DN = PS::DN, NST = PS::NST;
+  constexpr int NT = W * 64, D = PS::D, N = PS::N, T = PS::T, Tp = PS::Tp, DN = PS::DN, NST = PS::NST;
   constexpr int NJ = S::NJ;
   constexpr int nkinds = NJ < D ? 2 : 1;
-  constexpr EvSmem L = ev_smem<S>(nkinds);
+  constexpr EvSmem L = ev_smem<S, W>(nkinds);
   constexpr int PIMG = round_up(DN * 4, 16) / 4, TIMG = round_up(DN * 8, 16) / 8;
   static_assert((T * D) % 4 == 0 && (DN % 2) == 0, "per-trajectory encode: whole 16-byte rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -578,8 +592,8 @@ __global__ __launch_bounds__(RV_W * 64) void k_encode_v(const float* __restrict_
   float* whi = reinterpret_cast<float*>(smem + L.whi);
   int* lcol = reinterpret_cast<int*>(smem + L.lcol);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int64_t b0 = (int64_t)blockIdx.x * RV_W;
-  const int nb = (int)min<int64_t>(RV_W, B - b0);
+  const int64_t b0 = (int64_t)blockIdx.x * W;
+  const int nb = (int)min<int64_t>(W, B - b0);
   const bool quant = a.tokens_out != nullptr;
   STAMP(0, 0);
   BSTAMP(0, 0);
@@ -1062,24 +1076,24 @@ __host__ __device__ constexpr RvSmem rv_smem(int nkinds) {
   RvSmem s{};
   constexpr int per = S::D * S::N;
   int o = 0;
-  s.tok = o;  o += round_up(RV_W * per * 8, 1024);           // DMA: whole wave-instructions
+  s.tok = o;  o += round_up(RV_WR * per * 8, 1024);           // DMA: whole wave-instructions
   s.wlo = o;  o += round_up(per * 4, 256);
   s.whi = o;  o += round_up(per * 4, 256);
   s.dst = o;  o += round_up(S::D * 4, 256);
   s.phi = o;  o += round_up(nkinds * S::T * S::N * 4, 1024);
   s.lut = o;  o += round_up(LUT_MAX * 4, 16);
-  s.wimg = o; o += round_up(RV_W * per * 4, 16);              // W[j][d][n] (d n), one per wave
-  s.img = o;  o += RV_W * round_up(S::T * S::D * 4, 16);        // pos[j] [T][D], one per wave
+  s.wimg = o; o += round_up(RV_WR * per * 4, 16);              // W[j][d][n] (d n), one per wave
+  s.img = o;  o += RV_WR * round_up(S::T * S::D * 4, 16);        // pos[j] [T][D], one per wave
   s.total = o;
   return s;
 }
 
 template <int KS, class S, int SP>
-__global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restrict__ tsrc, int64_t B, int esz,
+__global__ __launch_bounds__(RV_WR * 64) void k_reconstruct_v(const void* __restrict__ tsrc, int64_t B, int esz,
                                                              RecVArgs a) {
   static_assert(S::fixed && S::T > 0 && S::T <= 64 && S::D <= 16 && S::DL == S::D && 4 * KS >= S::N,
                 "per-trajectory reconstruct: fixed shape, T <= 64, D <= 16, ndo == D");
-  constexpr int NT = RV_W * 64, D = S::D, N = S::N, T = S::T, per = D * N;
+  constexpr int NT = RV_WR * 64, D = S::D, N = S::N, T = S::T, per = D * N;
   constexpr int NJ = S::NJ;
   constexpr int nkinds = NJ < D ? 2 : 1;
   constexpr RvSmem L = rv_smem<S>(nkinds);
@@ -1093,11 +1107,11 @@ __global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restr
   float* phi = reinterpret_cast<float*>(smem + L.phi);
   float* lut = reinterpret_cast<float*>(smem + L.lut);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int64_t b0 = (int64_t)blockIdx.x * RV_W;
+  const int64_t b0 = (int64_t)blockIdx.x * RV_WR;
   STAMP(1, 0);
   BSTAMP(1, 0);
   // ---- prologue: the token tile, bounds, DoF map and raw basis by DMA, all in flight together
-  stage_rows<NT>(smem + L.tok, tsrc, B, esz, b0, per, RV_W);
+  stage_rows<NT>(smem + L.tok, tsrc, B, esz, b0, per, RV_WR);
   STAMP(1, 9);
   dma4<NT>(wlo, a.w_min, per);
   dma4<NT>(whi, a.w_max, per);
@@ -1113,7 +1127,7 @@ __global__ __launch_bounds__(RV_W * 64) void k_reconstruct_v(const void* __restr
   __syncthreads();   // every DMA and the LUT are in place
   STAMP(1, 2);
   const int j = wave;
-  const int nb = (int)min<int64_t>(RV_W, B - b0);
+  const int nb = (int)min<int64_t>(RV_WR, B - b0);
   if (j >= nb) return;   // no barrier follows
   // ---- W[j][d][n] of this wave's trajectory (bit-exact discrete_to_continuous, init_p for n = 0 of
   //      the joint DoFs: reference :505-510) into its LDS image
@@ -1384,20 +1398,25 @@ int launch_fn(const void* kernel, std::atomic<hipFunction_t> (&cache)[16], unsig
   return BEAST_OK;
 }
 
-template <class S>
-int launch_encode_v(EncArgs a, hipStream_t s) {
-  constexpr EvSmem L = ev_smem<S>(S::NJ < S::D ? 2 : 1);
-  static_assert(L.total <= 80 * 1024, "k_encode_v LDS");
-  a.g = make_geom<RV_W>(S::D, S::NJ, S::N, S::T);
-  a.ntiles = (a.B + RV_W - 1) / RV_W;
-  // write-through stores in the latency regime, write-back for bulk launches (as k_encode's widths)
-  static std::atomic<hipFunction_t> fn[2][16] = {};
-  const bool lat = a.ntiles <= 2 * (int64_t)cu_count();
-  return launch_fn(lat ? reinterpret_cast<const void*>(&k_encode_v<S, LAT_SP>)
-                       : reinterpret_cast<const void*>(&k_encode_v<S, 0>),
-                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_encode_v", a.traj, a.B,
+template <class S, int W, int SP>
+int launch_encode_vw(EncArgs a, hipStream_t s) {
+  constexpr EvSmem L = ev_smem<S, W>(S::NJ < S::D ? 2 : 1);
+  static_assert(L.total <= (W <= 8 ? 80 : 160) * 1024, "k_encode_v LDS");
+  a.g = make_geom<W>(S::D, S::NJ, S::N, S::T);
+  a.ntiles = (a.B + W - 1) / W;
+  static std::atomic<hipFunction_t> fn[16] = {};
+  return launch_fn(reinterpret_cast<const void*>(&k_encode_v<S, SP, W>), fn, (unsigned)a.ntiles, W * 64, L.total, s,
+                   "k_encode_v", a.traj, a.B,
                    EncVArgs{a.dof_src, a.proj, a.w_min, a.w_max, a.tokens_out, a.params_out, a.tok_offset, a.vocab,
                             a.phases});
+}
+
+// write-through stores and RV_WE-wave tiles in the latency regime (at most one 16-trajectory tile
+// per CU), write-back stores and 8-wave tiles for bulk launches
+template <class S>
+int launch_encode_v(EncArgs a, hipStream_t s) {
+  const bool lat = a.B <= 16 * (int64_t)cu_count();
+  return lat ? launch_encode_vw<S, RV_WE, LAT_SP>(a, s) : launch_encode_vw<S, RV_WE_BULK, 0>(a, s);
 }
 
 template <int TBT, class S>
@@ -1496,14 +1515,14 @@ template <class S>
 int launch_rec_v(RecArgs a, hipStream_t s) {
   constexpr int KS = (S::N + 3) / 4;
   constexpr RvSmem L = rv_smem<S>(S::NJ < S::D ? 2 : 1);
-  static_assert(L.total <= 64 * 1024, "k_reconstruct_v LDS");
-  a.tbt = RV_W;
-  a.ntiles = (a.B + RV_W - 1) / RV_W;
+  static_assert(L.total <= (RV_WR <= 8 ? 64 : 160) * 1024, "k_reconstruct_v LDS");
+  a.tbt = RV_WR;
+  a.ntiles = (a.B + RV_WR - 1) / RV_WR;
   static std::atomic<hipFunction_t> fn[2][16] = {};
-  const bool lat = a.ntiles <= 2 * (int64_t)cu_count();
+  const bool lat = a.B <= 16 * (int64_t)cu_count();   // <= 2 eight-trajectory tiles per CU
   return launch_fn(lat ? reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, LAT_SP>)
                        : reinterpret_cast<const void*>(&k_reconstruct_v<KS, S, 0>),
-                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_W * 64, L.total, s, "k_reconstruct_v",
+                   fn[lat ? 1 : 0], (unsigned)a.ntiles, RV_WR * 64, L.total, s, "k_reconstruct_v",
                    static_cast<const void*>(a.tokens), a.B, 8,
                    RecVArgs{a.w_min, a.w_max, a.basis, a.dof_dst, a.init_p, a.init_p_src, a.pos_out, a.tok_offset,
                             a.init_p_sb, a.vocab, a.lut_n, a.phases});

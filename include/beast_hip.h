@@ -46,7 +46,7 @@ const char* beast_last_error(void);
  * reconstruct use their runtime-shape kernels even where a shape-specialised kernel
  * exists (the BEAST defaults T = 50, N = 10, D = 7 / 14); results are identical.
  * BEAST_OPT_BLOCK_WAVES = 4 or 7 forces the workgroup width of the specialised 14-DoF
- * kernels, 8 forces the per-trajectory 8-wave kernels (0 = chosen by batch size); results are
+ * kernels, 8 forces the per-trajectory kernels (16 waves since round 6; 0 = chosen by batch size); results are
  * identical.
  * BEAST_OPT_MERGE_LDS_MIN = n: BPE merges of pairs counted >= n privatise their pair-count deltas
  * in LDS (default 4096; below, global atomics); results are identical.

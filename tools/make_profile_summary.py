@@ -37,7 +37,7 @@ from pmc_summary import summarise  # noqa: E402
 
 # short name -> predicate on the rocprof kernel name (the B = 4,096 instantiations bench.py times)
 KERNELS = {
-    "k_encode_v": lambda n: "k_encode_v<" in n and "14, 4>, 2>" in n,        # write-through: B = 4,096
+    "k_encode_v": lambda n: "k_encode_v<" in n and "14, 4>, 2, 16>" in n,    # write-through, 16 waves: B = 4,096
     "k_reconstruct_v": lambda n: "k_reconstruct_v<" in n and "14, 4>, 2>" in n,
     "k_merge_batch": lambda n: "k_merge_batch(" in n,
     "k_apply_batch": lambda n: "k_apply_batch<" in n,
