@@ -16,7 +16,8 @@ per-pass all-reduce of the pair-count deltas) and checks both against the K5 gol
 cost of issuing it and the GPU's cost of running it (``host_issue_split``).
 
 Timing: W untimed warm-up steps, then ``--windows`` windows of exactly K steps, each
-bracketed by barrier + device synchronize (wall clock, max over ranks); ``value`` /
+bracketed by barrier + device synchronize (wall clock from after the opening synchronize to the
+closing one, the barrier after it; max over ranks); ``value`` /
 ``ms_per_step`` come from the median window (one 20-step window is ~0.2 ms of wall clock:
 start-up jitter would dominate a single one).  Nothing else runs inside a timed window; the
 HIP-event times of the same windows are taken in separate, untimed windows.
@@ -844,14 +845,19 @@ def main():
     # the timed windows hold the K steps and nothing else: HIP events recorded inside a window cost
     # the step ~15 % of wall time on the box (tools/window_probe.py: 12.75 vs 10.81 us per step at
     # K = 20), so the GPU-side times come from windows of their own below
+    # each rank's window ends when ITS device has finished the K steps; the barrier that aligns the
+    # ranks comes after the clock stops, and the max over ranks takes the slowest (at N > 1 a
+    # barrier inside the window would add a collective's latency to every rank's 20 steps)
     walls = []
     for _ in range(max(args.windows, 1)):
         sync(world)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         sync(world)
-        walls.append(max_over_ranks(time.perf_counter() - t0, world, dev))
+        walls.append(max_over_ranks(t1 - t0, world, dev))
     el = float(np.median(walls))
     gpu_ms = []
     for _ in range(5):   # untimed: the same windows with HIP events on the kernels' stream
