@@ -586,21 +586,25 @@ __global__ __launch_bounds__(256) void k_dedup_gather(const uint32_t* __restrict
 // (k_copy_words_cp).  Rows the lane-parallel pass does not take (over PT_LC code points, code
 // points outside [0, 2^31), token offsets from 2^32) set a flag and the host runs the two-pass
 // pipeline instead; a table that fills up sets another and the host retries with a larger one.
+// (round 6) The distinct-word list is compacted from the table afterwards (k_pd_compact) instead
+// of being flushed from per-wave LDS lists: 12 KB less LDS a workgroup, so three workgroups a CU
+// (24 waves instead of 16) -- K5 setup kernels 2.95 -> 2.62 ms (profiles/r06/bpe_setup_ab_r06n.jsonl).
 struct PdWs {
   unsigned long long* keys;   // [cap] tag << 42 | cp length << 32 | token offset; 0 = free
   uint32_t* cnt;              // [cap] occurrences per slot
   uint32_t* rep;              // [cap] distinct word -> token offset of its first occurrence
   uint32_t* lens;             // [cap] distinct word -> cp length << 16 | byte-symbol length
   uint32_t* slot;             // [cap] distinct word -> table slot
+  uint32_t* slens;            // [cap] slot -> cp length << 16 | byte-symbol length
   unsigned long long* info;   // [4] distinct words, words, byte symbols, flags (PD_OVERFLOW | PD_UNSUPPORTED)
   uint64_t cap;
   uint32_t max_probe;
   int tag_bits;               // 22, or fewer (tests force tag collisions)
 };
 constexpr unsigned long long PD_OVERFLOW = 1, PD_UNSUPPORTED = 2, PD_LONG = 4;
-constexpr int PD_NEW = 128;     // per-wave LDS list of new distinct words, flushed with one atomic
 constexpr int PD_LDS = 2048;    // per-workgroup LDS occurrence counts (slot -> count)
 constexpr int PD_WAVES = 8;     // rows (waves) per workgroup
+constexpr int PD_GRID = 3;      // workgroups a CU: all resident at once (49 KB of LDS each)
 
 __device__ __forceinline__ uint64_t cp_hash(const int32_t* cps, int cs, int ce) {
   uint64_t h = 0xcbf29ce484222325ull ^ (uint64_t)(ce - cs);
@@ -609,7 +613,7 @@ __device__ __forceinline__ uint64_t cp_hash(const int32_t* cps, int cs, int ce) 
   return h;
 }
 
-// LC: the longest row the LDS image holds (256 first: four workgroups of 8 waves a CU for BEAST's
+// LC: the longest row the LDS image holds (256 first: three workgroups of 8 waves a CU for BEAST's
 // rows of D * N bins; a longer row flags PD_LONG and the host reruns with 512)
 template <int LC>
 __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long* __restrict__ tok,
@@ -619,7 +623,6 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
   __shared__ PtLdsT<LC> lds[PD_WAVES];
   __shared__ uint8_t s_lut[256];
   __shared__ uint32_t lkey[PD_LDS], lcnt[PD_LDS];
-  __shared__ uint32_t nrep[PD_WAVES][PD_NEW], nlen[PD_WAVES][PD_NEW], nslot[PD_WAVES][PD_NEW];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 256; i += blockDim.x) s_lut[i] = i < lut_n ? lut[i] : (uint8_t)CLS_OTHER;
   for (int i = threadIdx.x; i < PD_LDS; i += blockDim.x) { lkey[i] = 0; lcnt[i] = 0; }
@@ -627,21 +630,7 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
   PtLdsT<LC>& L = lds[wv];
   const uint64_t mask = ws.cap - 1;
   const uint32_t tag_mask = (1u << ws.tag_bits) - 1u;
-  int ncnt = 0;                          // this wave's list length (uniform)
   unsigned long long nwords = 0, nsyms = 0;
-  auto flush_new = [&]() {               // the wave's new distinct words -> the global list
-    if (ncnt == 0) return;
-    unsigned long long b = 0;
-    if (lane == 0) b = atomicAdd(&ws.info[0], (unsigned long long)ncnt);
-    b = __shfl(b, 0);
-    for (int i = lane; i < ncnt; i += 64) {
-      ws.rep[b + i] = nrep[wv][i];
-      ws.lens[b + i] = nlen[wv][i];
-      ws.slot[b + i] = nslot[wv][i];
-    }
-    ncnt = 0;
-    pt_wave_sync();
-  };
   constexpr int PF = LC / 64;
   // the 512 kernel runs after the 256 one and takes only the rows that one left (257..512 code
   // points); it returns at once when there were none (the flag, a kernel boundary ago)
@@ -691,7 +680,6 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
     nsyms += carry;
     // 4. the sequence's words into the distinct-word table, a lane per word
     for (int wb = 0; wb < nw; wb += 64) {
-      if (ncnt > PD_NEW - 64) flush_new();   // uniform
       const int w = wb + lane;
       bool have = false, is_new = false;
       uint64_t k = 0;
@@ -729,19 +717,11 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
           }
         }
       }
-      // new distinct words -> this wave's LDS list (a ballot, no atomics)
-      const unsigned long long nb = __ballot(is_new);
-      if (is_new) {
-        const int u = ncnt + (int)__popcll(nb & ((1ull << lane) - 1ull));
-        nrep[wv][u] = (uint32_t)(r0 + L.wcp[w]);
-        nlen[wv][u] = lens;
-        nslot[wv][u] = (uint32_t)k;
-      }
-      ncnt += (int)__popcll(nb);
+      if (is_new) ws.slens[k] = lens;   // the distinct-word list is compacted from the table afterwards
       // the occurrence, counted in LDS (the frequent words occur millions of times)
       if (have) {
         const uint32_t key = (uint32_t)k + 1u;
-        uint32_t j = (key * 0x9E3779B1u) >> (32 - 11);
+        uint32_t j = (key * 0x9E3779B1u) >> (32 - __builtin_ctz(PD_LDS));
         bool done = false;
         for (int probe = 0; probe < 8 && !done; ++probe) {
           const uint32_t cur = atomicCAS(&lkey[j], 0u, key);
@@ -753,7 +733,6 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
     }
     pt_wave_sync();   // LDS is reused by the next sequence
   }
-  flush_new();
   if (lane == 0) {
     atomicAdd(&ws.info[1], nwords);
     atomicAdd(&ws.info[2], nsyms);
@@ -761,6 +740,42 @@ __global__ __launch_bounds__(64 * PD_WAVES) void k_pretok_dedup(const long long*
   __syncthreads();
   for (int i = threadIdx.x; i < PD_LDS; i += blockDim.x)
     if (lkey[i]) atomicAdd(&ws.cnt[lkey[i] - 1u], lcnt[i]);
+}
+
+// the distinct-word list from the table: 4,096 slots a workgroup (16 a thread, coalesced), one
+// atomic a workgroup for its place in the list
+constexpr int PDC_PER = 16;
+__global__ __launch_bounds__(256) void k_pd_compact(PdWs ws) {
+  __shared__ uint32_t wtot[4];
+  __shared__ unsigned long long gbase;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * (256 * PDC_PER);
+  unsigned long long key[PDC_PER];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < PDC_PER; ++j) {
+    const uint64_t sl = base + (uint64_t)j * 256 + threadIdx.x;
+    key[j] = sl < ws.cap ? ws.keys[sl] : 0ull;
+    cnt += (int)__popcll(__ballot(key[j] != 0ull));
+  }
+  if (lane == 0) wtot[wv] = (uint32_t)cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) gbase = atomicAdd(&ws.info[0], (unsigned long long)(wtot[0] + wtot[1] + wtot[2] + wtot[3]));
+  __syncthreads();
+  unsigned long long o = gbase;
+  for (int i = 0; i < wv; ++i) o += wtot[i];
+#pragma unroll
+  for (int j = 0; j < PDC_PER; ++j) {
+    const uint64_t sl = base + (uint64_t)j * 256 + threadIdx.x;
+    const unsigned long long m = __ballot(key[j] != 0ull);
+    if (key[j] != 0ull) {
+      const unsigned long long i = o + __popcll(m & ((1ull << lane) - 1ull));
+      ws.rep[i] = (uint32_t)key[j];
+      ws.lens[i] = ws.slens[sl];
+      ws.slot[i] = (uint32_t)sl;
+    }
+    o += __popcll(m);
+  }
 }
 
 // distinct word i -> (token offset, byte length, count) for the repack
@@ -1083,41 +1098,45 @@ static uint64_t pd_cap(int64_t n_tokens) {   // ~ n_tokens / 5 slots (K5: 4.85 M
   while (c < (uint64_t)std::max<int64_t>(n_tokens, 1) / 5) c <<= 1;
   return c;
 }
+constexpr uint64_t PD_SLOT_BYTES = 28;   // keys 8, cnt 4, rep 4, lens 4, slot 4, slens 4
 static PdWs pd_view(void* workspace, size_t ws_bytes) {
   PdWs w{};
-  w.cap = 1024;   // the largest power of two the workspace holds (24 bytes a slot)
-  while ((w.cap * 2) * 24 + 64 <= ws_bytes) w.cap *= 2;
+  w.cap = 1024;   // the largest power of two the workspace holds (PD_SLOT_BYTES a slot)
+  while ((w.cap * 2) * PD_SLOT_BYTES + 64 <= ws_bytes) w.cap *= 2;
   char* p = static_cast<char*>(workspace);
   w.keys = reinterpret_cast<unsigned long long*>(p);  p += w.cap * 8;
   w.cnt = reinterpret_cast<uint32_t*>(p);             p += w.cap * 4;
   w.rep = reinterpret_cast<uint32_t*>(p);             p += w.cap * 4;
   w.lens = reinterpret_cast<uint32_t*>(p);            p += w.cap * 4;
   w.slot = reinterpret_cast<uint32_t*>(p);            p += w.cap * 4;
+  w.slens = reinterpret_cast<uint32_t*>(p);           p += w.cap * 4;
   w.info = reinterpret_cast<unsigned long long*>(p);
   w.max_probe = DEDUP_MAX_PROBE;
   w.tag_bits = std::min(22, std::max(1, beast::g_bpe_dedup_key_bits));
   return w;
 }
-extern "C" size_t beast_bpe_pretok_dedup_workspace_bytes(int64_t n_tokens) { return pd_cap(n_tokens) * 24 + 64; }
+extern "C" size_t beast_bpe_pretok_dedup_workspace_bytes(int64_t n_tokens) { return pd_cap(n_tokens) * PD_SLOT_BYTES + 64; }
 
 extern "C" int beast_bpe_pretok_dedup(const int64_t* tok, const int64_t* seq_off, int64_t n_seq, int64_t min_tok,
                                       const uint8_t* cls_lut, int64_t lut_n, void* workspace, size_t ws_bytes,
                                       int64_t* out_info, void* stream) {
   BEAST_REQUIRE(tok && seq_off && cls_lut && workspace && out_info, "beast_bpe_pretok_dedup: null pointer");
-  BEAST_REQUIRE(n_seq >= 0 && ws_bytes >= 1024 * 24 + 64, "beast_bpe_pretok_dedup: bad sizes");
+  BEAST_REQUIRE(n_seq >= 0 && ws_bytes >= 1024 * PD_SLOT_BYTES + 64, "beast_bpe_pretok_dedup: bad sizes");
   hipStream_t s = beast::as_stream(stream);
   PdWs w = pd_view(workspace, ws_bytes);
   BEAST_HIP(hipMemsetAsync(w.keys, 0, w.cap * 12, s), "pretok_dedup memset");   // keys + counts
   BEAST_HIP(hipMemsetAsync(w.info, 0, 32, s), "pretok_dedup memset");
   if (n_seq > 0) {
-    // the waves walk the sequences grid-stride; rows of <= 256 code points first (37 KB of LDS a
+    // the waves walk the sequences grid-stride; rows of <= 256 code points first (49 KB of LDS a
     // workgroup), rows of 257..512 by the 512 kernel only when some row needs it
-    hipLaunchKernelGGL(k_pretok_dedup<256>, dim3(grid_for(n_seq, PD_WAVES, 4 * 256)), dim3(64 * PD_WAVES), 0, s,
+    hipLaunchKernelGGL(k_pretok_dedup<256>, dim3(grid_for(n_seq, PD_WAVES, PD_GRID * 256)), dim3(64 * PD_WAVES), 0, s,
                        reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n, w);
     BEAST_LAUNCHED("k_pretok_dedup<256>");
     hipLaunchKernelGGL(k_pretok_dedup<PT_LC>, dim3(grid_for(n_seq, PD_WAVES, 2 * 256)), dim3(64 * PD_WAVES), 0, s,
                        reinterpret_cast<const long long*>(tok), seq_off, n_seq, (long long)min_tok, cls_lut, lut_n, w);
     BEAST_LAUNCHED("k_pretok_dedup<512>");
+    hipLaunchKernelGGL(k_pd_compact, dim3((unsigned)((w.cap + 256 * PDC_PER - 1) / (256 * PDC_PER))), dim3(256), 0, s, w);
+    BEAST_LAUNCHED("k_pd_compact");
   }
   BEAST_HIP(hipMemcpyAsync(out_info, w.info, 32, hipMemcpyDeviceToDevice, s), "pretok_dedup info");
   return BEAST_OK;

@@ -82,7 +82,7 @@ REC_BYTES = N * D * 8 + T * D * 4                # read tokens, write positions
 FIT_BYTES = T * D * 4 + D * N * 4 * (1 + 4)      # read traj; params written once, read/written per radix pass
 FIT_FLOPS = 2 * T * N * D                        # per trajectory per direction
 K5_GOLDEN = os.path.join(REPO, "tests", "golden", "k5_bpe.json")
-PROFILE = os.path.join(REPO, "profiles", "r05", "profile_summary.json")
+PROFILE = os.path.join(REPO, "profiles", "r06", "profile_summary.json")
 K5_CHUNK = 8192
 # what this rank computed, returned by main() (tests/test_gpu_bench_dist.py compares the ranks)
 RANK_INFO: dict = {}

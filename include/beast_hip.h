@@ -421,7 +421,7 @@ int beast_bpe_dedup_words(const uint16_t* sym, const uint32_t* wstart, const uin
  * bit 0: the table filled up (retry with 4x the workspace), bit 1: a row the one-pass kernel does
  * not take (over 512 code points, a code point outside [0, 2^31), token offsets from 2^32): run
  * the two-pass functions above instead.  Workspace: beast_bpe_pretok_dedup_workspace_bytes(total
- * tokens); it keeps the distinct-word list for beast_bpe_pretok_dedup_repack, which writes the
+ * tokens; 28 bytes a table slot); it keeps the distinct-word list for beast_bpe_pretok_dedup_repack, which writes the
  * same outputs as beast_bpe_dedup_words + beast_bpe_repack_words (words of >= 2 symbols in
  * length order, their counts), byte symbols made from the code points (byte2id as pretok_emit).
  * repack_ws_bytes >= beast_bpe_repack_workspace_bytes(n_distinct) + 8 * (n_distinct + 1). */

@@ -699,7 +699,7 @@ def test_bpe_pretok_dedup_equals_two_pass(gpu_device, mode):
             lib.beast_set_option(_lib.OPT_BPE_DEDUP_KEY_BITS, 3)
         if mode == "overflow":   # 2,048 slots for thousands of distinct words: the kernel flags it, ops retries
             ops_lib = _lib.load()
-            ops_lib.beast_bpe_pretok_dedup_workspace_bytes = lambda n: 2048 * 24 + 64
+            ops_lib.beast_bpe_pretok_dedup_workspace_bytes = lambda n: saved(5 * 2048)   # a 2,048-slot table
         res = ops.pretok_dedup(flat, off, 17, lut, byte2id)
     finally:
         lib.beast_set_option(_lib.OPT_BPE_DEDUP_KEY_BITS, 64)
