@@ -660,16 +660,17 @@ def test_bpe_dedup_and_compact_match_counter(gpu_device):
     assert got_c == sorted(keep)
 
 
-@pytest.mark.parametrize("mode", ["plain", "tag3", "overflow", "mixed_utf8"])
+@pytest.mark.parametrize("mode", ["plain", "tag3", "overflow", "mixed_utf8", "long_rows"])
 def test_bpe_pretok_dedup_equals_two_pass(gpu_device, mode):
-    """The one-pass setup (k_pretok_dedup + repack from code points) gives exactly the two-pass
-    pipeline's distinct words x counts, in the same layout (length order, 4-symbol spans), and the
-    same word / symbol totals: with forced 3-bit hash tags (every tag collides; the code-point
-    compare keeps words apart), with a table too small for the words (the retry), and over
-    code points of 1-3 UTF-8 bytes."""
+    """The one-pass setup (k_pretok_dedup + the table compaction + repack from code points) gives
+    exactly the two-pass pipeline's distinct words x counts, in the same layout (length order,
+    4-symbol spans), and the same word / symbol totals: with forced 3-bit hash tags (every tag
+    collides; the code-point compare keeps words apart), with a table too small for the words (the
+    retry), over code points of 1-3 UTF-8 bytes, and over ragged rows of which some take the
+    512-code-point kernel (257..512 code points)."""
     from collections import Counter
     from beast_tokenizer_amd import _lib
-    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, fixed_rows_to_device
+    from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet, fixed_rows_to_device, sequences_to_device
     from beast_tokenizer_amd.pretok import class_lut
     rng = np.random.default_rng(23)
     hi = 3000 if mode == "mixed_utf8" else 300
@@ -677,7 +678,14 @@ def test_bpe_pretok_dedup_equals_two_pass(gpu_device, mode):
     arr = base[rng.integers(0, 9, size=(4000, 60))]
     arr[::7] = rng.integers(0, hi, size=(arr[::7].shape[0], 60))
     arr[::11, ::5] = 32   # spaces: more, shorter words
-    flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64) + 17).to(gpu_device))
+    if mode == "long_rows":
+        seqs = [base[rng.integers(0, 9, size=n)] for n in rng.choice([40, 256, 257, 300, 512], size=900)]
+        for q in seqs[::5]:
+            q[::6] = 32
+        arr = np.concatenate(seqs)
+        flat, off = sequences_to_device([q.astype(np.int64) + 17 for q in seqs], gpu_device)
+    else:
+        flat, off = fixed_rows_to_device(torch.from_numpy(arr.astype(np.int64) + 17).to(gpu_device))
     present = np.zeros(hi, dtype=bool)
     present[np.unique(arr)] = True
     _, _, byte2id = build_alphabet(present, [chr(i) for i in range(hi)], [])
