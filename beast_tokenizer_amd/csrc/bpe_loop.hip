@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t merge_global(uint16_t* __restrict__ s, uint3
   }
   if (!hit) return 0;
   const int32_t cnt = wcount ? (int32_t)wcount[w] : 1;
-  uint32_t r = 0, o = 0;
+  uint32_t r = 0, o = 0, py = 0;
   unsigned long long sg = 0;
   while (r < L) {
     uint32_t y = s[r];
@@ -115,8 +115,9 @@ __device__ __forceinline__ uint32_t merge_global(uint16_t* __restrict__ s, uint3
     } else {
       r += 1;
     }
+    sg |= sig_sym(y) | (o ? sig_pair(py, y) : 0ull);
+    py = y;
     s[o++] = (uint16_t)y;
-    sg |= sig_bit(y);
   }
   g = sg;
   return o;
@@ -167,7 +168,7 @@ __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2
                                                int32_t cnt, const Op& m, unsigned long long& g, uint32_t& napp) {
   const uint32_t a = (uint32_t)m.a, b = (uint32_t)m.b, nid = (uint32_t)m.nid;
   uint2* __restrict__ out = reinterpret_cast<uint2*>(s);
-  uint32_t o = 0;
+  uint32_t o = 0, py = 0;
   bool skip = false;
   unsigned long long sg = 0, acc = 0, occ = 0;
 #pragma unroll
@@ -180,7 +181,8 @@ __device__ __forceinline__ uint32_t merge_regs(const uint32_t (&v)[MERGE_REG + 2
     const uint32_t y = hit ? nid : v[i];
     if (emit) {
       acc |= (unsigned long long)y << (16 * (o & 3u));
-      sg |= sig_bit(y);
+      sg |= sig_sym(y) | (o ? sig_pair(py, y) : 0ull);
+      py = y;
       ++o;
       if ((o & 3u) == 0) {
         out[(o >> 2) - 1] = make_uint2((uint32_t)acc, (uint32_t)(acc >> 32));
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(256) void k_merge(uint16_t* __restrict__ sym, const
   __syncthreads();
   const uint32_t newlen = tlen[a] + tlen[b];
   const MergeOp mop{a, b, nid, max_len, newlen, tlen, dv, dv + Vt, dv + 2 * Vt, dv + 3 * Vt};
-  const unsigned long long need = sig_bit(a) | sig_bit(b);
+  const unsigned long long need = sig_need((uint32_t)a, (uint32_t)b);
   bool any = false;
   auto merge_word = [&](int64_t w) {
     const uint32_t L = wlen[w];
@@ -879,7 +881,7 @@ __global__ __launch_bounds__(256) void k_merge_batch(uint16_t* __restrict__ sym,
     s_nid[threadIdx.x] = rn;
     s_len[threadIdx.x] = rl;
     s_apps[threadIdx.x] = 0;
-    s_need[threadIdx.x] = (int)threadIdx.x < n ? sig_bit((uint32_t)ra) | sig_bit((uint32_t)rb) : ~0ull;
+    s_need[threadIdx.x] = (int)threadIdx.x < n ? sig_need((uint32_t)ra, (uint32_t)rb) : ~0ull;
   }
   if (threadIdx.x == 0) { cn = 0; touched = 0; }
   const int stride = vcur + n;

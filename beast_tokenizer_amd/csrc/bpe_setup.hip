@@ -931,9 +931,7 @@ __global__ __launch_bounds__(256) void k_word_sig(const uint16_t* __restrict__ s
                                                   unsigned long long* __restrict__ sig) {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
     const uint16_t* s = sym + wstart[w];
-    unsigned long long g = 0;
-    for (uint32_t i = 0, L = wlen[w]; i < L; ++i) g |= sig_bit(s[i]);
-    sig[w] = g;
+    sig[w] = sig_of([&](uint32_t i) { return (uint32_t)s[i]; }, wlen[w]);
   }
 }
 
