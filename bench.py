@@ -216,19 +216,26 @@ def host_issue_split(step, stream: torch.cuda.Stream, K: int, rounds: int = 7) -
             step()
         est = (time.perf_counter() - t0) * 1e6 / K
         torch.cuda.synchronize()
-        # a sleep of ~10x the estimated issue time (>= 2 ms), its duration measured on the GPU
+        # a sleep of ~10x the estimated issue time (>= 2 ms), its duration measured on the GPU.  The
+        # sleep kernel is launched once untimed first: its first launch carries the module load, and
+        # a calibration on it alone once left every round's sleep too short (all rounds dropped)
+        target = max(10.0 * est * K, 2000.0)
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
         cycles = 100000
-        for _ in range(4):
+        for _ in range(8):
             s0.record(stream)
             torch.cuda._sleep(cycles)
             s.record(stream)
             s.synchronize()
             sleep_us = s0.elapsed_time(s) * 1e3
-            if sleep_us >= max(10.0 * est * K, 2000.0):
+            if sleep_us >= target:
                 break
-            cycles = int(cycles * max(2.0, 1.2 * max(10.0 * est * K, 2000.0) / max(sleep_us, 1.0)))
+            cycles = int(cycles * max(2.0, 1.2 * target / max(sleep_us, 1.0)))
         host, gpu, dropped = [], [], 0
-        for _ in range(rounds):
+        for _ in range(rounds + 6):
+            if len(host) == rounds:
+                break
             torch.cuda.synchronize()
             s0.record(stream)
             torch.cuda._sleep(cycles)
@@ -240,9 +247,11 @@ def host_issue_split(step, stream: torch.cuda.Stream, K: int, rounds: int = 7) -
             e.record(stream)
             torch.cuda.synchronize()
             # the launches were all queued while the sleep still ran (it started no earlier than t0
-            # minus a launch, and lasted sleep_us): otherwise the GPU time may hold host gaps
+            # minus a launch, and lasted sleep_us): otherwise the GPU time may hold host gaps, and
+            # the next round sleeps longer
             if (t1 - t0) * 1e6 > 0.8 * s0.elapsed_time(s) * 1e3:
                 dropped += 1
+                cycles *= 4
                 continue
             host.append((t1 - t0) * 1e6 / K)
             gpu.append(s.elapsed_time(e) * 1e3 / K)
