@@ -264,7 +264,10 @@ class GpuBpeModel:
         max_syms = max_row * _utf8_len(min(cp_bound, 0x10FFFF))
         ids = torch.empty((max(R, 1), max(max_syms, 1)), dtype=torch.int32, device=dev)
         st = torch.empty((2, max(R, 1)), dtype=torch.int32, device=dev)   # lens, status
-        args = ("beast_bpe_encode_rows", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+        # every row empty: no bin is read, but the C-ABI takes a non-null pointer (found by
+        # tests/test_gpu_properties.py: rows of width 0 raised "null pointer argument")
+        tok_p = tok.data_ptr() if tok.numel() else row_off.data_ptr()
+        args = ("beast_bpe_encode_rows", tok_p, row_off.data_ptr(), R, int(min_token),
                 -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
                 self.byte2id.data_ptr(), self.map.data_ptr(), self.n_merges, self.spec_cps.data_ptr(),
                 self.spec_len.data_ptr(), self.spec_id.data_ptr(), self.n_spec, self.unk_id, self.fuse_unk,
@@ -291,7 +294,8 @@ class GpuBpeModel:
         st = torch.empty((2, max(R, 1)), dtype=torch.int32, device=dev)   # lens, status
         if R == 0:
             return ids[:0], st[0, :0], st[1, :0]
-        _lib.run("beast_bpe_encode_rows_words", tok.data_ptr(), row_off.data_ptr(), R, int(min_token),
+        tok_p = tok.data_ptr() if tok.numel() else row_off.data_ptr()   # every row empty: nothing is read
+        _lib.run("beast_bpe_encode_rows_words", tok_p, row_off.data_ptr(), R, int(min_token),
                  -1 if max_span is None else int(max_span), self.lut.data_ptr(), self.lut.numel(),
                  self.byte2id.data_ptr(), self.wordmap.data_ptr(), self.wordmap_log2b, self.unk_id, self.fuse_unk,
                  int(max_row), int(max_syms), ids.data_ptr(), ids.shape[1], st[0].data_ptr(),
