@@ -21,7 +21,7 @@ import json
 import numpy as np
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, example, given, settings
 from hypothesis import strategies as st
 
 from beast_tokenizer_amd import BEASTBsplineTokenizer
@@ -39,9 +39,11 @@ def _dn_to_nd(t, B, D, N):
     return t.reshape(B, D, N).transpose(0, 2, 1).reshape(B, N * D)
 
 
-@settings(max_examples=60, **SETTINGS)
+@settings(max_examples=150, **SETTINGS)
 @given(vocab=st.sampled_from([2, 3, 17, 256, 1000, 4096]), D=st.integers(1, 16), N=st.integers(5, 12),
        B=st.integers(1, 300), seed=st.integers(0, 2 ** 31 - 1), offset=st.sampled_from([0, 31744]))
+@example(vocab=4096, D=16, N=12, B=300, seed=1, offset=31744)
+@example(vocab=256, D=14, N=10, B=4096, seed=2, offset=0)
 def test_prop_quantise_dequantise_bitexact(vocab, D, N, B, seed, offset, gpu_device):
     rng = np.random.default_rng(seed)
     m = D * N
@@ -78,9 +80,13 @@ def test_prop_quantise_dequantise_bitexact(vocab, D, N, B, seed, offset, gpu_dev
     assert np.array_equal(dec, O.discrete_to_continuous(t, lo, hi, vocab))
 
 
-@settings(max_examples=40, **SETTINGS)
+@settings(max_examples=100, **SETTINGS)
 @given(D=st.integers(1, 16), N=st.integers(5, 12), T=st.integers(8, 80), B=st.integers(1, 400),
        vocab=st.sampled_from([17, 256, 1024]), seed=st.integers(0, 2 ** 31 - 1), clamp=st.floats(0.0, 0.2))
+@example(D=14, N=10, T=50, B=4096, vocab=256, seed=3, clamp=0.01)     # the bench shape: k_encode_v / k_reconstruct_v
+@example(D=7, N=10, T=50, B=333, vocab=256, seed=4, clamp=0.05)       # fixed shape, a partial last tile
+@example(D=16, N=12, T=80, B=400, vocab=1024, seed=5, clamp=0.2)      # runtime shape, T > 64
+@example(D=1, N=5, T=8, B=1, vocab=17, seed=6, clamp=0.0)
 def test_prop_encode_reconstruct_shapes(D, N, T, B, vocab, seed, clamp, gpu_device):
     x = synth_trajectories(B, T, D, seed=seed % 100000)
     phi = O.basis(O.times_grid(2 * np.pi, T), F32(2 * np.pi), 4, N)
@@ -109,8 +115,9 @@ def test_prop_encode_reconstruct_shapes(D, N, T, B, vocab, seed, clamp, gpu_devi
 _CPS = np.array([ord(c) for c in "ab z09 '  \t\nstrevmld!?,.-"] + [0xA0, 0xC4, 0xE9, 0xB5, 0xD7, 0x85, 0x1F])
 
 
-@settings(max_examples=60, **SETTINGS)
+@settings(max_examples=150, **SETTINGS)
 @given(rows=st.lists(st.lists(st.integers(0, len(_CPS) - 1), max_size=700), min_size=1, max_size=24))
+@example(rows=[[i % len(_CPS) for i in range(700)], [], [3], [7] * 513])
 def test_prop_pretokenizer_matches_oracle(rows, gpu_device):
     from beast_tokenizer_amd.bpe_train import GpuBpeOps, build_alphabet
     from beast_tokenizer_amd.pretok import class_lut
@@ -145,9 +152,10 @@ def _hf_train(arr, vocab, min_freq):
     return bpe
 
 
-@settings(max_examples=25, **SETTINGS)
+@settings(max_examples=60, **SETTINGS)
 @given(seed=st.integers(0, 2 ** 31 - 1), alpha=st.integers(2, 40), span=st.sampled_from([20, 255, 700]),
        rows=st.integers(1, 300), width=st.integers(1, 80), extra=st.integers(0, 600), min_freq=st.integers(1, 4))
+@example(seed=7, alpha=40, span=700, rows=300, width=80, extra=600, min_freq=1)
 def test_prop_bpe_train_matches_hf(seed, alpha, span, rows, width, extra, min_freq, gpu_device):
     """The GPU trainer (setup kernels + the batched device loop) against HF's BpeTrainer on a
     random corpus: a few common bins (repetition, so merges chain) over a sparse wider range."""
@@ -182,9 +190,11 @@ def _codec_model(gpu_device):
     return _CODEC["hf"], _CODEC["model"]
 
 
-@settings(max_examples=50, **SETTINGS)
+@settings(max_examples=120, **SETTINGS)
 @given(seed=st.integers(0, 2 ** 31 - 1), n=st.integers(1, 64), width=st.integers(0, 300),
        sigma=st.sampled_from([0.0, 3.0, 20.0, 90.0]), path=st.sampled_from(["auto", "rows"]))
+@example(seed=8, n=64, width=300, sigma=90.0, path="rows")
+@example(seed=9, n=64, width=300, sigma=3.0, path="auto")
 def test_prop_bpe_codec_matches_hf(seed, n, width, sigma, path, gpu_device):
     """Random rows (smooth or noisy, empty, longer than the training rows) encode to HF's ids and
     HF's ids decode back to the rows, through the default path (k_bpe_words) and the per-row
