@@ -281,7 +281,9 @@ static int bpe_train_impl(const int64_t* tokens, const int64_t* seq_off, int64_t
     BEAST_REQUIRE(seq_off && cls_lut && out_min_token && out_max_token && out_vocab_bytes && out_vocab_off &&
                       out_n_vocab && out_merges && out_n_merges && (n_special == 0 || special_tokens),
                   "beast_bpe_train: null pointer argument");
-    BEAST_REQUIRE(n_seq >= 1 && vocab_size >= 1 && n_special >= 0, "beast_bpe_train: bad sizes");
+    // with a communicator a rank may hold no sequences at all (its shard of the corpus is empty;
+    // the total is checked below); alone, the reference's "no non-empty sequences" rule applies
+    BEAST_REQUIRE(n_seq >= (comm != nullptr ? 0 : 1) && vocab_size >= 1 && n_special >= 0, "beast_bpe_train: bad sizes");
     BEAST_HIP(hipMemcpyAsync(&n_tok, seq_off + n_seq, sizeof(int64_t), hipMemcpyDeviceToHost, s), "seq_off read");
     BEAST_HIP(hipStreamSynchronize(s), "stream sync");
     BEAST_REQUIRE(n_tok >= 0 && (n_tok == 0 || tokens != nullptr), "beast_bpe_train: null pointer argument");

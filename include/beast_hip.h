@@ -385,7 +385,7 @@ int beast_comm_allgatherv(beast_comm* comm, const void* send, void* recv, const 
  * words, the pair table is SUM-reduced once and each pass's pair-count changes are SUM-reduced
  * between its merge and apply launches (the host-driven loop: each merge's), so the words of
  * no single GPU need to hold the corpus.  Every rank returns the same vocabulary and merges; a
- * shard may be empty (replicated form).  All ranks must call it with the same options.  A failure
+ * shard may be empty (n_seq 0, or sequences without tokens), in either form.  All ranks must call it with the same options.  A failure
  * on one rank (an allocation, a launch, a shard over 2^32 symbols) is agreed over the communicator
  * before the next collective (the status all-reduced with MAX), so every rank returns an error
  * together: the failing rank its own, the others its code with a message naming the cause.

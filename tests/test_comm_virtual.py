@@ -4,7 +4,7 @@
 What runs here and nowhere else on a one-GPU box (RCCL cannot form a world > 1 on one device):
 * the reductions with rank-dependent inputs, so SUM / MIN / MAX are told apart, the all-gather
   and the all-gather-v with uneven counts and an empty rank (comm.hip's displacements);
-* ``beast_bpe_train_comm`` over 2 and 3 disjoint shards -- replicated (union_words' rank offsets,
+* ``beast_bpe_train_comm`` over 2, 3, 4 and 8 disjoint shards (one of them empty from 4 on) -- replicated (union_words' rank offsets,
   ``k_offset_starts``, and the all-gather-v of the words) and sharded (the per-pass delta
   all-reduce; the host-driven loop's per-merge one) -- against the HF golden merges of the whole
   corpus (tests/golden/bpe_hf.json; reference beast/beast_bpe_trainer.py:61-98) and the one-rank call;
@@ -46,14 +46,17 @@ def _on_threads(n, fn):
 
 
 def _shards(rows: np.ndarray, n: int):
-    """n disjoint, uneven row ranges covering rows."""
-    frac = {2: [0.4], 3: [0.25, 0.6]}[n]
+    """n disjoint, uneven row ranges covering rows; from 4 ranks on, rank 1's range is empty (a
+    rank with no words: SURVEY §4.3's 1/2/4/8 shards, the empty-shard paths of the collectives)."""
+    frac = {2: [0.4], 3: [0.25, 0.6]}.get(n) or [((k / n) ** 1.3) for k in range(1, n)]
     cuts = [0] + [int(len(rows) * f) for f in frac] + [len(rows)]
+    if n >= 4:
+        cuts[2] = cuts[1]
     return [rows[cuts[i]:cuts[i + 1]] for i in range(n)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_virtual_collectives_rank_dependent(gpu_device, n):
     import torch
     from beast_tokenizer_amd.comm import Communicator
@@ -99,7 +102,7 @@ CASES = ["skew/2048", "traj_k3/700", "runs/700", "wide3000/2048"]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 @pytest.mark.parametrize("replicate", [True, False])
 def test_virtual_bpe_train_comm_equals_hf(gpu_device, n, replicate):
     import torch
