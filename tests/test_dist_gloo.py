@@ -55,6 +55,10 @@ def _worker(rank, world, port, case, q):
             from beast_tokenizer_amd.bpe_train import fixed_rows_to_device, train_bpe
             arr = np.load(os.path.join(HERE, "golden", "bpe_corpora.npz"))[case[1]]
             shard = arr[rank::world]
+            if world > 2:   # uneven contiguous shards, rank 1's empty (a rank with no sequences)
+                cuts = [0] + [len(arr) * k // world for k in range(1, world)] + [len(arr)]
+                cuts[2] = cuts[1]
+                shard = arr[cuts[rank]:cuts[rank + 1]]
             flat, off = fixed_rows_to_device(torch.from_numpy(shard.astype(np.int64)))
             mode = case[3]
             res = train_bpe(flat, off, case[2], ops=NumpyBpeOps(batched=mode != "per_merge_allreduce"), reduce=red,
@@ -136,6 +140,18 @@ def test_bpe_two_ranks_matches_hf(cname, vs, mode):
     assert (lo0, hi0) == (ref["min_token"], ref["max_token"])
     assert v0 == ref["vocab"]
     assert m0 == ref["merges"]
+
+
+@pytest.mark.parametrize("mode", ["gather_words", "sharded_batched"])
+def test_bpe_four_ranks_one_empty_matches_hf(mode):
+    """World 4 (SURVEY §4.3's 1/2/4/8 shards) with rank 1 holding no sequences: both multi-rank
+    forms still equal the HF goldens on every rank."""
+    import json
+    ref = json.load(open(os.path.join(HERE, "golden", "bpe_hf.json")))["runs/700"]
+    out = _run(("bpe", "runs", 700, mode), world=4)
+    for _, v, m, lo, hi in out:
+        assert (lo, hi) == (ref["min_token"], ref["max_token"])
+        assert v == ref["vocab"] and m == ref["merges"]
 
 
 def test_update_bounds_two_ranks_match_one_process():
