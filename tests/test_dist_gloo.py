@@ -1,4 +1,4 @@
-"""World-size-2 gloo tests of the data-parallel drivers (CPU; no GPU).
+"""World-size-2 and -4 gloo tests of the data-parallel drivers (CPU; no GPU).
 
 The product drivers ``train_bpe`` and ``column_quantiles`` run unchanged with their
 torch.distributed all-reduce steps; the device kernels are replaced by the numpy
@@ -107,6 +107,9 @@ def _worker(rank, world, port, case, q):
             x = rng.standard_normal((1001, 12)).astype(np.float32)
             x[::3, 2] = 0.25
             shard = x[rank * 600: (rank + 1) * 600] if rank == 0 else x[600:]
+            if world > 2:   # uneven contiguous shards, rank 1's empty
+                cuts = [0, 137, 137] + [137 + (1001 - 137) * k // (world - 2) for k in range(1, world - 1)]
+                shard = x[cuts[rank]:cuts[rank + 1]]
             out = column_quantiles(torch.from_numpy(shard), [0.01, 0.99], red, ops=NumpyQuantileOps())
             q.put((rank, out.numpy(), np.stack([np.quantile(x, q, axis=0) for q in (0.01, 0.99)])))
     finally:
@@ -188,3 +191,11 @@ def test_quantile_two_ranks_matches_numpy():
     (r0, a, ref), (r1, b, _) = _run(("q",))
     assert np.array_equal(a, b)
     assert np.array_equal(a, ref)
+
+
+def test_quantile_four_ranks_one_empty_matches_numpy():
+    """fit_parameters' quantile collective at world 4 with an empty rank: np.quantile of the union
+    on every rank, bit for bit."""
+    out = _run(("q",), world=4)
+    for _, a, ref in out:
+        assert np.array_equal(a, ref)
