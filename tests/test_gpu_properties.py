@@ -227,3 +227,39 @@ def _codec_case(hf, model, seed, n, width, sigma, gpu_device):
     out, counts = out.cpu().numpy(), counts.cpu().numpy()
     assert counts.tolist() == [width] * n
     assert all(out[i, :width].tolist() == rows[i].tolist() for i in range(n))
+
+
+_COND = [(1, 0), (2, 0), (0, 1), (0, 2), (0, -1), (1, 1), (2, 2), (2, -1), (1, -1)]
+
+
+@settings(max_examples=60, **SETTINGS)
+@example(ic_ec=(2, -1), D=14, B=64, seed=10, clamp=0.02)
+@given(ic_ec=st.sampled_from(_COND), D=st.integers(1, 14), B=st.integers(2, 64), seed=st.integers(0, 2 ** 31 - 1),
+       clamp=st.floats(0.0, 0.1))
+def test_prop_conditioned_encode_reconstruct(ic_ec, D, B, seed, clamp, gpu_device):
+    """init_cond_order / end_cond_order != 0 over random DoF counts and
+    batches: params within 1e-5 of the float64 conditioned fit (oracle cond_fit), tokens equal to
+    the quantiser on the GPU params, and reconstruct (with the fit's boundary conditions) within
+    1e-5 of the oracle's cond_reconstruct_joint."""
+    ic, ec = ic_ec
+    N, T = 10, 50
+    x = synth_trajectories(B, T, D, seed=seed % 100000)
+    times = O.times_grid(2 * np.pi, T)
+    tau = F32(2 * np.pi)
+    want_p, st_ = O.cond_fit(x, times, tau, 4, N, ic, ec)
+    lo = np.quantile(want_p, clamp, axis=0).astype(F32) - F32(1e-3)
+    hi = np.quantile(want_p, 1 - clamp, axis=0).astype(F32) + F32(1e-3)
+    tok = BEASTBsplineTokenizer(num_dof=D, init_cond_order=ic, end_cond_order=ec, device=str(gpu_device))
+    tok.load_state_dict({"w_min": lo.tolist(), "w_max": hi.tolist()})
+    tokens, pd = tok.encode(torch.from_numpy(x).to(gpu_device))
+    got = pd["params"].cpu().numpy()
+    scale = np.maximum(1.0, np.abs(want_p).max(axis=1, keepdims=True))
+    assert np.all(np.abs(got - want_p) <= 1e-5 * scale), np.abs(got - want_p).max()
+    want_t = _dn_to_nd(O.continuous_to_discrete(O._clamp_t(got, lo, hi), lo, hi, 256), B, D, N)
+    assert np.array_equal(tokens.cpu().numpy(), want_t)
+    pos = tok.reconstruct_traj(tokens).cpu().numpy()
+    dec = O.decode(tokens.cpu().numpy(), O.Layout.make(D, None, False), N, lo, hi, 256).reshape(B, D, N)
+    full = O.cond_full_basis(times, tau, 4, N, ic, ec)
+    ref = O.cond_reconstruct_joint(dec, full, st_, ic, ec)
+    rs = np.maximum(1.0, np.abs(ref).max(axis=(1, 2), keepdims=True))
+    assert np.max(np.abs(pos - ref) / rs) <= 1e-5
