@@ -107,7 +107,7 @@ class _Plan:
 
     __slots__ = ("dev", "idx", "version", "wmin", "wmax", "keep", "T", "min_din", "dkey", "pinned",
                  "p_phi", "p_proj", "p_src", "p_dst", "p_wmn", "p_wmx", "enc", "rec", "fast", "fast_addr",
-                 "fast_enc", "fast_rec")
+                 "fast_enc", "fast_rec", "llm", "off")
 
     def __init__(self, tok: "BEASTBsplineTokenizer", dev: torch.device):
         lib = _lib.load()
@@ -118,6 +118,9 @@ class _Plan:
         self.dkey = tok.device                                  # the device argument it was built for
         self.pinned = torch.device(tok.device).index is not None
         self.wmin, self.wmax = tok.w_min, tok.w_max
+        # the LLM-vocabulary offset the hot path adds (reference :456-481): part of the plan's key
+        self.llm = tok.llm_vocab_size
+        self.off = tok.llm_vocab_size - tok.vocab_size if tok.llm_vocab_size is not None else 0
         self.keep = (phi, proj32, src, dst, wmn, wmx)          # owns every pointer below
         self.T = phi.shape[1]
         order = tok.joint_indices + tok.gripper_indices
@@ -272,11 +275,13 @@ class BEASTBsplineTokenizer(TokenizerBase):
         if p is not None:
             b = self._buffers
             if (p.version == self._times_version and p.wmin is b.get("w_min") and p.wmax is b.get("w_max")
-                    and p.dkey is self.device and (p.pinned or p.idx == torch.cuda.current_device())):
+                    and p.llm == self.llm_vocab_size and p.dkey is self.device
+                    and (p.pinned or p.idx == torch.cuda.current_device())):
                 return p
         dev = self._dev()
         p = self._plans.get(dev.index)
-        if p is None or p.version != self._times_version or p.wmin is not self.w_min or p.wmax is not self.w_max:
+        if (p is None or p.version != self._times_version or p.wmin is not self.w_min or p.wmax is not self.w_max
+                or p.llm != self.llm_vocab_size):
             p = _Plan(self, dev)
             if p.cacheable():
                 self._plans[dev.index] = p
@@ -669,12 +674,12 @@ class BEASTBsplineTokenizer(TokenizerBase):
         extremes of every rank's batch (one all-reduce; a collective call), so all ranks
         quantise with the same bounds -- those of one process encoding the global batch."""
         p = self._plan()
-        offset = (self.llm_vocab_size - self.vocab_size
-                  if respect_llm_vocab_size and self.llm_vocab_size is not None else 0)
         if not update_bounds and p.fast_enc is not None:
-            r = p.fast_enc(p.fast_addr, trajs, offset)   # (tokens, {"params": ..., conditions None})
+            # (tokens, {"params": ..., conditions None}); the plan carries the LLM offset
+            r = p.fast_enc(p.fast_addr, trajs, p.off if respect_llm_vocab_size else 0)
             if r is not None:
                 return r
+        offset = p.off if respect_llm_vocab_size else 0
         if update_bounds:
             with torch.no_grad():
                 params, _ = self._fit(trajs, None, p)
@@ -816,8 +821,8 @@ class BEASTBsplineTokenizer(TokenizerBase):
     def reconstruct_traj(self, tokens, times=None, **kwargs):
         """Positions [B, T, num_dof] from tokens (reference :498-536); kwargs: init_p [B, num_dof]."""
         p = self._plan()
-        if times is None and p.fast_rec is not None and kwargs.get("init_p") is None:
-            r = p.fast_rec(p.fast_addr, tokens, self._offset(True))
+        if times is None and not kwargs and p.fast_rec is not None:   # init_p=None takes the path below
+            r = p.fast_rec(p.fast_addr, tokens, p.off)
             if r is not None:
                 return r
         tokens = self._token_rows(tokens, p.dev)
