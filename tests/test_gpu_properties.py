@@ -263,3 +263,36 @@ def test_prop_conditioned_encode_reconstruct(ic_ec, D, B, seed, clamp, gpu_devic
     ref = O.cond_reconstruct_joint(dec, full, st_, ic, ec)
     rs = np.maximum(1.0, np.abs(ref).max(axis=(1, 2), keepdims=True))
     assert np.max(np.abs(pos - ref) / rs) <= 1e-5
+
+
+@settings(max_examples=60, **SETTINGS)
+@example(rows=1, cols=140, seed=11, kind=0, blocks=1, qs=(0.01, 0.99))
+@example(rows=70001, cols=140, seed=12, kind=3, blocks=4, qs=(0.01, 0.99))
+@given(rows=st.integers(1, 5000), cols=st.integers(1, 150), seed=st.integers(0, 2 ** 31 - 1),
+       kind=st.integers(0, 4), blocks=st.integers(1, 4),
+       qs=st.sampled_from([(0.01, 0.99), (0.0, 1.0), (0.5,), (0.25, 0.75, 0.01, 0.999)]))
+def test_prop_column_quantiles_equal_numpy(rows, cols, seed, kind, blocks, qs, gpu_device):
+    """fit_parameters' bounds (reference :211-214, np.quantile(params, q, axis=0)) by the radix
+    select kernels, bit for bit, over random column distributions: normal, heavy-tailed, few
+    distinct values (ties), constant columns, +-inf and NaN entries; the rows as one matrix or as
+    a list of row blocks (the per-batch params of fit_parameters, read in place)."""
+    from beast_tokenizer_amd.quantile import column_quantiles
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((rows, cols)).astype(F32)
+    if kind == 1:
+        x = (rng.standard_cauchy((rows, cols)) * 10).astype(F32)
+    elif kind == 2:
+        x = np.round(x * 2).astype(F32) / F32(2)              # a handful of distinct values
+    elif kind == 3:
+        x[:, ::3] = F32(0.125)                                 # constant columns
+        x[rng.random((rows, cols)) < 0.001] = np.inf
+        x[rng.random((rows, cols)) < 0.001] = -np.inf
+    elif kind == 4:
+        x[rng.random((rows, cols)) < 0.01] = np.nan            # NaN anywhere: np.quantile gives NaN
+    with np.errstate(invalid="ignore"):                        # inf - inf inside numpy's lerp
+        want = np.stack([np.quantile(x, F32(q), axis=0) for q in qs]).astype(F32)
+    xd = torch.from_numpy(x).to(gpu_device)
+    cuts = sorted(set([0, rows] + [int(c) for c in rng.integers(0, rows + 1, size=blocks - 1)]))
+    src = [xd[a:b] for a, b in zip(cuts[:-1], cuts[1:])] if blocks > 1 else xd
+    got = column_quantiles(src, list(qs)).cpu().numpy()
+    assert np.array_equal(got, want, equal_nan=True)
